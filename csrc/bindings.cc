@@ -1,0 +1,347 @@
+// pybind11 module `_core`: the Python face of the native runtime. Python only
+// wires things together (CLI, config, bench); every state machine, transport,
+// scheduler and data engine runs in C++ threads with the GIL released.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "core/log.h"
+#include "core/wire.h"
+#include "engine/engine.h"
+#include "gpu/gpu_api.h"
+#include "roles/node.h"
+#include "sched/maxflow.h"
+#include "store/store.h"
+#include "transport/transport.h"
+
+namespace py = pybind11;
+using namespace dissem;
+
+namespace {
+
+std::shared_ptr<HostBuffer> buffer_from_py(const py::object& obj) {
+  py::buffer buf = py::reinterpret_borrow<py::buffer>(obj);
+  py::buffer_info info = buf.request();
+  int64_t n = int64_t(info.size) * int64_t(info.itemsize);
+  auto hb = HostBuffer::alloc(n, false);
+  if (n) memcpy(hb->ptr, info.ptr, size_t(n));
+  return hb;
+}
+
+py::bytes host_bytes(const std::shared_ptr<HostBuffer>& b, int64_t off, int64_t n) {
+  if (!b) return py::bytes("");
+  if (n < 0) n = b->size - off;
+  return py::bytes(reinterpret_cast<const char*>(b->ptr + off), size_t(n));
+}
+
+Assignment assignment_from(const py::dict& d) {
+  Assignment a;
+  for (auto item : d) {
+    NodeID n = item.first.cast<NodeID>();
+    LayerIDs ids;
+    for (auto l : item.second) ids[l.cast<LayerID>()] = LayerMeta{};
+    a[n] = ids;
+  }
+  return a;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_core, m) {
+  m.doc() = "MI355X-native layer dissemination runtime (C++/HIP core)";
+
+  // ---- logging
+  m.def("set_log_level", &log::set_level);
+  m.def("set_log_file", &log::set_file);
+
+  // ---- enums
+  py::enum_<Location>(m, "Location")
+      .value("Inmem", Location::Inmem)
+      .value("Disk", Location::Disk)
+      .value("Client", Location::Client)
+      .value("Device", Location::Device);
+  py::enum_<SourceType>(m, "SourceType")
+      .value("Client", SourceType::Client)
+      .value("Disk", SourceType::Disk)
+      .value("Mem", SourceType::Mem)
+      .value("Device", SourceType::Device);
+  py::enum_<MsgType>(m, "MsgType")
+      .value("Announce", MsgType::Announce)
+      .value("Ack", MsgType::Ack)
+      .value("Layer", MsgType::Layer)
+      .value("Retransmit", MsgType::Retransmit)
+      .value("FlowRetransmit", MsgType::FlowRetransmit)
+      .value("ClientReq", MsgType::ClientReq)
+      .value("Startup", MsgType::Startup)
+      .value("Simple", MsgType::Simple)
+      .value("Transport", MsgType::Transport)
+      .value("Nack", MsgType::Nack)
+      .value("Bcast", MsgType::Bcast)
+      .value("Landed", MsgType::Landed);
+  m.attr("CLIENT_ID") = py::int_(kClientID);
+
+  py::class_<LayerMeta>(m, "LayerMeta")
+      .def(py::init<>())
+      .def(py::init([](Location loc, int64_t rate, SourceType st, int64_t size) {
+             return LayerMeta{loc, rate, st, size};
+           }),
+           py::arg("location") = Location::Inmem, py::arg("limit_rate") = 0,
+           py::arg("source_type") = SourceType::Client, py::arg("size") = 0)
+      .def_readwrite("location", &LayerMeta::location)
+      .def_readwrite("limit_rate", &LayerMeta::limit_rate)
+      .def_readwrite("source_type", &LayerMeta::source_type)
+      .def_readwrite("size", &LayerMeta::size)
+      .def("__eq__", [](const LayerMeta& a, const LayerMeta& b) {
+        return a.location == b.location && a.limit_rate == b.limit_rate && a.source_type == b.source_type;
+      })
+      .def("__repr__", [](const LayerMeta& x) {
+        return "LayerMeta(" + std::string(location_name(x.location)) + ", rate=" + std::to_string(x.limit_rate) +
+               ", src=" + std::to_string(int(x.source_type)) + ", size=" + std::to_string(x.size) + ")";
+      });
+
+  // ---- messages / codec
+  py::class_<Message, MessagePtr>(m, "Message")
+      .def(py::init<>())
+      .def_readwrite("type", &Message::type)
+      .def_readwrite("src", &Message::src)
+      .def_readwrite("src_str", &Message::src_str)
+      .def_readwrite("epoch", &Message::epoch)
+      .def_readwrite("layers", &Message::layers)
+      .def_readwrite("layer", &Message::layer)
+      .def_readwrite("dest", &Message::dest)
+      .def_readwrite("data_size", &Message::data_size)
+      .def_readwrite("offset", &Message::offset)
+      .def_readwrite("rate", &Message::rate)
+      .def_readwrite("total_size", &Message::total_size)
+      .def_readwrite("location", &Message::location)
+      .def_readwrite("save_disk", &Message::save_disk)
+      .def_readwrite("chunk_bytes", &Message::chunk_bytes)
+      .def_readwrite("crc", &Message::crc)
+      .def_readwrite("seq", &Message::seq)
+      .def_readwrite("peers", &Message::peers)
+      .def_readwrite("src_addr", &Message::src_addr)
+      .def_readwrite("payload_str", &Message::payload_str)
+      .def("payload_bytes", [](const Message& x) { return host_bytes(x.data, x.data_off, x.data_size); })
+      .def("__str__", &Message::str)
+      .def("__repr__", [](const Message& x) { return std::string("<Message ") + msg_type_name(x.type) + " " + x.str() + ">"; });
+  m.def("simple_msg", [](const std::string& src, const std::string& payload) {
+    auto x = std::make_shared<Message>();
+    x->type = MsgType::Simple;
+    x->src_addr = src;
+    x->payload_str = payload;
+    return x;
+  });
+  m.def("encode_envelope", [](const Message& x) { return py::bytes(encode_envelope(x)); });
+  m.def("decode_envelope", [](const std::string& s) { return decode_envelope(Json::parse(s)); });
+  m.def("json_roundtrip", [](const std::string& s) { return Json::parse(s).dump(); });
+  m.def("json_parse_prefix", [](const std::string& s) {
+    Json out;
+    size_t n = Json::parse_prefix(s.data(), s.size(), out);
+    return py::make_tuple(n, n ? out.dump() : std::string());
+  });
+
+  // ---- layers
+  py::class_<LayerSrc>(m, "LayerSrc")
+      .def(py::init<>())
+      .def_static("inmem", [](py::object data_or_size, int64_t rate, SourceType st) {
+        LayerSrc s;
+        if (py::isinstance<py::int_>(data_or_size)) {
+          int64_t n = data_or_size.cast<int64_t>();
+          s.host = HostBuffer::alloc(n < 0 ? 0 : n, true);  // cmd/config.go:159-171 (negative clamps to 0)
+        } else {
+          s.host = buffer_from_py(data_or_size);
+        }
+        s.data_size = s.host->size;
+        s.meta = LayerMeta{Location::Inmem, rate, st, s.data_size};
+        return s;
+      }, py::arg("data_or_size"), py::arg("limit_rate") = 0, py::arg("source_type") = SourceType::Mem)
+      .def_static("disk", [](const std::string& path, int64_t size, int64_t rate, SourceType st) {
+        LayerSrc s;
+        s.path = path;
+        s.data_size = size;
+        s.meta = LayerMeta{Location::Disk, rate, st, size};
+        return s;
+      }, py::arg("path"), py::arg("size"), py::arg("limit_rate") = 0, py::arg("source_type") = SourceType::Disk)
+      .def_static("client", [](int64_t size, int64_t rate) {
+        LayerSrc s;
+        s.data_size = size;
+        s.meta = LayerMeta{Location::Client, rate, SourceType::Client, size};
+        return s;
+      }, py::arg("size"), py::arg("limit_rate") = 0)
+      .def_readwrite("path", &LayerSrc::path)
+      .def_readwrite("data_size", &LayerSrc::data_size)
+      .def_readwrite("offset", &LayerSrc::offset)
+      .def_readwrite("meta", &LayerSrc::meta)
+      .def_property_readonly("has_host", [](const LayerSrc& s) { return bool(s.host); })
+      .def_property_readonly("dev_ptr", [](const LayerSrc& s) { return reinterpret_cast<uintptr_t>(s.dev); })
+      .def("host_bytes", [](const LayerSrc& s) { return host_bytes(s.host, 0, s.host ? s.host->size : 0); });
+
+  // ---- transports
+  py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")
+      .def("send", [](Transport& t, NodeID dest, const Message& msg) {
+        py::gil_scoped_release nogil;
+        t.send(dest, msg);
+      })
+      .def("broadcast", [](Transport& t, const Message& msg) {
+        py::gil_scoped_release nogil;
+        t.broadcast(msg);
+      })
+      .def("deliver", [](Transport& t, double timeout) -> py::object {
+        std::optional<MessagePtr> r;
+        {
+          py::gil_scoped_release nogil;
+          r = t.deliver().pop_for(timeout);
+        }
+        if (!r) return py::none();
+        return py::cast(*r);
+      }, py::arg("timeout") = 1.0)
+      .def("register_pipe", &Transport::register_pipe)
+      .def("address", &Transport::address)
+      .def("set_registry", &Transport::set_registry)
+      .def("add_peer", &Transport::add_peer)
+      .def("registry", &Transport::registry)
+      .def_property_readonly("bytes_sent", [](const Transport& t) { return t.bytes_sent.load(); })
+      .def_property_readonly("bytes_received", [](const Transport& t) { return t.bytes_received.load(); })
+      .def("close", [](Transport& t) {
+        py::gil_scoped_release nogil;
+        t.close();
+      });
+  m.def("inproc_transport", &make_inproc_transport, py::arg("addr"), py::arg("registry") = AddrRegistry{});
+  m.def("tcp_transport", [](const std::string& addr, const AddrRegistry& reg, bool is_client) {
+    py::gil_scoped_release nogil;
+    return make_tcp_transport(addr, reg, is_client);
+  }, py::arg("addr"), py::arg("registry") = AddrRegistry{}, py::arg("is_client") = false);
+
+  // ---- engines
+  py::class_<DataEngine, std::shared_ptr<DataEngine>>(m, "DataEngine")
+      .def_property_readonly("name", &DataEngine::name)
+      .def_property_readonly("target", &DataEngine::target)
+      .def("shutdown", [](DataEngine& e) {
+        py::gil_scoped_release nogil;
+        e.shutdown();
+      });
+  m.def("host_engine", &make_host_engine);
+
+  // ---- roles
+  py::class_<NodeConfig>(m, "NodeConfig")
+      .def(py::init<>())
+      .def_readwrite("id", &NodeConfig::id)
+      .def_readwrite("leader", &NodeConfig::leader)
+      .def_readwrite("mode", &NodeConfig::mode)
+      .def_readwrite("epoch", &NodeConfig::epoch)
+      .def_readwrite("seed", &NodeConfig::seed)
+      .def_readwrite("owner_policy", &NodeConfig::owner_policy)
+      .def_readwrite("pull_window", &NodeConfig::pull_window)
+      .def_readwrite("network_bw", &NodeConfig::network_bw)
+      .def_readwrite("link_bw", &NodeConfig::link_bw)
+      .def_readwrite("integer_seconds", &NodeConfig::integer_seconds)
+      .def_readwrite("align", &NodeConfig::align)
+      .def_readwrite("storage_path", &NodeConfig::storage_path);
+  py::class_<NodeStats>(m, "NodeStats")
+      .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
+      .def_readonly("bytes_planned", &NodeStats::bytes_planned)
+      .def_readonly("jobs_dispatched", &NodeStats::jobs_dispatched)
+      .def_readonly("layers_received", &NodeStats::layers_received)
+      .def_readonly("bytes_received", &NodeStats::bytes_received)
+      .def_readonly("flow_T", &NodeStats::flow_T)
+      .def_readonly("plan_ms", &NodeStats::plan_ms);
+  py::class_<Node, std::shared_ptr<Node>>(m, "Node")
+      .def(py::init([](const NodeConfig& cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEngine> e,
+                       const LayersSrc& layers, const py::dict& assignment, bool is_leader) {
+             return std::make_shared<Node>(cfg, t, e, layers, assignment_from(assignment), is_leader);
+           }),
+           py::arg("cfg"), py::arg("transport"), py::arg("engine"), py::arg("layers"),
+           py::arg("assignment") = py::dict(), py::arg("is_leader") = false)
+      .def("start", &Node::start)
+      .def("stop", [](Node& n) {
+        py::gil_scoped_release nogil;
+        n.stop();
+      })
+      .def("announce", [](Node& n) {
+        py::gil_scoped_release nogil;
+        n.announce();
+      })
+      .def("wait_ready", [](Node& n, double t) {
+        py::gil_scoped_release nogil;
+        return n.wait_ready(t);
+      }, py::arg("timeout") = 1.0)
+      .def("wait_start", [](Node& n, double t) {
+        py::gil_scoped_release nogil;
+        return n.wait_start(t);
+      }, py::arg("timeout") = 1.0)
+      .def("assignment", [](Node& n) {
+        std::map<NodeID, std::vector<LayerID>> out;
+        for (auto& kv : n.assignment())
+          for (auto& l : kv.second) out[kv.first].push_back(l.first);
+        return out;
+      })
+      .def("status", &Node::status)
+      .def("stats", &Node::stats)
+      .def("inventory", [](Node& n) { return n.store().inventory(); })
+      .def("layer", [](Node& n, LayerID l) -> py::object {
+        LayerSrc s;
+        if (!n.store().get(l, &s)) return py::none();
+        return py::cast(s);
+      })
+      .def("add_node", &Node::add_node)
+      .def("update_leader", &Node::update_leader)
+      .def("next_hop", &Node::next_hop)
+      .def_property_readonly("id", &Node::id);
+  py::class_<ClientNode, std::shared_ptr<ClientNode>>(m, "ClientNode")
+      .def(py::init<NodeID, std::shared_ptr<Transport>, const LayersSrc&>())
+      .def("start", &ClientNode::start)
+      .def("stop", [](ClientNode& c) {
+        py::gil_scoped_release nogil;
+        c.stop();
+      });
+
+  // ---- scheduler
+  py::class_<FlowJob>(m, "FlowJob")
+      .def_readonly("sender", &FlowJob::sender)
+      .def_readonly("layer", &FlowJob::layer)
+      .def_readonly("dest", &FlowJob::dest)
+      .def_readonly("size", &FlowJob::size)
+      .def_readonly("offset", &FlowJob::offset)
+      .def("__repr__", [](const FlowJob& j) {
+        return "FlowJob(s" + std::to_string(j.sender) + "->d" + std::to_string(j.dest) + " l" +
+               std::to_string(j.layer) + " [" + std::to_string(j.offset) + "+" + std::to_string(j.size) + "])";
+      });
+  py::class_<FlowPlan>(m, "FlowPlan")
+      .def_readonly("T", &FlowPlan::T)
+      .def_readonly("required", &FlowPlan::required)
+      .def_readonly("max_flow", &FlowPlan::max_flow)
+      .def_readonly("solves", &FlowPlan::solves)
+      .def_readonly("feasible", &FlowPlan::feasible)
+      .def_readonly("jobs", &FlowPlan::jobs);
+  m.def("solve_flow", [](const std::map<NodeID, LayerIDs>& holdings,
+                         const std::vector<std::tuple<LayerID, NodeID, int64_t>>& demands,
+                         const std::map<NodeID, int64_t>& egress, const std::map<NodeID, int64_t>& ingress,
+                         const std::map<std::pair<NodeID, NodeID>, int64_t>& links, int64_t align,
+                         bool integer_seconds, bool allow_self) {
+    FlowProblem p;
+    p.holdings = holdings;
+    for (auto& d : demands) p.demands.push_back({std::get<0>(d), std::get<1>(d), std::get<2>(d)});
+    p.egress_bps = egress;
+    p.ingress_bps = ingress;
+    p.link_bps = links;
+    p.align = align;
+    p.integer_seconds = integer_seconds;
+    p.allow_self = allow_self;
+    py::gil_scoped_release nogil;
+    return solve_flow(p);
+  }, py::arg("holdings"), py::arg("demands"), py::arg("egress") = std::map<NodeID, int64_t>{},
+     py::arg("ingress") = std::map<NodeID, int64_t>{},
+     py::arg("links") = std::map<std::pair<NodeID, NodeID>, int64_t>{}, py::arg("align") = 1,
+     py::arg("integer_seconds") = false, py::arg("allow_self") = false);
+
+  py::class_<RangeSet>(m, "RangeSet")
+      .def(py::init<>())
+      .def("add", &RangeSet::add)
+      .def("covered", &RangeSet::covered)
+      .def("contains", &RangeSet::contains)
+      .def("ranges", &RangeSet::ranges);
+
+  // ---- GPU runtime (HIP kernels, device store, RCCL engine): csrc/gpu/
+  register_gpu_bindings(m.ptr());
+}

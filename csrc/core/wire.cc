@@ -1,0 +1,293 @@
+#include "core/wire.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+
+namespace dissem {
+
+const char* location_name(Location l) {
+  switch (l) {
+    case Location::Inmem: return "inmem";
+    case Location::Disk: return "disk";
+    case Location::Client: return "client";
+    case Location::Device: return "device";
+  }
+  return "?";
+}
+
+std::shared_ptr<HostBuffer> HostBuffer::alloc(int64_t size, bool zero) {
+  auto b = std::make_shared<HostBuffer>();
+  b->size = size;
+  size_t n = size_t(size > 0 ? size : 1);
+  void* p = zero ? calloc(1, n) : malloc(n);
+  if (!p) throw std::bad_alloc();
+  b->ptr = static_cast<uint8_t*>(p);
+  b->owner = std::shared_ptr<void>(p, free);
+  return b;
+}
+
+std::shared_ptr<HostBuffer> HostBuffer::wrap(uint8_t* p, int64_t size, std::shared_ptr<void> owner) {
+  auto b = std::make_shared<HostBuffer>();
+  b->ptr = p;
+  b->size = size;
+  b->owner = std::move(owner);
+  return b;
+}
+
+const char* msg_type_name(MsgType t) {
+  switch (t) {
+    case MsgType::Announce: return "announce";
+    case MsgType::Ack: return "ack";
+    case MsgType::Layer: return "layer";
+    case MsgType::Retransmit: return "retransmit";
+    case MsgType::FlowRetransmit: return "flow_retransmit";
+    case MsgType::ClientReq: return "client_req";
+    case MsgType::Startup: return "startup";
+    case MsgType::Simple: return "simple";
+    case MsgType::Transport: return "transport";
+    case MsgType::Nack: return "nack";
+    case MsgType::Bcast: return "bcast";
+    case MsgType::Landed: return "landed";
+    case MsgType::SendDone: return "send_done";
+    case MsgType::Tick: return "tick";
+    case MsgType::Stop: return "stop";
+  }
+  return "?";
+}
+
+std::string node_str(NodeID id) { return std::to_string(id); }
+
+NodeID parse_node_id(const std::string& s) {
+  char* end = nullptr;
+  unsigned long long v = strtoull(s.c_str(), &end, 10);
+  if (s.empty() || (end && *end)) throw std::runtime_error("bad node id: " + s);
+  return NodeID(v);
+}
+
+std::string Message::str() const {
+  std::ostringstream o;
+  switch (type) {
+    case MsgType::Announce: {
+      o << src << ": [";
+      bool first = true;
+      for (auto& kv : layers) {
+        o << (first ? "" : " ") << kv.first;
+        first = false;
+      }
+      o << "]";
+      break;
+    }
+    case MsgType::Ack: o << src << ": " << layer; break;
+    case MsgType::Retransmit: o << "from " << src << ": layer " << layer << ", to " << dest << ", "; break;
+    case MsgType::FlowRetransmit:
+      o << "from " << src << ": layer " << layer << ", to " << dest << ", size: " << data_size
+        << ", offset: " << offset << ", rate: " << rate;
+      break;
+    case MsgType::Layer:
+      o << "from " << src << ": layer " << layer << ", location: " << int(location) << ", rate: " << rate;
+      break;
+    case MsgType::ClientReq: o << "from " << src << ": layer " << layer; break;
+    case MsgType::Startup: o << "from " << src << ": startup"; break;
+    case MsgType::Simple: o << src_addr << ": " << payload_str; break;
+    default: o << msg_type_name(type) << " from " << src << " layer " << layer; break;
+  }
+  return o.str();
+}
+
+static Json layer_ids_json(const LayerIDs& ids) {
+  Json obj = Json::object();
+  for (auto& kv : ids) {
+    Json m = Json::object();
+    m["Location"] = Json(unsigned(kv.second.location));
+    m["LimitRate"] = Json(kv.second.limit_rate);
+    m["SourceType"] = Json(unsigned(kv.second.source_type));
+    if (kv.second.size) m["DataSize"] = Json(kv.second.size);
+    obj[std::to_string(kv.first)] = m;
+  }
+  return obj;
+}
+
+static LayerIDs layer_ids_from(const Json* j) {
+  LayerIDs out;
+  if (!j || !j->is_object()) return out;
+  for (auto& kv : j->as_object()) {
+    LayerMeta meta;
+    if (kv.second.is_object()) {
+      meta.location = Location(kv.second.get_u64("Location", 0));
+      meta.limit_rate = kv.second.get_i64("LimitRate", 0);
+      meta.source_type = SourceType(kv.second.get_u64("SourceType", 0));
+      meta.size = kv.second.get_i64("DataSize", 0);
+    }
+    out[LayerID(strtoull(kv.first.c_str(), nullptr, 10))] = meta;
+  }
+  return out;
+}
+
+Json encode_layer_header(const Message& m) {
+  Json h = Json::object();
+  h["SrcID"] = Json(uint64_t(m.src));
+  h["LayerID"] = Json(uint64_t(m.layer));
+  h["LayerSize"] = Json(m.data_size);
+  h["TotalSize"] = Json(m.total_size);
+  h["Offert"] = Json(m.offset);  // sic: reference field name (transport.go:52)
+  if (m.epoch) h["Epoch"] = Json(uint64_t(m.epoch));
+  if (m.chunk_bytes) h["ChunkBytes"] = Json(m.chunk_bytes);
+  if (m.seq) h["Seq"] = Json(uint64_t(m.seq));
+  if (m.rate) h["Rate"] = Json(m.rate);
+  if (!m.crc.empty()) {
+    Json arr = Json::array();
+    for (uint32_t c : m.crc) arr.push_back(Json(unsigned(c)));
+    h["Crc"] = arr;
+  }
+  return h;
+}
+
+Json encode_payload(const Message& m) {
+  Json p = Json::object();
+  auto src_id = [&] { p["SrcID"] = Json(uint64_t(m.src)); };
+  switch (m.type) {
+    case MsgType::Announce:
+      src_id();
+      p["LayerIDs"] = layer_ids_json(m.layers);
+      break;
+    case MsgType::Ack:
+      src_id();
+      p["LayerID"] = Json(uint64_t(m.layer));
+      p["Location"] = Json(unsigned(m.location));  // extension (unexported in reference)
+      break;
+    case MsgType::Retransmit:
+      src_id();
+      p["LayerID"] = Json(uint64_t(m.layer));
+      p["DestID"] = Json(uint64_t(m.dest));
+      break;
+    case MsgType::FlowRetransmit:
+      src_id();
+      p["LayerID"] = Json(uint64_t(m.layer));
+      p["DestID"] = Json(uint64_t(m.dest));
+      p["DataSize"] = Json(m.data_size);
+      p["Offset"] = Json(m.offset);
+      p["Rate"] = Json(m.rate);
+      break;
+    case MsgType::ClientReq:
+      src_id();
+      p["LayerID"] = Json(uint64_t(m.layer));
+      p["SaveDisk"] = Json(m.save_disk);
+      break;
+    case MsgType::Startup:
+      src_id();
+      break;
+    case MsgType::Simple:
+      p["SrcAddr"] = Json(m.src_addr);
+      p["PayloadStr"] = Json(m.payload_str);
+      break;
+    case MsgType::Layer:
+      return encode_layer_header(m);
+    case MsgType::Nack:
+      src_id();
+      p["LayerID"] = Json(uint64_t(m.layer));
+      p["DestID"] = Json(uint64_t(m.dest));
+      p["DataSize"] = Json(m.data_size);
+      p["Offset"] = Json(m.offset);
+      break;
+    case MsgType::Bcast: {
+      src_id();
+      p["LayerID"] = Json(uint64_t(m.layer));
+      p["TotalSize"] = Json(m.total_size);
+      p["Seq"] = Json(uint64_t(m.seq));
+      p["ChunkBytes"] = Json(m.chunk_bytes);
+      Json arr = Json::array();
+      for (auto n : m.peers) arr.push_back(Json(uint64_t(n)));
+      p["Peers"] = arr;
+      if (!m.crc.empty()) {
+        Json c = Json::array();
+        for (uint32_t x : m.crc) c.push_back(Json(unsigned(x)));
+        p["Crc"] = c;
+      }
+      break;
+    }
+    default:
+      throw std::runtime_error(std::string("cannot serialize internal message ") + msg_type_name(m.type));
+  }
+  if (m.epoch) p["Epoch"] = Json(uint64_t(m.epoch));
+  return p;
+}
+
+std::string encode_envelope(const Message& m) {
+  Json env = Json::object();
+  env["type"] = Json(unsigned(m.type));
+  env["src"] = Json(m.type == MsgType::Simple ? m.src_addr : node_str(m.src));
+  env["payload"] = encode_payload(m);
+  return env.dump();
+}
+
+MessagePtr decode_envelope(const Json& env) {
+  auto m = std::make_shared<Message>();
+  if (!env.is_object()) throw std::runtime_error("envelope is not an object");
+  m->type = MsgType(env.get_u64("type", 255));
+  m->src_str = env.get_str("src");
+  const Json* pp = env.find("payload");
+  static const Json kEmpty = Json::object();
+  const Json& p = (pp && pp->is_object()) ? *pp : kEmpty;
+  m->src = p.get_u64("SrcID", 0);
+  m->epoch = p.get_u64("Epoch", 0);
+  switch (m->type) {
+    case MsgType::Announce:
+      m->layers = layer_ids_from(p.find("LayerIDs"));
+      break;
+    case MsgType::Ack:
+      m->layer = p.get_u64("LayerID");
+      m->location = Location(p.get_u64("Location", 0));
+      break;
+    case MsgType::Retransmit:
+      m->layer = p.get_u64("LayerID");
+      m->dest = p.get_u64("DestID");
+      break;
+    case MsgType::FlowRetransmit:
+    case MsgType::Nack:
+      m->layer = p.get_u64("LayerID");
+      m->dest = p.get_u64("DestID");
+      m->data_size = p.get_i64("DataSize");
+      m->offset = p.get_i64("Offset");
+      m->rate = p.get_i64("Rate");
+      break;
+    case MsgType::ClientReq:
+      m->layer = p.get_u64("LayerID");
+      m->save_disk = p.get_bool("SaveDisk");
+      break;
+    case MsgType::Startup:
+      break;
+    case MsgType::Simple:
+      m->src_addr = p.get_str("SrcAddr");
+      m->payload_str = p.get_str("PayloadStr");
+      break;
+    case MsgType::Layer: {
+      m->layer = p.get_u64("LayerID");
+      m->data_size = p.get_i64("LayerSize");
+      m->total_size = p.get_i64("TotalSize");
+      m->offset = p.get_i64("Offert", p.get_i64("Offset", 0));
+      m->chunk_bytes = p.get_i64("ChunkBytes", 0);
+      m->seq = p.get_u64("Seq", 0);
+      m->rate = p.get_i64("Rate", 0);
+      if (auto* c = p.find("Crc"); c && c->is_array())
+        for (auto& x : c->as_array()) m->crc.push_back(uint32_t(x.as_u64()));
+      break;
+    }
+    case MsgType::Bcast: {
+      m->layer = p.get_u64("LayerID");
+      m->total_size = p.get_i64("TotalSize");
+      m->seq = p.get_u64("Seq");
+      m->chunk_bytes = p.get_i64("ChunkBytes");
+      if (auto* a = p.find("Peers"); a && a->is_array())
+        for (auto& x : a->as_array()) m->peers.push_back(x.as_u64());
+      if (auto* c = p.find("Crc"); c && c->is_array())
+        for (auto& x : c->as_array()) m->crc.push_back(uint32_t(x.as_u64()));
+      break;
+    }
+    default:
+      throw std::runtime_error("unknown MsgType: " + std::to_string(unsigned(m->type)));
+  }
+  return m;
+}
+
+}  // namespace dissem

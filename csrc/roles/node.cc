@@ -1,0 +1,827 @@
+#include "roles/node.h"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+
+#include "core/log.h"
+#include "sched/maxflow.h"
+
+namespace dissem {
+
+namespace {
+bool at(const LayerIDs& ids, LayerID l, Location loc) {
+  auto it = ids.find(l);
+  return it != ids.end() && it->second.location == loc;
+}
+}  // namespace
+
+Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEngine> e, const LayersSrc& layers,
+           const Assignment& assignment, bool is_leader)
+    : cfg_(std::move(cfg)),
+      t_(std::move(t)),
+      e_(std::move(e)),
+      store_(layers, e_->target()),
+      assignment_(assignment),
+      is_leader_(is_leader),
+      rng_(cfg_.seed) {
+  if (cfg_.id != cfg_.leader) add_node(cfg_.leader);  // node.go:58-60
+  if (is_leader_) status_[cfg_.id] = store_.inventory();  // node.go:252-257
+  e_->bind(this);
+  if (e_->target() == Location::Inmem) {
+    // TCP payload bytes land directly in this node's store slot.
+    t_->set_landing([this](const Message& h) -> uint8_t* {
+      if (h.epoch && cfg_.epoch && h.epoch != cfg_.epoch) return nullptr;
+      try {
+        int64_t total = h.total_size ? h.total_size : h.data_size;
+        if (h.offset < 0 || h.offset + h.data_size > total) return nullptr;
+        return store_.host_landing(h.layer, total) + h.offset;
+      } catch (...) {
+        return nullptr;
+      }
+    });
+  }
+}
+
+Node::~Node() { stop(); }
+
+void Node::start() {
+  if (running_.exchange(true)) return;
+  loop_th_ = std::thread([this] { loop(); });
+}
+
+void Node::stop() {
+  if (!running_.exchange(false)) return;
+  e_->quiesce();
+  auto m = std::make_shared<Message>();
+  m->type = MsgType::Stop;
+  t_->inject(m);
+  if (loop_th_.joinable()) loop_th_.join();
+}
+
+void Node::add_routing(NodeID goal, NodeID next_hop, unsigned hops) {
+  std::lock_guard<std::mutex> lk(rt_mu_);
+  routing_[goal] = {next_hop, hops};
+}
+
+NodeID Node::next_hop(NodeID goal) {
+  std::lock_guard<std::mutex> lk(rt_mu_);
+  auto it = routing_.find(goal);
+  if (it == routing_.end()) throw std::runtime_error("routing entry for the specified the goal does not exist");
+  return it->second.first;
+}
+
+void Node::update_leader(NodeID leader) {
+  std::lock_guard<std::mutex> lk(rt_mu_);
+  if (!routing_.count(leader)) throw std::runtime_error("routing entry for the specified leader does not exist");
+  cfg_.leader = leader;
+}
+
+bool Node::send_msg(NodeID dest, Message m) {
+  m.src = cfg_.id;
+  m.epoch = cfg_.epoch;
+  try {
+    t_->send(dest, m);
+    return true;
+  } catch (const std::exception& e) {
+    log::error(int64_t(cfg_.id)).s("error", e.what()).msg(std::string("failed to send ") + msg_type_name(m.type) +
+                                                          " to " + std::to_string(dest));
+    return false;
+  }
+}
+
+void Node::announce() {
+  if (is_leader_ && cfg_.id == cfg_.leader) return;  // the leader's status is seeded at construction
+  Message m;
+  m.type = MsgType::Announce;
+  m.layers = store_.inventory();
+  NodeID hop = next_hop(cfg_.leader);
+  if (!send_msg(hop, m)) throw std::runtime_error("announce failed");
+}
+
+bool Node::wait_ready(double timeout_s) {
+  std::unique_lock<std::mutex> lk(sig_mu_);
+  return sig_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] {
+    return is_leader_ ? satisfied_ : ready_;
+  });
+}
+
+bool Node::wait_start(double timeout_s) {
+  std::unique_lock<std::mutex> lk(sig_mu_);
+  return sig_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return started_; });
+}
+
+Status Node::status() {
+  // Snapshot through the event loop would be cleaner; status_ is only written on the
+  // loop thread and this accessor is for tests after completion.
+  std::lock_guard<std::mutex> lk(sig_mu_);
+  return status_;
+}
+
+NodeStats Node::stats() {
+  std::lock_guard<std::mutex> lk(sig_mu_);
+  return stats_;
+}
+
+void Node::loop() {
+  for (;;) {
+    auto m = t_->deliver().pop();
+    if (!m) break;
+    if ((*m)->type == MsgType::Stop) break;
+    try {
+      handle(*m);
+    } catch (const std::exception& e) {
+      log::error(int64_t(cfg_.id)).s("error", e.what()).msg(std::string("handler failed for ") +
+                                                          msg_type_name((*m)->type));
+    }
+  }
+}
+
+void Node::handle(const MessagePtr& m) {
+  if (m->epoch && cfg_.epoch && m->epoch != cfg_.epoch) {
+    log::debug(int64_t(cfg_.id)).u("epoch", m->epoch).msg("dropping message from another session");
+    return;
+  }
+  if (log::level() <= log::Debug)
+    log::debug(int64_t(cfg_.id)).msg(std::string("incoming msg[") + msg_type_name(m->type) + "]: " + m->str());
+  if (e_->on_message(m)) return;
+  switch (m->type) {
+    case MsgType::Announce:
+      if (is_leader_) on_announce(m);
+      break;
+    case MsgType::Ack:
+      if (is_leader_) on_ack(m);
+      break;
+    case MsgType::Layer:
+      on_layer(m);
+      break;
+    case MsgType::Landed:
+      on_landed(m->layer, m->offset, m->data_size, m->total_size, m->src, m->dur_ms);
+      break;
+    case MsgType::Retransmit:
+      on_retransmit(m);
+      break;
+    case MsgType::FlowRetransmit:
+      on_flow_retransmit(m);
+      break;
+    case MsgType::Startup:
+      on_startup(m);
+      break;
+    case MsgType::Simple:
+      log::info(int64_t(cfg_.id)).s("from", m->src_addr).msg(m->payload_str);
+      break;
+    default:
+      break;
+  }
+}
+
+// ------------------------------------------------------------ receiver side
+
+void Node::on_layer(const MessagePtr& m) {
+  // A payload that arrived over the transport (node.go:1354-1384 / 1520-1567).
+  int64_t total = m->total_size ? m->total_size : m->data_size;
+  if (!m->in_place && m->data) {
+    if (e_->target() == Location::Inmem) {
+      uint8_t* dst = store_.host_landing(m->layer, total);
+      if (m->offset < 0 || m->offset + m->data_size > total) throw std::runtime_error("layer range out of bounds");
+      memcpy(dst + m->offset, m->data->ptr + m->data_off, size_t(m->data_size));
+    } else {
+      // Device target: keep the host copy (e.g. from the external client), then
+      // stage it into HBM; the engine reports Landed when it is resident.
+      uint8_t* dst = store_.host_landing(m->layer, total);
+      memcpy(dst + m->offset, m->data->ptr + m->data_off, size_t(m->data_size));
+      LayerSrc src;
+      if (store_.get(m->layer, &src)) {
+        src.meta.location = Location::Inmem;
+        store_.put(m->layer, src);
+      }
+      e_->load_range(m->layer, m->offset, m->data_size, total, 0);
+      return;
+    }
+  }
+  on_landed(m->layer, m->offset, m->data_size, total, m->src, m->dur_ms);
+}
+
+void Node::on_landed(LayerID layer, int64_t off, int64_t size, int64_t total, NodeID from, double dur_ms) {
+  bool complete = store_.mark_landed(layer, off, size, total);
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.bytes_received += size;
+  }
+  if (size < total && !complete) {
+    log::info(int64_t(cfg_.id)).msg("l" + std::to_string(layer) + " downloaded (" +
+                                    std::to_string(store_.landed_bytes(layer)) + " B / " + std::to_string(total) +
+                                    " B)");
+  }
+  if (complete) {
+    log::info(int64_t(cfg_.id)).u("layer", layer).i("total_bytes", total).u("from", from).f("duration[ms]", dur_ms)
+        .msg("layer fully received");
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.layers_received++;
+    }
+    send_ack(layer);
+  }
+}
+
+void Node::send_ack(LayerID layer) {
+  Message a;
+  a.type = MsgType::Ack;
+  a.layer = layer;
+  a.location = e_->target();
+  send_msg(cfg_.leader, a);
+}
+
+void Node::on_retransmit(const MessagePtr& m) {
+  // node.go:1462-1484: add the dest as a neighbor, then push our copy.
+  add_node(m->dest);
+  LayerSrc src;
+  if (!store_.get(m->layer, &src)) {
+    log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(m->layer));
+    return;
+  }
+  send_layer(m->dest, m->layer, 0, src.data_size, src.meta.limit_rate);
+}
+
+void Node::on_flow_retransmit(const MessagePtr& m) {
+  // node.go:1592-1643 (sender side of mode 3, also self-loads when dest == me).
+  add_node(m->dest);
+  log::info(int64_t(cfg_.id)).u("layer", m->layer).u("dest", m->dest).i("size", m->data_size).i("rate", m->rate)
+      .msg("start sending layer");
+  send_layer(m->dest, m->layer, m->offset, m->data_size, m->rate);
+}
+
+void Node::on_startup(const MessagePtr&) {
+  // node.go:1387-1389: tell the application the layers are ready.
+  std::lock_guard<std::mutex> lk(sig_mu_);
+  ready_ = true;
+  sig_cv_.notify_all();
+}
+
+// -------------------------------------------------------------- sender side
+
+void Node::send_layer(NodeID dest, LayerID layer, int64_t offset, int64_t size, int64_t rate) {
+  LayerSrc src;
+  if (!store_.get(layer, &src)) {
+    log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(layer));
+    return;
+  }
+  int64_t total = src.data_size;
+  if (size < 0 || offset + size > total) size = total - offset;
+  if (dest == cfg_.id) {
+    // Local promotion into the target tier (the reference sends to itself over
+    // TCP loopback, node.go:1239-1247 / mode-2 own jobs).
+    if (store_.has_target(layer)) {
+      send_ack(layer);  // already resident: acks are idempotent at the leader
+      return;
+    }
+    if (src.meta.location == Location::Client) {
+      fetch_from_client(layer, cfg_.id);
+      return;
+    }
+    e_->load_range(layer, offset, size, total, rate);
+    return;
+  }
+  if (src.meta.location == Location::Client && !store_.has_target(layer)) {
+    fetch_from_client(layer, dest);  // node.go:357-361 / 1470-1474
+    return;
+  }
+  e_->send_range(dest, layer, offset, size, total, rate);
+}
+
+void Node::fetch_from_client(LayerID layer, NodeID dest) {
+  log::debug(int64_t(cfg_.id)).u("layerID", layer).msg("ask the client to send the layer");
+  if (dest != cfg_.id) {
+    try {
+      t_->register_pipe(layer, dest);
+    } catch (const std::exception& e) {
+      log::error(int64_t(cfg_.id)).s("error", e.what()).msg("register pipe");
+    }
+  }
+  Message r;
+  r.type = MsgType::ClientReq;
+  r.layer = layer;
+  r.save_disk = false;
+  send_msg(kClientID, r);
+}
+
+// -------------------------------------------------------------- leader side
+
+int64_t Node::layer_size(LayerID l) {
+  int64_t sz = 0;
+  for (auto& kv : status_) {
+    auto it = kv.second.find(l);
+    if (it != kv.second.end()) sz = std::max(sz, it->second.size);
+  }
+  if (!sz) {
+    LayerSrc src;
+    if (store_.get(l, &src)) sz = src.data_size;
+  }
+  return sz;
+}
+
+void Node::on_announce(const MessagePtr& m) {
+  // node.go:295-324
+  if (!status_.count(m->src)) {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    status_[m->src] = m->layers;
+    add_node(m->src);
+  }
+  if (started_) return;
+  for (auto& kv : assignment_)
+    if (!status_.count(kv.first)) return;
+  start_distribution();
+}
+
+void Node::start_distribution() {
+  int64_t planned = 0;
+  for (auto& kv : assignment_)
+    for (auto& l : kv.second)
+      if (!at(status_[kv.first], l.first, e_->target())) planned += layer_size(l.first);
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    started_ = true;
+    t_start_us_ = log::now_us();
+    stats_.bytes_planned = planned;
+    sig_cv_.notify_all();
+  }
+  log::info(int64_t(cfg_.id)).i("mode", cfg_.mode).i("bytes_planned", planned).msg("timer start");
+  int64_t t0 = log::now_us();
+  switch (cfg_.mode) {
+    case 0: schedule_mode0(); break;
+    case 1: schedule_mode1(); break;
+    case 2: schedule_mode2(); break;
+    case 3: schedule_mode3(); break;
+    default: log::error(int64_t(cfg_.id)).msg("unknown mode");
+  }
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.plan_ms = double(log::now_us() - t0) / 1e3;
+  }
+  if (!satisfied_ && assignment_satisfied()) {
+    // Nothing had to move (the reference would wait forever for acks).
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    satisfied_ = true;
+    t_ready_us_ = log::now_us();
+    stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
+    sig_cv_.notify_all();
+  }
+}
+
+bool Node::assignment_satisfied() {
+  // node.go:435-446: every assigned layer must be resident in the target tier.
+  for (auto& kv : assignment_) {
+    auto st = status_.find(kv.first);
+    if (st == status_.end()) return false;
+    for (auto& l : kv.second)
+      if (!at(st->second, l.first, e_->target())) return false;
+  }
+  return true;
+}
+
+void Node::send_startup() {
+  // node.go:456-469 (continues past per-peer errors instead of returning early).
+  for (auto& kv : status_) {
+    Message s;
+    s.type = MsgType::Startup;
+    send_msg(kv.first, s);
+  }
+}
+
+void Node::on_ack(const MessagePtr& m) {
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    LayerMeta meta;
+    meta.location = m->location;
+    meta.size = layer_size(m->layer);
+    status_[m->src][m->layer] = meta;  // node.go:413-417
+  }
+  if (!satisfied_ && assignment_satisfied()) {
+    // Fire exactly once (quirk Q13).
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      satisfied_ = true;
+      t_ready_us_ = log::now_us();
+      stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
+    }
+    log::info(int64_t(cfg_.id)).f("time_to_deliver_s", stats_.time_to_deliver_s).msg("timer stop: startup");
+    send_startup();
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    sig_cv_.notify_all();
+  }
+  if (cfg_.mode != 2) return;
+  // Mode 2 pull loop (node.go:764-807): retire the job, pull the next one.
+  auto lj = jobs_.find(m->layer);
+  if (lj == jobs_.end()) return;
+  auto jt = lj->second.find(m->src);
+  if (jt == lj->second.end()) return;
+  Job job = jt->second;
+  lj->second.erase(jt);
+  if (job.state == JobState::Sending) {
+    double dur = double(log::now_us() - job.t_us);
+    auto& pf = perf_[job.sender];
+    pf.first = pf.second == 0 ? dur : 0.5 * pf.first + 0.5 * dur;  // EWMA (quirk Q9)
+    pf.second++;
+    inflight_[job.sender] = std::max(0, inflight_[job.sender] - 1);
+    log::info(int64_t(cfg_.id)).u("node", job.sender).u("layerID", m->layer).f("duration[ms]", dur / 1e3)
+        .msg("job completed");
+  } else {
+    load_[job.sender] = std::max<int64_t>(0, load_[job.sender] - 1);
+  }
+  while (inflight_[job.sender] < cfg_.pull_window && assign_new_job(job.sender)) {
+  }
+  // The destination now owns a copy it can serve (status grew above): let it pull too.
+  if (m->src != job.sender)
+    while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
+    }
+}
+
+void Node::retransmit(LayerID layer, NodeID owner, NodeID dest) {
+  // node.go:611-626; the leader's own sends are asynchronous (quirk Q4).
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.jobs_dispatched++;
+  }
+  if (owner == cfg_.id) {
+    LayerSrc src;
+    int64_t rate = store_.get(layer, &src) ? src.meta.limit_rate : 0;
+    send_layer(dest, layer, 0, -1, rate);
+    return;
+  }
+  Message r;
+  r.type = MsgType::Retransmit;
+  r.layer = layer;
+  r.dest = dest;
+  send_msg(owner, r);
+}
+
+void Node::schedule_mode0() {
+  // node.go:326-352: the leader pushes every missing (dest, layer) itself.
+  std::map<LayerID, std::vector<NodeID>> need;
+  for (auto& kv : assignment_)
+    for (auto& l : kv.second)
+      if (!at(status_[kv.first], l.first, e_->target())) need[l.first].push_back(kv.first);
+  for (auto& kv : need) {
+    LayerSrc src;
+    if (!store_.get(kv.first, &src)) {
+      log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(kv.first));
+      continue;
+    }
+    std::vector<NodeID> remote;
+    for (NodeID d : kv.second) {
+      if (d == cfg_.id) {
+        send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
+      } else {
+        remote.push_back(d);
+      }
+    }
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.jobs_dispatched += int64_t(kv.second.size());
+    }
+    if (remote.size() >= 2 && e_->supports_broadcast() && src.meta.location != Location::Client) {
+      e_->broadcast_layer(kv.first, src.data_size, remote);
+    } else {
+      for (NodeID d : remote) send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
+    }
+  }
+}
+
+void Node::schedule_mode1() {
+  // node.go:554-608: a random current owner retransmits each missing layer.
+  for (auto& kv : status_)
+    for (auto& l : kv.second) owners_[l.first].insert(kv.first);  // initialized on demand (quirk Q3)
+  for (auto& kv : assignment_) {
+    NodeID dest = kv.first;
+    for (auto& l : kv.second) {
+      LayerID layer = l.first;
+      if (at(status_[dest], layer, e_->target())) continue;
+      auto oit = owners_.find(layer);
+      if (oit != owners_.end() && !oit->second.empty()) {
+        if (oit->second.count(dest)) {
+          // The dest holds it in a lower tier (disk/host/client): promote locally.
+          retransmit(layer, dest, dest);
+          continue;
+        }
+        std::vector<NodeID> cand(oit->second.begin(), oit->second.end());
+        NodeID owner;
+        if (cfg_.owner_policy == "balanced") {
+          int64_t best = INT64_MAX;
+          std::vector<NodeID> ties;
+          for (NodeID c : cand) {
+            int64_t b = owner_bytes_[c];
+            if (b < best) {
+              best = b;
+              ties.assign(1, c);
+            } else if (b == best) {
+              ties.push_back(c);
+            }
+          }
+          owner = ties[size_t(rng_() % ties.size())];
+        } else {
+          owner = cand[size_t(rng_() % cand.size())];  // uniform (quirk Q5)
+        }
+        owner_bytes_[owner] += layer_size(layer);
+        retransmit(layer, owner, dest);
+      } else {
+        LayerSrc src;
+        if (!store_.get(layer, &src)) {
+          log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(layer));
+          continue;
+        }
+        retransmit(layer, cfg_.id, dest);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------- mode 2
+
+NodeID Node::min_loaded_sender(LayerID layer) {
+  // node.go:948-978 (the code picks the FASTEST source; quirk Q16 keeps that).
+  NodeID best = 0;
+  bool found = false;
+  int64_t best_rate = 0;
+  int64_t min_count = INT64_MAX;
+  for (auto& kv : load_) {
+    NodeID sender = kv.first;
+    auto st = status_.find(sender);
+    if (st == status_.end()) continue;
+    auto it = st->second.find(layer);
+    if (it == st->second.end()) continue;
+    int64_t eff = it->second.limit_rate == 0 ? INT64_MAX : it->second.limit_rate;
+    int64_t count = kv.second;
+    if (!found || eff > best_rate || (eff == best_rate && (count < min_count || (count == min_count && sender < best)))) {
+      best = sender;
+      best_rate = eff;
+      min_count = count;
+      found = true;
+    }
+  }
+  return found ? best : kClientID;
+}
+
+bool Node::rarest_own_job(NodeID node, LayerID* layer, NodeID* dest) {
+  // node.go:981-1010
+  bool ok = false;
+  size_t min_owners = SIZE_MAX;
+  auto st = status_.find(node);
+  if (st == status_.end()) return false;
+  for (auto& l : st->second) {
+    auto lj = jobs_.find(l.first);
+    if (lj == jobs_.end()) continue;
+    for (auto& jd : lj->second) {
+      if (jd.second.sender != node || jd.second.state != JobState::Pending) continue;
+      size_t cnt = owners_[l.first].size();
+      if (!ok || cnt < min_owners || (cnt == min_owners && l.first < *layer)) {
+        min_owners = cnt;
+        *layer = l.first;
+        *dest = jd.first;
+        ok = true;
+      }
+    }
+  }
+  return ok;
+}
+
+bool Node::rarest_stealable_job(NodeID node, LayerID* layer, NodeID* dest, NodeID* victim) {
+  // node.go:1012-1073
+  struct Cand {
+    LayerID layer;
+    NodeID dest, sender;
+    size_t owners;
+    double ttf;
+  };
+  bool have = false;
+  Cand best{};
+  auto st = status_.find(node);
+  if (st == status_.end()) return false;
+  for (auto& l : st->second) {
+    auto lj = jobs_.find(l.first);
+    if (lj == jobs_.end()) continue;
+    size_t cnt = owners_[l.first].size();
+    for (auto& jd : lj->second) {
+      NodeID sender = jd.second.sender;
+      int64_t sender_rate = 0;
+      if (auto s2 = status_.find(sender); s2 != status_.end())
+        if (auto x = s2->second.find(l.first); x != s2->second.end()) sender_rate = x->second.limit_rate;
+      int64_t node_rate = l.second.limit_rate;
+      if (sender == node || jd.second.state != JobState::Pending || load_[sender] == 0 ||
+          (node_rate != 0 && node_rate < sender_rate))
+        continue;
+      double ttf = perf_.count(sender) ? perf_[sender].first * double(load_[sender]) : 1e300;
+      Cand c{l.first, jd.first, sender, cnt, ttf};
+      if (!have || c.owners < best.owners || (c.owners == best.owners && c.ttf > best.ttf)) {
+        best = c;
+        have = true;
+      }
+    }
+  }
+  if (!have) return false;
+  *layer = best.layer;
+  *dest = best.dest;
+  *victim = best.sender;
+  return true;
+}
+
+bool Node::assign_new_job(NodeID node) {
+  // node.go:909-945
+  LayerID layer = 0;
+  NodeID dest = 0, victim = 0;
+  if (rarest_own_job(node, &layer, &dest)) {
+    Job& j = jobs_[layer][dest];
+    j.state = JobState::Sending;
+    j.t_us = log::now_us();
+    load_[node] = std::max<int64_t>(0, load_[node] - 1);
+    inflight_[node]++;
+    log::debug(int64_t(cfg_.id)).u("node", node).u("layer", layer).msg("pass a job initially assigned");
+    retransmit(layer, node, dest);
+    return true;
+  }
+  if (rarest_stealable_job(node, &layer, &dest, &victim)) {
+    log::debug(int64_t(cfg_.id)).u("layer", layer)
+        .msg("steal a job from the most loaded node (" + std::to_string(victim) + ") to node " + std::to_string(node));
+    load_[victim] = std::max<int64_t>(0, load_[victim] - 1);
+    Job& j = jobs_[layer][dest];
+    j.sender = node;
+    j.state = JobState::Sending;
+    j.t_us = log::now_us();
+    inflight_[node]++;
+    retransmit(layer, node, dest);
+    return true;
+  }
+  log::debug(int64_t(cfg_.id)).u("node", node).msg("there is no job left to assign");
+  return false;
+}
+
+void Node::schedule_mode2() {
+  // node.go:810-904
+  for (auto& kv : status_)
+    for (auto& l : kv.second) owners_[l.first].insert(kv.first);
+  std::vector<LayerID> sorted;
+  for (auto& kv : owners_) sorted.push_back(kv.first);
+  std::stable_sort(sorted.begin(), sorted.end(), [&](LayerID a, LayerID b) {
+    if (owners_[a].size() != owners_[b].size()) return owners_[a].size() < owners_[b].size();
+    return a < b;  // rarest first, tiebreak by id
+  });
+  for (auto& kv : assignment_)
+    for (auto& l : kv.second)
+      if (!at(status_[kv.first], l.first, e_->target())) jobs_[l.first][kv.first] = Job{};
+  for (auto& kv : status_) load_.emplace(kv.first, 0);
+  for (LayerID layer : sorted) {
+    auto lj = jobs_.find(layer);
+    if (lj == jobs_.end()) continue;
+    for (auto& jd : lj->second) {
+      NodeID sender = min_loaded_sender(layer);
+      if (sender == kClientID) {
+        log::error(int64_t(cfg_.id)).u("layer", layer).msg("no owner holds the layer");
+        continue;
+      }
+      jd.second = Job{sender, JobState::Pending, 0};
+      load_[sender]++;
+      log::info(int64_t(cfg_.id)).msg("job assignment: layer: " + std::to_string(layer) +
+                                      ", sender: " + std::to_string(sender));
+    }
+  }
+  // Kick every node that has queued jobs or is a destination (quirk Q10:
+  // the reference kicks only assignment keys, stranding pure senders).
+  std::set<NodeID> kick;
+  for (auto& kv : assignment_) kick.insert(kv.first);
+  for (auto& kv : load_)
+    if (kv.second > 0) kick.insert(kv.first);
+  for (NodeID n : kick)
+    while (inflight_[n] < cfg_.pull_window && assign_new_job(n)) {
+    }
+}
+
+// ------------------------------------------------------------------- mode 3
+
+void Node::schedule_mode3() {
+  // node.go:1200-1288 + flow.go
+  FlowProblem p;
+  const Location tgt = e_->target();
+  std::vector<FlowDemand> demands;
+  struct SelfJob {
+    NodeID dest;
+    LayerID layer;
+    int64_t size, rate;
+  };
+  std::vector<SelfJob> self_jobs;
+  for (auto& kv : assignment_) {
+    for (auto& l : kv.second) {
+      auto& st = status_[kv.first];
+      if (at(st, l.first, tgt)) continue;
+      auto it = st.find(l.first);
+      if (it != st.end()) {
+        self_jobs.push_back({kv.first, l.first, layer_size(l.first), it->second.limit_rate});
+      } else {
+        demands.push_back({l.first, kv.first, layer_size(l.first)});
+      }
+    }
+  }
+  for (auto& sj : self_jobs) {
+    Message f;
+    f.type = MsgType::FlowRetransmit;
+    f.layer = sj.layer;
+    f.dest = sj.dest;
+    f.data_size = sj.size;
+    f.offset = 0;
+    f.rate = sj.rate;
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.jobs_dispatched++;
+    }
+    send_msg(sj.dest, f);
+  }
+  if (demands.empty()) {
+    log::info(int64_t(cfg_.id)).msg("No jobs to assign other than self-assignment");
+    return;
+  }
+  p.demands = demands;
+  p.holdings = status_;
+  for (auto& kv : cfg_.network_bw) {
+    p.egress_bps[kv.first] = kv.second;
+    p.ingress_bps[kv.first] = kv.second;
+  }
+  p.link_bps = cfg_.link_bw;
+  p.align = cfg_.align;
+  p.integer_seconds = cfg_.integer_seconds;
+  log::info(int64_t(cfg_.id)).msg("assigning a job...");
+  int64_t t0 = log::now_us();
+  FlowPlan plan = solve_flow(p);
+  log::info(int64_t(cfg_.id)).f("computation time[ms]", double(log::now_us() - t0) / 1e3).i("solves", plan.solves)
+      .msg("Job assignment completed");
+  log::info(int64_t(cfg_.id)).f("required minimum time(s)", plan.T).b("feasible", plan.feasible)
+      .msg("job assignment calculated");
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.flow_T = plan.T;
+  }
+  for (auto& j : plan.jobs) {
+    Message f;
+    f.type = MsgType::FlowRetransmit;
+    f.layer = j.layer;
+    f.dest = j.dest;
+    f.data_size = j.size;
+    f.offset = j.offset;
+    f.rate = plan.T > 0 ? int64_t(double(j.size) / plan.T) : 0;  // node.go:1281 (pace to finish together)
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.jobs_dispatched++;
+    }
+    send_msg(j.sender, f);
+  }
+}
+
+// ------------------------------------------------------------------- client
+
+ClientNode::ClientNode(NodeID node_id, std::shared_ptr<Transport> t, const LayersSrc& layers)
+    : node_id_(node_id), t_(std::move(t)), layers_(layers) {}
+
+ClientNode::~ClientNode() { stop(); }
+
+void ClientNode::start() {
+  th_ = std::thread([this] {
+    for (;;) {
+      auto m = t_->deliver().pop();
+      if (!m || (*m)->type == MsgType::Stop) break;
+      if ((*m)->type != MsgType::ClientReq) continue;
+      LayerID layer = (*m)->layer;
+      auto it = layers_.find(layer);
+      if (it == layers_.end() || !it->second.host) {
+        log::error(-1).u("layerID", layer).msg("client does not hold the layer");
+        continue;
+      }
+      LayerSrc src = it->second;
+      workers_.spawn([this, layer, src] {
+        // client.go:48-63: stream the whole layer to the attached node.
+        Message lm;
+        lm.type = MsgType::Layer;
+        lm.src = kClientID;
+        lm.layer = layer;
+        lm.data_size = src.data_size;
+        lm.total_size = src.data_size;
+        lm.offset = 0;
+        lm.rate = src.meta.limit_rate;
+        LayerPayload p;
+        p.host = src.host;
+        try {
+          t_->send(node_id_, lm, &p);
+        } catch (const std::exception& e) {
+          log::error(-1).s("error", e.what()).msg("failed to send layer to " + std::to_string(node_id_));
+        }
+      });
+    }
+  });
+}
+
+void ClientNode::stop() {
+  if (!th_.joinable()) return;
+  auto m = std::make_shared<Message>();
+  m->type = MsgType::Stop;
+  t_->inject(m);
+  th_.join();
+  workers_.join_all();
+}
+
+}  // namespace dissem

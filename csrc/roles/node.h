@@ -1,0 +1,173 @@
+// Roles: leader (coordinator) and receiver state machines for distribution
+// modes 0-3, plus the external client (reference: distributor/node.go,
+// client.go).
+//
+// The reference builds a class hierarchy (LeaderNode -> RetransmitLeaderNode ->
+// Pull/Flow leaders, ReceiverNode -> Retransmit/Flow receivers) and spawns a
+// goroutine per message, guarding shared maps with RWMutexes (several of which
+// race). Here one Node owns all role state and processes its inbox
+// on a single event-loop thread; a leader is a Node with `is_leader` set, and
+// every node (the leader included) can act as a sender or receiver. Mode policy
+// lives in small strategy functions (mode0/1/2/3 in node.cc).
+#pragma once
+
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <random>
+#include <set>
+#include <thread>
+
+#include "engine/engine.h"
+#include "store/store.h"
+#include "transport/transport.h"
+
+namespace dissem {
+
+struct NodeConfig {
+  NodeID id = 0;
+  NodeID leader = 0;
+  int mode = 0;                     // 0 naive, 1 retransmit, 2 pull, 3 flow
+  uint64_t epoch = 0;               // session id carried in messages (0 = none)
+  uint64_t seed = 0;                // mode-1 owner RNG (quirk Q5: seeded uniform choice)
+  std::string owner_policy = "random";  // mode 1: "random" (reference) or "balanced"
+  int pull_window = 1;              // mode 2: concurrent jobs per sender (reference: 1)
+  std::map<NodeID, int64_t> network_bw;  // mode 3: NetworkBW per node (B/s, 0 = unlimited)
+  std::map<std::pair<NodeID, NodeID>, int64_t> link_bw;  // mode 3 topology: per directed link
+  bool integer_seconds = false;     // mode 3: reference T search over integer seconds
+  int64_t align = 1;                // mode 3: byte alignment of ranges
+  std::string storage_path;         // receiver persist dir ("" = none)
+};
+
+struct NodeStats {
+  double time_to_deliver_s = 0;  // leader: start -> assignment satisfied
+  int64_t bytes_planned = 0;     // leader: bytes that had to move at start
+  int64_t jobs_dispatched = 0;
+  int64_t layers_received = 0;
+  int64_t bytes_received = 0;
+  double flow_T = 0;             // mode 3 planned completion time (s)
+  double plan_ms = 0;            // scheduling time
+};
+
+class Node {
+ public:
+  Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEngine> e, const LayersSrc& layers,
+       const Assignment& assignment, bool is_leader);
+  ~Node();
+
+  void start();
+  void stop();
+
+  // Receiver API (node.go:1291-1297).
+  void announce();
+  bool wait_ready(double timeout_s);
+  // Leader API (node.go:214-226).
+  bool wait_start(double timeout_s);
+  Assignment assignment() const { return assignment_; }
+  Status status();
+  NodeStats stats();
+
+  // Routing (node.go:17-122): 1-hop table; updateLeader kept for failover.
+  void add_node(NodeID goal) { add_routing(goal, goal, 1); }
+  void add_routing(NodeID goal, NodeID next_hop, unsigned hops);
+  NodeID next_hop(NodeID goal);
+  void update_leader(NodeID leader);
+
+  // Accessors for engines.
+  NodeID id() const { return cfg_.id; }
+  NodeID leader() const { return cfg_.leader; }
+  uint64_t epoch() const { return cfg_.epoch; }
+  Transport* transport() { return t_.get(); }
+  LayerStore& store() { return store_; }
+  DataEngine* engine() { return e_.get(); }
+  void inject(MessagePtr m) { t_->inject(std::move(m)); }
+  // Safe send from any thread (logs on failure).
+  bool send_msg(NodeID dest, Message m);
+  bool is_leader() const { return is_leader_; }
+
+ private:
+  void loop();
+  void handle(const MessagePtr& m);
+  // receiver-side
+  void on_layer(const MessagePtr& m);
+  void on_landed(LayerID layer, int64_t off, int64_t size, int64_t total, NodeID from, double dur_ms);
+  void on_retransmit(const MessagePtr& m);
+  void on_flow_retransmit(const MessagePtr& m);
+  void on_startup(const MessagePtr& m);
+  void send_ack(LayerID layer);
+  // sender-side
+  void send_layer(NodeID dest, LayerID layer, int64_t offset, int64_t size, int64_t rate);
+  void fetch_from_client(LayerID layer, NodeID dest);
+  // leader-side
+  void on_announce(const MessagePtr& m);
+  void on_ack(const MessagePtr& m);
+  bool assignment_satisfied();
+  void send_startup();
+  void start_distribution();
+  int64_t layer_size(LayerID l);
+  void retransmit(LayerID layer, NodeID owner, NodeID dest);
+  void schedule_mode0();
+  void schedule_mode1();
+  void schedule_mode2();
+  void schedule_mode3();
+  // mode 2 (node.go:628-1073)
+  bool assign_new_job(NodeID node);
+  NodeID min_loaded_sender(LayerID layer);
+  bool rarest_own_job(NodeID node, LayerID* layer, NodeID* dest);
+  bool rarest_stealable_job(NodeID node, LayerID* layer, NodeID* dest, NodeID* victim);
+
+  NodeConfig cfg_;
+  std::shared_ptr<Transport> t_;
+  std::shared_ptr<DataEngine> e_;
+  LayerStore store_;
+  Assignment assignment_;
+  bool is_leader_;
+  std::thread loop_th_;
+  std::atomic<bool> running_{false};
+
+  std::mutex rt_mu_;
+  std::map<NodeID, std::pair<NodeID, unsigned>> routing_;
+
+  // leader state (event-loop thread only, except where noted)
+  Status status_;
+  std::map<LayerID, NodeIDs> owners_;
+  std::mt19937_64 rng_;
+  std::map<NodeID, int64_t> owner_bytes_;  // balanced owner policy
+  enum class JobState { Pending, Sending };
+  struct Job {
+    NodeID sender = 0;
+    JobState state = JobState::Pending;
+    int64_t t_us = 0;
+  };
+  std::map<LayerID, std::map<NodeID, Job>> jobs_;
+  std::map<NodeID, int64_t> load_;        // senderLoadCounter
+  std::map<NodeID, int> inflight_;        // jobs currently sending per sender
+  std::map<NodeID, std::pair<double, uint64_t>> perf_;  // sender -> (EWMA job us, count) (quirk Q9)
+
+  // cross-thread signalling
+  std::mutex sig_mu_;
+  std::condition_variable sig_cv_;
+  bool started_ = false, satisfied_ = false, ready_ = false;
+  int64_t t_start_us_ = 0, t_ready_us_ = 0;
+  NodeStats stats_;
+  std::set<LayerID> acked_;
+};
+
+// External client: a separate process holding rate-limited layers in memory
+// that streams a layer to its node on ClientReq (reference: client.go).
+class ClientNode {
+ public:
+  ClientNode(NodeID node_id, std::shared_ptr<Transport> t, const LayersSrc& layers);
+  ~ClientNode();
+  void start();
+  void stop();
+
+ private:
+  NodeID node_id_;
+  std::shared_ptr<Transport> t_;
+  LayersSrc layers_;
+  std::thread th_;
+  WorkerSet workers_;
+};
+
+}  // namespace dissem

@@ -1,0 +1,94 @@
+// Control-plane transport (reference: distributor/transport.go:18-25).
+//
+// A Transport delivers decoded Messages into an inbox queue. Two
+// implementations: TcpTransport (JSON envelopes on persistent connections, a
+// fresh connection per layer payload, token-bucket pacing, cut-through "pipe")
+// and InprocTransport (a process-global registry of queues; the test fake).
+// On MI355X the layer bytes normally move on the RCCL data plane instead
+// (csrc/gpu/rccl_engine.cc); the TCP payload path is the CPU/loopback plane.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "core/queue.h"
+#include "core/wire.h"
+
+namespace dissem {
+
+using AddrRegistry = std::map<NodeID, std::string>;  // transport.go:57
+
+// Layer-send source descriptor: bytes from host memory or a file range.
+struct LayerPayload {
+  std::shared_ptr<HostBuffer> host;  // if set: bytes at host->ptr + host_off
+  int64_t host_off = 0;
+  std::string path;                  // else: file, read at file_off
+  int64_t file_off = 0;
+};
+
+// Receiver-side landing: given a Layer header, return where its bytes go
+// (host memory, at least data_size bytes), or nullptr to allocate a buffer.
+using LandingFn = std::function<uint8_t*(const Message& hdr)>;
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  // Control message or (for MsgType::Layer) header + payload.
+  virtual void send(NodeID dest, const Message& m, const LayerPayload* payload = nullptr) = 0;
+  virtual void register_pipe(LayerID layer, NodeID dest) = 0;
+  virtual void broadcast(const Message& m) = 0;
+  virtual std::string address() const = 0;
+  virtual void close() = 0;
+
+  BlockingQueue<MessagePtr>& deliver() { return inbox_; }
+  // Node-internal events (engine completions) enter the same inbox.
+  void inject(MessagePtr m) { inbox_.push(std::move(m)); }
+
+  void set_registry(const AddrRegistry& reg) {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    registry_ = reg;
+  }
+  void add_peer(NodeID id, const std::string& addr) {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    registry_[id] = addr;
+  }
+  AddrRegistry registry() const {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    return registry_;
+  }
+  void set_landing(LandingFn fn) {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    landing_ = std::move(fn);
+  }
+
+  // Counters for observability.
+  std::atomic<int64_t> bytes_sent{0};
+  std::atomic<int64_t> bytes_received{0};
+
+ protected:
+  bool lookup(NodeID id, std::string* addr) const {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    auto it = registry_.find(id);
+    if (it == registry_.end()) return false;
+    *addr = it->second;
+    return true;
+  }
+  LandingFn landing() const {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    return landing_;
+  }
+
+  mutable std::mutex reg_mu_;
+  AddrRegistry registry_;
+  LandingFn landing_;
+  BlockingQueue<MessagePtr> inbox_;
+};
+
+std::shared_ptr<Transport> make_inproc_transport(const std::string& addr, const AddrRegistry& reg);
+std::shared_ptr<Transport> make_tcp_transport(const std::string& addr, const AddrRegistry& reg,
+                                              bool is_client = false);
+
+}  // namespace dissem
