@@ -23,17 +23,17 @@ PKG       := distributed_llm_dissemination_amd
 TARGET    := $(PKG)/_core$(EXT)
 BUILD     := build
 
-CXXFLAGS  := -O2 -g -std=c++17 -fPIC -Wall -Wno-sign-compare -Icsrc -I$(PYINC) -I$(PYBIND) \
-             -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -fvisibility=hidden
+CXXFLAGS  := -O2 -g1 -std=c++17 -fPIC -Wall -Wno-sign-compare -Wno-unused-result -Icsrc -I$(PYINC) -I$(PYBIND) \
+             -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(ROCM)/include/rccl -fvisibility=hidden
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Icsrc -I$(ROCM)/include -Wno-unused-result \
              -fvisibility=hidden
 LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -lpthread
 
-CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/transport/inproc.cc \
+CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/transport/inproc.cc \
              csrc/transport/tcp.cc csrc/store/store.cc csrc/sched/maxflow.cc csrc/roles/node.cc \
              csrc/engine/host_engine.cc
-BIND_SRC  := csrc/bindings.cc csrc/gpu/gpu_bindings.cc
-GPU_SRC   := $(wildcard csrc/gpu/*.hip.cc)
+BIND_SRC  := csrc/bindings.cc
+GPU_SRC   := $(wildcard csrc/gpu/*.cc)
 HIP_SRC   := $(wildcard csrc/kernels/*.hip)
 
 CORE_OBJ  := $(patsubst csrc/%.cc,$(BUILD)/%.o,$(CORE_SRC))
@@ -50,11 +50,7 @@ $(BUILD)/%.hip.o: csrc/%.hip csrc/kernels/*.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/gpu/%.hip.o: csrc/gpu/%.hip.cc csrc/gpu/*.h csrc/engine/engine.h csrc/roles/node.h
-	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
-
-$(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h)
+$(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h) Makefile
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 

@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Headline benchmark: aggregate GB/s + time-to-full-placement of 80 x 1 GiB
+layers, mode 1 (peer retransmission), one rank per MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` runs N
+ranks of one node (torchrun for N > 1). A *step* is one complete dissemination
+session: every rank announces, the leader plans mode-1 retransmissions, layers
+move into every GPU's HBM (host->HBM staging over PCIe, GPU->GPU over RCCL/xGMI),
+every chunk is CRC32C-verified on the receiving GPU, all ranks ack, and the
+leader broadcasts startup. W untimed warmup steps, then K steps, each bracketed
+by barrier + device synchronize on both sides; the slowest rank's time counts.
+
+Workload (BASELINE.json config #3, weak scaling): 80 layers x 1 GiB of random
+bytes; InitialLayers seeded by a balanced random permutation into the pinned
+host memory of the ranks (each rank holds 80/N layers); the Assignment gives
+every rank all 80 layers (full replication, DP-serving placement). Each GPU
+therefore receives 80 GiB into HBM per step at every N: at N = 1 all of it
+crosses PCIe; at N = 8, 10 GiB per GPU crosses PCIe and 70 GiB arrives over
+xGMI. value = N x 80 GiB / step time (GB/s, 1e9 bytes).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BASELINE_METRIC = "aggregate GB/s + time-to-full-placement, 80×1 GiB layers, mode 1, 8 ranks"
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE or 1)")
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--mode", type=int, default=1, choices=[0, 1, 2, 3])
+    p.add_argument("--layers", type=int, default=80)
+    p.add_argument("--layer-mib", type=int, default=1024)
+    p.add_argument("--chunk-mib", type=int, default=64)
+    p.add_argument("--tier", default="host", choices=["host", "device", "disk"])
+    p.add_argument("--seeding", default="random", choices=["random", "leader", "uniform"])
+    p.add_argument("--copies", type=int, default=1)
+    p.add_argument("--assignment", default="replicate", choices=["replicate", "pipeline"])
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--timeout", type=float, default=300.0)
+    p.add_argument("--pull-window", type=int, default=0, help="mode 2 jobs in flight per sender (0 = peers)")
+    p.add_argument("--storage", default="", help="disk tier directory")
+    return p.parse_args(argv)
+
+
+def relaunch_with_torchrun(args) -> int:
+    # Launched for N > 1 without torchrun: start it as a child (never exec after GPU init).
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch_with_torchrun(args)
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+
+    sys.path.insert(0, HERE)
+    import torch
+    import torch.distributed as dist
+
+    import distributed_llm_dissemination_amd as dl
+    from distributed_llm_dissemination_amd import _core
+    from distributed_llm_dissemination_amd.models.catalog import delivered_bytes, make_workload
+    from distributed_llm_dissemination_amd.parallel.runtime import Runtime
+
+    _core.set_log_level(2)
+
+    def log(msg):
+        print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    if not torch.cuda.is_available():
+        print("error: no GPU visible", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        barrier = dist.barrier
+    else:
+        barrier = lambda: None  # noqa: E731
+
+    layer_bytes = args.layer_mib << 20
+    cfg = make_workload(world, args.layers, layer_bytes, seeding=args.seeding, tier=args.tier, copies=args.copies,
+                        seed=args.seed, assignment=args.assignment, chunk_bytes=args.chunk_mib << 20)
+    total_bytes = delivered_bytes(cfg)
+
+    uid = _core.nccl_unique_id() if (world > 1 and rank == 0) else None
+    if world > 1:
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    free, tot = _core.mem_info()
+    log(f"HBM free {free / 2**30:.1f} / {tot / 2**30:.1f} GiB; setting up {args.layers} x {args.layer_mib} MiB")
+    t_setup = time.time()
+    rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
+                 verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
+                 barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage)
+    if world > 1:
+        addrs = [None] * world
+        dist.all_gather_object(addrs, rt.transport.address())
+        rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
+    log(f"setup done in {time.time() - t_setup:.1f}s")
+
+    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1))
+
+    def step(timed: bool):
+        rt.prepare(args.mode, **policy)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = rt.execute(args.timeout)
+        torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        if not res.ok:
+            log(f"session failed: {res.error}")
+            raise SystemExit(1)
+        return dt, res
+
+    for i in range(args.warmup):
+        dt, res = step(False)
+        log(f"warmup {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s)")
+    times = []
+    last = None
+    for i in range(args.steps):
+        dt, last = step(True)
+        times.append(dt)
+        log(f"step {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s) ttd={last.time_to_deliver_s * 1e3:.1f} ms")
+    total = sum(times)
+    if world > 1:
+        t = torch.tensor([total], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        total = float(t.item())
+    ms_per_step = total / max(1, args.steps) * 1e3
+    value = total_bytes * args.steps / total / 1e9
+    if rank == 0:
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bytes (bf16-sized layer shards)",
+            "data": "synthetic: random-byte layers (splitmix64), balanced random seeding in pinned host memory",
+            "config": {
+                "model": f"{args.layers}x{args.layer_mib}MiB layers (Llama-3-70B-sized shards)",
+                "global_batch": None,
+                "seq_len": None,
+                "parallelism": f"dp{world} (full replication)" if args.assignment == "replicate" else f"pp{world}",
+                "mode": args.mode,
+                "tier": args.tier,
+                "seeding": args.seeding,
+                "chunk_mib": args.chunk_mib,
+                "verify": not args.no_verify,
+                "bytes_per_step": total_bytes,
+                "time_to_full_placement_s": round(ms_per_step / 1e3, 6),
+                "leader_time_to_deliver_s": round(last.time_to_deliver_s, 6) if last else None,
+                "engine": "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)",
+            },
+        }
+        if last is not None and last.engine_stats:
+            out["config"]["engine_stats_rank0"] = last.engine_stats
+        print(json.dumps(out), flush=True)
+    rt.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

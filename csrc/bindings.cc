@@ -237,7 +237,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("link_bw", &NodeConfig::link_bw)
       .def_readwrite("integer_seconds", &NodeConfig::integer_seconds)
       .def_readwrite("align", &NodeConfig::align)
-      .def_readwrite("storage_path", &NodeConfig::storage_path);
+      .def_readwrite("storage_path", &NodeConfig::storage_path)
+      .def_readwrite("relay", &NodeConfig::relay);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)

@@ -48,6 +48,7 @@ const char* msg_type_name(MsgType t) {
     case MsgType::Transport: return "transport";
     case MsgType::Nack: return "nack";
     case MsgType::Bcast: return "bcast";
+    case MsgType::XferBatch: return "xfer_batch";
     case MsgType::Landed: return "landed";
     case MsgType::SendDone: return "send_done";
     case MsgType::Tick: return "tick";
@@ -150,7 +151,41 @@ Json encode_payload(const Message& m) {
     case MsgType::Announce:
       src_id();
       p["LayerIDs"] = layer_ids_json(m.layers);
+      if (!m.manifest.empty()) {
+        Json man = Json::object();
+        for (auto& kv : m.manifest) {
+          Json e = Json::array();
+          e.push_back(Json(kv.second.chunk_bytes));
+          Json c = Json::array();
+          for (uint32_t x : kv.second.crc) c.push_back(Json(unsigned(x)));
+          e.push_back(c);
+          man[std::to_string(kv.first)] = e;
+        }
+        p["Manifest"] = man;
+      }
       break;
+    case MsgType::XferBatch: {
+      src_id();
+      p["Batch"] = Json(uint64_t(m.batch));
+      Json arr = Json::array();
+      for (auto& j : m.jobs) {
+        Json e = Json::array();
+        e.push_back(Json(uint64_t(j.seq)));
+        e.push_back(Json(uint64_t(j.src)));
+        e.push_back(Json(uint64_t(j.dst)));
+        e.push_back(Json(uint64_t(j.layer)));
+        e.push_back(Json(j.offset));
+        e.push_back(Json(j.size));
+        e.push_back(Json(j.total));
+        e.push_back(Json(j.chunk_bytes));
+        Json c = Json::array();
+        for (uint32_t x : j.crc) c.push_back(Json(unsigned(x)));
+        e.push_back(c);
+        arr.push_back(e);
+      }
+      p["Jobs"] = arr;
+      break;
+    }
     case MsgType::Ack:
       src_id();
       p["LayerID"] = Json(uint64_t(m.layer));
@@ -234,6 +269,34 @@ MessagePtr decode_envelope(const Json& env) {
   switch (m->type) {
     case MsgType::Announce:
       m->layers = layer_ids_from(p.find("LayerIDs"));
+      if (auto* man = p.find("Manifest"); man && man->is_object()) {
+        for (auto& kv : man->as_object()) {
+          const auto& e = kv.second.as_array();
+          CrcManifest cm;
+          cm.chunk_bytes = e.at(0).as_i64();
+          for (auto& x : e.at(1).as_array()) cm.crc.push_back(uint32_t(x.as_u64()));
+          m->manifest[LayerID(strtoull(kv.first.c_str(), nullptr, 10))] = cm;
+        }
+      }
+      break;
+    case MsgType::XferBatch:
+      m->batch = p.get_u64("Batch");
+      if (auto* arr = p.find("Jobs"); arr && arr->is_array()) {
+        for (auto& e : arr->as_array()) {
+          const auto& a = e.as_array();
+          XferJob j;
+          j.seq = a.at(0).as_u64();
+          j.src = a.at(1).as_u64();
+          j.dst = a.at(2).as_u64();
+          j.layer = a.at(3).as_u64();
+          j.offset = a.at(4).as_i64();
+          j.size = a.at(5).as_i64();
+          j.total = a.at(6).as_i64();
+          j.chunk_bytes = a.at(7).as_i64();
+          for (auto& x : a.at(8).as_array()) j.crc.push_back(uint32_t(x.as_u64()));
+          m->jobs.push_back(std::move(j));
+        }
+      }
       break;
     case MsgType::Ack:
       m->layer = p.get_u64("LayerID");

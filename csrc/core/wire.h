@@ -30,6 +30,7 @@ enum class MsgType : uint8_t {
   // ---- extensions ----
   Nack = 9,        // receiver -> sender: chunk CRC mismatch, resend range
   Bcast = 10,      // leader -> participants: collective broadcast descriptor (GPU mode 0)
+  XferBatch = 11,  // leader -> ranks: sequence-numbered transfer jobs (GPU planned data plane)
   // ---- node-internal events (never serialized) ----
   Landed = 32,     // a byte range of a layer is now resident in the target tier
   SendDone = 33,   // a sender finished pushing a range
@@ -38,6 +39,25 @@ enum class MsgType : uint8_t {
 };
 
 const char* msg_type_name(MsgType t);
+
+// One transfer of a byte range of a layer from `src` to `dst` (src == dst: a
+// local promotion into HBM). Jobs carry a leader-assigned global sequence
+// number; every rank executes its jobs in sequence order, which makes the
+// RCCL point-to-point schedule deadlock-free (csrc/gpu/gpu_engine.cc).
+struct XferJob {
+  uint64_t seq = 0;
+  NodeID src = 0, dst = 0;
+  LayerID layer = 0;
+  int64_t offset = 0, size = 0, total = 0;
+  int64_t chunk_bytes = 0;     // CRC chunk grid of the layer
+  std::vector<uint32_t> crc;   // expected CRC32C of the grid chunks the range covers
+};
+
+// Per-layer integrity manifest announced by holders: CRC32C per chunk.
+struct CrcManifest {
+  int64_t chunk_bytes = 0;
+  std::vector<uint32_t> crc;
+};
 
 struct Message {
   MsgType type = MsgType::Simple;
@@ -61,6 +81,10 @@ struct Message {
   std::vector<uint32_t> crc;    // expected CRC32C per chunk of the range
   uint64_t seq = 0;             // per (src,dest) stream sequence number
   std::vector<NodeID> peers;    // Bcast participants
+  // XferBatch / Announce extensions
+  uint64_t batch = 0;
+  std::vector<XferJob> jobs;
+  std::map<LayerID, CrcManifest> manifest;
   // Simple
   std::string src_addr, payload_str;
 

@@ -44,6 +44,12 @@ class DataEngine {
   // Collective broadcast of a whole layer from this node to `dests` (GPU mode 0).
   virtual bool supports_broadcast() const { return false; }
   virtual void broadcast_layer(LayerID, int64_t, const std::vector<NodeID>&) {}
+  // Planned engines (GPU) do not take per-message pushes: the leader batches
+  // sequence-numbered XferJobs and sends each rank its share (MsgType::XferBatch).
+  virtual bool planned() const { return false; }
+  virtual int64_t chunk_bytes() const { return 0; }
+  // Per-layer CRC manifests of layers this rank can serve (sent with Announce).
+  virtual std::map<LayerID, CrcManifest> manifest() { return {}; }
   // Wait until every transfer this engine started for its node has finished.
   virtual void quiesce() {}
   virtual void shutdown() {}

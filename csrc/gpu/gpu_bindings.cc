@@ -1,10 +1,222 @@
+// Python bindings of the GPU runtime: device helpers, gfx950 kernels on raw
+// device pointers, pinned host buffers, and the RCCL data engine.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "core/crc32c.h"
 #include "gpu/gpu_api.h"
+#include "gpu/gpu_engine.h"
+#include "kernels/kernels.h"
 
 namespace py = pybind11;
+using namespace dissem;
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Per-device scratch for synchronous CRC calls from Python.
+struct Scratch {
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  uint32_t* out = nullptr;  // pinned
+  size_t out_n = 0;
+};
+std::mutex g_scratch_mu;
+std::map<int, Scratch> g_scratch;
+
+std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk, uint64_t stream) {
+  int dev = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  Scratch& s = g_scratch[dev];
+  size_t need = kern::crc32c_workspace_bytes(bytes, chunk);
+  if (s.ws_bytes < need) {
+    if (s.ws) check(hipFree(s.ws), "hipFree");
+    check(hipMalloc(&s.ws, need), "hipMalloc");
+    s.ws_bytes = need;
+  }
+  size_t n = size_t(bytes > 0 ? (bytes + chunk - 1) / chunk : 0);
+  if (s.out_n < n) {
+    if (s.out) check(hipHostFree(s.out), "hipHostFree");
+    check(hipHostMalloc(reinterpret_cast<void**>(&s.out), std::max<size_t>(n, 1) * 4, hipHostMallocMapped), "hipHostMalloc");
+    s.out_n = n;
+  }
+  uint32_t* dout = nullptr;
+  check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dout), s.out, 0), "hipHostGetDevicePointer");
+  check(kern::crc32c_chunks(reinterpret_cast<const void*>(ptr), bytes, chunk, dout, s.ws, as_stream(stream)),
+        "crc32c_chunks");
+  check(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize");
+  return std::vector<uint32_t>(s.out, s.out + n);
+}
+
+}  // namespace
 
 void register_gpu_bindings(PyObject* module) {
   py::module_ m = py::reinterpret_borrow<py::module_>(module);
-  (void)m;
+
+  // ---- host CRC32C reference + GF(2) helpers (tests compare kernels against these)
+  m.def("crc32c", [](py::buffer b, uint32_t crc) {
+    py::buffer_info info = b.request();
+    return crc32c(info.ptr, size_t(info.size * info.itemsize), crc);
+  }, py::arg("data"), py::arg("crc") = 0);
+  m.def("crc32c_shift", &crc32c_shift);
+  m.def("crc32c_multmodp", &crc32c_multmodp);
+  m.def("fill_random_host", [](int64_t n, uint64_t seed, int64_t offset) {
+    std::string out(size_t(n), '\0');
+    {
+      py::gil_scoped_release nogil;
+      kern::fill_random_host(out.data(), n, seed, offset);
+    }
+    return py::bytes(out);
+  }, py::arg("n"), py::arg("seed"), py::arg("offset") = 0);
+
+  // ---- device helpers
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("set_device", [](int d) { check(hipSetDevice(d), "hipSetDevice"); });
+  m.def("device_synchronize", [] {
+    py::gil_scoped_release nogil;
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  });
+  m.def("device_malloc", [](int64_t n) {
+    void* p = nullptr;
+    check(hipMalloc(&p, size_t(n)), "hipMalloc");
+    return reinterpret_cast<uint64_t>(p);
+  });
+  m.def("device_free", [](uint64_t p) { check(hipFree(reinterpret_cast<void*>(p)), "hipFree"); });
+  m.def("memcpy", [](uint64_t dst, uint64_t src, int64_t n, uint64_t stream) {
+    py::gil_scoped_release nogil;
+    check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<void*>(src), size_t(n), hipMemcpyDefault,
+                         as_stream(stream)),
+          "hipMemcpyAsync");
+    check(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize");
+  }, py::arg("dst"), py::arg("src"), py::arg("n"), py::arg("stream") = 0);
+  m.def("memset", [](uint64_t dst, int v, int64_t n, uint64_t stream) {
+    check(hipMemsetAsync(reinterpret_cast<void*>(dst), v, size_t(n), as_stream(stream)), "hipMemsetAsync");
+  }, py::arg("dst"), py::arg("value"), py::arg("n"), py::arg("stream") = 0);
+  m.def("mem_info", [] {
+    size_t f = 0, t = 0;
+    check(hipMemGetInfo(&f, &t), "hipMemGetInfo");
+    return py::make_tuple(f, t);
+  });
+
+  // ---- pinned host memory as a HostBuffer usable by LayerSrc
+  py::class_<HostBuffer, std::shared_ptr<HostBuffer>>(m, "HostBuffer")
+      .def_static("pinned", [](int64_t n) {
+        py::gil_scoped_release nogil;
+        return alloc_pinned(n);
+      })
+      .def_static("malloc", [](int64_t n) { return HostBuffer::alloc(n, true); })
+      .def_property_readonly("ptr", [](const HostBuffer& b) { return reinterpret_cast<uint64_t>(b.ptr); })
+      .def_property_readonly("size", [](const HostBuffer& b) { return b.size; })
+      .def("view", [](HostBuffer& b) {
+        return py::memoryview::from_memory(b.ptr, py::ssize_t(b.size), false);
+      })
+      .def("bytes", [](const HostBuffer& b, int64_t off, int64_t n) {
+        if (n < 0) n = b.size - off;
+        return py::bytes(reinterpret_cast<const char*>(b.ptr + off), size_t(n));
+      }, py::arg("off") = 0, py::arg("n") = -1);
+  m.def("layer_src_from_buffer", [](std::shared_ptr<HostBuffer> b, int64_t rate, SourceType st) {
+    LayerSrc s;
+    s.host = std::move(b);
+    s.data_size = s.host->size;
+    s.meta = LayerMeta{Location::Inmem, rate, st, s.data_size};
+    return s;
+  }, py::arg("buffer"), py::arg("limit_rate") = 0, py::arg("source_type") = SourceType::Mem);
+  m.def("layer_src_device", [](uint64_t dev_ptr, int64_t size) {
+    LayerSrc s;
+    s.dev = reinterpret_cast<uint8_t*>(dev_ptr);
+    s.data_size = size;
+    s.meta = LayerMeta{Location::Device, 0, SourceType::Device, size};
+    return s;
+  });
+
+  // ---- kernels on raw device pointers (stream = hipStream_t as int, 0 = null stream)
+  m.def("fill_random", [](uint64_t ptr, int64_t n, uint64_t seed, uint64_t stream) {
+    check(kern::fill_random(reinterpret_cast<void*>(ptr), n, seed, as_stream(stream)), "fill_random");
+  }, py::arg("ptr"), py::arg("nbytes"), py::arg("seed"), py::arg("stream") = 0);
+  m.def("crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t stream) {
+    py::gil_scoped_release nogil;
+    return crc_chunks_sync(ptr, n, chunk, stream);
+  }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("stream") = 0);
+  m.def("crc32c_chunks_async", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t out_dev, uint64_t ws,
+                                  uint64_t stream) {
+    check(kern::crc32c_chunks(reinterpret_cast<const void*>(ptr), n, chunk, reinterpret_cast<uint32_t*>(out_dev),
+                              reinterpret_cast<void*>(ws), as_stream(stream)),
+          "crc32c_chunks");
+  });
+  m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
+  m.def("fp8_pack", [](uint64_t bf16, int64_t n, uint64_t fp8, uint64_t scales, int block, uint64_t stream) {
+    check(kern::fp8_pack(reinterpret_cast<const uint16_t*>(bf16), n, reinterpret_cast<uint8_t*>(fp8),
+                         reinterpret_cast<float*>(scales), block, as_stream(stream)),
+          "fp8_pack");
+  }, py::arg("bf16"), py::arg("n"), py::arg("fp8"), py::arg("scales"), py::arg("block") = 128, py::arg("stream") = 0);
+  m.def("fp8_unpack", [](uint64_t fp8, uint64_t scales, int64_t n, uint64_t bf16, int block, uint64_t stream) {
+    check(kern::fp8_unpack(reinterpret_cast<const uint8_t*>(fp8), reinterpret_cast<const float*>(scales), n,
+                           reinterpret_cast<uint16_t*>(bf16), block, as_stream(stream)),
+          "fp8_unpack");
+  }, py::arg("fp8"), py::arg("scales"), py::arg("n"), py::arg("bf16"), py::arg("block") = 128, py::arg("stream") = 0);
+
+  // ---- RCCL engine
+  m.def("nccl_unique_id", [] { return py::bytes(nccl_unique_id()); });
+  py::class_<CrcManifest>(m, "CrcManifest")
+      .def(py::init<>())
+      .def(py::init([](int64_t cb, std::vector<uint32_t> crc) { return CrcManifest{cb, std::move(crc)}; }))
+      .def_readwrite("chunk_bytes", &CrcManifest::chunk_bytes)
+      .def_readwrite("crc", &CrcManifest::crc);
+  py::class_<GpuEngineConfig>(m, "GpuEngineConfig")
+      .def(py::init<>())
+      .def_readwrite("device", &GpuEngineConfig::device)
+      .def_readwrite("rank", &GpuEngineConfig::rank)
+      .def_readwrite("world", &GpuEngineConfig::world)
+      .def_readwrite("rank_nodes", &GpuEngineConfig::rank_nodes)
+      .def_property("nccl_uid", [](const GpuEngineConfig& c) { return py::bytes(c.nccl_uid); },
+                    [](GpuEngineConfig& c, py::bytes b) { c.nccl_uid = std::string(b); })
+      .def_readwrite("chunk_bytes", &GpuEngineConfig::chunk_bytes)
+      .def_readwrite("verify", &GpuEngineConfig::verify)
+      .def_readwrite("poison", &GpuEngineConfig::poison)
+      .def_readwrite("max_inflight_groups", &GpuEngineConfig::max_inflight_groups)
+      .def_readwrite("group_peers", &GpuEngineConfig::group_peers);
+  py::class_<GpuEngineStats>(m, "GpuEngineStats")
+      .def_readonly("bytes_sent", &GpuEngineStats::bytes_sent)
+      .def_readonly("bytes_recv", &GpuEngineStats::bytes_recv)
+      .def_readonly("bytes_staged", &GpuEngineStats::bytes_staged)
+      .def_readonly("bytes_verified", &GpuEngineStats::bytes_verified)
+      .def_readonly("groups", &GpuEngineStats::groups)
+      .def_readonly("pieces", &GpuEngineStats::pieces)
+      .def_readonly("verify_failures", &GpuEngineStats::verify_failures)
+      .def_readonly("unverified_pieces", &GpuEngineStats::unverified_pieces)
+      .def_readonly("issue_ms", &GpuEngineStats::issue_ms);
+  py::class_<GpuEngine, DataEngine, std::shared_ptr<GpuEngine>>(m, "GpuEngine")
+      .def(py::init([](const GpuEngineConfig& c) {
+        py::gil_scoped_release nogil;
+        return std::make_shared<GpuEngine>(c);
+      }))
+      .def("provision", [](GpuEngine& e, LayerID l, int64_t n) { return reinterpret_cast<uint64_t>(e.provision(l, n)); })
+      .def("device_ptr", [](GpuEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.device_ptr(l)); })
+      .def("set_manifest", &GpuEngine::set_manifest)
+      .def("set_seeded", &GpuEngine::set_seeded)
+      .def("reset_session", [](GpuEngine& e) {
+        py::gil_scoped_release nogil;
+        e.reset_session();
+      })
+      .def("quiesce", [](GpuEngine& e) {
+        py::gil_scoped_release nogil;
+        e.quiesce();
+      })
+      .def("stats", &GpuEngine::stats)
+      .def("error", &GpuEngine::error)
+      .def_property_readonly("comm_stream", [](const GpuEngine& e) { return reinterpret_cast<uint64_t>(e.comm_stream()); });
 }

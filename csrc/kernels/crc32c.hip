@@ -1,0 +1,226 @@
+// Per-chunk CRC32C on gfx950 (receiver-side verification of every landed chunk).
+//
+// CRC is a serial recurrence, so the kernel works with raw (un-inverted) CRC
+// registers, which are linear over GF(2):
+//   raw(A || B) = shift(raw(A), |B|) xor raw(B),  shift(r, L) = r * x^(8L) mod P.
+// Decomposition:
+//  * a chunk is cut into 64 KiB segments; one wave owns a segment;
+//  * lane l of the wave reads 16-B words l, l+64, l+128, ... (each wave
+//    instruction reads 1 KiB contiguous: fully coalesced) and keeps the raw CRC
+//    of its strided sub-message: s = shift_1024B(s) xor crc16(word), i.e. 4 + 16
+//    table lookups from LDS-resident slice-by-16 and shift tables;
+//  * lanes are aligned to the segment end with one GF(2) multiply by a per-lane
+//    constant x^(8*16*m) and XOR-reduced with cross-lane shuffles;
+//  * a second, tiny kernel folds the segments of each chunk (one wave per
+//    chunk) and applies the init/xorout term, writing the standard CRC32C.
+// The result is the exact CRC32C of each chunk for any chunk length that is a
+// multiple of 16 (the final chunk may have any length).
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "core/crc32c.h"
+#include "kernels/kernels.h"
+
+namespace dissem {
+namespace kern {
+
+namespace {
+
+constexpr int kSegBytes = 64 * 1024;
+constexpr int kT16 = 16 * 256;   // slice-by-16 tables
+constexpr int kA = 4 * 256;      // shift-by-1024-bytes map
+constexpr int kLanePow = 64;     // x^(8*16*m), m = 0..63
+constexpr int kAS = 4 * 256;     // shift-by-one-segment map
+constexpr int kX2N = 64;         // x^(2^k)
+constexpr int kConstWords = kT16 + kA + kLanePow + kAS + kX2N;
+constexpr int kSegKernelLds = kT16 + kA + kLanePow;
+
+__device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 1
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    b = (b & 1) ? (b >> 1) ^ kCrc32cPoly : b >> 1;
+  }
+  return p;
+}
+
+__device__ inline uint32_t xpow8n(const uint32_t* x2n, uint64_t n) {
+  uint32_t p = 1u << 31;
+  int k = 3;
+#pragma unroll 1
+  while (n) {
+    if (n & 1) p = multmodp(x2n[k & 63], p);
+    n >>= 1;
+    ++k;
+  }
+  return p;
+}
+
+__device__ inline uint32_t shift_map(const uint32_t* A, uint32_t s) {
+  return A[s & 255] ^ A[256 + ((s >> 8) & 255)] ^ A[512 + ((s >> 16) & 255)] ^ A[768 + (s >> 24)];
+}
+
+__device__ inline uint32_t crc16raw(const uint32_t* T, uint4 w) {
+  return T[15 * 256 + (w.x & 255)] ^ T[14 * 256 + ((w.x >> 8) & 255)] ^ T[13 * 256 + ((w.x >> 16) & 255)] ^
+         T[12 * 256 + (w.x >> 24)] ^ T[11 * 256 + (w.y & 255)] ^ T[10 * 256 + ((w.y >> 8) & 255)] ^
+         T[9 * 256 + ((w.y >> 16) & 255)] ^ T[8 * 256 + (w.y >> 24)] ^ T[7 * 256 + (w.z & 255)] ^
+         T[6 * 256 + ((w.z >> 8) & 255)] ^ T[5 * 256 + ((w.z >> 16) & 255)] ^ T[4 * 256 + (w.z >> 24)] ^
+         T[3 * 256 + (w.w & 255)] ^ T[2 * 256 + ((w.w >> 8) & 255)] ^ T[1 * 256 + ((w.w >> 16) & 255)] ^
+         T[0 * 256 + (w.w >> 24)];
+}
+
+__device__ inline uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One wave per 64 KiB segment; writes the segment's raw CRC to seg_out[g].
+__global__ void __launch_bounds__(256) crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes,
+                                                              int64_t chunk_bytes, int64_t spc,
+                                                              int64_t total_segs,
+                                                              const uint32_t* __restrict__ consts,
+                                                              uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t lds[kSegKernelLds];
+  for (int i = threadIdx.x; i < kSegKernelLds; i += blockDim.x) lds[i] = consts[i];
+  __syncthreads();
+  const uint32_t* T = lds;
+  const uint32_t* A = lds + kT16;
+  const uint32_t* lanepow = lds + kT16 + kA;
+
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
+  for (int64_t g = wave; g < total_segs; g += nwaves) {
+    const int64_t c = g / spc, k = g % spc;
+    const int64_t chunk_start = c * chunk_bytes;
+    const int64_t chunk_len = min(chunk_bytes, bytes - chunk_start);
+    const int64_t seg_start = k * kSegBytes;
+    const int64_t seg_len = min(int64_t(kSegBytes), chunk_len - seg_start);
+    const int64_t nw = seg_len >> 4;
+    const uint4* words = reinterpret_cast<const uint4*>(src + chunk_start + seg_start);
+    uint32_t s = 0;
+    int64_t j = lane;
+    if (nw == kSegBytes / 16) {
+      // Full segment: 64 words per lane, loads issued 8 ahead.
+#pragma unroll 8
+      for (int it = 0; it < kSegBytes / 16 / 64; ++it) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        const u32x4 wv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * it));
+        const uint4 w = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        s = shift_map(A, s) ^ crc16raw(T, w);
+      }
+      s = multmodp(lanepow[63 - lane], s);
+    } else {
+      int64_t last = -1;
+      for (; j < nw; j += 64) {
+        uint4 w = words[j];
+        s = shift_map(A, s) ^ crc16raw(T, w);
+        last = j;
+      }
+      if (last >= 0) s = multmodp(lanepow[nw - 1 - last], s);
+    }
+    s = wave_xor(s);
+    if (lane == 0) {
+      // Byte tail (only the buffer's final segment can have one).
+      const uint8_t* tail = src + chunk_start + seg_start + (nw << 4);
+      for (int64_t b = 0; b < (seg_len & 15); ++b) s = T[(s ^ tail[b]) & 255] ^ (s >> 8);
+      seg_out[g] = s;
+    }
+  }
+}
+
+// One wave per chunk: fold the chunk's segment CRCs and finalize.
+__global__ void __launch_bounds__(64) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
+                                                         int64_t chunk_bytes, int64_t spc,
+                                                         const uint32_t* __restrict__ consts,
+                                                         uint32_t* __restrict__ out) {
+  __shared__ uint32_t AS[kAS];
+  __shared__ uint32_t X2N[kX2N];
+  for (int i = threadIdx.x; i < kAS; i += 64) AS[i] = consts[kT16 + kA + kLanePow + i];
+  for (int i = threadIdx.x; i < kX2N; i += 64) X2N[i] = consts[kT16 + kA + kLanePow + kAS + i];
+  __syncthreads();
+  const int lane = threadIdx.x;
+  const int64_t c = blockIdx.x;
+  const int64_t chunk_start = c * chunk_bytes;
+  const int64_t chunk_len = min(chunk_bytes, bytes - chunk_start);
+  const int64_t n = (chunk_len + kSegBytes - 1) / kSegBytes;
+  const int64_t q = (n + 63) / 64;
+  const int64_t b = min(n, int64_t(lane) * q), e = min(n, int64_t(lane + 1) * q);
+  uint32_t r = 0;
+  for (int64_t k = b; k < e; ++k) {
+    const int64_t len = min(int64_t(kSegBytes), chunk_len - k * kSegBytes);
+    r = (len == kSegBytes ? shift_map(AS, r) : multmodp(xpow8n(X2N, uint64_t(len)), r)) ^ seg_out[c * spc + k];
+  }
+  const int64_t end_byte = min(e * kSegBytes, chunk_len);
+  if (r && e > b) r = multmodp(xpow8n(X2N, uint64_t(chunk_len - end_byte)), r);
+  r = wave_xor(e > b ? r : 0u);
+  if (lane == 0) out[c] = r ^ multmodp(xpow8n(X2N, uint64_t(chunk_len)), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+}
+
+struct DeviceConsts {
+  std::mutex mu;
+  std::map<int, uint32_t*> by_device;
+};
+DeviceConsts g_consts;
+
+uint32_t* device_consts() {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_consts.mu);
+  auto it = g_consts.by_device.find(dev);
+  if (it != g_consts.by_device.end()) return it->second;
+  std::vector<uint32_t> h(kConstWords);
+  crc32c_slice16_tables(h.data());
+  crc32c_shift_tables(1024, h.data() + kT16);
+  for (int m = 0; m < 64; ++m) h[size_t(kT16 + kA + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
+  crc32c_shift_tables(kSegBytes, h.data() + kT16 + kA + kLanePow);
+  uint32_t p = 1u << 30;
+  for (int k = 0; k < 64; ++k) {
+    h[size_t(kT16 + kA + kLanePow + kAS + k)] = p;
+    p = crc32c_multmodp(p, p);
+  }
+  uint32_t* d = nullptr;
+  if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+  g_consts.by_device[dev] = d;
+  return d;
+}
+
+}  // namespace
+
+size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes) {
+  if (bytes <= 0 || chunk_bytes <= 0) return 16;
+  int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
+  int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
+  return size_t(nchunks * spc * 4 + 16);
+}
+
+hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
+                         hipStream_t s) {
+  if (bytes <= 0) return hipSuccess;
+  if (chunk_bytes <= 0 || chunk_bytes % 16 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
+  uint32_t* consts = device_consts();
+  if (!consts) return hipErrorOutOfMemory;
+  const int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
+  const int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
+  const int64_t last_len = bytes - (nchunks - 1) * chunk_bytes;
+  const int64_t total_segs = (nchunks - 1) * spc + (last_len + kSegBytes - 1) / kSegBytes;
+  int64_t blocks = (total_segs + 3) / 4;
+  if (blocks > 256 * 6) blocks = 256 * 6;
+  auto* seg = static_cast<uint32_t*>(workspace);
+  crc32c_segments_kernel<<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(static_cast<const uint8_t*>(src), bytes,
+                                                                      chunk_bytes, spc, total_segs, consts, seg);
+  crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, chunk_bytes, spc, consts, out);
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace dissem

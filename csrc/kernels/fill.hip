@@ -1,0 +1,72 @@
+// Random layer payloads (BASELINE: "synthetic dummy-layer payloads of the
+// configured LayerSize filled with random bytes"; the reference fills zeros,
+// cmd/config.go:141,161).
+//
+// Counter-based: u64 word j of the stream = splitmix64(seed + (j+1)*golden).
+// Memory-bound: each lane stores 16 B (two words) per iteration, grid-strided
+// over ~8 blocks/CU so the store stream saturates HBM.
+#include <hip/hip_runtime.h>
+
+#include "kernels/kernels.h"
+
+namespace dissem {
+namespace kern {
+
+__host__ __device__ inline uint64_t mix64(uint64_t seed, uint64_t j) {
+  uint64_t z = seed + (j + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) fill_random_kernel(ulonglong2* __restrict__ dst, int64_t nvec,
+                                                          uint64_t seed) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    ulonglong2 v;
+    v.x = mix64(seed, uint64_t(2 * i));
+    v.y = mix64(seed, uint64_t(2 * i + 1));
+    __builtin_nontemporal_store(v.x, &dst[i].x);
+    __builtin_nontemporal_store(v.y, &dst[i].y);
+  }
+}
+
+__global__ void fill_tail_kernel(uint8_t* __restrict__ dst, int64_t first, int64_t bytes, uint64_t seed) {
+  int64_t b = first + threadIdx.x;
+  if (b >= bytes) return;
+  uint64_t w = mix64(seed, uint64_t(b >> 3));
+  dst[b] = uint8_t(w >> (8 * (b & 7)));
+}
+
+hipError_t fill_random(void* dst, int64_t bytes, uint64_t seed, hipStream_t s) {
+  if (bytes <= 0) return hipSuccess;
+  if (reinterpret_cast<uintptr_t>(dst) & 15) return hipErrorInvalidValue;
+  int64_t nvec = bytes / 16;
+  if (nvec) {
+    int64_t blocks = (nvec + 255) / 256;
+    if (blocks > 2048) blocks = 2048;  // 8 per CU, grid-stride the rest
+    fill_random_kernel<<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(static_cast<ulonglong2*>(dst), nvec, seed);
+  }
+  if (bytes % 16)
+    fill_tail_kernel<<<1, 64, 0, s>>>(static_cast<uint8_t*>(dst), nvec * 16, bytes, seed);
+  return hipGetLastError();
+}
+
+void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset) {
+  // Bytes [offset, offset+bytes) of the stream (offset: any byte position).
+  auto* p = static_cast<uint8_t*>(dst);
+  for (int64_t i = 0; i < bytes;) {
+    const int64_t b = offset + i;
+    if ((b & 7) == 0 && bytes - i >= 8) {
+      uint64_t w = mix64(seed, uint64_t(b >> 3));
+      for (int k = 0; k < 8; ++k) p[i + k] = uint8_t(w >> (8 * k));
+      i += 8;
+    } else {
+      p[i] = uint8_t(mix64(seed, uint64_t(b >> 3)) >> (8 * (b & 7)));
+      ++i;
+    }
+  }
+}
+
+}  // namespace kern
+}  // namespace dissem

@@ -1,0 +1,128 @@
+// bf16 <-> OCP fp8 e4m3fn block-scaled pack/unpack (BASELINE config #5: the
+// 405B-sized run ships layers as fp8 on the wire to halve xGMI bytes).
+//
+// gfx950 converts with v_cvt_pk_fp8_f32 / v_cvt_pk_f32_fp8, which use the OCP
+// e4m3fn encoding on CDNA4 (not MI300's fnuz). One f32 scale per `block`
+// elements: scale = amax/448 over the block's finite values (1 if none), so
+// q = x * (448/amax) fits the e4m3fn range; +-inf saturate to +-448 and NaN
+// stays NaN (0x7F) - random bf16 payload bit patterns contain both.
+//
+// Each thread moves 8 elements: a 16-B bf16 load and an 8-B fp8 store (pack),
+// or the reverse (unpack). A block of `block` elements is handled by
+// block/8 adjacent lanes that reduce the amax with cross-lane shuffles.
+#include <hip/hip_runtime.h>
+
+#include "kernels/kernels.h"
+
+namespace dissem {
+namespace kern {
+
+namespace {
+
+__device__ inline float bf16_to_f32(uint16_t b) { return __uint_as_float(uint32_t(b) << 16); }
+
+__device__ inline uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+__device__ inline bool finite(float x) { return (__float_as_uint(x) & 0x7F800000u) != 0x7F800000u; }
+
+template <int LANES>  // lanes per scale block (block / 8)
+__global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__ in, int64_t nthreads,
+                                                       uint2* __restrict__ out, float* __restrict__ scales) {
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool active = t < nthreads;
+  uint4 v = active ? in[t] : make_uint4(0, 0, 0, 0);
+  float x[8];
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x[2 * i] = bf16_to_f32(uint16_t(w[i] & 0xFFFF));
+    x[2 * i + 1] = bf16_to_f32(uint16_t(w[i] >> 16));
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (finite(x[i])) amax = fmaxf(amax, fabsf(x[i]));
+#pragma unroll
+  for (int o = LANES / 2; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  const float inv = amax > 0.f ? 448.0f / amax : 1.0f;
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    y[i] = x[i] * inv;
+    // Saturate finite and infinite values; NaN is left for the converter (-> NaN).
+    if (y[i] == y[i]) y[i] = __builtin_amdgcn_fmed3f(y[i], 448.0f, -448.0f);
+  }
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[4], y[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], hi, true);
+  if (!active) return;
+  out[t] = make_uint2(uint32_t(lo), uint32_t(hi));
+  if ((threadIdx.x % LANES) == 0) scales[t / LANES] = amax > 0.f ? amax / 448.0f : 1.0f;
+}
+
+template <int LANES>
+__global__ void __launch_bounds__(256) fp8_unpack_kernel(const uint2* __restrict__ in,
+                                                         const float* __restrict__ scales, int64_t nthreads,
+                                                         uint4* __restrict__ out) {
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= nthreads) return;
+  const uint2 q = in[t];
+  const float s = scales[t / LANES];
+  const auto f0 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.x), false);
+  const auto f1 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.x), true);
+  const auto f2 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.y), false);
+  const auto f3 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.y), true);
+  auto pk = [s](float a, float b) {
+    return uint32_t(f32_to_bf16_rne(a * s)) | (uint32_t(f32_to_bf16_rne(b * s)) << 16);
+  };
+  out[t] = make_uint4(pk(f0[0], f0[1]), pk(f1[0], f1[1]), pk(f2[0], f2[1]), pk(f3[0], f3[1]));
+}
+
+}  // namespace
+
+hipError_t fp8_pack(const uint16_t* bf16, int64_t n, uint8_t* fp8, float* scales, int block, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n % block || (reinterpret_cast<uintptr_t>(bf16) & 15) || (reinterpret_cast<uintptr_t>(fp8) & 7))
+    return hipErrorInvalidValue;
+  const int64_t nt = n / 8;
+  const unsigned grid = unsigned((nt + 255) / 256);
+  auto* in = reinterpret_cast<const uint4*>(bf16);
+  auto* out = reinterpret_cast<uint2*>(fp8);
+  switch (block) {
+    case 32: fp8_pack_kernel<4><<<grid, 256, 0, s>>>(in, nt, out, scales); break;
+    case 64: fp8_pack_kernel<8><<<grid, 256, 0, s>>>(in, nt, out, scales); break;
+    case 128: fp8_pack_kernel<16><<<grid, 256, 0, s>>>(in, nt, out, scales); break;
+    case 256: fp8_pack_kernel<32><<<grid, 256, 0, s>>>(in, nt, out, scales); break;
+    case 512: fp8_pack_kernel<64><<<grid, 256, 0, s>>>(in, nt, out, scales); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t fp8_unpack(const uint8_t* fp8, const float* scales, int64_t n, uint16_t* bf16, int block, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n % block || (reinterpret_cast<uintptr_t>(bf16) & 15) || (reinterpret_cast<uintptr_t>(fp8) & 7))
+    return hipErrorInvalidValue;
+  const int64_t nt = n / 8;
+  const unsigned grid = unsigned((nt + 255) / 256);
+  auto* in = reinterpret_cast<const uint2*>(fp8);
+  auto* out = reinterpret_cast<uint4*>(bf16);
+  switch (block) {
+    case 32: fp8_unpack_kernel<4><<<grid, 256, 0, s>>>(in, scales, nt, out); break;
+    case 64: fp8_unpack_kernel<8><<<grid, 256, 0, s>>>(in, scales, nt, out); break;
+    case 128: fp8_unpack_kernel<16><<<grid, 256, 0, s>>>(in, scales, nt, out); break;
+    case 256: fp8_unpack_kernel<32><<<grid, 256, 0, s>>>(in, scales, nt, out); break;
+    case 512: fp8_unpack_kernel<64><<<grid, 256, 0, s>>>(in, scales, nt, out); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace dissem

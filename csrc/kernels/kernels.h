@@ -1,0 +1,31 @@
+// Launchers for the gfx950 kernels. Callable from host C++ (g++ objects); the
+// kernels themselves are in csrc/kernels/*.hip, compiled for gfx950 only.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace dissem {
+namespace kern {
+
+// ---- fill.hip: counter-based random bytes (splitmix64 of (seed, u64 index)),
+// 16 B per lane stores; byte-identical to kern::fill_random_host.
+hipError_t fill_random(void* dst, int64_t bytes, uint64_t seed, hipStream_t s);
+void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset = 0);
+
+// ---- crc32c.hip: CRC32C of every `chunk_bytes` chunk of [src, src+bytes).
+// out[c] (device or host-mapped memory) receives the standard CRC32C of chunk c.
+// `workspace` must hold crc32c_workspace_bytes(bytes, chunk_bytes) bytes of
+// device memory. chunk_bytes must be a multiple of 16 and src 16-B aligned.
+size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes);
+hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
+                         hipStream_t s);
+
+// ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements
+// (scale = amax/448; non-finite inputs: +-inf saturate, NaN stays NaN), and back.
+hipError_t fp8_pack(const uint16_t* bf16, int64_t n, uint8_t* fp8, float* scales, int block, hipStream_t s);
+hipError_t fp8_unpack(const uint8_t* fp8, const float* scales, int64_t n, uint16_t* bf16, int block, hipStream_t s);
+
+}  // namespace kern
+}  // namespace dissem

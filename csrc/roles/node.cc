@@ -28,6 +28,7 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
   if (cfg_.id != cfg_.leader) add_node(cfg_.leader);  // node.go:58-60
   if (is_leader_) status_[cfg_.id] = store_.inventory();  // node.go:252-257
   e_->bind(this);
+  if (is_leader_ && e_->planned()) manifests_ = e_->manifest();
   if (e_->target() == Location::Inmem) {
     // TCP payload bytes land directly in this node's store slot.
     t_->set_landing([this](const Message& h) -> uint8_t* {
@@ -95,6 +96,7 @@ void Node::announce() {
   Message m;
   m.type = MsgType::Announce;
   m.layers = store_.inventory();
+  if (e_->planned()) m.manifest = e_->manifest();
   NodeID hop = next_hop(cfg_.leader);
   if (!send_msg(hop, m)) throw std::runtime_error("announce failed");
 }
@@ -327,6 +329,14 @@ void Node::on_announce(const MessagePtr& m) {
     status_[m->src] = m->layers;
     add_node(m->src);
   }
+  for (auto& kv : m->manifest) {
+    auto it = manifests_.find(kv.first);
+    if (it == manifests_.end()) {
+      manifests_[kv.first] = kv.second;
+    } else if (it->second.chunk_bytes == kv.second.chunk_bytes && it->second.crc != kv.second.crc) {
+      log::error(int64_t(cfg_.id)).u("layer", kv.first).u("from", m->src).msg("conflicting CRC manifest for layer");
+    }
+  }
   if (started_) return;
   for (auto& kv : assignment_)
     if (!status_.count(kv.first)) return;
@@ -354,6 +364,7 @@ void Node::start_distribution() {
     case 3: schedule_mode3(); break;
     default: log::error(int64_t(cfg_.id)).msg("unknown mode");
   }
+  flush_batch();
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     stats_.plan_ms = double(log::now_us() - t0) / 1e3;
@@ -434,6 +445,60 @@ void Node::on_ack(const MessagePtr& m) {
   if (m->src != job.sender)
     while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
     }
+  flush_batch();
+}
+
+void Node::add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase) {
+  XferJob j;
+  j.src = src;
+  j.dst = dst;
+  j.layer = layer;
+  j.total = layer_size(layer);
+  j.offset = offset;
+  j.size = size < 0 ? j.total - offset : size;
+  auto it = manifests_.find(layer);
+  j.chunk_bytes = e_->chunk_bytes();
+  if (it != manifests_.end() && it->second.chunk_bytes > 0) {
+    j.chunk_bytes = it->second.chunk_bytes;
+    int64_t first = j.offset / j.chunk_bytes;
+    int64_t last = (j.offset + j.size + j.chunk_bytes - 1) / j.chunk_bytes;
+    for (int64_t c = first; c < last && c < int64_t(it->second.crc.size()); ++c) j.crc.push_back(it->second.crc[size_t(c)]);
+  }
+  pending_jobs_.push_back({j, phase});
+}
+
+void Node::flush_batch() {
+  // Assign global sequence numbers: by phase (relay hops after the hops that
+  // feed them), then round-robin over (src, dst) pairs so that consecutive
+  // sequence numbers spread over distinct xGMI links.
+  if (pending_jobs_.empty()) return;
+  std::map<int, std::map<std::pair<NodeID, NodeID>, std::vector<XferJob>>> by_phase;
+  for (auto& pj : pending_jobs_) by_phase[pj.phase][{pj.job.src, pj.job.dst}].push_back(pj.job);
+  pending_jobs_.clear();
+  std::map<NodeID, Message> per_rank;
+  for (auto& ph : by_phase) {
+    for (size_t round = 0;; ++round) {
+      bool any = false;
+      for (auto& pr : ph.second) {
+        if (round >= pr.second.size()) continue;
+        any = true;
+        XferJob j = pr.second[round];
+        j.seq = next_seq_++;
+        per_rank[j.src].jobs.push_back(j);
+        if (j.dst != j.src) per_rank[j.dst].jobs.push_back(j);
+      }
+      if (!any) break;
+    }
+  }
+  const uint64_t batch = next_batch_++;
+  int64_t njobs = 0;
+  for (auto& kv : per_rank) {
+    kv.second.type = MsgType::XferBatch;
+    kv.second.batch = batch;
+    njobs += int64_t(kv.second.jobs.size());
+    send_msg(kv.first, kv.second);
+  }
+  log::debug(int64_t(cfg_.id)).u("batch", batch).i("job_copies", njobs).msg("dispatched transfer batch");
 }
 
 void Node::retransmit(LayerID layer, NodeID owner, NodeID dest) {
@@ -441,6 +506,10 @@ void Node::retransmit(LayerID layer, NodeID owner, NodeID dest) {
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     stats_.jobs_dispatched++;
+  }
+  if (e_->planned()) {
+    add_job(owner, dest, layer, 0, -1);
+    return;
   }
   if (owner == cfg_.id) {
     LayerSrc src;
@@ -470,7 +539,8 @@ void Node::schedule_mode0() {
     std::vector<NodeID> remote;
     for (NodeID d : kv.second) {
       if (d == cfg_.id) {
-        send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
+        if (e_->planned()) add_job(d, d, kv.first, 0, -1);
+        else send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
       } else {
         remote.push_back(d);
       }
@@ -479,7 +549,28 @@ void Node::schedule_mode0() {
       std::lock_guard<std::mutex> lk(sig_mu_);
       stats_.jobs_dispatched += int64_t(kv.second.size());
     }
-    if (remote.size() >= 2 && e_->supports_broadcast() && src.meta.location != Location::Client) {
+    if (e_->planned()) {
+      const int64_t total = src.data_size;
+      const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1);
+      if (cfg_.relay && remote.size() >= 2 && total >= int64_t(remote.size()) * cb) {
+        // Bandwidth-optimal broadcast on a fully connected xGMI mesh: scatter
+        // 1/k of the layer to each of k dests, then every dest relays its share
+        // to the other k-1 (per-link load 2/k of the layer instead of 1).
+        const int64_t nchunks = (total + cb - 1) / cb;
+        const int64_t k = int64_t(remote.size());
+        int64_t off = 0;
+        for (int64_t i = 0; i < k; ++i) {
+          int64_t cnt = nchunks / k + (i < nchunks % k ? 1 : 0);
+          int64_t len = std::min(total - off, cnt * cb);
+          add_job(cfg_.id, remote[size_t(i)], kv.first, off, len, 0);
+          for (int64_t j = 0; j < k; ++j)
+            if (j != i) add_job(remote[size_t(i)], remote[size_t(j)], kv.first, off, len, 1);
+          off += len;
+        }
+      } else {
+        for (NodeID d : remote) add_job(cfg_.id, d, kv.first, 0, -1);
+      }
+    } else if (remote.size() >= 2 && e_->supports_broadcast() && src.meta.location != Location::Client) {
       e_->broadcast_layer(kv.first, src.data_size, remote);
     } else {
       for (NodeID d : remote) send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
@@ -731,7 +822,8 @@ void Node::schedule_mode3() {
       std::lock_guard<std::mutex> lk(sig_mu_);
       stats_.jobs_dispatched++;
     }
-    send_msg(sj.dest, f);
+    if (e_->planned()) add_job(sj.dest, sj.dest, sj.layer, 0, sj.size);
+    else send_msg(sj.dest, f);
   }
   if (demands.empty()) {
     log::info(int64_t(cfg_.id)).msg("No jobs to assign other than self-assignment");
@@ -769,7 +861,8 @@ void Node::schedule_mode3() {
       std::lock_guard<std::mutex> lk(sig_mu_);
       stats_.jobs_dispatched++;
     }
-    send_msg(j.sender, f);
+    if (e_->planned()) add_job(j.sender, j.dest, j.layer, j.offset, j.size);
+    else send_msg(j.sender, f);
   }
 }
 

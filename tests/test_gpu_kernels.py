@@ -1,0 +1,101 @@
+"""gfx950 kernel numerics vs host / PyTorch fp32 references."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev_bytes(n):
+    return torch.empty(n, dtype=torch.uint8, device="cuda")
+
+
+@pytest.mark.parametrize("n", [16, 1000, (1 << 20) + 7, 64 << 20])
+def test_fill_random_matches_host(gpu, n):
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 99)
+    torch.cuda.synchronize()
+    assert t.cpu().numpy().tobytes() == gpu.fill_random_host(n, 99)
+
+
+@pytest.mark.parametrize(
+    "n,chunk",
+    [
+        (64 << 10, 64 << 10),
+        ((1 << 20) + 16, 1 << 20),  # tail chunk of 16 bytes
+        ((3 << 20) + 5, 1 << 20),  # byte tail (not a multiple of 16)
+        (5 << 20, (1 << 20) + 4096),  # chunk not a multiple of the 64 KiB segment
+        (7 << 20, 48 << 10),  # chunks smaller than a segment
+        (64 << 20, 64 << 20),
+    ],
+)
+def test_crc32c_chunks_match_host(gpu, n, chunk):
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 7 + n)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    got = gpu.crc32c_chunks(t.data_ptr(), n, chunk)
+    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
+    assert got == want
+
+
+def test_crc32c_detects_single_bit_flip(gpu):
+    n = 4 << 20
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 5)
+    a = gpu.crc32c_chunks(t.data_ptr(), n, 1 << 20)
+    t[3 * (1 << 20) + 12345] ^= 1
+    b = gpu.crc32c_chunks(t.data_ptr(), n, 1 << 20)
+    assert a[:3] == b[:3] and a[3] != b[3]
+
+
+def _fp8_reference(x_bf16: torch.Tensor, block: int):
+    """fp32 reference of the pack: per-block amax over finite values, scale = amax/448."""
+    x = x_bf16.float().view(-1, block)
+    fin = torch.isfinite(x)
+    amax = torch.where(fin, x.abs(), torch.zeros_like(x)).amax(dim=1)
+    inv = torch.where(amax > 0, 448.0 / amax, torch.ones_like(amax))
+    y = x * inv[:, None]
+    y = torch.where(torch.isnan(y), y, y.clamp(-448.0, 448.0))
+    q = y.to(torch.float8_e4m3fn)
+    scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    return q.view(torch.uint8).reshape(-1), scale
+
+
+@pytest.mark.parametrize("block", [32, 128, 512])
+def test_fp8_pack_matches_torch(gpu, block):
+    n = 1 << 20
+    x = (torch.randn(n, device="cuda") * 3).to(torch.bfloat16)
+    q = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.empty(n // block, dtype=torch.float32, device="cuda")
+    gpu.fp8_pack(x.data_ptr(), n, q.data_ptr(), s.data_ptr(), block)
+    torch.cuda.synchronize()
+    qr, sr = _fp8_reference(x.cpu(), block)
+    torch.testing.assert_close(s.cpu(), sr, rtol=0, atol=0)
+    mism = (q.cpu() != qr).sum().item()
+    assert mism == 0, f"{mism} fp8 codes differ"
+
+
+def test_fp8_roundtrip_random_bit_patterns(gpu):
+    # Random payload bytes reinterpreted as bf16 include NaN/Inf: NaN stays NaN, +-inf saturate.
+    n = 1 << 20
+    raw = _dev_bytes(2 * n)
+    gpu.fill_random(raw.data_ptr(), 2 * n, 3)
+    x = raw.view(torch.bfloat16)
+    q = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s = torch.empty(n // 128, dtype=torch.float32, device="cuda")
+    y = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    gpu.fp8_pack(x.data_ptr(), n, q.data_ptr(), s.data_ptr(), 128)
+    gpu.fp8_unpack(q.data_ptr(), s.data_ptr(), n, y.data_ptr(), 128)
+    torch.cuda.synchronize()
+    xf, yf = x.float().cpu(), y.float().cpu()
+    assert torch.equal(torch.isnan(xf), torch.isnan(yf))
+    fin = torch.isfinite(xf)
+    blk_amax = torch.where(fin, xf.abs(), torch.zeros_like(xf)).view(-1, 128).amax(1)
+    tol = (blk_amax / 448.0 * 0.07 + 1e-30).repeat_interleave(128)  # e4m3: 3 mantissa bits + bf16 rounding
+    err = (yf - xf).abs()
+    ok = (err <= tol + xf.abs() * 0.0625) | ~fin
+    assert ok.all()
+    inf = torch.isinf(xf)
+    assert torch.equal(yf[inf].sign(), xf[inf].sign())
