@@ -31,7 +31,7 @@ LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -lpt
 
 CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/transport/inproc.cc \
              csrc/transport/tcp.cc csrc/store/store.cc csrc/sched/maxflow.cc csrc/roles/node.cc \
-             csrc/engine/host_engine.cc
+             csrc/engine/host_engine.cc csrc/engine/planned_engine.cc csrc/engine/sim_backend.cc
 BIND_SRC  := csrc/bindings.cc
 GPU_SRC   := $(wildcard csrc/gpu/*.cc)
 HIP_SRC   := $(wildcard csrc/kernels/*.hip)

@@ -6,9 +6,11 @@
 
 #include <cstring>
 
+#include "core/crc32c.h"
 #include "core/log.h"
 #include "core/wire.h"
 #include "engine/engine.h"
+#include "engine/planned_engine.h"
 #include "gpu/gpu_api.h"
 #include "roles/node.h"
 #include "sched/maxflow.h"
@@ -222,6 +224,69 @@ PYBIND11_MODULE(_core, m) {
         e.shutdown();
       });
   m.def("host_engine", &make_host_engine);
+
+  py::class_<CrcManifest>(m, "CrcManifest")
+      .def(py::init<>())
+      .def(py::init([](int64_t cb, std::vector<uint32_t> crc) { return CrcManifest{cb, std::move(crc)}; }))
+      .def_readwrite("chunk_bytes", &CrcManifest::chunk_bytes)
+      .def_readwrite("crc", &CrcManifest::crc);
+  py::class_<PlannedConfig>(m, "PlannedConfig")
+      .def(py::init<>())
+      .def_readwrite("rank", &PlannedConfig::rank)
+      .def_readwrite("world", &PlannedConfig::world)
+      .def_readwrite("rank_nodes", &PlannedConfig::rank_nodes)
+      .def_readwrite("chunk_bytes", &PlannedConfig::chunk_bytes)
+      .def_readwrite("verify", &PlannedConfig::verify)
+      .def_readwrite("poison", &PlannedConfig::poison)
+      .def_readwrite("max_inflight_groups", &PlannedConfig::max_inflight_groups)
+      .def_readwrite("group_peers", &PlannedConfig::group_peers);
+  py::class_<PlannedStats>(m, "PlannedStats")
+      .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
+      .def_readonly("bytes_recv", &PlannedStats::bytes_recv)
+      .def_readonly("bytes_staged", &PlannedStats::bytes_staged)
+      .def_readonly("bytes_verified", &PlannedStats::bytes_verified)
+      .def_readonly("groups", &PlannedStats::groups)
+      .def_readonly("pieces", &PlannedStats::pieces)
+      .def_readonly("verify_failures", &PlannedStats::verify_failures)
+      .def_readonly("unverified_pieces", &PlannedStats::unverified_pieces)
+      .def_readonly("issue_ms", &PlannedStats::issue_ms);
+  py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
+      .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
+        return reinterpret_cast<uint64_t>(e.provision(l, n));
+      })
+      .def("device_ptr", [](PlannedEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.device_ptr(l)); })
+      .def("set_manifest", &PlannedEngine::set_manifest)
+      .def("set_seeded", &PlannedEngine::set_seeded)
+      .def("reset_session", [](PlannedEngine& e) {
+        py::gil_scoped_release nogil;
+        e.reset_session();
+      })
+      .def("quiesce", [](PlannedEngine& e) {
+        py::gil_scoped_release nogil;
+        e.quiesce();
+      })
+      .def("stats", &PlannedEngine::stats)
+      .def("error", &PlannedEngine::error)
+      .def_property_readonly("backend", [](PlannedEngine& e) { return e.backend()->name(); });
+  // Simulated fabric (CPU): host "device" memory, RCCL P2P matching semantics between
+  // in-process ranks that share `comm_key`.
+  m.def("sim_engine", [](const PlannedConfig& cfg, const std::string& comm_key) {
+    return std::make_shared<PlannedEngine>(cfg, make_sim_backend(comm_key, cfg.rank, cfg.world));
+  });
+  m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
+  m.def("sim_read", [](uint64_t ptr, int64_t n) {
+    return py::bytes(reinterpret_cast<const char*>(ptr), size_t(n));
+  });
+  m.def("sim_write", [](uint64_t ptr, py::bytes data) {
+    std::string s(data);
+    memcpy(reinterpret_cast<void*>(ptr), s.data(), s.size());
+  });
+  m.def("host_crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk) {
+    std::vector<uint32_t> out;
+    for (int64_t off = 0; off < n; off += chunk)
+      out.push_back(crc32c(reinterpret_cast<const void*>(ptr + uint64_t(off)), size_t(std::min(chunk, n - off))));
+    return out;
+  });
 
   // ---- roles
   py::class_<NodeConfig>(m, "NodeConfig")

@@ -1,0 +1,548 @@
+// Planned data engine (see planned_engine.h).
+//
+// Deadlock freedom. Every piece p has a global key k(p) = (batch, piece index
+// within its job, job sequence number), known identically to its sender and
+// receiver. Each rank posts its pieces in increasing key order, cut into
+// consecutive groups on one ordered comm queue. A group finishes once every one
+// of its pieces is posted by the partner rank. Suppose ranks were stuck: take
+// the unfinished piece with the smallest key k*. Its partner has already
+// finished every piece it owns with a key < k* (minimality), so it reaches k*
+// in its own order and posts it, and so does the owner of k* - a contradiction.
+// Hence no deadlock for any interleaving of batches, including mode 2's dynamic
+// dispatch. Host-side waits precede a post only for data that no earlier piece
+// can produce, which the leader never schedules. tests/test_planned_sim.py
+// checks this on the simulated fabric for every mode at up to 8 ranks.
+#include "engine/planned_engine.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <set>
+
+#include "core/log.h"
+#include "roles/node.h"
+
+namespace dissem {
+
+PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> backend)
+    : cfg_(cfg), backend_(std::move(backend)) {
+  if (cfg_.world < 1 || cfg_.rank < 0 || cfg_.rank >= cfg_.world) throw std::runtime_error("bad rank/world");
+  if (cfg_.rank_nodes.empty())
+    for (int r = 0; r < cfg_.world; ++r) cfg_.rank_nodes.push_back(NodeID(r));
+  if (int(cfg_.rank_nodes.size()) != cfg_.world) throw std::runtime_error("rank_nodes size != world");
+  if (cfg_.chunk_bytes <= 0 || cfg_.chunk_bytes % 4096)
+    throw std::runtime_error("chunk_bytes must be a positive multiple of 4 KiB");
+  if (cfg_.group_peers < 1) cfg_.group_peers = 1;
+  for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
+  self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
+  th_ = std::thread([this] { run(); });
+}
+
+PlannedEngine::~PlannedEngine() { shutdown(); }
+
+void PlannedEngine::shutdown() {
+  if (stopped_.exchange(true)) return;
+  stop_req_ = true;
+  req_cv_.notify_all();
+  if (th_.joinable()) th_.join();
+  idle_cv_.notify_all();
+  backend_->sync_all();
+  for (auto& kv : layers_)
+    if (kv.second.dev) backend_->free(kv.second.dev);
+  layers_.clear();
+  backend_->destroy(failed_.load());
+}
+
+int PlannedEngine::rank_of(NodeID n) const {
+  auto it = node_rank_.find(n);
+  if (it == node_rank_.end()) throw std::runtime_error("node " + std::to_string(n) + " has no rank");
+  return it->second;
+}
+
+// --------------------------------------------------------------- setup API
+
+PlannedEngine::Layer& PlannedEngine::layer(LayerID id, int64_t size_hint) {
+  Layer& L = layers_[id];
+  if (!L.size && size_hint) L.size = size_hint;
+  int64_t n = L.size ? (L.size + cfg_.chunk_bytes - 1) / cfg_.chunk_bytes : 0;
+  if (int64_t(L.st.size()) != n) {
+    L.st.assign(size_t(n), L.seeded ? 2 : 0);
+    L.ev.assign(size_t(n), 0);
+    L.want.assign(size_t(n), 0);
+  }
+  return L;
+}
+
+uint8_t* PlannedEngine::provision(LayerID id, int64_t size) {
+  std::lock_guard<std::mutex> lk(req_mu_);  // setup runs while the issue thread is idle
+  Layer& L = layer(id, size);
+  if (L.size != size) throw std::runtime_error("layer " + std::to_string(id) + " re-provisioned with another size");
+  if (!L.dev) L.dev = backend_->alloc(size);
+  return L.dev;
+}
+
+uint8_t* PlannedEngine::device_ptr(LayerID id) {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  auto it = layers_.find(id);
+  return it == layers_.end() ? nullptr : it->second.dev;
+}
+
+void PlannedEngine::set_manifest(LayerID id, const CrcManifest& m) {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  if (m.chunk_bytes != cfg_.chunk_bytes) throw std::runtime_error("manifest chunk_bytes must equal the engine chunk");
+  layers_[id].manifest = m;
+}
+
+void PlannedEngine::set_seeded(LayerID id, bool resident) {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  Layer& L = layers_[id];
+  L.seeded = resident;
+  for (auto& s : L.st) s = resident ? 2 : 0;
+}
+
+std::map<LayerID, CrcManifest> PlannedEngine::manifest() {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  std::map<LayerID, CrcManifest> out;
+  for (auto& kv : layers_)
+    if (!kv.second.manifest.crc.empty()) out[kv.first] = kv.second.manifest;
+  return out;
+}
+
+PlannedStats PlannedEngine::stats() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  return stats_;
+}
+
+std::string PlannedEngine::error() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  return error_;
+}
+
+void PlannedEngine::fail(const std::string& what) {
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    if (error_.empty()) error_ = what;
+  }
+  failed_ = true;
+  log::error(int64_t(self_node_)).s("error", what).msg("data engine failure");
+  idle_cv_.notify_all();
+}
+
+// ------------------------------------------------------------ DataEngine
+
+bool PlannedEngine::on_message(const MessagePtr& m) {
+  if (m->type != MsgType::XferBatch) return false;
+  {
+    std::lock_guard<std::mutex> lk(req_mu_);
+    reqs_.push_back(Req{Req::Batch, m->jobs, 0, 0, 0});
+    busy_ = true;
+  }
+  req_cv_.notify_all();
+  return true;
+}
+
+void PlannedEngine::send_range(NodeID dest, LayerID layer_id, int64_t, int64_t, int64_t, int64_t) {
+  log::error(int64_t(self_node_)).u("layer", layer_id).u("dest", dest)
+      .msg("planned engine: sends are scheduled by the leader's XferBatch, not pushed");
+}
+
+void PlannedEngine::load_range(LayerID layer_id, int64_t offset, int64_t size, int64_t, int64_t) {
+  {
+    std::lock_guard<std::mutex> lk(req_mu_);
+    reqs_.push_back(Req{Req::Load, {}, layer_id, offset, size});
+    busy_ = true;
+  }
+  req_cv_.notify_all();
+}
+
+void PlannedEngine::quiesce() {
+  std::unique_lock<std::mutex> lk(req_mu_);
+  // Bounded: a transfer whose peer died must not hang the caller forever.
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+  bool ok = idle_cv_.wait_until(lk, deadline, [&] {
+    return (reqs_.empty() && !busy_) || failed_.load() || stopped_.load();
+  });
+  if (!ok) log::error(int64_t(self_node_)).msg("quiesce timed out: data plane still busy");
+}
+
+void PlannedEngine::reset_session() {
+  quiesce();
+  uint64_t want;
+  {
+    std::lock_guard<std::mutex> lk(req_mu_);
+    want = resets_done_ + 1;
+    reqs_.push_back(Req{Req::Reset, {}, 0, 0, 0});
+    busy_ = true;
+  }
+  req_cv_.notify_all();
+  {
+    std::unique_lock<std::mutex> lk(req_mu_);
+    idle_cv_.wait(lk, [&] { return resets_done_ >= want || failed_.load() || stopped_.load(); });
+  }
+  if (failed_) throw std::runtime_error("data engine failed: " + error());
+}
+
+// ------------------------------------------------------------ issue thread
+
+uint32_t PlannedEngine::crc_slot() {
+  uint32_t s = crc_next_;
+  crc_next_ = (crc_next_ + 1) % kCrcSlots;
+  return s;
+}
+
+void PlannedEngine::landed(const Piece& p) {
+  if (!node_) return;
+  auto m = std::make_shared<Message>();
+  m->type = MsgType::Landed;
+  m->src = p.src_node;
+  m->layer = p.layer;
+  m->offset = p.off;
+  m->data_size = p.len;
+  m->total_size = p.total;
+  node_->inject(m);
+}
+
+void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
+  if (!L.host) {
+    LayerSrc src;
+    if (!node_ || !node_->store().get(id, &src) || !src.host)
+      throw std::runtime_error("layer " + std::to_string(id) + " has no host source to stage");
+    L.host = src.host->ptr + src.offset;
+  }
+  const int64_t off = c * cfg_.chunk_bytes;
+  const int64_t len = std::min(cfg_.chunk_bytes, L.size - off);
+  if (!L.dev) L.dev = backend_->alloc(L.size);
+  Ev e = backend_->stage(L.dev + off, L.host + off, len);
+  L.st[size_t(c)] = 1;
+  L.ev[size_t(c)] = e;
+  Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
+  p.src_node = self_node_;
+  Verify v;
+  if (cfg_.verify && int64_t(L.manifest.crc.size()) > c) {
+    p.has_crc = true;
+    p.crc = L.manifest.crc[size_t(c)];
+    uint32_t slot = crc_slot();
+    v.ev = backend_->crc(L.dev + off, len, slot, e);
+    v.slots.push_back(slot);
+  } else {
+    v.ev = backend_->crc(nullptr, 0, 0, e);
+    v.slots.push_back(~0u);
+  }
+  v.pieces.push_back(p);
+  verifies_.push_back(std::move(v));
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.bytes_staged += len;
+}
+
+bool PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed) {
+  if (want_landed) L.want[size_t(c)] = 1;
+  uint8_t s = L.st[size_t(c)];
+  if (s == 2) {
+    if (want_landed) {
+      const int64_t off = c * cfg_.chunk_bytes;
+      Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, std::min(cfg_.chunk_bytes, L.size - off), L.size, c, true};
+      p.src_node = self_node_;
+      landed(p);
+      L.want[size_t(c)] = 0;
+    }
+    return true;
+  }
+  if (s == 1) return true;
+  LayerSrc src;
+  if (L.host || (node_ && node_->store().get(id, &src) && src.host)) {
+    stage_chunk(L, id, c);
+    return true;
+  }
+  return false;
+}
+
+void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
+  std::sort(jobs.begin(), jobs.end(), [](const XferJob& a, const XferJob& b) { return a.seq < b.seq; });
+  std::vector<Piece> pieces;
+  const int64_t cb = cfg_.chunk_bytes;
+  for (auto& j : jobs) {
+    Kind kind;
+    int peer;
+    if (j.src == self_node_ && j.dst == self_node_) {
+      kind = Kind::Local;
+      peer = cfg_.rank;
+    } else if (j.src == self_node_) {
+      kind = Kind::Send;
+      peer = rank_of(j.dst);
+    } else if (j.dst == self_node_) {
+      kind = Kind::Recv;
+      peer = rank_of(j.src);
+    } else {
+      continue;
+    }
+    if (j.chunk_bytes && j.chunk_bytes != cb) {
+      fail("job chunk grid " + std::to_string(j.chunk_bytes) + " != engine chunk " + std::to_string(cb));
+      return;
+    }
+    Layer& L = layer(j.layer, j.total);
+    if (L.size != j.total) {
+      fail("layer " + std::to_string(j.layer) + " size mismatch");
+      return;
+    }
+    const int64_t end = j.offset + j.size;
+    const int64_t first_chunk = j.offset / cb;
+    int64_t pidx = 0;
+    for (int64_t pos = j.offset; pos < end; ++pidx) {
+      const int64_t c = pos / cb;
+      const int64_t cend = std::min((c + 1) * cb, L.size);
+      const int64_t e = std::min(cend, end);
+      Piece p{kind, j.seq, pidx, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
+      p.src_node = j.src;
+      const int64_t ci = c - first_chunk;
+      if (p.full && ci < int64_t(j.crc.size())) {
+        p.has_crc = true;
+        p.crc = j.crc[size_t(ci)];
+      }
+      pieces.push_back(p);
+      pos = e;
+    }
+  }
+  std::stable_sort(pieces.begin(), pieces.end(), [](const Piece& a, const Piece& b) {
+    return a.pidx != b.pidx ? a.pidx < b.pidx : a.seq < b.seq;
+  });
+  for (auto& p : pieces) {
+    if (p.kind == Kind::Local) {
+      // Local promotions take no part in the P2P order: stage right away so PCIe
+      // runs ahead of the xGMI rounds that forward the same chunks.
+      Layer& L = layer(p.layer);
+      if (!ensure_chunk(L, p.layer, p.chunk, true)) fail("no source to load layer " + std::to_string(p.layer));
+      continue;
+    }
+    ops_.push_back(p);
+  }
+}
+
+bool PlannedEngine::issue_some() {
+  bool progress = false;
+  while (!ops_.empty() && int(groups_inflight_.size()) < cfg_.max_inflight_groups && !failed_) {
+    std::vector<Piece> group;
+    std::map<int, int> nsend, nrecv;
+    std::set<std::pair<LayerID, int64_t>> recv_chunks;
+    size_t take = 0;
+    for (; take < ops_.size(); ++take) {
+      Piece& p = ops_[take];
+      if (p.kind == Kind::Send) {
+        if (nsend[p.peer] >= cfg_.group_peers) break;
+        if (recv_chunks.count({p.layer, p.chunk})) break;  // forward only after its recv is posted
+        Layer& L = layer(p.layer);
+        if (!ensure_chunk(L, p.layer, p.chunk, false)) break;  // not here yet and not stageable
+        nsend[p.peer]++;
+      } else {
+        if (nrecv[p.peer] >= cfg_.group_peers) break;
+        nrecv[p.peer]++;
+        recv_chunks.insert({p.layer, p.chunk});
+      }
+      group.push_back(p);
+    }
+    if (group.empty()) break;
+    ops_.erase(ops_.begin(), ops_.begin() + int64_t(take));
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<Ev> waits;
+    std::vector<XOp> xops;
+    int64_t sent = 0, recvd = 0;
+    for (auto& p : group) {
+      Layer& L = layers_[p.layer];
+      if (!L.dev) L.dev = backend_->alloc(L.size);
+      if (p.kind == Kind::Send) {
+        if (L.st[size_t(p.chunk)] == 1 && L.ev[size_t(p.chunk)]) {
+          Ev e = L.ev[size_t(p.chunk)];
+          if (std::find(waits.begin(), waits.end(), e) == waits.end()) waits.push_back(e);
+        }
+        sent += p.len;
+      } else {
+        recvd += p.len;
+      }
+      xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len});
+    }
+    Ev g = backend_->group(xops, waits);
+    groups_inflight_.push_back(g);
+    // Receivers: chunks are valid behind `g` on the comm queue; check them on the verify queue.
+    Verify v;
+    Ev last = 0;
+    for (auto& p : group) {
+      if (p.kind != Kind::Recv) continue;
+      Layer& L = layers_[p.layer];
+      L.st[size_t(p.chunk)] = 1;
+      L.ev[size_t(p.chunk)] = 0;  // pending on the comm queue itself: later sends are ordered behind it
+      uint32_t slot = ~0u;
+      if (cfg_.verify && p.has_crc && p.full) {
+        slot = crc_slot();
+        if (last) backend_->release(last);
+        last = backend_->crc(L.dev + p.off, p.len, slot, g);
+      }
+      v.pieces.push_back(p);
+      v.slots.push_back(slot);
+    }
+    if (!v.pieces.empty()) {
+      if (!last) last = backend_->crc(nullptr, 0, 0, g);
+      v.ev = last;
+      verifies_.push_back(std::move(v));
+    } else if (last) {
+      backend_->release(last);
+    }
+    {
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.groups++;
+      stats_.pieces += int64_t(group.size());
+      stats_.bytes_sent += sent;
+      stats_.bytes_recv += recvd;
+      stats_.issue_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    progress = true;
+  }
+  return progress;
+}
+
+void PlannedEngine::poll() {
+  while (!groups_inflight_.empty()) {
+    int r = backend_->query(groups_inflight_.front());
+    if (r == 0) break;
+    if (r < 0) {
+      fail("P2P group failed: " + backend_->async_error());
+      return;
+    }
+    backend_->release(groups_inflight_.front());
+    groups_inflight_.pop_front();
+  }
+  for (auto it = verifies_.begin(); it != verifies_.end();) {
+    int r = backend_->query(it->ev);
+    if (r == 0) {
+      ++it;
+      continue;
+    }
+    if (r < 0) {
+      fail("landing failed: " + backend_->async_error());
+      return;
+    }
+    for (size_t i = 0; i < it->pieces.size(); ++i) {
+      const Piece& p = it->pieces[i];
+      Layer& L = layers_[p.layer];
+      if (it->slots[i] != ~0u) {
+        uint32_t got = backend_->crc_result(it->slots[i]);
+        if (got != p.crc) {
+          {
+            std::lock_guard<std::mutex> lk(stats_mu_);
+            stats_.verify_failures++;
+          }
+          char buf[160];
+          snprintf(buf, sizeof buf, "CRC32C mismatch layer %llu chunk %lld: got %08x want %08x",
+                   (unsigned long long)p.layer, (long long)p.chunk, got, p.crc);
+          fail(buf);
+          return;
+        }
+        std::lock_guard<std::mutex> lk(stats_mu_);
+        stats_.bytes_verified += p.len;
+      } else if (p.kind == Kind::Recv) {
+        std::lock_guard<std::mutex> lk(stats_mu_);
+        stats_.unverified_pieces++;
+      }
+      if (p.full) L.st[size_t(p.chunk)] = 2;
+      if (L.ev[size_t(p.chunk)]) {
+        backend_->release(L.ev[size_t(p.chunk)]);
+        L.ev[size_t(p.chunk)] = 0;
+      }
+      if (p.kind == Kind::Recv) {
+        landed(p);
+      } else if (L.want[size_t(p.chunk)]) {
+        landed(p);
+        L.want[size_t(p.chunk)] = 0;
+      }
+    }
+    backend_->release(it->ev);
+    it = verifies_.erase(it);
+  }
+}
+
+void PlannedEngine::take_requests(bool block) {
+  std::deque<Req> got;
+  {
+    std::unique_lock<std::mutex> lk(req_mu_);
+    if (block && reqs_.empty() && !stop_req_) {
+      busy_ = false;
+      idle_cv_.notify_all();
+      req_cv_.wait_for(lk, std::chrono::milliseconds(50), [&] { return !reqs_.empty() || stop_req_.load(); });
+    }
+    got.swap(reqs_);
+    if (!got.empty()) busy_ = true;
+  }
+  for (auto& r : got) {
+    switch (r.type) {
+      case Req::Batch:
+        add_batch(r.jobs);
+        break;
+      case Req::Load: {
+        Layer& L = layer(r.layer);
+        if (!L.size) break;
+        for (int64_t c = r.off / cfg_.chunk_bytes; c * cfg_.chunk_bytes < r.off + r.len && c < int64_t(L.st.size()); ++c)
+          if (!ensure_chunk(L, r.layer, c, true)) fail("no source to load layer " + std::to_string(r.layer));
+        break;
+      }
+      case Req::Reset: {
+        for (auto& kv : layers_) {
+          Layer& L = kv.second;
+          for (size_t c = 0; c < L.st.size(); ++c) {
+            L.st[c] = L.seeded ? 2 : 0;
+            if (L.ev[c]) backend_->release(L.ev[c]);
+            L.ev[c] = 0;
+            L.want[c] = 0;
+          }
+          L.host = nullptr;  // re-read the source from the next session's store
+          if (cfg_.poison && !L.seeded && L.dev) backend_->zero_sync(L.dev, L.size);
+        }
+        std::lock_guard<std::mutex> lk(req_mu_);
+        resets_done_++;
+        idle_cv_.notify_all();
+        break;
+      }
+      case Req::Stop:
+        break;
+    }
+  }
+}
+
+void PlannedEngine::run() {
+  try {
+    backend_->init_thread();
+    auto last_async_check = std::chrono::steady_clock::now();
+    while (!stop_req_) {
+      take_requests(idle());
+      if (stop_req_) break;
+      if (failed_) {
+        // Drop queued work; in-flight P2P ops are aborted at shutdown.
+        ops_.clear();
+        verifies_.clear();
+        groups_inflight_.clear();
+        std::lock_guard<std::mutex> lk(req_mu_);
+        busy_ = false;
+        idle_cv_.notify_all();
+        continue;
+      }
+      bool progress = issue_some();
+      poll();
+      {
+        std::lock_guard<std::mutex> lk(req_mu_);
+        busy_ = !idle() || !reqs_.empty();
+        if (!busy_) idle_cv_.notify_all();
+      }
+      auto now = std::chrono::steady_clock::now();
+      if (now - last_async_check > std::chrono::milliseconds(100)) {
+        last_async_check = now;
+        std::string e = backend_->async_error();
+        if (!e.empty()) fail("async error: " + e);
+      }
+      if (!progress && !idle()) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  } catch (const std::exception& e) {
+    fail(e.what());
+  }
+  std::lock_guard<std::mutex> lk(req_mu_);
+  busy_ = false;
+  idle_cv_.notify_all();
+}
+
+}  // namespace dissem

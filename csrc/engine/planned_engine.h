@@ -1,0 +1,160 @@
+// Planned data engine: executes the leader's sequence-numbered transfer jobs
+// (XferBatch) as grouped point-to-point rounds on a device backend.
+//
+// Execution model (replaces the reference's "goroutine + fresh TCP connection
+// per layer", transport.go:267-275):
+//  * The leader turns every scheduling decision (mode 0/1/2/3) into XferJobs
+//    with global sequence numbers and sends each rank its share.
+//  * Each job is cut into pieces on a fixed chunk grid. A rank orders its pieces
+//    by the key (batch, piece index within the job, sequence number) - a key its
+//    partner computes identically - and issues them as groups of at most one
+//    send and one recv per peer: each group is an all-to-all round that keeps
+//    every xGMI link of the GPU busy. Because every rank posts its pieces in one
+//    global key order, the schedule cannot deadlock (planned_engine.cc).
+//  * Host-tier sources are staged chunk by chunk on the copy queue; a send
+//    waits on its chunk's staging event, so PCIe staging and xGMI transfer
+//    pipeline per chunk (the reference's pipe/tee, at chunk grain).
+//  * Every landed chunk is CRC32C-checked on the verify queue against the
+//    holder's announced manifest before the node acks it.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine/backend.h"
+#include "engine/engine.h"
+
+namespace dissem {
+
+struct PlannedConfig {
+  int rank = 0;
+  int world = 1;
+  std::vector<NodeID> rank_nodes;  // rank -> node id
+  int64_t chunk_bytes = 64ll << 20;
+  bool verify = true;
+  bool poison = true;              // zero non-seeded slots between sessions
+  int max_inflight_groups = 64;
+  int group_peers = 1;             // ops per peer and direction per group
+};
+
+struct PlannedStats {
+  int64_t bytes_sent = 0, bytes_recv = 0, bytes_staged = 0, bytes_verified = 0;
+  int64_t groups = 0, pieces = 0, verify_failures = 0, unverified_pieces = 0;
+  double issue_ms = 0;  // host time spent enqueueing groups
+};
+
+class PlannedEngine : public DataEngine {
+ public:
+  PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> backend);
+  ~PlannedEngine() override;
+
+  // ---- setup (call while no session runs)
+  uint8_t* provision(LayerID layer, int64_t size);
+  uint8_t* device_ptr(LayerID layer);
+  void set_manifest(LayerID layer, const CrcManifest& m);
+  void set_seeded(LayerID layer, bool device_resident);
+  void reset_session();  // wait idle, forget landed chunks, poison non-seeded slots
+  PlannedStats stats();
+  std::string error();
+  Backend* backend() { return backend_.get(); }
+
+  // ---- DataEngine
+  std::string name() const override { return backend_->name(); }
+  Location target() const override { return Location::Device; }
+  bool planned() const override { return true; }
+  int64_t chunk_bytes() const override { return cfg_.chunk_bytes; }
+  std::map<LayerID, CrcManifest> manifest() override;
+  bool on_message(const MessagePtr& m) override;
+  void send_range(NodeID dest, LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
+  void load_range(LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
+  void quiesce() override;
+  void shutdown() override;
+  int rank_of(NodeID n) const;
+
+ private:
+  enum class Kind : uint8_t { Send, Recv, Local };
+  struct Piece {
+    Kind kind;
+    uint64_t seq;
+    int64_t pidx;  // piece index inside its job (ordering key, major)
+    int peer;      // rank
+    LayerID layer;
+    int64_t off, len, total;
+    int64_t chunk;  // grid chunk index
+    bool full;      // covers the whole grid chunk
+    bool has_crc = false;
+    uint32_t crc = 0;
+    NodeID src_node = 0;
+  };
+  struct Layer {
+    int64_t size = 0;
+    uint8_t* dev = nullptr;
+    bool seeded = false;
+    CrcManifest manifest;
+    const uint8_t* host = nullptr;   // host-tier source (set at first staging)
+    std::vector<uint8_t> st;         // per chunk: 0 absent, 1 pending, 2 resident
+    std::vector<Ev> ev;              // staging event of a pending chunk (0: pending on the comm queue)
+    std::vector<uint8_t> want;       // inject Landed when resident (assigned here)
+  };
+  struct Verify {  // landing (recv group or staging copy) awaiting its check
+    Ev ev = 0;
+    std::vector<Piece> pieces;
+    std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
+  };
+  struct Req {
+    enum Type { Batch, Load, Reset, Stop } type;
+    std::vector<XferJob> jobs;
+    LayerID layer = 0;
+    int64_t off = 0, len = 0;
+  };
+
+  void run();
+  void take_requests(bool block);
+  void add_batch(std::vector<XferJob>& jobs);
+  bool issue_some();
+  void poll();
+  bool idle() const { return ops_.empty() && verifies_.empty() && groups_inflight_.empty(); }
+  Layer& layer(LayerID id, int64_t size_hint = 0);
+  bool ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed);
+  void stage_chunk(Layer& L, LayerID id, int64_t c);
+  void landed(const Piece& p);
+  uint32_t crc_slot();
+  void fail(const std::string& what);
+
+  PlannedConfig cfg_;
+  std::unique_ptr<Backend> backend_;
+  NodeID self_node_ = 0;
+  std::map<NodeID, int> node_rank_;
+  uint32_t crc_next_ = 0;
+
+  std::mutex req_mu_;
+  std::condition_variable req_cv_, idle_cv_;
+  std::deque<Req> reqs_;
+  bool busy_ = false;
+  uint64_t resets_done_ = 0;
+
+  // issue-thread state
+  std::map<LayerID, Layer> layers_;
+  std::deque<Piece> ops_;
+  std::deque<Verify> verifies_;
+  std::deque<Ev> groups_inflight_;
+
+  std::mutex stats_mu_;
+  PlannedStats stats_;
+  std::string error_;
+  std::atomic<bool> failed_{false};
+  std::atomic<bool> stopped_{false};
+  std::atomic<bool> stop_req_{false};
+  std::thread th_;
+};
+
+constexpr uint32_t kCrcSlots = 1u << 16;
+
+}  // namespace dissem

@@ -1,0 +1,292 @@
+// Simulated device backend: host memory, in-order worker queues, and an
+// in-process fabric with RCCL point-to-point matching semantics.
+//
+// The fabric matches the i-th send from rank A to rank B with the i-th recv on
+// B from A (FIFO per directed pair, like NCCL/RCCL P2P). A group occupies its
+// rank's comm queue until every op in it has been matched and copied, so a
+// schedule that could deadlock on GPUs deadlocks here too; a bounded wait turns
+// that into a reported failure instead of a hang.
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "core/crc32c.h"
+#include "engine/backend.h"
+#include "engine/planned_engine.h"
+
+namespace dissem {
+
+namespace {
+
+struct SimEvent {
+  std::atomic<int> state{0};  // 0 pending, 1 done, -1 failed
+};
+
+struct Posted {
+  uint8_t* ptr;
+  int64_t len;
+  bool done = false;
+  bool bad = false;
+};
+
+struct Fabric {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<std::pair<int, int>, std::pair<std::deque<Posted*>, std::deque<Posted*>>> ch;  // (src,dst) -> sends, recvs
+  SimFabricStats stats;
+
+  void post(int src, int dst, bool send, Posted* op) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto& c = ch[{src, dst}];
+    (send ? c.first : c.second).push_back(op);
+    while (!c.first.empty() && !c.second.empty()) {
+      Posted* s = c.first.front();
+      Posted* r = c.second.front();
+      c.first.pop_front();
+      c.second.pop_front();
+      if (s->len != r->len) {
+        s->bad = r->bad = true;
+      } else {
+        memcpy(r->ptr, s->ptr, size_t(s->len));
+        stats.matched++;
+        stats.bytes += s->len;
+      }
+      s->done = r->done = true;
+    }
+    cv.notify_all();
+  }
+  // Returns false on timeout (deadlock) or a size mismatch.
+  bool wait_all(const std::vector<std::unique_ptr<Posted>>& ops, double timeout_s) {
+    std::unique_lock<std::mutex> lk(mu);
+    bool ok = cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] {
+      for (auto& o : ops)
+        if (!o->done) return false;
+      return true;
+    });
+    if (!ok) return false;
+    for (auto& o : ops)
+      if (o->bad) return false;
+    return true;
+  }
+};
+
+std::mutex g_fab_mu;
+std::map<std::string, std::shared_ptr<Fabric>> g_fabrics;
+
+std::shared_ptr<Fabric> fabric(const std::string& key) {
+  std::lock_guard<std::mutex> lk(g_fab_mu);
+  auto& f = g_fabrics[key];
+  if (!f) f = std::make_shared<Fabric>();
+  return f;
+}
+
+class Queue {
+ public:
+  Queue() : th_([this] { loop(); }) {}
+  ~Queue() { stop(); }
+  void push(std::function<void()> fn) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(fn));
+    }
+    cv_.notify_all();
+  }
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return q_.empty() && !running_; });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stop_) return;
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty() || stop_; });
+        if (q_.empty()) return;
+        fn = std::move(q_.front());
+        q_.pop_front();
+        running_ = true;
+      }
+      fn();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        running_ = false;
+      }
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false, running_ = false;
+  std::thread th_;
+};
+
+bool wait_event(const std::shared_ptr<SimEvent>& e, double timeout_s) {
+  auto dl = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  while (e->state.load() == 0) {
+    if (std::chrono::steady_clock::now() > dl) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  return e->state.load() > 0;
+}
+
+class SimBackend : public Backend {
+ public:
+  SimBackend(const std::string& key, int rank, int world)
+      : key_(key), rank_(rank), world_(world), fab_(fabric(key)), results_(kCrcSlots, 0) {}
+  ~SimBackend() override { destroy(false); }
+  std::string name() const override { return "sim"; }
+
+  uint8_t* alloc(int64_t n) override {
+    auto* p = new uint8_t[size_t(std::max<int64_t>(n, 1))]();
+    return p;
+  }
+  void free(uint8_t* p) override { delete[] p; }
+  void zero_sync(uint8_t* p, int64_t n) override {
+    sync_all();
+    memset(p, 0, size_t(n));
+  }
+
+  Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {
+    auto [id, ev] = make_event();
+    copy_.push([=] {
+      memcpy(dst, src, size_t(n));
+      ev->state = 1;
+    });
+    return id;
+  }
+
+  Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) override {
+    auto [id, ev] = make_event();
+    std::vector<std::shared_ptr<SimEvent>> deps;
+    for (Ev w : waits) deps.push_back(lookup(w));
+    int rank = rank_;
+    auto fab = fab_;
+    comm_.push([=] {
+      for (auto& d : deps)
+        if (!d || !wait_event(d, kTimeout)) {
+          set_error("group dependency failed");
+          ev->state = -1;
+          return;
+        }
+      std::vector<std::unique_ptr<Posted>> posted;
+      for (auto& o : ops) {
+        if (o.peer < 0 || o.peer >= world_ || o.peer == rank) {
+          set_error("bad peer");
+          ev->state = -1;
+          return;
+        }
+        posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
+        if (o.send) fab->post(rank, o.peer, true, posted.back().get());
+        else fab->post(o.peer, rank, false, posted.back().get());
+      }
+      if (!fab->wait_all(posted, kTimeout)) {
+        set_error("P2P group did not complete (deadlock or size mismatch)");
+        ev->state = -1;
+        return;
+      }
+      ev->state = 1;
+    });
+    return id;
+  }
+
+  Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
+    auto [id, ev] = make_event();
+    auto dep = lookup(after);
+    verify_.push([=] {
+      if (dep && !wait_event(dep, kTimeout)) {
+        ev->state = -1;
+        return;
+      }
+      if (n > 0) results_[slot] = crc32c(p, size_t(n));
+      ev->state = 1;
+    });
+    return id;
+  }
+
+  int query(Ev e) override {
+    auto ev = lookup(e);
+    if (!ev) return -1;
+    return ev->state.load();
+  }
+  void release(Ev e) override {
+    std::lock_guard<std::mutex> lk(ev_mu_);
+    events_.erase(e);
+  }
+  uint32_t crc_result(uint32_t slot) override { return results_[slot]; }
+  std::string async_error() override {
+    std::lock_guard<std::mutex> lk(ev_mu_);
+    return error_;
+  }
+  void sync_all() override {
+    comm_.drain();
+    copy_.drain();
+    verify_.drain();
+  }
+  void destroy(bool) override {
+    comm_.stop();
+    copy_.stop();
+    verify_.stop();
+  }
+
+ private:
+  static constexpr double kTimeout = 30.0;
+  std::pair<Ev, std::shared_ptr<SimEvent>> make_event() {
+    auto e = std::make_shared<SimEvent>();
+    std::lock_guard<std::mutex> lk(ev_mu_);
+    Ev id = ++next_;
+    events_[id] = e;
+    return {id, e};
+  }
+  std::shared_ptr<SimEvent> lookup(Ev e) {
+    if (!e) return nullptr;
+    std::lock_guard<std::mutex> lk(ev_mu_);
+    auto it = events_.find(e);
+    return it == events_.end() ? nullptr : it->second;
+  }
+  void set_error(const std::string& s) {
+    std::lock_guard<std::mutex> lk(ev_mu_);
+    if (error_.empty()) error_ = s;
+  }
+
+  std::string key_;
+  int rank_, world_;
+  std::shared_ptr<Fabric> fab_;
+  std::vector<uint32_t> results_;
+  std::mutex ev_mu_;
+  std::map<Ev, std::shared_ptr<SimEvent>> events_;
+  Ev next_ = 0;
+  std::string error_;
+  Queue comm_, copy_, verify_;
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_sim_backend(const std::string& comm_key, int rank, int world) {
+  return std::make_unique<SimBackend>(comm_key, rank, world);
+}
+
+SimFabricStats sim_fabric_stats(const std::string& comm_key) {
+  auto f = fabric(comm_key);
+  std::lock_guard<std::mutex> lk(f->mu);
+  return f->stats;
+}
+
+}  // namespace dissem

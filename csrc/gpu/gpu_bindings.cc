@@ -9,7 +9,7 @@
 
 #include "core/crc32c.h"
 #include "gpu/gpu_api.h"
-#include "gpu/gpu_engine.h"
+#include "gpu/hip_backend.h"
 #include "kernels/kernels.h"
 
 namespace py = pybind11;
@@ -169,54 +169,16 @@ void register_gpu_bindings(PyObject* module) {
           "fp8_unpack");
   }, py::arg("fp8"), py::arg("scales"), py::arg("n"), py::arg("bf16"), py::arg("block") = 128, py::arg("stream") = 0);
 
-  // ---- RCCL engine
+  // ---- RCCL engine = planned engine on the HIP backend
   m.def("nccl_unique_id", [] { return py::bytes(nccl_unique_id()); });
-  py::class_<CrcManifest>(m, "CrcManifest")
-      .def(py::init<>())
-      .def(py::init([](int64_t cb, std::vector<uint32_t> crc) { return CrcManifest{cb, std::move(crc)}; }))
-      .def_readwrite("chunk_bytes", &CrcManifest::chunk_bytes)
-      .def_readwrite("crc", &CrcManifest::crc);
-  py::class_<GpuEngineConfig>(m, "GpuEngineConfig")
-      .def(py::init<>())
-      .def_readwrite("device", &GpuEngineConfig::device)
-      .def_readwrite("rank", &GpuEngineConfig::rank)
-      .def_readwrite("world", &GpuEngineConfig::world)
-      .def_readwrite("rank_nodes", &GpuEngineConfig::rank_nodes)
-      .def_property("nccl_uid", [](const GpuEngineConfig& c) { return py::bytes(c.nccl_uid); },
-                    [](GpuEngineConfig& c, py::bytes b) { c.nccl_uid = std::string(b); })
-      .def_readwrite("chunk_bytes", &GpuEngineConfig::chunk_bytes)
-      .def_readwrite("verify", &GpuEngineConfig::verify)
-      .def_readwrite("poison", &GpuEngineConfig::poison)
-      .def_readwrite("max_inflight_groups", &GpuEngineConfig::max_inflight_groups)
-      .def_readwrite("group_peers", &GpuEngineConfig::group_peers);
-  py::class_<GpuEngineStats>(m, "GpuEngineStats")
-      .def_readonly("bytes_sent", &GpuEngineStats::bytes_sent)
-      .def_readonly("bytes_recv", &GpuEngineStats::bytes_recv)
-      .def_readonly("bytes_staged", &GpuEngineStats::bytes_staged)
-      .def_readonly("bytes_verified", &GpuEngineStats::bytes_verified)
-      .def_readonly("groups", &GpuEngineStats::groups)
-      .def_readonly("pieces", &GpuEngineStats::pieces)
-      .def_readonly("verify_failures", &GpuEngineStats::verify_failures)
-      .def_readonly("unverified_pieces", &GpuEngineStats::unverified_pieces)
-      .def_readonly("issue_ms", &GpuEngineStats::issue_ms);
-  py::class_<GpuEngine, DataEngine, std::shared_ptr<GpuEngine>>(m, "GpuEngine")
-      .def(py::init([](const GpuEngineConfig& c) {
-        py::gil_scoped_release nogil;
-        return std::make_shared<GpuEngine>(c);
-      }))
-      .def("provision", [](GpuEngine& e, LayerID l, int64_t n) { return reinterpret_cast<uint64_t>(e.provision(l, n)); })
-      .def("device_ptr", [](GpuEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.device_ptr(l)); })
-      .def("set_manifest", &GpuEngine::set_manifest)
-      .def("set_seeded", &GpuEngine::set_seeded)
-      .def("reset_session", [](GpuEngine& e) {
-        py::gil_scoped_release nogil;
-        e.reset_session();
-      })
-      .def("quiesce", [](GpuEngine& e) {
-        py::gil_scoped_release nogil;
-        e.quiesce();
-      })
-      .def("stats", &GpuEngine::stats)
-      .def("error", &GpuEngine::error)
-      .def_property_readonly("comm_stream", [](const GpuEngine& e) { return reinterpret_cast<uint64_t>(e.comm_stream()); });
+  m.def("gpu_engine", [](const PlannedConfig& cfg, int device, py::bytes uid) {
+    HipBackendConfig hc;
+    hc.device = device;
+    hc.rank = cfg.rank;
+    hc.world = cfg.world;
+    hc.nccl_uid = std::string(uid);
+    hc.max_crc_bytes = cfg.chunk_bytes;
+    py::gil_scoped_release nogil;
+    return std::make_shared<PlannedEngine>(cfg, make_hip_backend(hc));
+  }, py::arg("cfg"), py::arg("device") = 0, py::arg("nccl_uid") = py::bytes(""));
 }

@@ -1,0 +1,186 @@
+#include "gpu/hip_backend.h"
+
+#include <hip/hip_runtime_api.h>
+#include <rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "core/log.h"
+#include "kernels/kernels.h"
+
+namespace dissem {
+
+namespace {
+
+#define HIP_OK(expr)                                                                                        \
+  do {                                                                                                      \
+    hipError_t _e = (expr);                                                                                 \
+    if (_e != hipSuccess) throw std::runtime_error(std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+  } while (0)
+
+#define NCCL_OK(expr)                                                                                         \
+  do {                                                                                                        \
+    ncclResult_t _r = (expr);                                                                                 \
+    if (_r != ncclSuccess) throw std::runtime_error(std::string(#expr " failed: ") + ncclGetErrorString(_r)); \
+  } while (0)
+
+class HipBackend : public Backend {
+ public:
+  explicit HipBackend(const HipBackendConfig& cfg) : cfg_(cfg) {
+    HIP_OK(hipSetDevice(cfg_.device));
+    HIP_OK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&verify_, hipStreamNonBlocking));
+    HIP_OK(hipMalloc(&ws_, kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes)));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&crc_dev_), crc_host_, 0));
+    if (cfg_.world > 1) {
+      if (cfg_.nccl_uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("nccl_uid must be ncclUniqueId bytes");
+      ncclUniqueId id;
+      memcpy(&id, cfg_.nccl_uid.data(), sizeof id);
+      auto t0 = log::now_us();
+      NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
+      log::info(cfg_.rank).i("world", cfg_.world).f("init_ms", double(log::now_us() - t0) / 1e3)
+          .msg("rccl communicator ready");
+    }
+  }
+  ~HipBackend() override { destroy(false); }
+  std::string name() const override { return "rccl"; }
+
+  void init_thread() override { HIP_OK(hipSetDevice(cfg_.device)); }
+
+  uint8_t* alloc(int64_t n) override {
+    HIP_OK(hipSetDevice(cfg_.device));
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, size_t(std::max<int64_t>(n, 1))));
+    return static_cast<uint8_t*>(p);
+  }
+  void free(uint8_t* p) override { (void)hipFree(p); }
+  void zero_sync(uint8_t* p, int64_t n) override {
+    HIP_OK(hipMemsetAsync(p, 0, size_t(n), comm_));
+    HIP_OK(hipStreamSynchronize(comm_));
+  }
+
+  Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {
+    HIP_OK(hipMemcpyAsync(dst, src, size_t(n), hipMemcpyHostToDevice, copy_));
+    return record(copy_);
+  }
+
+  Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) override {
+    for (Ev w : waits) HIP_OK(hipStreamWaitEvent(comm_, ev(w), 0));
+    if (!ops.empty()) {
+      if (!nccl_) throw std::runtime_error("P2P group on a single-rank engine");
+      NCCL_OK(ncclGroupStart());
+      for (auto& o : ops) {
+        if (o.send) NCCL_OK(ncclSend(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
+        else NCCL_OK(ncclRecv(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
+      }
+      NCCL_OK(ncclGroupEnd());
+    }
+    return record(comm_);
+  }
+
+  Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
+    if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
+    if (n > 0) {
+      if (n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
+      HIP_OK(kern::crc32c_chunks(p, n, n, crc_dev_ + slot, ws_, verify_));
+    }
+    return record(verify_);
+  }
+
+  int query(Ev e) override {
+    hipError_t r = hipEventQuery(ev(e));
+    if (r == hipSuccess) return 1;
+    if (r == hipErrorNotReady) return 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (err_.empty()) err_ = hipGetErrorString(r);
+    return -1;
+  }
+  void release(Ev e) override {
+    if (e) pool_.push_back(ev(e));
+  }
+  uint32_t crc_result(uint32_t slot) override { return __atomic_load_n(&crc_host_[slot], __ATOMIC_ACQUIRE); }
+  std::string async_error() override {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!err_.empty()) return err_;
+    }
+    if (!nccl_) return "";
+    ncclResult_t ar = ncclSuccess;
+    if (ncclCommGetAsyncError(nccl_, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress)
+      return ncclGetErrorString(ar);
+    return "";
+  }
+  void sync_all() override {
+    (void)hipSetDevice(cfg_.device);
+    (void)hipStreamSynchronize(comm_);
+    (void)hipStreamSynchronize(copy_);
+    (void)hipStreamSynchronize(verify_);
+  }
+  void destroy(bool abort) override {
+    if (destroyed_) return;
+    destroyed_ = true;
+    (void)hipSetDevice(cfg_.device);
+    if (!abort) sync_all();
+    if (nccl_) {
+      if (abort) ncclCommAbort(nccl_);
+      else ncclCommDestroy(nccl_);
+      nccl_ = nullptr;
+    }
+    for (auto e : pool_) (void)hipEventDestroy(e);
+    pool_.clear();
+    if (ws_) (void)hipFree(ws_);
+    if (crc_host_) (void)hipHostFree(crc_host_);
+    (void)hipStreamDestroy(comm_);
+    (void)hipStreamDestroy(copy_);
+    (void)hipStreamDestroy(verify_);
+  }
+
+ private:
+  static hipEvent_t ev(Ev e) { return reinterpret_cast<hipEvent_t>(e); }
+  Ev record(hipStream_t s) {
+    hipEvent_t e;
+    if (!pool_.empty()) {
+      e = pool_.back();
+      pool_.pop_back();
+    } else {
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIP_OK(hipEventRecord(e, s));
+    return reinterpret_cast<Ev>(e);
+  }
+
+  HipBackendConfig cfg_;
+  hipStream_t comm_ = nullptr, copy_ = nullptr, verify_ = nullptr;
+  ncclComm_t nccl_ = nullptr;
+  void* ws_ = nullptr;
+  uint32_t* crc_host_ = nullptr;
+  uint32_t* crc_dev_ = nullptr;
+  std::vector<hipEvent_t> pool_;  // issue-thread only
+  std::mutex mu_;
+  std::string err_;
+  bool destroyed_ = false;
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg) { return std::make_unique<HipBackend>(cfg); }
+
+std::shared_ptr<HostBuffer> alloc_pinned(int64_t size) {
+  void* p = nullptr;
+  HIP_OK(hipHostMalloc(&p, size_t(std::max<int64_t>(size, 1)), hipHostMallocDefault));
+  return HostBuffer::wrap(static_cast<uint8_t*>(p), size,
+                          std::shared_ptr<void>(p, [](void* q) { (void)hipHostFree(q); }));
+}
+
+std::string nccl_unique_id() {
+  ncclUniqueId id;
+  NCCL_OK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof id);
+}
+
+}  // namespace dissem

@@ -1,0 +1,29 @@
+// MI355X backend of the planned engine: HBM slots (hipMalloc), RCCL grouped
+// point-to-point on one world communicator over xGMI (comm stream),
+// hipMemcpyAsync staging from pinned host memory (copy stream), and the gfx950
+// CRC32C kernel (verify stream). Three streams + PyTorch's default stream fit
+// the 4 hardware queues a process gets by default (GPU_MAX_HW_QUEUES), so no
+// two of our queues serialize behind each other.
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "engine/backend.h"
+#include "engine/planned_engine.h"
+
+namespace dissem {
+
+struct HipBackendConfig {
+  int device = 0;
+  int rank = 0;
+  int world = 1;
+  std::string nccl_uid;  // ncclUniqueId bytes (world > 1)
+  int64_t max_crc_bytes = 64ll << 20;  // largest chunk the verify workspace must hold
+};
+
+std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg);
+std::shared_ptr<HostBuffer> alloc_pinned(int64_t size);
+std::string nccl_unique_id();
+
+}  // namespace dissem

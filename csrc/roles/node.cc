@@ -49,6 +49,13 @@ Node::~Node() { stop(); }
 void Node::start() {
   if (running_.exchange(true)) return;
   loop_th_ = std::thread([this] { loop(); });
+  if (is_leader_) {
+    // A leader whose assignment names only itself gets no announce: check once at start.
+    auto m = std::make_shared<Message>();
+    m->type = MsgType::Tick;
+    m->epoch = cfg_.epoch;
+    t_->inject(m);
+  }
 }
 
 void Node::stop() {
@@ -171,6 +178,13 @@ void Node::handle(const MessagePtr& m) {
       break;
     case MsgType::Simple:
       log::info(int64_t(cfg_.id)).s("from", m->src_addr).msg(m->payload_str);
+      break;
+    case MsgType::Tick:
+      if (is_leader_ && !started_) {
+        bool all = true;
+        for (auto& kv : assignment_) all = all && status_.count(kv.first);
+        if (all && !assignment_.empty()) start_distribution();
+      }
       break;
     default:
       break;
@@ -371,10 +385,15 @@ void Node::start_distribution() {
   }
   if (!satisfied_ && assignment_satisfied()) {
     // Nothing had to move (the reference would wait forever for acks).
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      satisfied_ = true;
+      t_ready_us_ = log::now_us();
+      stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
+    }
+    log::info(int64_t(cfg_.id)).msg("timer stop: startup");
+    send_startup();
     std::lock_guard<std::mutex> lk(sig_mu_);
-    satisfied_ = true;
-    t_ready_us_ = log::now_us();
-    stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
     sig_cv_.notify_all();
   }
 }

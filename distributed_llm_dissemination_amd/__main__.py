@@ -1,0 +1,200 @@
+"""CLI with the reference's flags (cmd/main.go:15-220).
+
+    python -m distributed_llm_dissemination_amd -id 0 -f conf/config.json -m 1 [-s DIR] [-l] [-c] [-v]
+
+One process per node. With ``--engine rccl`` the processes are GPU ranks
+launched by torchrun (``-id`` defaults to the node at position RANK in the
+sorted node ids) and layers move over RCCL/xGMI into HBM; with the default
+``--engine host`` layers move over TCP into host memory, as in the reference.
+Stdout contract kept: ``launching leader...`` / ``launching receiver...`` banners
+and ``Time to deliver: <Go duration>``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import sys
+import time
+
+USAGE = "usage: -id 0 -f config.json -s . -m 2 -l -v"
+
+
+def go_duration(seconds: float) -> str:
+    """time.Duration.String() formatting (e.g. 59.87s, 1m2.5s, 150.2ms, 12µs)."""
+    ns = int(round(seconds * 1e9))
+    if ns == 0:
+        return "0s"
+    neg = ns < 0
+    ns = abs(ns)
+
+    def trim(v: float) -> str:
+        s = f"{v:.9f}".rstrip("0").rstrip(".")
+        return s
+
+    if ns < 1000:
+        out = f"{ns}ns"
+    elif ns < 1_000_000:
+        out = trim(ns / 1e3) + "µs"
+    elif ns < 1_000_000_000:
+        out = trim(ns / 1e6) + "ms"
+    else:
+        h, rem = divmod(ns, 3600 * 10**9)
+        m, rem = divmod(rem, 60 * 10**9)
+        s = trim(rem / 1e9) + "s"
+        out = (f"{h}h" if h else "") + (f"{m}m" if (h or m) else "") + s
+    return ("-" if neg else "") + out
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="distributor", add_help=True)
+    p.add_argument("-id", type=int, default=None, help="my ID")
+    p.add_argument("-f", default="", help="filename of topology JSON file")
+    p.add_argument("-s", default="", help="path of storing layers")
+    p.add_argument("-m", type=int, default=-1, help="0: naive, 1: layer retransmit, 2: pull, 3: flow")
+    p.add_argument("-l", action="store_true", help="create layer files and exit")
+    p.add_argument("-c", action="store_true", help="if the process is client")
+    p.add_argument("-v", action="store_true", help="output debug messages")
+    # extensions
+    p.add_argument("--engine", default="host", choices=["host", "rccl"])
+    p.add_argument("--chunk-mib", type=int, default=64)
+    p.add_argument("--seed", type=int, default=0, help="mode-1 owner RNG seed")
+    p.add_argument("--owner-policy", default="random", choices=["random", "balanced"])
+    p.add_argument("--pull-window", type=int, default=1)
+    p.add_argument("--no-relay", action="store_true", help="mode 0 on rccl: leader fan-out instead of relay")
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--timeout", type=float, default=3600.0)
+    p.add_argument("--json-summary", action="store_true")
+    p.add_argument("--example-config", action="store_true")
+    p.add_argument("--log-file", default="")
+    return p
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    if args.example_config:
+        from .utils.config import example_config
+
+        print(json.dumps(example_config().to_json(), indent=2))
+        return 0
+    torchrun_rank = os.environ.get("RANK") if args.engine == "rccl" else None
+    if (args.id is None and torchrun_rank is None) or (args.id is not None and args.id < 0) or not args.f:
+        print(USAGE)
+        print()
+        return 0
+
+    from . import _core
+    from .utils.config import ConfigError, load_config
+
+    _core.set_log_level(0 if args.v else 1)  # cmd/main.go:38-42
+    if args.log_file:
+        _core.set_log_file(args.log_file)
+    try:
+        cfg = load_config(args.f)
+        leader = cfg.leader()
+    except ConfigError as e:
+        print(json.dumps({"level": "error", "error": str(e), "message": "config"}), file=sys.stderr)
+        return 1
+    node_ids = sorted(n.id for n in cfg.nodes)
+    my_id = args.id if args.id is not None else node_ids[int(torchrun_rank)]
+    try:
+        me = cfg.node(my_id)
+    except ConfigError as e:
+        print(json.dumps({"level": "error", "error": str(e), "message": "node not found in config"}), file=sys.stderr)
+        return 1
+
+    if args.c:
+        return run_client(cfg, my_id)
+
+    from .parallel.runtime import Runtime
+
+    barrier = None
+    uid = None
+    device = me.device
+    if args.engine == "rccl":
+        import torch
+        import torch.distributed as dist
+
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        device = me.device if me.device is not None else local_rank
+        torch.cuda.set_device(device)
+        if world > 1:
+            dist.init_process_group("gloo")
+            box = [_core.nccl_unique_id() if dist.get_rank() == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+            barrier = dist.barrier
+    registry = cfg.registry()
+    client = cfg.client(my_id)
+    if client is not None:
+        registry[_core.CLIENT_ID] = client.addr
+    rt = Runtime(cfg, my_id, engine=args.engine, storage_path=args.s, chunk_bytes=args.chunk_mib << 20,
+                 verify=not args.no_verify, registry=registry, barrier=barrier, nccl_uid=uid, device=device)
+    if args.l:
+        print(json.dumps({"level": "info", "node": my_id, "message": "layer set up"}), file=sys.stderr)
+        rt.close()
+        return 0
+    role = "leader" if my_id == leader.id else "receiver"
+    print(f"launching {role}...\n[addr: {rt.transport.address()}, id: {my_id}, filename: {args.f}, "
+          f"storagePath: {args.s}, mode: {args.m}]", flush=True)
+    if args.m not in (0, 1, 2, 3):
+        print(json.dumps({"level": "error", "node": my_id, "error": "unknown mode", "message": f"{role} failed"}),
+              file=sys.stderr)
+        return 1
+    policy = dict(seed=args.seed, owner_policy=args.owner_policy, pull_window=args.pull_window,
+                  relay=not args.no_relay)
+    rt.prepare(args.m, **policy)
+    if barrier:
+        barrier()
+    res = rt.execute(args.timeout, announce_retry_s=30.0)
+    if role == "leader" and res.ok:
+        print(f"Time to deliver: {go_duration(res.time_to_deliver_s)}", flush=True)
+        if args.json_summary:
+            gbps = res.bytes_planned / res.time_to_deliver_s / 1e9 if res.time_to_deliver_s > 0 else 0.0
+            print(json.dumps({"time_to_full_placement_s": res.time_to_deliver_s, "aggregate_GBps": gbps,
+                              "bytes_moved": res.bytes_planned, "ranks": len(cfg.nodes), "mode": args.m,
+                              "engine": args.engine, "plan_ms": res.plan_ms}), flush=True)
+    if not res.ok:
+        print(json.dumps({"level": "error", "node": my_id, "error": res.error, "message": f"{role} failed"}),
+              file=sys.stderr)
+    if barrier:
+        barrier()
+    time.sleep(0.05)  # let startup messages flush before sockets close
+    rt.close()
+    return 0 if res.ok else 1
+
+
+def run_client(cfg, node_id: int) -> int:
+    """cmd/main.go:69-91: external client serving rate-limited in-memory layers to its node."""
+    from . import _core
+    from .parallel.runtime import layer_seed
+
+    cc = cfg.client(node_id)
+    if cc is None:
+        print(json.dumps({"level": "info", "message": "external client not found in config"}), file=sys.stderr)
+        return 1
+    node = cfg.node(node_id)
+    t = _core.tcp_transport(cc.addr or "127.0.0.1:0", {node_id: node.addr}, True)
+    layers = {
+        l: _core.LayerSrc.inmem(_core.fill_random_host(cfg.layer_size, layer_seed(0, l)), rate)
+        for l, rate in cc.layers.items()
+    }
+    client = _core.ClientNode(node_id, t, layers)
+    client.start()
+    stop = {"flag": False}
+    signal.signal(signal.SIGTERM, lambda *_: stop.update(flag=True))
+    try:
+        while not stop["flag"]:
+            time.sleep(0.2)  # select {} (serve forever)
+    except KeyboardInterrupt:
+        pass
+    client.stop()
+    t.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -71,6 +71,7 @@ class Runtime:
         device: Optional[int] = None,
         listen_addr: Optional[str] = None,
         poison: bool = True,
+        sim_key: str = "sim",
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -98,32 +99,54 @@ class Runtime:
             reg[node_id] = self.transport.address()
             self.transport.set_registry(reg)
 
-        if engine == "rccl":
-            gcfg = _core.GpuEngineConfig()
-            gcfg.device = device if device is not None else (self.me.device if self.me.device is not None else 0)
-            gcfg.rank = self.rank
-            gcfg.world = self.world
-            gcfg.rank_nodes = self.node_ids
-            if self.world > 1:
-                if nccl_uid is None:
+        if engine in ("rccl", "sim"):
+            pcfg = _core.PlannedConfig()
+            pcfg.rank = self.rank
+            pcfg.world = self.world
+            pcfg.rank_nodes = self.node_ids
+            pcfg.chunk_bytes = self.chunk_bytes
+            pcfg.verify = verify
+            pcfg.poison = poison
+            if engine == "rccl":
+                dev = device if device is not None else (self.me.device if self.me.device is not None else 0)
+                if self.world > 1 and nccl_uid is None:
                     raise ValueError("rccl engine with world > 1 needs an nccl unique id from the bootstrap")
-                gcfg.nccl_uid = nccl_uid
-            gcfg.chunk_bytes = self.chunk_bytes
-            gcfg.verify = verify
-            gcfg.poison = poison
-            _core.set_device(gcfg.device)
-            self.engine = _core.GpuEngine(gcfg)
+                _core.set_device(dev)
+                self.engine = _core.gpu_engine(pcfg, dev, nccl_uid or b"")
+            else:
+                # Simulated fabric: ranks in this process sharing `sim_key` exchange bytes
+                # with RCCL P2P matching semantics (CPU tests of the GPU schedule).
+                self.engine = _core.sim_engine(pcfg, sim_key)
         elif engine == "host":
             self.engine = None  # host engines are per session (they bind to one node)
         else:
             raise ValueError(f"unknown engine {engine}")
         self.layers = self._materialize()
 
+    # ---- "device" memory helpers: HIP kernels for rccl, host code for the simulator
+    def _dev_fill(self, ptr: int, size: int, seed: int) -> None:
+        if self.engine_kind == "rccl":
+            _core.fill_random(ptr, size, seed)
+            _core.device_synchronize()
+        else:
+            _core.sim_write(ptr, _core.fill_random_host(size, seed))
+
+    def _dev_crc(self, ptr: int, size: int) -> List[int]:
+        if self.engine_kind == "rccl":
+            return _core.crc32c_chunks(ptr, size, self.chunk_bytes)
+        return _core.host_crc32c_chunks(ptr, size, self.chunk_bytes)
+
+    def _dev_to_host(self, dst: int, src: int, size: int) -> None:
+        if self.engine_kind == "rccl":
+            _core.memcpy(dst, src, size)
+        else:
+            _core.sim_write(dst, _core.sim_read(src, size))
+
     # ------------------------------------------------------------ layers
     def _materialize(self) -> Dict[int, "_core.LayerSrc"]:
         """cmd/config.go:94-198 (CreateLayers / AddClientLayers), MI355X tiers added."""
         layers: Dict[int, _core.LayerSrc] = {}
-        gpu = self.engine_kind == "rccl"
+        gpu = self.engine is not None
         if gpu:
             # Every layer this rank may hold in HBM gets a slot up front (one arena per rank).
             want = set(self.cfg.assignment.get(self.node_id, []))
@@ -144,13 +167,12 @@ class Runtime:
                         self._gpu_manifest_from_host(l, size, seed)
                 elif st == SOURCE_DEVICE and gpu:
                     ptr = self.engine.device_ptr(l)
-                    _core.fill_random(ptr, size, seed)
-                    _core.device_synchronize()
-                    self.engine.set_manifest(l, _core.CrcManifest(self.chunk_bytes, _core.crc32c_chunks(ptr, size, self.chunk_bytes)))
+                    self._dev_fill(ptr, size, seed)
+                    self.engine.set_manifest(l, _core.CrcManifest(self.chunk_bytes, self._dev_crc(ptr, size)))
                     self.engine.set_seeded(l, True)
                     layers[l] = _core.layer_src_device(ptr, size)
                 elif gpu:
-                    buf = _core.HostBuffer.pinned(size)
+                    buf = _core.HostBuffer.pinned(size) if self.engine_kind == "rccl" else _core.HostBuffer.malloc(size)
                     self._gpu_fill_host(l, buf, size, seed)
                     layers[l] = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
                 else:
@@ -182,17 +204,15 @@ class Runtime:
     def _gpu_fill_host(self, layer: int, buf, size: int, seed: int) -> None:
         """Random payload generated on the GPU, checksummed, then copied into pinned host memory."""
         ptr = self.engine.device_ptr(layer)
-        _core.fill_random(ptr, size, seed)
-        _core.device_synchronize()
-        crc = _core.crc32c_chunks(ptr, size, self.chunk_bytes)
-        _core.memcpy(buf.ptr, ptr, size)
+        self._dev_fill(ptr, size, seed)
+        crc = self._dev_crc(ptr, size)
+        self._dev_to_host(buf.ptr, ptr, size)
         self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, crc))
 
     def _gpu_manifest_from_host(self, layer: int, size: int, seed: int) -> None:
         ptr = self.engine.device_ptr(layer)
-        _core.fill_random(ptr, size, seed)
-        _core.device_synchronize()
-        self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, _core.crc32c_chunks(ptr, size, self.chunk_bytes)))
+        self._dev_fill(ptr, size, seed)
+        self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, self._dev_crc(ptr, size)))
 
     # ---------------------------------------------------------- sessions
     def run(self, mode: int, *, timeout: float = 600.0, **policy) -> SessionResult:
@@ -234,12 +254,24 @@ class Runtime:
         node.start()
         self._node = node
 
-    def execute(self, timeout: float = 600.0) -> SessionResult:
-        """Announce, then block until Ready (leader: assignment satisfied; receiver: startup)."""
+    def execute(self, timeout: float = 600.0, announce_retry_s: float = 0.0) -> SessionResult:
+        """Announce, then block until Ready (leader: assignment satisfied; receiver: startup).
+
+        ``announce_retry_s`` retries the announce while the leader is not listening yet
+        (separately launched processes); the reference fails on the first dial error.
+        """
         node = self._node
         t0 = time.perf_counter()
         if not self.is_leader:
-            node.announce()
+            deadline = time.monotonic() + announce_retry_s
+            while True:
+                try:
+                    node.announce()
+                    break
+                except RuntimeError:
+                    if time.monotonic() >= deadline:
+                        raise
+                    time.sleep(0.1)
         ok = node.wait_ready(timeout)
         t1 = time.perf_counter()
         err = ""
@@ -274,6 +306,8 @@ class Runtime:
         """Bytes of a layer in this rank's target tier (tests / verification)."""
         if self.engine is not None:
             ptr = self.engine.device_ptr(layer)
+            if self.engine_kind == "sim":
+                return _core.sim_read(ptr, self.sizes[layer])
             buf = _core.HostBuffer.malloc(self.sizes[layer])
             _core.memcpy(buf.ptr, ptr, self.sizes[layer])
             return buf.bytes()

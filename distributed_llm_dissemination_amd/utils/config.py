@@ -165,6 +165,12 @@ def parse_config(raw: Dict[str, Any]) -> Config:
     nodes_raw = _get(raw, "Nodes")
     if not isinstance(nodes_raw, list) or not nodes_raw:
         raise ConfigError("config has no Nodes")
+    # Schema form is decided per file: nested if any node uses the nested form, or
+    # if there is no top-level LayerSize (the flat form sizes layers by it).
+    nested_file = any(
+        isinstance(nr, dict) and isinstance(_get(nr, "InitialLayers"), dict) and _is_nested(_get(nr, "InitialLayers"))
+        for nr in nodes_raw
+    ) or not layer_size
     nodes: List[NodeConf] = []
     for i, nr in enumerate(nodes_raw):
         if not isinstance(nr, dict):
@@ -177,7 +183,7 @@ def parse_config(raw: Dict[str, Any]) -> Config:
         if not isinstance(init_raw, dict):
             raise ConfigError(f"Nodes[{i}].InitialLayers must be an object")
         initial: Dict[int, Dict[int, int]] = {}
-        if _is_nested(init_raw):
+        if nested_file:
             for st, per in init_raw.items():
                 layers: Dict[int, int] = {}
                 for lid, lconf in (per or {}).items():

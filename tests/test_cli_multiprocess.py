@@ -1,0 +1,91 @@
+"""BASELINE config #1: 2-process loopback TCP on CPU, 4 layers x 1 MiB, mode 0,
+through the reference-compatible CLI (one OS process per node)."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def write_config(tmp_path, ports, layers=4, size=1 << 20, holders=None, assign=None):
+    holders = holders or {0: list(range(layers))}
+    assign = assign or {1: list(range(layers))}
+    nodes = []
+    for i, p in enumerate(ports):
+        nodes.append({
+            "Id": i, "Addr": f"127.0.0.1:{p}", "NetworkBW": 1562500000, "IsLeader": i == 0,
+            "Sources": {"2": 0},
+            "InitialLayers": {"2": {str(l): {"LayerSize": size} for l in holders.get(i, [])}},
+        })
+    cfg = {"Nodes": nodes, "Assignment": {str(k): {str(l): {} for l in v} for k, v in assign.items()}}
+    path = tmp_path / "config.json"
+    path.write_text(json.dumps(cfg))
+    return str(path)
+
+
+def run_nodes(cfg_path, ids, mode, extra=()):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    procs = [
+        subprocess.Popen([sys.executable, "-m", "distributed_llm_dissemination_amd", "-id", str(i), "-f", cfg_path,
+                          "-m", str(mode), "--json-summary", *extra],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT)
+        for i in ids
+    ]
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out, err))
+    return outs
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("mode", [0, 1])
+def test_two_process_loopback_mode(tmp_path, mode):
+    ports = free_ports(2)
+    cfg = write_config(tmp_path, ports)
+    (rc0, out0, err0), (rc1, out1, err1) = run_nodes(cfg, [0, 1], mode)
+    assert rc0 == 0, err0
+    assert rc1 == 0, err1
+    assert "launching leader..." in out0 and "launching receiver..." in out1
+    assert "Time to deliver:" in out0
+    summary = json.loads(out0.strip().splitlines()[-1])
+    assert summary["bytes_moved"] == 4 << 20 and summary["mode"] == mode
+
+
+def test_usage_without_flags():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "distributed_llm_dissemination_amd"], capture_output=True, text=True,
+                       env=env, cwd=ROOT, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("usage: -id 0 -f config.json -s . -m 2 -l -v")
+
+
+def test_go_duration_format():
+    from distributed_llm_dissemination_amd.__main__ import go_duration
+
+    assert go_duration(59.87) == "59.87s"
+    assert go_duration(0.1502) == "150.2ms"
+    assert go_duration(62.5) == "1m2.5s"
+    assert go_duration(12e-6) == "12µs"
+    assert go_duration(0) == "0s"

