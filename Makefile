@@ -57,7 +57,7 @@ $(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h) Makefile
 tools: bin/diskspeed
 
 bin/diskspeed: csrc/tools/diskspeed.cc
-	$(HIPCC) -O2 -std=c++17 -Icsrc -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
+	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Icsrc -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lpthread
 
 # ---- host-only sanitizer builds of the core
 SAN_SRC := $(CORE_SRC) csrc/tests/core_selftest.cc
