@@ -37,6 +37,9 @@ class Backend {
   virtual uint8_t* alloc(int64_t n) = 0;
   virtual void free(uint8_t* p) = 0;
   virtual void zero_sync(uint8_t* p, int64_t n) = 0;
+  // page-aligned host staging memory the copy queue can DMA from (pinned on GPUs)
+  virtual uint8_t* alloc_host(int64_t n) = 0;
+  virtual void free_host(uint8_t* p) = 0;
   // copy queue: async host -> device copy; event fires when it landed
   virtual Ev stage(uint8_t* dst, const uint8_t* src_host, int64_t n) = 0;
   // comm queue: wait for `waits`, then one grouped set of P2P sends/recvs

@@ -45,8 +45,14 @@ void PlannedEngine::shutdown() {
   stop_req_ = true;
   req_cv_.notify_all();
   if (th_.joinable()) th_.join();
+  disk_cv_.notify_all();
+  for (auto& t : readers_) t.join();
+  readers_.clear();
   idle_cv_.notify_all();
   backend_->sync_all();
+  for (auto* b : bounce_all_) backend_->free_host(b);
+  bounce_all_.clear();
+  bounce_free_.clear();
   for (auto& kv : layers_)
     if (kv.second.dev) backend_->free(kv.second.dev);
   layers_.clear();
@@ -203,16 +209,115 @@ void PlannedEngine::landed(const Piece& p) {
 }
 
 void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
-  if (!L.host) {
+  if (!L.host && L.path.empty()) {
     LayerSrc src;
-    if (!node_ || !node_->store().get(id, &src) || !src.host)
-      throw std::runtime_error("layer " + std::to_string(id) + " has no host source to stage");
-    L.host = src.host->ptr + src.offset;
+    if (!node_ || !node_->store().get(id, &src) || (!src.host && src.path.empty()))
+      throw std::runtime_error("layer " + std::to_string(id) + " has no host or disk source to stage");
+    if (src.host) {
+      L.host = src.host->ptr + src.offset;
+    } else {
+      L.path = src.path;
+      L.path_off = src.offset;
+    }
   }
+  if (L.host) {
+    stage_from(L, id, c, L.host + c * cfg_.chunk_bytes, nullptr);
+  } else {
+    submit_disk(L, id, c);
+  }
+}
+
+void PlannedEngine::submit_disk(Layer& L, LayerID id, int64_t c) {
+  if (readers_.empty()) {
+    for (int i = 0; i < std::max(1, cfg_.disk_ring); ++i) {
+      uint8_t* b = backend_->alloc_host(cfg_.chunk_bytes);
+      bounce_all_.push_back(b);
+      bounce_free_.push_back(b);
+    }
+    for (int i = 0; i < std::max(1, cfg_.disk_readers); ++i) readers_.emplace_back([this] { reader_loop(); });
+  }
+  L.st[size_t(c)] = 3;
+  DiskRead d;
+  d.layer = id;
+  d.chunk = c;
+  d.file_off = L.path_off + c * cfg_.chunk_bytes;
+  d.len = std::min(cfg_.chunk_bytes, L.size - c * cfg_.chunk_bytes);
+  d.path = L.path;
+  disk_wait_.push_back(std::move(d));
+  pump_disk();
+}
+
+void PlannedEngine::pump_disk() {
+  // Hand waiting reads to the readers while bounce buffers are free.
+  while (!disk_wait_.empty() && !bounce_free_.empty()) {
+    DiskRead d = std::move(disk_wait_.front());
+    disk_wait_.pop_front();
+    d.bounce = bounce_free_.back();
+    bounce_free_.pop_back();
+    disk_inflight_++;
+    {
+      std::lock_guard<std::mutex> lk(disk_mu_);
+      disk_todo_.push_back(std::move(d));
+    }
+    disk_cv_.notify_one();
+  }
+  // Reads that finished: DMA them into HBM from their bounce buffer.
+  std::deque<DiskRead> done;
+  {
+    std::lock_guard<std::mutex> lk(disk_mu_);
+    done.swap(disk_done_);
+  }
+  for (auto& d : done) {
+    disk_inflight_--;
+    if (!d.ok) {
+      fail("disk read failed for layer " + std::to_string(d.layer) + " chunk " + std::to_string(d.chunk));
+      continue;
+    }
+    Layer& L = layers_[d.layer];
+    stage_from(L, d.layer, d.chunk, d.bounce, d.bounce);
+  }
+}
+
+void PlannedEngine::reader_loop() {
+  std::map<std::string, int> fds;
+  for (;;) {
+    DiskRead d;
+    {
+      std::unique_lock<std::mutex> lk(disk_mu_);
+      disk_cv_.wait(lk, [&] { return !disk_todo_.empty() || stop_req_.load(); });
+      if (disk_todo_.empty()) break;
+      d = std::move(disk_todo_.front());
+      disk_todo_.pop_front();
+    }
+    int& fd = fds[d.path];
+    if (fd <= 0) {
+      fd = ::open(d.path.c_str(), O_RDONLY | O_DIRECT | O_CLOEXEC);
+      if (fd < 0) fd = ::open(d.path.c_str(), O_RDONLY | O_CLOEXEC);  // e.g. tmpfs: no O_DIRECT
+    }
+    // O_DIRECT needs 4 KiB aligned lengths; the bounce buffer holds a whole chunk.
+    const int64_t want = std::min<int64_t>(((d.len + 4095) / 4096) * 4096, cfg_.chunk_bytes);
+    int64_t got = 0;
+    while (fd >= 0 && got < d.len) {
+      ssize_t r = ::pread(fd, d.bounce + got, size_t(want - got), off_t(d.file_off + got));
+      if (r <= 0) break;
+      got += r;
+    }
+    d.ok = got >= d.len;
+    {
+      std::lock_guard<std::mutex> lk(disk_mu_);
+      disk_done_.push_back(std::move(d));
+    }
+    req_cv_.notify_all();
+  }
+  for (auto& kv : fds)
+    if (kv.second > 0) ::close(kv.second);
+}
+
+void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* src, uint8_t* bounce) {
   const int64_t off = c * cfg_.chunk_bytes;
   const int64_t len = std::min(cfg_.chunk_bytes, L.size - off);
   if (!L.dev) L.dev = backend_->alloc(L.size);
-  Ev e = backend_->stage(L.dev + off, L.host + off, len);
+  Ev e = backend_->stage(L.dev + off, src, len);
   L.st[size_t(c)] = 1;
   L.ev[size_t(c)] = e;
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
@@ -229,12 +334,13 @@ void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
     v.slots.push_back(~0u);
   }
   v.pieces.push_back(p);
+  v.bounce = bounce;
   verifies_.push_back(std::move(v));
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.bytes_staged += len;
 }
 
-bool PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed) {
+int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed) {
   if (want_landed) L.want[size_t(c)] = 1;
   uint8_t s = L.st[size_t(c)];
   if (s == 2) {
@@ -245,15 +351,16 @@ bool PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_land
       landed(p);
       L.want[size_t(c)] = 0;
     }
-    return true;
+    return 1;
   }
-  if (s == 1) return true;
+  if (s == 1) return 1;
+  if (s == 3) return 0;  // disk read in flight
   LayerSrc src;
-  if (L.host || (node_ && node_->store().get(id, &src) && src.host)) {
+  if (L.host || !L.path.empty() || (node_ && node_->store().get(id, &src) && (src.host || !src.path.empty()))) {
     stage_chunk(L, id, c);
-    return true;
+    return L.st[size_t(c)] == 1 ? 1 : 0;
   }
-  return false;
+  return -1;
 }
 
 void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
@@ -310,7 +417,7 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       // Local promotions take no part in the P2P order: stage right away so PCIe
       // runs ahead of the xGMI rounds that forward the same chunks.
       Layer& L = layer(p.layer);
-      if (!ensure_chunk(L, p.layer, p.chunk, true)) fail("no source to load layer " + std::to_string(p.layer));
+      if (ensure_chunk(L, p.layer, p.chunk, true) < 0) fail("no source to load layer " + std::to_string(p.layer));
       continue;
     }
     ops_.push_back(p);
@@ -330,7 +437,7 @@ bool PlannedEngine::issue_some() {
         if (nsend[p.peer] >= cfg_.group_peers) break;
         if (recv_chunks.count({p.layer, p.chunk})) break;  // forward only after its recv is posted
         Layer& L = layer(p.layer);
-        if (!ensure_chunk(L, p.layer, p.chunk, false)) break;  // not here yet and not stageable
+        if (ensure_chunk(L, p.layer, p.chunk, false) <= 0) break;  // still reading from disk (or no source yet)
         nsend[p.peer]++;
       } else {
         if (nrecv[p.peer] >= cfg_.group_peers) break;
@@ -454,6 +561,7 @@ void PlannedEngine::poll() {
       }
     }
     backend_->release(it->ev);
+    if (it->bounce) bounce_free_.push_back(it->bounce);
     it = verifies_.erase(it);
   }
 }
@@ -479,7 +587,7 @@ void PlannedEngine::take_requests(bool block) {
         Layer& L = layer(r.layer);
         if (!L.size) break;
         for (int64_t c = r.off / cfg_.chunk_bytes; c * cfg_.chunk_bytes < r.off + r.len && c < int64_t(L.st.size()); ++c)
-          if (!ensure_chunk(L, r.layer, c, true)) fail("no source to load layer " + std::to_string(r.layer));
+          if (ensure_chunk(L, r.layer, c, true) < 0) fail("no source to load layer " + std::to_string(r.layer));
         break;
       }
       case Req::Reset: {
@@ -522,6 +630,7 @@ void PlannedEngine::run() {
         idle_cv_.notify_all();
         continue;
       }
+      pump_disk();
       bool progress = issue_some();
       poll();
       {

@@ -42,6 +42,8 @@ struct PlannedConfig {
   bool poison = true;              // zero non-seeded slots between sessions
   int max_inflight_groups = 64;
   int group_peers = 1;             // ops per peer and direction per group
+  int disk_readers = 4;            // NVMe reader threads (O_DIRECT pread into pinned bounce buffers)
+  int disk_ring = 8;               // pinned bounce buffers of chunk_bytes each
 };
 
 struct PlannedStats {
@@ -99,7 +101,9 @@ class PlannedEngine : public DataEngine {
     bool seeded = false;
     CrcManifest manifest;
     const uint8_t* host = nullptr;   // host-tier source (set at first staging)
-    std::vector<uint8_t> st;         // per chunk: 0 absent, 1 pending, 2 resident
+    std::string path;                // disk-tier source
+    int64_t path_off = 0;
+    std::vector<uint8_t> st;         // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk
     std::vector<Ev> ev;              // staging event of a pending chunk (0: pending on the comm queue)
     std::vector<uint8_t> want;       // inject Landed when resident (assigned here)
   };
@@ -107,6 +111,14 @@ class PlannedEngine : public DataEngine {
     Ev ev = 0;
     std::vector<Piece> pieces;
     std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
+    uint8_t* bounce = nullptr;    // disk staging buffer to recycle once landed
+  };
+  struct DiskRead {  // chunk of a disk-tier layer: pread into a bounce buffer, then H2D
+    LayerID layer;
+    int64_t chunk, file_off, len;
+    std::string path;
+    uint8_t* bounce = nullptr;
+    bool ok = true;
   };
   struct Req {
     enum Type { Batch, Load, Reset, Stop } type;
@@ -120,10 +132,17 @@ class PlannedEngine : public DataEngine {
   void add_batch(std::vector<XferJob>& jobs);
   bool issue_some();
   void poll();
-  bool idle() const { return ops_.empty() && verifies_.empty() && groups_inflight_.empty(); }
+  bool idle() const {
+    return ops_.empty() && verifies_.empty() && groups_inflight_.empty() && disk_inflight_ == 0 && disk_wait_.empty();
+  }
   Layer& layer(LayerID id, int64_t size_hint = 0);
-  bool ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed);
+  // 1: resident or in flight on a device queue, 0: still reading from disk, -1: no source
+  int ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed);
   void stage_chunk(Layer& L, LayerID id, int64_t c);
+  void stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* src, uint8_t* bounce);
+  void submit_disk(Layer& L, LayerID id, int64_t c);
+  void pump_disk();
+  void reader_loop();
   void landed(const Piece& p);
   uint32_t crc_slot();
   void fail(const std::string& what);
@@ -145,6 +164,15 @@ class PlannedEngine : public DataEngine {
   std::deque<Piece> ops_;
   std::deque<Verify> verifies_;
   std::deque<Ev> groups_inflight_;
+
+  // disk tier: issue thread owns bounce_free_/disk_wait_; readers exchange via disk_mu_
+  std::vector<uint8_t*> bounce_all_, bounce_free_;
+  std::deque<DiskRead> disk_wait_;                 // waiting for a bounce buffer
+  std::mutex disk_mu_;
+  std::condition_variable disk_cv_;
+  std::deque<DiskRead> disk_todo_, disk_done_;
+  std::vector<std::thread> readers_;
+  int disk_inflight_ = 0;
 
   std::mutex stats_mu_;
   PlannedStats stats_;

@@ -159,6 +159,12 @@ class SimBackend : public Backend {
     return p;
   }
   void free(uint8_t* p) override { delete[] p; }
+  uint8_t* alloc_host(int64_t n) override {
+    void* p = nullptr;
+    if (posix_memalign(&p, 4096, size_t(std::max<int64_t>(n, 4096)))) throw std::bad_alloc();
+    return static_cast<uint8_t*>(p);
+  }
+  void free_host(uint8_t* p) override { ::free(p); }
   void zero_sync(uint8_t* p, int64_t n) override {
     sync_all();
     memset(p, 0, size_t(n));

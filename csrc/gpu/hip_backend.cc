@@ -59,6 +59,12 @@ class HipBackend : public Backend {
     return static_cast<uint8_t*>(p);
   }
   void free(uint8_t* p) override { (void)hipFree(p); }
+  uint8_t* alloc_host(int64_t n) override {
+    void* p = nullptr;
+    HIP_OK(hipHostMalloc(&p, size_t(std::max<int64_t>(n, 4096)), hipHostMallocDefault));
+    return static_cast<uint8_t*>(p);
+  }
+  void free_host(uint8_t* p) override { (void)hipHostFree(p); }
   void zero_sync(uint8_t* p, int64_t n) override {
     HIP_OK(hipMemsetAsync(p, 0, size_t(n), comm_));
     HIP_OK(hipStreamSynchronize(comm_));
