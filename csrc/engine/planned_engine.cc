@@ -14,6 +14,9 @@
 // checks this on the simulated fabric for every mode at up to 8 ranks.
 #include "engine/planned_engine.h"
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>

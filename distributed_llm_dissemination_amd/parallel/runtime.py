@@ -235,6 +235,7 @@ class Runtime:
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()
+            self._stats0 = self._engine_stats()
         nc = _core.NodeConfig()
         nc.id = self.node_id
         nc.leader = self.cfg.leader().id
@@ -291,16 +292,21 @@ class Runtime:
             error=err if err else ("" if ok else "timeout waiting for Ready()"),
         )
         if self.engine is not None and ok:
-            es = self.engine.stats()
-            res.engine_stats = {
-                k: getattr(es, k)
-                for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
-                          "verify_failures", "unverified_pieces", "issue_ms")
-            }
+            self.engine.quiesce()  # trailing verifications of chunks nobody waited for
+            now = self._engine_stats()
+            res.engine_stats = {k: now[k] - self._stats0.get(k, 0) for k in now}
         if ok:
             node.stop()
         self._last_node = node  # on failure keep it alive for inspection
         return res
+
+    def _engine_stats(self) -> Dict[str, float]:
+        es = self.engine.stats()
+        return {
+            k: getattr(es, k)
+            for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
+                      "verify_failures", "unverified_pieces", "issue_ms")
+        }
 
     def layer_bytes(self, layer: int) -> bytes:
         """Bytes of a layer in this rank's target tier (tests / verification)."""

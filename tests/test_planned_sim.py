@@ -96,3 +96,32 @@ def test_ranges_not_aligned_to_chunks_mode3():
     # Chunk grid 1 MiB, layer 2.5 MiB: pieces of partial chunks are still exact.
     cfg = make_workload(3, 3, 2 * MiB + MiB // 2, tier="host", seeding="random", copies=2, chunk_bytes=MiB)
     run_cluster(cfg, 3)
+
+
+def test_disk_tier_staging_through_bounce_ring(tmp_path):
+    """BASELINE config #4 shape on the simulator: layers on disk, staged disk ->
+    page-aligned bounce ring -> device by reader threads, then P2P + verify."""
+    cfg = make_workload(4, 6, 3 * MiB + 8192, tier="disk", seeding="random", chunk_bytes=MiB)
+    key = f"sim{next(_keys)}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+                   storage_path=str(tmp_path)) for i in range(4)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for _ in range(2):
+            for r in rts:
+                r.prepare(1)
+            res = [None] * 4
+            ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(4)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            assert all(x.ok for x in res), [x.error for x in res]
+            for i, r in enumerate(rts):
+                for l in range(6):
+                    assert r.layer_bytes(l) == _core.fill_random_host(3 * MiB + 8192, layer_seed(0, l))
+    finally:
+        for r in rts:
+            r.close()
