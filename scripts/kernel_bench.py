@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Kernel throughput on one MI355X: random fill, CRC32C verify, fp8 pack/unpack.
+
+Each kernel runs on a buffer larger than the 256 MiB Infinity Cache so the
+numbers are HBM-bound, timed with HIP events over several repetitions, and
+reported as GB/s of bytes touched (read + write) against the ~6.3 TB/s measured
+HBM copy ceiling.
+"""
+
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+from distributed_llm_dissemination_amd import _core  # noqa: E402
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+
+
+def main():
+    n = 1 << 30
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    out = {}
+    t = timed(lambda: _core.fill_random(buf.data_ptr(), n, 7))
+    out["fill_random_GBps"] = n / t / 1e9
+    chunk = 64 << 20
+    nch = n // chunk
+    ws = torch.empty(_core.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    res = torch.empty(nch, dtype=torch.int32, device="cuda")
+    t = timed(lambda: _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0))
+    out["crc32c_GBps"] = n / t / 1e9
+    # one 64 MiB chunk alone (the per-landing verify in the data engine)
+    ws1 = torch.empty(_core.crc32c_workspace_bytes(chunk, chunk), dtype=torch.uint8, device="cuda")
+    t = timed(lambda: _core.crc32c_chunks_async(buf.data_ptr(), chunk, chunk, res.data_ptr(), ws1.data_ptr(), 0), 50)
+    out["crc32c_one_64MiB_chunk_us"] = t * 1e6
+    ne = n // 2
+    x = buf.view(torch.bfloat16)[:ne]
+    q = torch.empty(ne, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(ne // 128, dtype=torch.float32, device="cuda")
+    y = torch.empty(ne, dtype=torch.bfloat16, device="cuda")
+    t = timed(lambda: _core.fp8_pack(x.data_ptr(), ne, q.data_ptr(), sc.data_ptr(), 128))
+    out["fp8_pack_GBps"] = (2 * ne + ne + ne // 32) / t / 1e9
+    t = timed(lambda: _core.fp8_unpack(q.data_ptr(), sc.data_ptr(), ne, y.data_ptr(), 128))
+    out["fp8_unpack_GBps"] = (ne + ne // 32 + 2 * ne) / t / 1e9
+    t = timed(lambda: buf[: n // 2].copy_(buf[n // 2 :]))
+    out["torch_copy_GBps"] = n / t / 1e9
+    print(json.dumps({k: round(v, 2) for k, v in out.items()}))
+
+
+if __name__ == "__main__":
+    main()
