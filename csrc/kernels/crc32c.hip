@@ -29,7 +29,10 @@ namespace kern {
 
 namespace {
 
-constexpr int kSegBytes = 64 * 1024;
+// 16 KiB per wave: 16 strided words per lane. Small enough that one 64 MiB
+// landing chunk spreads over 4096 waves (16 per CU), large enough that the
+// per-wave lane-alignment multiply is amortized.
+constexpr int kSegBytes = 16 * 1024;
 constexpr int kT16 = 16 * 256;   // slice-by-16 tables
 constexpr int kA = 4 * 256;      // shift-by-1024-bytes map
 constexpr int kLanePow = 64;     // x^(8*16*m), m = 0..63
@@ -137,10 +140,13 @@ __global__ void __launch_bounds__(256) crc32c_segments_kernel(const uint8_t* __r
   }
 }
 
-// One wave per chunk: fold the chunk's segment CRCs and finalize.
+// One wave per chunk: fold the chunk's segment CRCs and finalize. `fold` holds
+// host-computed constants for full chunks: per lane x^(8*bytes after its run)
+// and the init/xorout term; only a short final chunk computes them here.
 __global__ void __launch_bounds__(64) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
                                                          int64_t chunk_bytes, int64_t spc,
                                                          const uint32_t* __restrict__ consts,
+                                                         const uint32_t* __restrict__ fold,
                                                          uint32_t* __restrict__ out) {
   __shared__ uint32_t AS[kAS];
   __shared__ uint32_t X2N[kX2N];
@@ -159,17 +165,42 @@ __global__ void __launch_bounds__(64) crc32c_fold_kernel(const uint32_t* __restr
     const int64_t len = min(int64_t(kSegBytes), chunk_len - k * kSegBytes);
     r = (len == kSegBytes ? shift_map(AS, r) : multmodp(xpow8n(X2N, uint64_t(len)), r)) ^ seg_out[c * spc + k];
   }
+  const bool full = chunk_len == chunk_bytes;
   const int64_t end_byte = min(e * kSegBytes, chunk_len);
-  if (r && e > b) r = multmodp(xpow8n(X2N, uint64_t(chunk_len - end_byte)), r);
+  if (r && e > b) r = multmodp(full ? fold[lane] : xpow8n(X2N, uint64_t(chunk_len - end_byte)), r);
   r = wave_xor(e > b ? r : 0u);
-  if (lane == 0) out[c] = r ^ multmodp(xpow8n(X2N, uint64_t(chunk_len)), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+  if (lane == 0)
+    out[c] = r ^ (full ? fold[64] : (multmodp(xpow8n(X2N, uint64_t(chunk_len)), 0xFFFFFFFFu) ^ 0xFFFFFFFFu));
 }
 
 struct DeviceConsts {
   std::mutex mu;
   std::map<int, uint32_t*> by_device;
+  std::map<std::pair<int, int64_t>, uint32_t*> fold;  // (device, chunk_bytes) -> 65 fold constants
 };
 DeviceConsts g_consts;
+
+uint32_t* fold_consts(int64_t chunk_bytes) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_consts.mu);
+  auto key = std::make_pair(dev, chunk_bytes);
+  auto it = g_consts.fold.find(key);
+  if (it != g_consts.fold.end()) return it->second;
+  const int64_t n = (chunk_bytes + kSegBytes - 1) / kSegBytes, q = (n + 63) / 64;
+  std::vector<uint32_t> h(65);
+  for (int l = 0; l < 64; ++l) {
+    int64_t e = std::min(n, int64_t(l + 1) * q);
+    int64_t end_byte = std::min(e * kSegBytes, chunk_bytes);
+    h[size_t(l)] = crc32c_xpow8n(uint64_t(chunk_bytes - end_byte));
+  }
+  h[64] = crc32c_init_term(uint64_t(chunk_bytes));
+  uint32_t* d = nullptr;
+  if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+  g_consts.fold[key] = d;
+  return d;
+}
 
 uint32_t* device_consts() {
   int dev = 0;
@@ -208,7 +239,8 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
   if (bytes <= 0) return hipSuccess;
   if (chunk_bytes <= 0 || chunk_bytes % 16 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
   uint32_t* consts = device_consts();
-  if (!consts) return hipErrorOutOfMemory;
+  uint32_t* fold = fold_consts(chunk_bytes);
+  if (!consts || !fold) return hipErrorOutOfMemory;
   const int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
   const int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
   const int64_t last_len = bytes - (nchunks - 1) * chunk_bytes;
@@ -218,7 +250,7 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
   auto* seg = static_cast<uint32_t*>(workspace);
   crc32c_segments_kernel<<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(static_cast<const uint8_t*>(src), bytes,
                                                                       chunk_bytes, spc, total_segs, consts, seg);
-  crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, chunk_bytes, spc, consts, out);
+  crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, chunk_bytes, spc, consts, fold, out);
   return hipGetLastError();
 }
 
