@@ -21,13 +21,13 @@ void Json::detach() {
 }
 
 int64_t Json::as_i64() const {
-  if (kind_ == Kind::Int) return neg_ ? -int64_t(mag_) : int64_t(mag_);
+  if (kind_ == Kind::Int) return int64_t(neg_ ? uint64_t(0) - mag_ : mag_);  // two's complement, no signed overflow
   if (kind_ == Kind::Float) return int64_t(d_);
   if (kind_ == Kind::Bool) return b_ ? 1 : 0;
   type_error("a number");
 }
 uint64_t Json::as_u64() const {
-  if (kind_ == Kind::Int) return neg_ ? uint64_t(-int64_t(mag_)) : mag_;
+  if (kind_ == Kind::Int) return neg_ ? uint64_t(0) - mag_ : mag_;
   if (kind_ == Kind::Float) return d_ < 0 ? 0 : uint64_t(d_);
   if (kind_ == Kind::Bool) return b_ ? 1 : 0;
   type_error("a number");
@@ -301,7 +301,10 @@ struct Parser {
       unsigned long long mag = strtoull(digits, &ep, 10);
       if (*ep != 0) fail("bad integer");
       if (errno == ERANGE) return Json(strtod(tok.c_str(), nullptr));
-      if (neg) return Json(-int64_t(mag));
+      if (neg) {
+        if (mag > (1ull << 63)) return Json(-double(mag));
+        return Json(int64_t(uint64_t(0) - uint64_t(mag)));
+      }
       return Json(uint64_t(mag));
     }
     char* ep = nullptr;

@@ -12,6 +12,17 @@
 
 namespace dissem {
 
+// Timed condition wait on a system_clock deadline. libstdc++ lowers
+// steady_clock waits to pthread_cond_clockwait, which GCC 11's ThreadSanitizer
+// does not intercept (it then reports false double locks and races); the
+// system_clock form uses pthread_cond_timedwait, which it does.
+template <class Lock, class Pred>
+bool cv_wait_for(std::condition_variable& cv, Lock& lk, double seconds, Pred pred) {
+  auto dl = std::chrono::system_clock::now() +
+            std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(seconds));
+  return cv.wait_until(lk, dl, pred);
+}
+
 template <class T>
 class BlockingQueue {
  public:
@@ -36,9 +47,7 @@ class BlockingQueue {
   }
   std::optional<T> pop_for(double seconds) {
     std::unique_lock<std::mutex> lk(mu_);
-    auto dl = std::chrono::steady_clock::now() +
-              std::chrono::microseconds(int64_t(seconds * 1e6));
-    if (!cv_.wait_until(lk, dl, [&] { return !q_.empty() || closed_; })) return std::nullopt;
+    if (!cv_wait_for(cv_, lk, seconds, [&] { return !q_.empty() || closed_; })) return std::nullopt;
     if (q_.empty()) return std::nullopt;
     T v = std::move(q_.front());
     q_.pop_front();

@@ -23,6 +23,7 @@
 #include <set>
 
 #include "core/log.h"
+#include "core/queue.h"
 #include "roles/node.h"
 
 namespace dissem {
@@ -167,8 +168,7 @@ void PlannedEngine::load_range(LayerID layer_id, int64_t offset, int64_t size, i
 void PlannedEngine::quiesce() {
   std::unique_lock<std::mutex> lk(req_mu_);
   // Bounded: a transfer whose peer died must not hang the caller forever.
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
-  bool ok = idle_cv_.wait_until(lk, deadline, [&] {
+  bool ok = cv_wait_for(idle_cv_, lk, 120.0, [&] {
     return (reqs_.empty() && !busy_) || failed_.load() || stopped_.load();
   });
   if (!ok) log::error(int64_t(self_node_)).msg("quiesce timed out: data plane still busy");
@@ -576,7 +576,7 @@ void PlannedEngine::take_requests(bool block) {
     if (block && reqs_.empty() && !stop_req_) {
       busy_ = false;
       idle_cv_.notify_all();
-      req_cv_.wait_for(lk, std::chrono::milliseconds(50), [&] { return !reqs_.empty() || stop_req_.load(); });
+      cv_wait_for(req_cv_, lk, 0.05, [&] { return !reqs_.empty() || stop_req_.load(); });
     }
     got.swap(reqs_);
     if (!got.empty()) busy_ = true;

@@ -17,6 +17,7 @@
 #include <thread>
 
 #include "core/crc32c.h"
+#include "core/queue.h"
 #include "engine/backend.h"
 #include "engine/planned_engine.h"
 
@@ -64,7 +65,7 @@ struct Fabric {
   // Returns false on timeout (deadlock) or a size mismatch.
   bool wait_all(const std::vector<std::unique_ptr<Posted>>& ops, double timeout_s) {
     std::unique_lock<std::mutex> lk(mu);
-    bool ok = cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] {
+    bool ok = cv_wait_for(cv, lk, timeout_s, [&] {
       for (auto& o : ops)
         if (!o->done) return false;
       return true;

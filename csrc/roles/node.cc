@@ -110,14 +110,12 @@ void Node::announce() {
 
 bool Node::wait_ready(double timeout_s) {
   std::unique_lock<std::mutex> lk(sig_mu_);
-  return sig_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] {
-    return is_leader_ ? satisfied_ : ready_;
-  });
+  return cv_wait_for(sig_cv_, lk, timeout_s, [&] { return is_leader_ ? satisfied_ : ready_; });
 }
 
 bool Node::wait_start(double timeout_s) {
   std::unique_lock<std::mutex> lk(sig_mu_);
-  return sig_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return started_; });
+  return cv_wait_for(sig_cv_, lk, timeout_s, [&] { return started_; });
 }
 
 Status Node::status() {

@@ -201,7 +201,8 @@ class TcpTransport : public Transport {
 
  private:
   struct Reader {
-    int fd;
+    int fd;  // -1 once the reader has closed it
+    uint64_t id;
     std::thread th;
   };
 
@@ -269,6 +270,8 @@ class TcpTransport : public Transport {
         return;
       }
       // Reap readers whose connection already ended (one per layer payload).
+      // A finished reader has released its fd under this lock and only returns
+      // afterwards, so the join is short.
       for (auto it = readers_.begin(); it != readers_.end();) {
         if (it->fd == -1) {
           if (it->th.joinable()) it->th.join();
@@ -277,8 +280,9 @@ class TcpTransport : public Transport {
           ++it;
         }
       }
-      readers_.push_back(Reader{fd, std::thread()});
-      readers_.back().th = std::thread([this, fd] { read_loop(fd); });
+      uint64_t id = ++next_reader_;
+      readers_.push_back(Reader{fd, id, std::thread()});
+      readers_.back().th = std::thread([this, fd, id] { read_loop(fd, id); });
     }
   }
 
@@ -297,7 +301,7 @@ class TcpTransport : public Transport {
     return true;
   }
 
-  void read_loop(int fd) {
+  void read_loop(int fd, uint64_t id) {
     std::string buf;
     for (;;) {
       Json env;
@@ -326,10 +330,13 @@ class TcpTransport : public Transport {
       }
       if (!receive_layer(fd, buf, m)) break;
     }
-    ::close(fd);
+    // Release the fd under the lock and match by reader id: the fd number may
+    // be reused by the next accept the moment it is closed, and close() must
+    // still shut down that new connection.
     std::lock_guard<std::mutex> lk(readers_mu_);
+    ::close(fd);
     for (auto& r : readers_)
-      if (r.fd == fd) r.fd = -1;
+      if (r.id == id) r.fd = -1;
   }
 
   bool receive_layer(int fd, std::string& buf, MessagePtr m) {
@@ -407,6 +414,7 @@ class TcpTransport : public Transport {
   std::thread acceptor_;
   std::mutex readers_mu_;
   std::list<Reader> readers_;
+  uint64_t next_reader_ = 0;
   std::mutex conns_mu_;
   std::map<std::string, std::shared_ptr<Conn>> conns_;
   std::mutex pipe_mu_;
