@@ -29,7 +29,7 @@ HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Icsrc -I$(ROCM)/includ
              -fvisibility=hidden
 LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -lpthread
 
-CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/transport/inproc.cc \
+CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/core/fp8.cc csrc/transport/inproc.cc \
              csrc/transport/tcp.cc csrc/store/store.cc csrc/sched/maxflow.cc csrc/roles/node.cc \
              csrc/engine/host_engine.cc csrc/engine/planned_engine.cc csrc/engine/sim_backend.cc
 BIND_SRC  := csrc/bindings.cc

@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "core/crc32c.h"
+#include "core/fp8.h"
 #include "core/log.h"
 #include "core/wire.h"
 #include "engine/engine.h"
@@ -223,7 +224,7 @@ PYBIND11_MODULE(_core, m) {
         py::gil_scoped_release nogil;
         e.shutdown();
       });
-  m.def("host_engine", &make_host_engine);
+  m.def("host_engine", &make_host_engine, py::arg("link_rate") = std::map<NodeID, int64_t>{});
 
   py::class_<CrcManifest>(m, "CrcManifest")
       .def(py::init<>())
@@ -239,7 +240,15 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("verify", &PlannedConfig::verify)
       .def_readwrite("poison", &PlannedConfig::poison)
       .def_readwrite("max_inflight_groups", &PlannedConfig::max_inflight_groups)
-      .def_readwrite("group_peers", &PlannedConfig::group_peers);
+      .def_readwrite("group_peers", &PlannedConfig::group_peers)
+      .def_readwrite("disk_readers", &PlannedConfig::disk_readers)
+      .def_readwrite("disk_ring", &PlannedConfig::disk_ring)
+      .def_readwrite("pack", &PlannedConfig::pack)
+      .def_readwrite("pack_block", &PlannedConfig::pack_block)
+      .def_readwrite("max_retries", &PlannedConfig::max_retries)
+      .def_readwrite("inject_corrupt", &PlannedConfig::inject_corrupt)
+      .def_readwrite("inject_seed", &PlannedConfig::inject_seed)
+      .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)
@@ -249,13 +258,20 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("pieces", &PlannedStats::pieces)
       .def_readonly("verify_failures", &PlannedStats::verify_failures)
       .def_readonly("unverified_pieces", &PlannedStats::unverified_pieces)
-      .def_readonly("issue_ms", &PlannedStats::issue_ms);
+      .def_readonly("nacks", &PlannedStats::nacks)
+      .def_readonly("injected", &PlannedStats::injected)
+      .def_readonly("issue_ms", &PlannedStats::issue_ms)
+      .def_readonly("peer_sent", &PlannedStats::peer_sent)
+      .def_readonly("peer_recv", &PlannedStats::peer_recv);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
         return reinterpret_cast<uint64_t>(e.provision(l, n));
       })
+      .def("slot_size", &PlannedEngine::slot_size)
+      .def_property_readonly("chunk_grid", &PlannedEngine::chunk_bytes)
       .def("device_ptr", [](PlannedEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.device_ptr(l)); })
       .def("set_manifest", &PlannedEngine::set_manifest)
+      .def("manifest", &PlannedEngine::manifest)
       .def("set_seeded", &PlannedEngine::set_seeded)
       .def("reset_session", [](PlannedEngine& e) {
         py::gil_scoped_release nogil;
@@ -287,6 +303,36 @@ PYBIND11_MODULE(_core, m) {
       out.push_back(crc32c(reinterpret_cast<const void*>(ptr + uint64_t(off)), size_t(std::min(chunk, n - off))));
     return out;
   });
+  // fp8 wire/storage format (core/fp8.h), host reference
+  m.def("fp8_packed_size", &fp8::packed_size, py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block") = 128);
+  m.def("fp8_source_size", &fp8::source_size, py::arg("packed"), py::arg("src_chunk"), py::arg("block") = 128);
+  m.def("fp8_pack_layer_host", [](py::bytes src, int64_t src_chunk, int block) {
+    std::string s(src);
+    std::string out(size_t(fp8::packed_size(int64_t(s.size()), src_chunk, block)), '\0');
+    {
+      py::gil_scoped_release nogil;
+      fp8::pack_layer_host(reinterpret_cast<const uint8_t*>(s.data()), int64_t(s.size()), src_chunk, block,
+                           reinterpret_cast<uint8_t*>(out.data()));
+    }
+    return py::bytes(out);
+  }, py::arg("src"), py::arg("src_chunk"), py::arg("block") = 128);
+  m.def("fp8_pack_layer_into", [](uint64_t src, int64_t src_bytes, int64_t src_chunk, int block, uint64_t dst) {
+    py::gil_scoped_release nogil;
+    fp8::pack_layer_host(reinterpret_cast<const uint8_t*>(src), src_bytes, src_chunk, block,
+                         reinterpret_cast<uint8_t*>(dst));
+  });
+  m.def("fp8_unpack_layer_host", [](py::bytes packed, int64_t src_bytes, int64_t src_chunk, int block) {
+    std::string s(packed);
+    if (int64_t(s.size()) != fp8::packed_size(src_bytes, src_chunk, block))
+      throw std::runtime_error("packed buffer size does not match src_bytes");
+    std::string out(size_t(src_bytes), '\0');
+    {
+      py::gil_scoped_release nogil;
+      fp8::unpack_layer_host(reinterpret_cast<const uint8_t*>(s.data()), src_bytes, src_chunk, block,
+                             reinterpret_cast<uint8_t*>(out.data()));
+    }
+    return py::bytes(out);
+  }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block") = 128);
 
   // ---- roles
   py::class_<NodeConfig>(m, "NodeConfig")
@@ -303,7 +349,10 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("integer_seconds", &NodeConfig::integer_seconds)
       .def_readwrite("align", &NodeConfig::align)
       .def_readwrite("storage_path", &NodeConfig::storage_path)
-      .def_readwrite("relay", &NodeConfig::relay);
+      .def_readwrite("relay", &NodeConfig::relay)
+      .def_readwrite("job_timeout_s", &NodeConfig::job_timeout_s)
+      .def_readwrite("job_min_rate", &NodeConfig::job_min_rate)
+      .def_readwrite("max_redispatch", &NodeConfig::max_redispatch);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)
@@ -311,7 +360,10 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("layers_received", &NodeStats::layers_received)
       .def_readonly("bytes_received", &NodeStats::bytes_received)
       .def_readonly("flow_T", &NodeStats::flow_T)
-      .def_readonly("plan_ms", &NodeStats::plan_ms);
+      .def_readonly("plan_ms", &NodeStats::plan_ms)
+      .def_readonly("nacks", &NodeStats::nacks)
+      .def_readonly("redispatched", &NodeStats::redispatched)
+      .def_readonly("suspects", &NodeStats::suspects);
   py::class_<Node, std::shared_ptr<Node>>(m, "Node")
       .def(py::init([](const NodeConfig& cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEngine> e,
                        const LayersSrc& layers, const py::dict& assignment, bool is_leader) {

@@ -42,8 +42,14 @@ class Backend {
   virtual void free_host(uint8_t* p) = 0;
   // copy queue: async host -> device copy; event fires when it landed
   virtual Ev stage(uint8_t* dst, const uint8_t* src_host, int64_t n) = 0;
+  // copy queue: host -> device copy of `n_src` bytes of bf16, then fp8-pack them
+  // into dst in the packed chunk layout of core/fp8.h
+  virtual Ev stage_pack(uint8_t* dst, const uint8_t* src_host, int64_t n_src, int block) = 0;
   // comm queue: wait for `waits`, then one grouped set of P2P sends/recvs
   virtual Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) = 0;
+  // comm queue (fault injection): overwrite 4 bytes at p behind everything
+  // queued so far, e.g. a chunk a group just received
+  virtual Ev corrupt(uint8_t* p) = 0;
   // verify queue: after `after`, CRC32C of [p, p+n) into result slot `slot`
   // (n == 0: just an ordering marker on the verify queue)
   virtual Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) = 0;

@@ -5,10 +5,10 @@
 //  * HostEngine  - bytes in host memory / files, pushed as Layer messages over
 //                  the node's Transport (TCP: fresh connection per payload,
 //                  in-proc: pointer hand-off). Target tier: host RAM.
-//  * RcclEngine  - bytes in HBM, pushed with RCCL point-to-point over xGMI on
-//                  per-peer HIP streams; staging from host/NVMe on copy streams;
-//                  CRC32C verification by a gfx950 kernel (csrc/gpu/). Target
-//                  tier: Device.
+//  * PlannedEngine (planned_engine.h) - bytes in HBM, moved by leader-planned
+//                  grouped RCCL point-to-point rounds over xGMI (HipBackend) or a
+//                  simulated fabric (SimBackend); staging from host/NVMe on a copy
+//                  queue; CRC32C verification by a gfx950 kernel. Target: Device.
 //
 // Engines report completions by injecting MsgType::Landed into the owning
 // node's inbox, so every role state transition happens on the node's single
@@ -19,6 +19,7 @@
 #include <condition_variable>
 #include <functional>
 #include <list>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -75,6 +76,8 @@ class WorkerSet {
   std::atomic<int> active_{0};
 };
 
-std::shared_ptr<DataEngine> make_host_engine();
+// `link_rate`: per-destination pacing cap in B/s (fault injection
+// --inject slow-link=S,D,RATE on sender S); 0 / absent = unlimited.
+std::shared_ptr<DataEngine> make_host_engine(const std::map<NodeID, int64_t>& link_rate = {});
 
 }  // namespace dissem

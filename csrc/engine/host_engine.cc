@@ -5,6 +5,7 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include "core/log.h"
@@ -37,6 +38,7 @@ namespace {
 
 class HostEngine : public DataEngine {
  public:
+  explicit HostEngine(std::map<NodeID, int64_t> link_rate) : link_rate_(std::move(link_rate)) {}
   ~HostEngine() override { workers_.join_all(); }
   std::string name() const override { return "host"; }
   Location target() const override { return Location::Inmem; }
@@ -45,6 +47,8 @@ class HostEngine : public DataEngine {
     LayerSrc src;
     if (!node_->store().get(layer, &src)) return;
     Node* node = node_;
+    if (auto it = link_rate_.find(dest); it != link_rate_.end() && it->second > 0)
+      rate = rate > 0 ? std::min(rate, it->second) : it->second;
     workers_.spawn([node, dest, layer, offset, size, total, rate, src] {
       Message lm;
       lm.type = MsgType::Layer;
@@ -127,11 +131,14 @@ class HostEngine : public DataEngine {
   void shutdown() override { workers_.join_all(); }
 
  private:
+  std::map<NodeID, int64_t> link_rate_;
   WorkerSet workers_;
 };
 
 }  // namespace
 
-std::shared_ptr<DataEngine> make_host_engine() { return std::make_shared<HostEngine>(); }
+std::shared_ptr<DataEngine> make_host_engine(const std::map<NodeID, int64_t>& link_rate) {
+  return std::make_shared<HostEngine>(link_rate);
+}
 
 }  // namespace dissem

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <set>
 
+#include "core/fp8.h"
 #include "core/log.h"
 #include "core/queue.h"
 #include "roles/node.h"
@@ -37,6 +38,14 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
   if (cfg_.chunk_bytes <= 0 || cfg_.chunk_bytes % 4096)
     throw std::runtime_error("chunk_bytes must be a positive multiple of 4 KiB");
   if (cfg_.group_peers < 1) cfg_.group_peers = 1;
+  grid_ = cfg_.chunk_bytes;
+  if (cfg_.pack == 1) {
+    fp8::check(cfg_.chunk_bytes, cfg_.chunk_bytes, cfg_.pack_block);
+    grid_ = fp8::packed_chunk(cfg_.chunk_bytes, cfg_.pack_block);
+  } else if (cfg_.pack != 0) {
+    throw std::runtime_error("unknown pack format " + std::to_string(cfg_.pack));
+  }
+  inject_rng_.seed(cfg_.inject_seed * 0x9E3779B97F4A7C15ull + uint64_t(cfg_.rank));
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
   self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
   th_ = std::thread([this] { run(); });
@@ -71,20 +80,38 @@ int PlannedEngine::rank_of(NodeID n) const {
 
 // --------------------------------------------------------------- setup API
 
+int64_t PlannedEngine::slot_size(int64_t src_bytes) const {
+  if (cfg_.pack == 1) {
+    fp8::check(src_bytes, cfg_.chunk_bytes, cfg_.pack_block);
+    return fp8::packed_size(src_bytes, cfg_.chunk_bytes, cfg_.pack_block);
+  }
+  return src_bytes;
+}
+
+int64_t PlannedEngine::src_len(const Layer& L, int64_t c) const {
+  if (cfg_.pack == 1) {
+    const int64_t src = fp8::source_size(L.size, cfg_.chunk_bytes, cfg_.pack_block);
+    return std::min(cfg_.chunk_bytes, src - c * cfg_.chunk_bytes);
+  }
+  return std::min(grid_, L.size - c * grid_);
+}
+
 PlannedEngine::Layer& PlannedEngine::layer(LayerID id, int64_t size_hint) {
   Layer& L = layers_[id];
   if (!L.size && size_hint) L.size = size_hint;
-  int64_t n = L.size ? (L.size + cfg_.chunk_bytes - 1) / cfg_.chunk_bytes : 0;
+  int64_t n = L.size ? (L.size + grid_ - 1) / grid_ : 0;
   if (int64_t(L.st.size()) != n) {
     L.st.assign(size_t(n), L.seeded ? 2 : 0);
     L.ev.assign(size_t(n), 0);
     L.want.assign(size_t(n), 0);
+    L.fails.assign(size_t(n), 0);
   }
   return L;
 }
 
 uint8_t* PlannedEngine::provision(LayerID id, int64_t size) {
   std::lock_guard<std::mutex> lk(req_mu_);  // setup runs while the issue thread is idle
+  if (cfg_.pack == 1) (void)fp8::source_size(size, cfg_.chunk_bytes, cfg_.pack_block);  // must be a packed size
   Layer& L = layer(id, size);
   if (L.size != size) throw std::runtime_error("layer " + std::to_string(id) + " re-provisioned with another size");
   if (!L.dev) L.dev = backend_->alloc(size);
@@ -99,7 +126,7 @@ uint8_t* PlannedEngine::device_ptr(LayerID id) {
 
 void PlannedEngine::set_manifest(LayerID id, const CrcManifest& m) {
   std::lock_guard<std::mutex> lk(req_mu_);
-  if (m.chunk_bytes != cfg_.chunk_bytes) throw std::runtime_error("manifest chunk_bytes must equal the engine chunk");
+  if (m.chunk_bytes != grid_) throw std::runtime_error("manifest chunk_bytes must equal the engine chunk grid");
   layers_[id].manifest = m;
 }
 
@@ -211,6 +238,43 @@ void PlannedEngine::landed(const Piece& p) {
   node_->inject(m);
 }
 
+void PlannedEngine::nack(const Piece& p, Layer& L, uint32_t got) {
+  const size_t c = size_t(p.chunk);
+  char buf[200];
+  snprintf(buf, sizeof buf, "CRC32C mismatch layer %llu chunk %lld from node %llu: got %08x want %08x",
+           (unsigned long long)p.layer, (long long)p.chunk, (unsigned long long)p.src_node, got, p.crc);
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.verify_failures++;
+  }
+  if (L.ev[c]) {
+    backend_->release(L.ev[c]);
+    L.ev[c] = 0;
+  }
+  if (++L.fails[c] > cfg_.max_retries || !node_) {
+    fail(std::string(buf) + (node_ ? " (retries exhausted)" : ""));
+    return;
+  }
+  log::warn(int64_t(self_node_)).msg(std::string(buf) + "; requesting a re-send");
+  L.st[c] = 4;
+  if (p.kind == Kind::Local) {
+    // The source bytes did not match their manifest on the way in: stage again
+    // (after the poll loop; staging appends to verifies_).
+    restage_.push_back({p.layer, p.chunk});
+    return;
+  }
+  Message n;
+  n.type = MsgType::Nack;
+  n.layer = p.layer;
+  n.dest = p.src_node;  // the sender whose bytes failed
+  n.offset = p.off;
+  n.data_size = p.len;
+  n.total_size = p.total;
+  node_->send_msg(node_->leader(), n);
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.nacks++;
+}
+
 void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
   if (!L.host && L.path.empty()) {
     LayerSrc src;
@@ -224,7 +288,7 @@ void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
     }
   }
   if (L.host) {
-    stage_from(L, id, c, L.host + c * cfg_.chunk_bytes, nullptr);
+    stage_from(L, id, c, L.host + c * cfg_.chunk_bytes, nullptr);  // source grid (== grid_ unless packing)
   } else {
     submit_disk(L, id, c);
   }
@@ -244,7 +308,7 @@ void PlannedEngine::submit_disk(Layer& L, LayerID id, int64_t c) {
   d.layer = id;
   d.chunk = c;
   d.file_off = L.path_off + c * cfg_.chunk_bytes;
-  d.len = std::min(cfg_.chunk_bytes, L.size - c * cfg_.chunk_bytes);
+  d.len = src_len(L, c);
   d.path = L.path;
   disk_wait_.push_back(std::move(d));
   pump_disk();
@@ -317,10 +381,12 @@ void PlannedEngine::reader_loop() {
 }
 
 void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* src, uint8_t* bounce) {
-  const int64_t off = c * cfg_.chunk_bytes;
-  const int64_t len = std::min(cfg_.chunk_bytes, L.size - off);
+  const int64_t off = c * grid_;
+  const int64_t len = std::min(grid_, L.size - off);
+  const int64_t slen = src_len(L, c);
   if (!L.dev) L.dev = backend_->alloc(L.size);
-  Ev e = backend_->stage(L.dev + off, src, len);
+  Ev e = cfg_.pack == 1 ? backend_->stage_pack(L.dev + off, src, slen, cfg_.pack_block)
+                        : backend_->stage(L.dev + off, src, len);
   L.st[size_t(c)] = 1;
   L.ev[size_t(c)] = e;
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
@@ -340,7 +406,7 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   v.bounce = bounce;
   verifies_.push_back(std::move(v));
   std::lock_guard<std::mutex> lk(stats_mu_);
-  stats_.bytes_staged += len;
+  stats_.bytes_staged += slen;
 }
 
 int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed) {
@@ -348,8 +414,8 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   uint8_t s = L.st[size_t(c)];
   if (s == 2) {
     if (want_landed) {
-      const int64_t off = c * cfg_.chunk_bytes;
-      Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, std::min(cfg_.chunk_bytes, L.size - off), L.size, c, true};
+      const int64_t off = c * grid_;
+      Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, std::min(grid_, L.size - off), L.size, c, true};
       p.src_node = self_node_;
       landed(p);
       L.want[size_t(c)] = 0;
@@ -358,6 +424,7 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   }
   if (s == 1) return 1;
   if (s == 3) return 0;  // disk read in flight
+  if (s == 4 && !want_landed) return 1;  // forward the bad copy; its receiver NACKs it as well
   LayerSrc src;
   if (L.host || !L.path.empty() || (node_ && node_->store().get(id, &src) && (src.host || !src.path.empty()))) {
     stage_chunk(L, id, c);
@@ -369,7 +436,7 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
 void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
   std::sort(jobs.begin(), jobs.end(), [](const XferJob& a, const XferJob& b) { return a.seq < b.seq; });
   std::vector<Piece> pieces;
-  const int64_t cb = cfg_.chunk_bytes;
+  const int64_t cb = grid_;
   for (auto& j : jobs) {
     Kind kind;
     int peer;
@@ -470,7 +537,20 @@ bool PlannedEngine::issue_some() {
       xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len});
     }
     Ev g = backend_->group(xops, waits);
-    groups_inflight_.push_back(g);
+    groups_inflight_.push_back({g, std::chrono::steady_clock::now()});
+    // Fault injection: damage some received chunks behind the group, before their check.
+    Ev landed_ev = g;
+    int64_t injected = 0;
+    if (cfg_.inject_corrupt > 0) {
+      std::uniform_real_distribution<double> u(0.0, 1.0);
+      for (auto& p : group) {
+        if (p.kind != Kind::Recv || p.len < 4 || u(inject_rng_) >= cfg_.inject_corrupt) continue;
+        Ev c = backend_->corrupt(layers_[p.layer].dev + p.off);
+        if (landed_ev != g) backend_->release(landed_ev);
+        landed_ev = c;
+        injected++;
+      }
+    }
     // Receivers: chunks are valid behind `g` on the comm queue; check them on the verify queue.
     Verify v;
     Ev last = 0;
@@ -483,13 +563,14 @@ bool PlannedEngine::issue_some() {
       if (cfg_.verify && p.has_crc && p.full) {
         slot = crc_slot();
         if (last) backend_->release(last);
-        last = backend_->crc(L.dev + p.off, p.len, slot, g);
+        last = backend_->crc(L.dev + p.off, p.len, slot, landed_ev);
       }
       v.pieces.push_back(p);
       v.slots.push_back(slot);
     }
+    if (!v.pieces.empty() && !last) last = backend_->crc(nullptr, 0, 0, landed_ev);
+    if (landed_ev != g) backend_->release(landed_ev);
     if (!v.pieces.empty()) {
-      if (!last) last = backend_->crc(nullptr, 0, 0, g);
       v.ev = last;
       verifies_.push_back(std::move(v));
     } else if (last) {
@@ -501,6 +582,8 @@ bool PlannedEngine::issue_some() {
       stats_.pieces += int64_t(group.size());
       stats_.bytes_sent += sent;
       stats_.bytes_recv += recvd;
+      stats_.injected += injected;
+      for (auto& p : group) (p.kind == Kind::Send ? stats_.peer_sent : stats_.peer_recv)[p.peer] += p.len;
       stats_.issue_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     progress = true;
@@ -510,13 +593,21 @@ bool PlannedEngine::issue_some() {
 
 void PlannedEngine::poll() {
   while (!groups_inflight_.empty()) {
-    int r = backend_->query(groups_inflight_.front());
-    if (r == 0) break;
+    int r = backend_->query(groups_inflight_.front().first);
+    if (r == 0) {
+      // Watchdog: a group whose partner never posts (dead or hung peer) would
+      // block the comm queue forever. Fail; shutdown aborts the communicator.
+      double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - groups_inflight_.front().second)
+                       .count();
+      if (cfg_.group_timeout_s > 0 && age > cfg_.group_timeout_s)
+        fail("P2P group pending for " + std::to_string(int(age)) + " s: a peer rank is dead or stuck");
+      break;
+    }
     if (r < 0) {
       fail("P2P group failed: " + backend_->async_error());
       return;
     }
-    backend_->release(groups_inflight_.front());
+    backend_->release(groups_inflight_.front().first);
     groups_inflight_.pop_front();
   }
   for (auto it = verifies_.begin(); it != verifies_.end();) {
@@ -535,15 +626,9 @@ void PlannedEngine::poll() {
       if (it->slots[i] != ~0u) {
         uint32_t got = backend_->crc_result(it->slots[i]);
         if (got != p.crc) {
-          {
-            std::lock_guard<std::mutex> lk(stats_mu_);
-            stats_.verify_failures++;
-          }
-          char buf[160];
-          snprintf(buf, sizeof buf, "CRC32C mismatch layer %llu chunk %lld: got %08x want %08x",
-                   (unsigned long long)p.layer, (long long)p.chunk, got, p.crc);
-          fail(buf);
-          return;
+          nack(p, L, got);
+          if (failed_) return;
+          continue;
         }
         std::lock_guard<std::mutex> lk(stats_mu_);
         stats_.bytes_verified += p.len;
@@ -567,6 +652,13 @@ void PlannedEngine::poll() {
     if (it->bounce) bounce_free_.push_back(it->bounce);
     it = verifies_.erase(it);
   }
+  std::vector<std::pair<LayerID, int64_t>> again;
+  again.swap(restage_);
+  for (auto& lc : again) {
+    Layer& L = layers_[lc.first];
+    L.st[size_t(lc.second)] = 0;
+    stage_chunk(L, lc.first, lc.second);
+  }
 }
 
 void PlannedEngine::take_requests(bool block) {
@@ -589,7 +681,7 @@ void PlannedEngine::take_requests(bool block) {
       case Req::Load: {
         Layer& L = layer(r.layer);
         if (!L.size) break;
-        for (int64_t c = r.off / cfg_.chunk_bytes; c * cfg_.chunk_bytes < r.off + r.len && c < int64_t(L.st.size()); ++c)
+        for (int64_t c = r.off / grid_; c * grid_ < r.off + r.len && c < int64_t(L.st.size()); ++c)
           if (ensure_chunk(L, r.layer, c, true) < 0) fail("no source to load layer " + std::to_string(r.layer));
         break;
       }
@@ -601,6 +693,7 @@ void PlannedEngine::take_requests(bool block) {
             if (L.ev[c]) backend_->release(L.ev[c]);
             L.ev[c] = 0;
             L.want[c] = 0;
+            L.fails[c] = 0;
           }
           L.host = nullptr;  // re-read the source from the next session's store
           if (cfg_.poison && !L.seeded && L.dev) backend_->zero_sync(L.dev, L.size);

@@ -19,11 +19,13 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -44,12 +46,27 @@ struct PlannedConfig {
   int group_peers = 1;             // ops per peer and direction per group
   int disk_readers = 4;            // NVMe reader threads (O_DIRECT pread into pinned bounce buffers)
   int disk_ring = 8;               // pinned bounce buffers of chunk_bytes each
+  // fp8 wire/storage format (core/fp8.h): layers are staged from bf16 sources
+  // and packed on the copy queue; HBM slots, transfers and CRCs use the packed
+  // chunk grid. chunk_bytes stays the SOURCE (bf16) chunk.
+  int pack = 0;                    // 0 none, 1 fp8 e4m3fn block-scaled
+  int pack_block = 128;            // elements per f32 scale
+  // Fault handling: a chunk that fails its CRC is NACKed to the
+  // leader, which re-sends it; after max_retries failures of one chunk the
+  // engine fails. inject_corrupt overwrites received chunks with this
+  // probability (fault injection, --inject drop-chunk=P).
+  int max_retries = 4;
+  double inject_corrupt = 0;
+  uint64_t inject_seed = 1;
+  double group_timeout_s = 300;    // a P2P group pending longer than this fails the engine (dead peer)
 };
 
 struct PlannedStats {
   int64_t bytes_sent = 0, bytes_recv = 0, bytes_staged = 0, bytes_verified = 0;
   int64_t groups = 0, pieces = 0, verify_failures = 0, unverified_pieces = 0;
+  int64_t nacks = 0, injected = 0;
   double issue_ms = 0;  // host time spent enqueueing groups
+  std::map<int, int64_t> peer_sent, peer_recv;  // bytes per peer rank (per-link counters)
 };
 
 class PlannedEngine : public DataEngine {
@@ -71,7 +88,10 @@ class PlannedEngine : public DataEngine {
   std::string name() const override { return backend_->name(); }
   Location target() const override { return Location::Device; }
   bool planned() const override { return true; }
-  int64_t chunk_bytes() const override { return cfg_.chunk_bytes; }
+  int64_t chunk_bytes() const override { return grid_; }  // chunk grid of HBM slots / transfers
+  // Bytes a layer of `src_bytes` source bytes occupies in HBM and on the wire.
+  int64_t slot_size(int64_t src_bytes) const;
+  const PlannedConfig& config() const { return cfg_; }
   std::map<LayerID, CrcManifest> manifest() override;
   bool on_message(const MessagePtr& m) override;
   void send_range(NodeID dest, LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
@@ -103,9 +123,13 @@ class PlannedEngine : public DataEngine {
     const uint8_t* host = nullptr;   // host-tier source (set at first staging)
     std::string path;                // disk-tier source
     int64_t path_off = 0;
-    std::vector<uint8_t> st;         // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk
+    // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk,
+    // 4 failed its CRC and awaits the leader's re-send (still forwardable: a
+    // later receiver detects it and NACKs too)
+    std::vector<uint8_t> st;
     std::vector<Ev> ev;              // staging event of a pending chunk (0: pending on the comm queue)
     std::vector<uint8_t> want;       // inject Landed when resident (assigned here)
+    std::vector<uint8_t> fails;      // CRC failures per chunk
   };
   struct Verify {  // landing (recv group or staging copy) awaiting its check
     Ev ev = 0;
@@ -144,10 +168,14 @@ class PlannedEngine : public DataEngine {
   void pump_disk();
   void reader_loop();
   void landed(const Piece& p);
+  void nack(const Piece& p, Layer& L, uint32_t got);
   uint32_t crc_slot();
   void fail(const std::string& what);
+  int64_t src_len(const Layer& L, int64_t c) const;  // source bytes of chunk c
 
   PlannedConfig cfg_;
+  int64_t grid_ = 0;  // chunk grid of HBM slots and transfers (packed chunk with pack=fp8)
+  std::mt19937_64 inject_rng_;
   std::unique_ptr<Backend> backend_;
   NodeID self_node_ = 0;
   std::map<NodeID, int> node_rank_;
@@ -163,7 +191,8 @@ class PlannedEngine : public DataEngine {
   std::map<LayerID, Layer> layers_;
   std::deque<Piece> ops_;
   std::deque<Verify> verifies_;
-  std::deque<Ev> groups_inflight_;
+  std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
+  std::deque<std::pair<Ev, std::chrono::steady_clock::time_point>> groups_inflight_;
 
   // disk tier: issue thread owns bounce_free_/disk_wait_; readers exchange via disk_mu_
   std::vector<uint8_t*> bounce_all_, bounce_free_;

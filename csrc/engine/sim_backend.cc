@@ -17,6 +17,7 @@
 #include <thread>
 
 #include "core/crc32c.h"
+#include "core/fp8.h"
 #include "core/queue.h"
 #include "engine/backend.h"
 #include "engine/planned_engine.h"
@@ -175,6 +176,26 @@ class SimBackend : public Backend {
     auto [id, ev] = make_event();
     copy_.push([=] {
       memcpy(dst, src, size_t(n));
+      ev->state = 1;
+    });
+    return id;
+  }
+
+  Ev stage_pack(uint8_t* dst, const uint8_t* src, int64_t n_src, int block) override {
+    auto [id, ev] = make_event();
+    copy_.push([=] {
+      const int64_t n = n_src / 2;
+      fp8::pack_host(reinterpret_cast<const uint16_t*>(src), n, dst, reinterpret_cast<float*>(dst + n), block);
+      ev->state = 1;
+    });
+    return id;
+  }
+
+  Ev corrupt(uint8_t* p) override {
+    auto [id, ev] = make_event();
+    comm_.push([=] {
+      const uint32_t pat = 0xA5A5A5A5u;
+      memcpy(p, &pat, 4);
       ev->state = 1;
     });
     return id;

@@ -8,6 +8,7 @@
 #include <mutex>
 
 #include "core/crc32c.h"
+#include "core/fp8.h"
 #include "gpu/gpu_api.h"
 #include "gpu/hip_backend.h"
 #include "kernels/kernels.h"
@@ -168,6 +169,37 @@ void register_gpu_bindings(PyObject* module) {
                            reinterpret_cast<uint16_t*>(bf16), block, as_stream(stream)),
           "fp8_unpack");
   }, py::arg("fp8"), py::arg("scales"), py::arg("n"), py::arg("bf16"), py::arg("block") = 128, py::arg("stream") = 0);
+  m.def("fp8_pack_chunks", [](uint64_t src, int64_t src_bytes, int64_t src_chunk, int block, uint64_t dst,
+                              uint64_t stream) {
+    check(kern::fp8_pack_chunks(reinterpret_cast<const void*>(src), src_bytes, src_chunk, block,
+                                reinterpret_cast<void*>(dst), as_stream(stream)),
+          "fp8_pack_chunks");
+  }, py::arg("src"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("dst"),
+        py::arg("stream") = 0);
+  // Fused verify + unpack (synchronous): writes the bf16 layer to `out`, returns
+  // the CRC32C of every packed chunk.
+  m.def("fp8_verify_unpack", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block, uint64_t out,
+                                uint64_t stream) {
+    py::gil_scoped_release nogil;
+    const int64_t pbytes = fp8::packed_size(src_bytes, src_chunk, block);
+    const int64_t pchunk = fp8::packed_chunk(src_chunk, block);
+    const size_t n = size_t((pbytes + pchunk - 1) / pchunk);
+    void* ws = nullptr;
+    uint32_t *host = nullptr, *dev = nullptr;
+    check(hipMalloc(&ws, kern::crc32c_workspace_bytes(pbytes, pchunk)), "hipMalloc");
+    check(hipHostMalloc(reinterpret_cast<void**>(&host), std::max<size_t>(n, 1) * 4, hipHostMallocMapped),
+          "hipHostMalloc");
+    check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
+    hipError_t e = kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
+                                           reinterpret_cast<uint16_t*>(out), dev, ws, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    std::vector<uint32_t> crc(host, host + n);
+    (void)hipFree(ws);
+    (void)hipHostFree(host);
+    check(e, "fp8_verify_unpack");
+    return crc;
+  }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
+        py::arg("stream") = 0);
 
   // ---- RCCL engine = planned engine on the HIP backend
   m.def("nccl_unique_id", [] { return py::bytes(nccl_unique_id()); });

@@ -75,6 +75,30 @@ class HipBackend : public Backend {
     return record(copy_);
   }
 
+  Ev stage_pack(uint8_t* dst, const uint8_t* src, int64_t n_src, int block) override {
+    // bf16 lands in a device scratch chunk, then the gfx950 pack kernel writes
+    // the packed chunk into the layer slot. One scratch suffices: both steps
+    // are ordered on the copy stream, and packing (~10 us per 64 MiB) is noise
+    // next to the PCIe copy (~1.2 ms).
+    if (n_src > scratch_bytes_) {
+      HIP_OK(hipStreamSynchronize(copy_));
+      if (scratch_) HIP_OK(hipFree(scratch_));
+      scratch_ = nullptr;
+      HIP_OK(hipMalloc(&scratch_, size_t(n_src)));
+      scratch_bytes_ = n_src;
+    }
+    HIP_OK(hipMemcpyAsync(scratch_, src, size_t(n_src), hipMemcpyHostToDevice, copy_));
+    const int64_t n = n_src / 2;
+    HIP_OK(kern::fp8_pack(static_cast<const uint16_t*>(scratch_), n, dst, reinterpret_cast<float*>(dst + n), block,
+                          copy_));
+    return record(copy_);
+  }
+
+  Ev corrupt(uint8_t* p) override {
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), 0xA5A5A5A5u, 1, comm_));
+    return record(comm_);
+  }
+
   Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) override {
     for (Ev w : waits) HIP_OK(hipStreamWaitEvent(comm_, ev(w), 0));
     if (!ops.empty()) {
@@ -140,6 +164,7 @@ class HipBackend : public Backend {
     for (auto e : pool_) (void)hipEventDestroy(e);
     pool_.clear();
     if (ws_) (void)hipFree(ws_);
+    if (scratch_) (void)hipFree(scratch_);
     if (crc_host_) (void)hipHostFree(crc_host_);
     (void)hipStreamDestroy(comm_);
     (void)hipStreamDestroy(copy_);
@@ -164,6 +189,8 @@ class HipBackend : public Backend {
   hipStream_t comm_ = nullptr, copy_ = nullptr, verify_ = nullptr;
   ncclComm_t nccl_ = nullptr;
   void* ws_ = nullptr;
+  void* scratch_ = nullptr;  // bf16 landing chunk for stage_pack
+  int64_t scratch_bytes_ = 0;
   uint32_t* crc_host_ = nullptr;
   uint32_t* crc_dev_ = nullptr;
   std::vector<hipEvent_t> pool_;  // issue-thread only

@@ -4,7 +4,7 @@
 // registers, which are linear over GF(2):
 //   raw(A || B) = shift(raw(A), |B|) xor raw(B),  shift(r, L) = r * x^(8L) mod P.
 // Decomposition:
-//  * a chunk is cut into 64 KiB segments; one wave owns a segment;
+//  * a chunk is cut into 16 KiB segments; one wave owns a segment;
 //  * lane l of the wave reads 16-B words l, l+64, l+128, ... (each wave
 //    instruction reads 1 KiB contiguous: fully coalesced) and keeps the raw CRC
 //    of its strided sub-message: s = shift_1024B(s) xor crc16(word), i.e. 4 + 16
@@ -85,7 +85,7 @@ __device__ inline uint32_t wave_xor(uint32_t v) {
   return v;
 }
 
-// One wave per 64 KiB segment; writes the segment's raw CRC to seg_out[g].
+// One wave per 16 KiB segment; writes the segment's raw CRC to seg_out[g].
 __global__ void __launch_bounds__(256) crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes,
                                                               int64_t chunk_bytes, int64_t spc,
                                                               int64_t total_segs,
@@ -140,6 +140,90 @@ __global__ void __launch_bounds__(256) crc32c_segments_kernel(const uint8_t* __r
   }
 }
 
+__device__ inline uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+// 16 e4m3fn values (one 16-B word) times their block scale -> 16 bf16 (two 16-B words).
+__device__ inline void unpack16(uint4 w, float s, uint4* __restrict__ dst) {
+  const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+  uint32_t o[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(int(d[i]), false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(int(d[i]), true);
+    o[2 * i] = uint32_t(f32_to_bf16_rne(lo[0] * s)) | (uint32_t(f32_to_bf16_rne(lo[1] * s)) << 16);
+    o[2 * i + 1] = uint32_t(f32_to_bf16_rne(hi[0] * s)) | (uint32_t(f32_to_bf16_rne(hi[1] * s)) << 16);
+  }
+  dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+  dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// Fused verify + unpack of fp8-packed chunks (core/fp8.h layout
+// [q: n bytes][scales: n/BLOCK f32] per chunk): one pass over the packed bytes
+// computes each segment's raw CRC exactly like crc32c_segments_kernel and, for
+// words in the q region, writes the dequantized bf16 values. Every packed byte
+// is read once from HBM; the scales (1/32 of the traffic) are re-read from L2.
+template <int BLOCK>
+__global__ void __launch_bounds__(256) verify_unpack_segments_kernel(
+    const uint8_t* __restrict__ src, int64_t bytes, int64_t pchunk, int64_t spc, int64_t total_segs,
+    int64_t out_chunk_elems, const uint32_t* __restrict__ consts, uint32_t* __restrict__ seg_out,
+    uint16_t* __restrict__ out) {
+  __shared__ uint32_t lds[kSegKernelLds];
+  for (int i = threadIdx.x; i < kSegKernelLds; i += blockDim.x) lds[i] = consts[i];
+  __syncthreads();
+  const uint32_t* T = lds;
+  const uint32_t* A = lds + kT16;
+  const uint32_t* lanepow = lds + kT16 + kA;
+
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
+  for (int64_t g = wave; g < total_segs; g += nwaves) {
+    const int64_t c = g / spc, k = g % spc;
+    const int64_t chunk_start = c * pchunk;
+    const int64_t chunk_len = min(pchunk, bytes - chunk_start);
+    const int64_t n_q = chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
+    const float* scales = reinterpret_cast<const float*>(src + chunk_start + n_q);
+    uint16_t* obase = out + c * out_chunk_elems;
+    const int64_t seg_start = k * kSegBytes;
+    const int64_t seg_len = min(int64_t(kSegBytes), chunk_len - seg_start);
+    const int64_t nw = seg_len >> 4;
+    const uint4* words = reinterpret_cast<const uint4*>(src + chunk_start + seg_start);
+    uint32_t s = 0;
+    auto consume = [&](const uint4 w, int64_t j) {
+      s = shift_map(A, s) ^ crc16raw(T, w);
+      const int64_t e = seg_start + 16 * j;  // byte offset in chunk = element index in the q region
+      if (e < n_q) unpack16(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
+    };
+    if (nw == kSegBytes / 16) {
+#pragma unroll 8
+      for (int it = 0; it < kSegBytes / 16 / 64; ++it) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        const u32x4 wv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * it));
+        consume(make_uint4(wv[0], wv[1], wv[2], wv[3]), lane + 64 * it);
+      }
+      s = multmodp(lanepow[63 - lane], s);
+    } else {
+      int64_t last = -1;
+      for (int64_t j = lane; j < nw; j += 64) {
+        consume(words[j], j);
+        last = j;
+      }
+      if (last >= 0) s = multmodp(lanepow[nw - 1 - last], s);
+    }
+    s = wave_xor(s);
+    if (lane == 0) {
+      const uint8_t* tail = src + chunk_start + seg_start + (nw << 4);
+      for (int64_t b = 0; b < (seg_len & 15); ++b) s = T[(s ^ tail[b]) & 255] ^ (s >> 8);
+      seg_out[g] = s;
+    }
+  }
+}
+
 // One wave per chunk: fold the chunk's segment CRCs and finalize. `fold` holds
 // host-computed constants for full chunks: per lane x^(8*bytes after its run)
 // and the init/xorout term; only a short final chunk computes them here.
@@ -182,7 +266,7 @@ DeviceConsts g_consts;
 
 uint32_t* fold_consts(int64_t chunk_bytes) {
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_consts.mu);
   auto key = std::make_pair(dev, chunk_bytes);
   auto it = g_consts.fold.find(key);
@@ -204,7 +288,7 @@ uint32_t* fold_consts(int64_t chunk_bytes) {
 
 uint32_t* device_consts() {
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_consts.mu);
   auto it = g_consts.by_device.find(dev);
   if (it != g_consts.by_device.end()) return it->second;
@@ -251,6 +335,39 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
   crc32c_segments_kernel<<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(static_cast<const uint8_t*>(src), bytes,
                                                                       chunk_bytes, spc, total_segs, consts, seg);
   crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, chunk_bytes, spc, consts, fold, out);
+  return hipGetLastError();
+}
+
+hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
+                             uint32_t* crc_out, void* workspace, hipStream_t s) {
+  if (src_bytes <= 0) return hipSuccess;
+  if (src_chunk <= 0 || src_chunk % 4096 || src_bytes % (2 * block) || (reinterpret_cast<uintptr_t>(packed) & 15) ||
+      (reinterpret_cast<uintptr_t>(out) & 15))
+    return hipErrorInvalidValue;
+  const int64_t pchunk = src_chunk / 2 + src_chunk / 2 / block * 4;
+  const int64_t full = src_bytes / src_chunk, tail = src_bytes % src_chunk;
+  const int64_t bytes = full * pchunk + (tail ? tail / 2 + tail / 2 / block * 4 : 0);
+  uint32_t* consts = device_consts();
+  uint32_t* fold = fold_consts(pchunk);
+  if (!consts || !fold) return hipErrorOutOfMemory;
+  const int64_t spc = (pchunk + kSegBytes - 1) / kSegBytes;
+  const int64_t nchunks = (bytes + pchunk - 1) / pchunk;
+  const int64_t last_len = bytes - (nchunks - 1) * pchunk;
+  const int64_t total_segs = (nchunks - 1) * spc + (last_len + kSegBytes - 1) / kSegBytes;
+  int64_t blocks = (total_segs + 3) / 4;
+  if (blocks > 256 * 6) blocks = 256 * 6;
+  auto* seg = static_cast<uint32_t*>(workspace);
+  auto* p = static_cast<const uint8_t*>(packed);
+  const dim3 grid{unsigned(blocks)}, tpb{256};
+  switch (block) {
+    case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
+    case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
+    case 128: verify_unpack_segments_kernel<128><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
+    case 256: verify_unpack_segments_kernel<256><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
+    case 512: verify_unpack_segments_kernel<512><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
+    default: return hipErrorInvalidValue;
+  }
+  crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, pchunk, spc, consts, fold, crc_out);
   return hipGetLastError();
 }
 

@@ -12,6 +12,8 @@
 // block/8 adjacent lanes that reduce the amax with cross-lane shuffles.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels/kernels.h"
 
 namespace dissem {
@@ -122,6 +124,20 @@ hipError_t fp8_unpack(const uint8_t* fp8, const float* scales, int64_t n, uint16
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t fp8_pack_chunks(const void* src, int64_t src_bytes, int64_t src_chunk, int block, void* dst,
+                           hipStream_t s) {
+  if (src_chunk <= 0 || src_chunk % (2 * block) || src_bytes % (2 * block)) return hipErrorInvalidValue;
+  const int64_t pchunk = src_chunk / 2 + src_chunk / 2 / block * 4;
+  for (int64_t off = 0, c = 0; off < src_bytes; off += src_chunk, ++c) {
+    const int64_t n = std::min(src_chunk, src_bytes - off) / 2;
+    uint8_t* out = static_cast<uint8_t*>(dst) + c * pchunk;
+    hipError_t e = fp8_pack(reinterpret_cast<const uint16_t*>(static_cast<const uint8_t*>(src) + off), n, out,
+                            reinterpret_cast<float*>(out + n), block, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace kern

@@ -26,6 +26,15 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
 // (scale = amax/448; non-finite inputs: +-inf saturate, NaN stays NaN), and back.
 hipError_t fp8_pack(const uint16_t* bf16, int64_t n, uint8_t* fp8, float* scales, int block, hipStream_t s);
 hipError_t fp8_unpack(const uint8_t* fp8, const float* scales, int64_t n, uint16_t* bf16, int block, hipStream_t s);
+// Whole layer into the chunked packed layout of core/fp8.h (one pack launch per chunk).
+hipError_t fp8_pack_chunks(const void* src, int64_t src_bytes, int64_t src_chunk, int block, void* dst,
+                           hipStream_t s);
+
+// ---- crc32c.hip: fused verify + unpack of a packed layer: crc_out[c] = CRC32C of
+// packed chunk c, out = the bf16 layer (src_bytes). One pass over the packed bytes.
+// `workspace`: crc32c_workspace_bytes(packed bytes, packed chunk) bytes.
+hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
+                             uint32_t* crc_out, void* workspace, hipStream_t s);
 
 }  // namespace kern
 }  // namespace dissem

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <tuple>
 
 #include "core/log.h"
 #include "sched/maxflow.h"
@@ -55,11 +56,30 @@ void Node::start() {
     m->type = MsgType::Tick;
     m->epoch = cfg_.epoch;
     t_->inject(m);
+    if (cfg_.job_timeout_s > 0) tick_th_ = std::thread([this] { ticker(); });
+  }
+}
+
+void Node::ticker() {
+  // Deadline checks run on the event loop: this thread only posts Ticks.
+  const double period = std::min(0.25, std::max(0.01, cfg_.job_timeout_s / 4));
+  std::unique_lock<std::mutex> lk(tick_mu_);
+  while (!cv_wait_for(tick_cv_, lk, period, [&] { return tick_stop_; })) {
+    auto m = std::make_shared<Message>();
+    m->type = MsgType::Tick;
+    m->epoch = cfg_.epoch;
+    t_->inject(m);
   }
 }
 
 void Node::stop() {
   if (!running_.exchange(false)) return;
+  {
+    std::lock_guard<std::mutex> lk(tick_mu_);
+    tick_stop_ = true;
+  }
+  tick_cv_.notify_all();
+  if (tick_th_.joinable()) tick_th_.join();
   e_->quiesce();
   auto m = std::make_shared<Message>();
   m->type = MsgType::Stop;
@@ -177,11 +197,16 @@ void Node::handle(const MessagePtr& m) {
     case MsgType::Simple:
       log::info(int64_t(cfg_.id)).s("from", m->src_addr).msg(m->payload_str);
       break;
+    case MsgType::Nack:
+      if (is_leader_) on_nack(m);
+      break;
     case MsgType::Tick:
       if (is_leader_ && !started_) {
         bool all = true;
         for (auto& kv : assignment_) all = all && status_.count(kv.first);
         if (all && !assignment_.empty()) start_distribution();
+      } else if (is_leader_) {
+        on_tick();
       }
       break;
     default:
@@ -367,6 +392,7 @@ void Node::start_distribution() {
     stats_.bytes_planned = planned;
     sig_cv_.notify_all();
   }
+  initial_status_ = status_;
   log::info(int64_t(cfg_.id)).i("mode", cfg_.mode).i("bytes_planned", planned).msg("timer start");
   int64_t t0 = log::now_us();
   switch (cfg_.mode) {
@@ -424,6 +450,7 @@ void Node::on_ack(const MessagePtr& m) {
     meta.size = layer_size(m->layer);
     status_[m->src][m->layer] = meta;  // node.go:413-417
   }
+  outstanding_.erase({m->src, m->layer});
   if (!satisfied_ && assignment_satisfied()) {
     // Fire exactly once (quirk Q13).
     {
@@ -462,6 +489,144 @@ void Node::on_ack(const MessagePtr& m) {
   if (m->src != job.sender)
     while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
     }
+  flush_batch();
+}
+
+// ------------------------------------------------------- failure handling
+
+void Node::track(NodeID sender, NodeID dest, LayerID layer, int64_t off, int64_t size) {
+  if (cfg_.job_timeout_s <= 0 || !is_leader_) return;
+  outstanding_[{dest, layer}].push_back({sender, off, size, log::now_us()});
+}
+
+NodeID Node::alternative_owner(LayerID layer, NodeID dest, NodeID avoid) {
+  // Any live holder of the layer (announced or acked since), the least busy first.
+  std::map<NodeID, int> busy;
+  for (auto& kv : outstanding_)
+    for (auto& o : kv.second) busy[o.sender]++;
+  NodeID best = kClientID;
+  int best_busy = INT_MAX;
+  for (auto& kv : status_) {
+    NodeID n = kv.first;
+    if (n == dest || n == avoid || suspects_.count(n) || !kv.second.count(layer)) continue;
+    if (busy[n] < best_busy) {
+      best = n;
+      best_busy = busy[n];
+    }
+  }
+  return best;
+}
+
+void Node::on_tick() {
+  if (!started_ || satisfied_ || cfg_.job_timeout_s <= 0 || e_->planned()) return;
+  const int64_t now = log::now_us();
+  struct Expired {
+    NodeID dest;
+    LayerID layer;
+    Outstanding o;
+  };
+  std::vector<Expired> expired;
+  for (auto it = outstanding_.begin(); it != outstanding_.end();) {
+    auto& v = it->second;
+    for (auto o = v.begin(); o != v.end();) {
+      double allow = cfg_.job_timeout_s + (cfg_.job_min_rate > 0 ? double(o->size) / cfg_.job_min_rate : 0.0);
+      if (double(now - o->t_us) / 1e6 > allow) {
+        expired.push_back({it->first.first, it->first.second, *o});
+        o = v.erase(o);
+      } else {
+        ++o;
+      }
+    }
+    it = v.empty() ? outstanding_.erase(it) : std::next(it);
+  }
+  for (auto& e : expired) {
+    if (!suspects_.count(e.o.sender) && e.o.sender != cfg_.id && e.o.sender != e.dest) {
+      suspects_.insert(e.o.sender);
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.suspects++;
+    }
+    int& n = redispatches_[{e.dest, e.layer, e.o.off}];
+    NodeID alt = alternative_owner(e.layer, e.dest, e.o.sender);
+    if (alt == kClientID || ++n > cfg_.max_redispatch) {
+      log::error(int64_t(cfg_.id)).u("layer", e.layer).u("dest", e.dest).u("sender", e.o.sender)
+          .msg(alt == kClientID ? "job deadline expired and no other owner holds the layer"
+                                : "job deadline expired too often; giving up on this range");
+      track(e.o.sender, e.dest, e.layer, e.o.off, e.o.size);  // keep watching the original sender
+      continue;
+    }
+    log::warn(int64_t(cfg_.id)).u("layer", e.layer).u("dest", e.dest).u("sender", e.o.sender).u("new_sender", alt)
+        .i("offset", e.o.off).i("size", e.o.size).msg("job deadline expired: re-dispatching from another owner");
+    {
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.redispatched++;
+    }
+    if (cfg_.mode == 2) {
+      // Keep the pull scheduler's books: the job now belongs to `alt`.
+      auto lj = jobs_.find(e.layer);
+      if (lj != jobs_.end()) {
+        auto jt = lj->second.find(e.dest);
+        if (jt != lj->second.end()) {
+          if (jt->second.state == JobState::Sending) inflight_[jt->second.sender] = std::max(0, inflight_[jt->second.sender] - 1);
+          jt->second.sender = alt;
+          jt->second.state = JobState::Sending;
+          jt->second.t_us = now;
+          inflight_[alt]++;
+        }
+      }
+    }
+    if (e.o.off == 0 && e.o.size >= layer_size(e.layer)) {
+      retransmit(e.layer, alt, e.dest);
+    } else {
+      track(alt, e.dest, e.layer, e.o.off, e.o.size);
+      if (alt == cfg_.id) {
+        send_layer(e.dest, e.layer, e.o.off, e.o.size, 0);
+      } else {
+        Message f;
+        f.type = MsgType::FlowRetransmit;
+        f.layer = e.layer;
+        f.dest = e.dest;
+        f.offset = e.o.off;
+        f.data_size = e.o.size;
+        send_msg(alt, f);
+      }
+    }
+  }
+  if (cfg_.mode == 2 && !expired.empty()) {
+    // Pending jobs queued on a suspect move to live senders.
+    for (auto& lj : jobs_)
+      for (auto& jd : lj.second)
+        if (jd.second.state == JobState::Pending && suspects_.count(jd.second.sender)) {
+          load_[jd.second.sender] = std::max<int64_t>(0, load_[jd.second.sender] - 1);
+          NodeID s = min_loaded_sender(lj.first);
+          if (s == kClientID) continue;
+          jd.second.sender = s;
+          load_[s]++;
+        }
+    for (auto& kv : load_)
+      if (!suspects_.count(kv.first))
+        while (inflight_[kv.first] < cfg_.pull_window && assign_new_job(kv.first)) {
+        }
+  }
+}
+
+void Node::on_nack(const MessagePtr& m) {
+  // A receiver's chunk failed its CRC (planned engines): re-send that range,
+  // preferably from a holder that had the layer before the session started
+  // (its copy was checked against the manifest when it was staged).
+  const NodeID dest = m->src, bad = m->dest;
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.nacks++;
+  }
+  std::vector<NodeID> cand;
+  for (auto& kv : initial_status_)
+    if (kv.first != dest && kv.first != bad && kv.second.count(m->layer)) cand.push_back(kv.first);
+  NodeID src = bad;
+  if (!cand.empty()) src = cand[size_t(rng_() % cand.size())];
+  log::warn(int64_t(cfg_.id)).u("layer", m->layer).u("dest", dest).u("bad_sender", bad).u("new_sender", src)
+      .i("offset", m->offset).i("size", m->data_size).msg("chunk failed its CRC: re-sending");
+  if (!e_->planned()) return;
+  add_job(src, dest, m->layer, m->offset, m->data_size);
   flush_batch();
 }
 
@@ -528,6 +693,7 @@ void Node::retransmit(LayerID layer, NodeID owner, NodeID dest) {
     add_job(owner, dest, layer, 0, -1);
     return;
   }
+  track(owner, dest, layer, 0, layer_size(layer));
   if (owner == cfg_.id) {
     LayerSrc src;
     int64_t rate = store_.get(layer, &src) ? src.meta.limit_rate : 0;
@@ -588,9 +754,13 @@ void Node::schedule_mode0() {
         for (NodeID d : remote) add_job(cfg_.id, d, kv.first, 0, -1);
       }
     } else if (remote.size() >= 2 && e_->supports_broadcast() && src.meta.location != Location::Client) {
+      for (NodeID d : remote) track(cfg_.id, d, kv.first, 0, src.data_size);
       e_->broadcast_layer(kv.first, src.data_size, remote);
     } else {
-      for (NodeID d : remote) send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
+      for (NodeID d : remote) {
+        track(cfg_.id, d, kv.first, 0, src.data_size);
+        send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
+      }
     }
   }
 }
@@ -653,6 +823,7 @@ NodeID Node::min_loaded_sender(LayerID layer) {
   int64_t min_count = INT64_MAX;
   for (auto& kv : load_) {
     NodeID sender = kv.first;
+    if (suspects_.count(sender)) continue;  // missed a deadline: no new work
     auto st = status_.find(sender);
     if (st == status_.end()) continue;
     auto it = st->second.find(layer);
@@ -736,6 +907,7 @@ bool Node::assign_new_job(NodeID node) {
   // node.go:909-945
   LayerID layer = 0;
   NodeID dest = 0, victim = 0;
+  if (suspects_.count(node)) return false;
   if (rarest_own_job(node, &layer, &dest)) {
     Job& j = jobs_[layer][dest];
     j.state = JobState::Sending;
@@ -839,8 +1011,12 @@ void Node::schedule_mode3() {
       std::lock_guard<std::mutex> lk(sig_mu_);
       stats_.jobs_dispatched++;
     }
-    if (e_->planned()) add_job(sj.dest, sj.dest, sj.layer, 0, sj.size);
-    else send_msg(sj.dest, f);
+    if (e_->planned()) {
+      add_job(sj.dest, sj.dest, sj.layer, 0, sj.size);
+    } else {
+      track(sj.dest, sj.dest, sj.layer, 0, sj.size);
+      send_msg(sj.dest, f);
+    }
   }
   if (demands.empty()) {
     log::info(int64_t(cfg_.id)).msg("No jobs to assign other than self-assignment");
@@ -878,8 +1054,12 @@ void Node::schedule_mode3() {
       std::lock_guard<std::mutex> lk(sig_mu_);
       stats_.jobs_dispatched++;
     }
-    if (e_->planned()) add_job(j.sender, j.dest, j.layer, j.offset, j.size);
-    else send_msg(j.sender, f);
+    if (e_->planned()) {
+      add_job(j.sender, j.dest, j.layer, j.offset, j.size);
+    } else {
+      track(j.sender, j.dest, j.layer, j.offset, j.size);
+      send_msg(j.sender, f);
+    }
   }
 }
 

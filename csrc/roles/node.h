@@ -38,6 +38,13 @@ struct NodeConfig {
   int64_t align = 1;                // mode 3: byte alignment of ranges
   std::string storage_path;         // receiver persist dir ("" = none)
   bool relay = true;                // planned mode 0: scatter + peer relay instead of leader fan-out
+  // Failure handling (the reference waits forever for a dead
+  // sender's ack). Leader, host engines: a job not acked within
+  // job_timeout_s + bytes/job_min_rate is re-dispatched from another owner and
+  // its sender is suspected (no new jobs). 0 = off (reference behavior).
+  double job_timeout_s = 0;
+  double job_min_rate = 0;          // B/s allowance added to the deadline (0 = flat timeout)
+  int max_redispatch = 8;           // per (dest, layer, range)
 };
 
 struct NodeStats {
@@ -48,6 +55,9 @@ struct NodeStats {
   int64_t bytes_received = 0;
   double flow_T = 0;             // mode 3 planned completion time (s)
   double plan_ms = 0;            // scheduling time
+  int64_t nacks = 0;             // leader: chunk re-sends requested by receivers (CRC mismatch)
+  int64_t redispatched = 0;      // leader: jobs re-sent from another owner after their deadline
+  int64_t suspects = 0;          // leader: senders that missed a deadline
 };
 
 class Node {
@@ -105,6 +115,12 @@ class Node {
   bool assignment_satisfied();
   void send_startup();
   void start_distribution();
+  // failure handling (leader)
+  void on_nack(const MessagePtr& m);
+  void on_tick();
+  void track(NodeID sender, NodeID dest, LayerID layer, int64_t off, int64_t size);
+  NodeID alternative_owner(LayerID layer, NodeID dest, NodeID avoid);
+  void ticker();
   int64_t layer_size(LayerID l);
   void retransmit(LayerID layer, NodeID owner, NodeID dest);
   void add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase = 0);
@@ -154,6 +170,19 @@ class Node {
   std::vector<PendingJob> pending_jobs_;
   uint64_t next_seq_ = 1, next_batch_ = 1;
   std::map<LayerID, CrcManifest> manifests_;
+  // failure handling (leader, event-loop thread)
+  struct Outstanding {
+    NodeID sender;
+    int64_t off, size, t_us;
+  };
+  std::map<std::pair<NodeID, LayerID>, std::vector<Outstanding>> outstanding_;  // (dest, layer)
+  std::map<std::tuple<NodeID, LayerID, int64_t>, int> redispatches_;
+  std::set<NodeID> suspects_;
+  Status initial_status_;  // inventories at start (re-send sources for NACKs)
+  std::thread tick_th_;
+  std::mutex tick_mu_;
+  std::condition_variable tick_cv_;
+  bool tick_stop_ = false;
 
   // cross-thread signalling
   std::mutex sig_mu_;

@@ -96,7 +96,7 @@ static void ring(bool tcp, int mode) {
 }
 
 // Planned engine on the simulated fabric: 4 ranks, full replication, mode 1.
-static void planned_sim(int mode) {
+static void planned_sim(int mode, double corrupt = 0) {
   const int n = 4, L = 6;
   const int64_t chunk = 1 << 16, size = 3 * chunk + 100;
   static int uniq = 0;
@@ -117,6 +117,8 @@ static void planned_sim(int mode) {
     pc.rank = i;
     pc.world = n;
     pc.chunk_bytes = chunk;
+    pc.inject_corrupt = corrupt;
+    pc.max_retries = 16;
     auto e = std::make_shared<PlannedEngine>(pc, make_sim_backend(key, i, n));
     LayersSrc mine;
     for (int l = 0; l < L; ++l) {
@@ -161,6 +163,7 @@ int main() {
     ring(true, mode);
   }
   for (int mode = 1; mode <= 3; ++mode) planned_sim(mode);
+  planned_sim(1, 0.3);  // NACK / re-send path under injected corruption
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;

@@ -58,8 +58,24 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-c", action="store_true", help="if the process is client")
     p.add_argument("-v", action="store_true", help="output debug messages")
     # extensions
-    p.add_argument("--engine", default="host", choices=["host", "rccl"])
+    p.add_argument("--engine", default="auto", choices=["auto", "host", "rccl"],
+                   help="data plane: host (TCP into RAM, the reference) or rccl (RCCL/xGMI into HBM); "
+                        "auto = rccl under torchrun with a GPU visible, else host")
+    p.add_argument("--transport", default=None, choices=["tcp", "rccl"], help="alias: tcp = --engine host")
     p.add_argument("--chunk-mib", type=int, default=64)
+    p.add_argument("--chunk-bytes", type=int, default=0, help="chunk grid in bytes (overrides --chunk-mib)")
+    p.add_argument("--pack", default="none", choices=["none", "fp8"],
+                   help="fp8: bf16 layers are packed to block-scaled e4m3fn on staging (wire + HBM format)")
+    p.add_argument("--pack-block", type=int, default=128, help="elements per fp8 scale")
+    p.add_argument("--verify", default="crc32c", choices=["none", "crc32c"])
+    p.add_argument("--streams-per-peer", type=int, default=1,
+                   help="P2P ops per peer and direction in one RCCL group")
+    p.add_argument("--inject", action="append", default=[], metavar="SPEC",
+                   help="fault injection: drop-chunk=P | kill-rank=R@T | slow-link=S:D:RATE")
+    p.add_argument("--job-timeout", type=float, default=0.0,
+                   help="leader: re-dispatch a job not acked within this many seconds (+ bytes/--job-min-rate)")
+    p.add_argument("--job-min-rate", type=float, default=0.0)
+    p.add_argument("--max-retries", type=int, default=4, help="CRC failures of one chunk before giving up")
     p.add_argument("--seed", type=int, default=0, help="mode-1 owner RNG seed")
     p.add_argument("--owner-policy", default="random", choices=["random", "balanced"])
     p.add_argument("--pull-window", type=int, default=1)
@@ -79,7 +95,16 @@ def main(argv=None) -> int:
 
         print(json.dumps(example_config().to_json(), indent=2))
         return 0
-    torchrun_rank = os.environ.get("RANK") if args.engine == "rccl" else None
+    if args.transport:
+        args.engine = "host" if args.transport == "tcp" else "rccl"
+    torchrun_rank = os.environ.get("RANK")
+    if args.engine == "auto":
+        args.engine = "host"
+        if torchrun_rank is not None:
+            import torch  # device_count() does not initialise the GPU
+
+            if torch.cuda.device_count() > 0:
+                args.engine = "rccl"
     if (args.id is None and torchrun_rank is None) or (args.id is not None and args.id < 0) or not args.f:
         print(USAGE)
         print()
@@ -109,6 +134,13 @@ def main(argv=None) -> int:
         return run_client(cfg, my_id)
 
     from .parallel.runtime import Runtime
+    from .utils.faults import arm_kill, parse_inject
+
+    try:
+        faults = parse_inject(args.inject)
+    except ValueError as e:
+        print(json.dumps({"level": "error", "error": str(e), "message": "--inject"}), file=sys.stderr)
+        return 2
 
     barrier = None
     uid = None
@@ -131,8 +163,12 @@ def main(argv=None) -> int:
     client = cfg.client(my_id)
     if client is not None:
         registry[_core.CLIENT_ID] = client.addr
-    rt = Runtime(cfg, my_id, engine=args.engine, storage_path=args.s, chunk_bytes=args.chunk_mib << 20,
-                 verify=not args.no_verify, registry=registry, barrier=barrier, nccl_uid=uid, device=device)
+    rt = Runtime(cfg, my_id, engine=args.engine, storage_path=args.s,
+                 chunk_bytes=args.chunk_bytes or (args.chunk_mib << 20),
+                 verify=not args.no_verify and args.verify != "none", registry=registry, barrier=barrier,
+                 nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block,
+                 inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
+                 host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer)
     if args.l:
         print(json.dumps({"level": "info", "node": my_id, "message": "layer set up"}), file=sys.stderr)
         rt.close()
@@ -145,18 +181,23 @@ def main(argv=None) -> int:
               file=sys.stderr)
         return 1
     policy = dict(seed=args.seed, owner_policy=args.owner_policy, pull_window=args.pull_window,
-                  relay=not args.no_relay)
+                  relay=not args.no_relay, job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate)
     rt.prepare(args.m, **policy)
     if barrier:
         barrier()
+    arm_kill(faults, my_id)
     res = rt.execute(args.timeout, announce_retry_s=30.0)
     if role == "leader" and res.ok:
         print(f"Time to deliver: {go_duration(res.time_to_deliver_s)}", flush=True)
         if args.json_summary:
             gbps = res.bytes_planned / res.time_to_deliver_s / 1e9 if res.time_to_deliver_s > 0 else 0.0
-            print(json.dumps({"time_to_full_placement_s": res.time_to_deliver_s, "aggregate_GBps": gbps,
-                              "bytes_moved": res.bytes_planned, "ranks": len(cfg.nodes), "mode": args.m,
-                              "engine": args.engine, "plan_ms": res.plan_ms}), flush=True)
+            summary = {"time_to_full_placement_s": res.time_to_deliver_s, "aggregate_GBps": gbps,
+                       "bytes_moved": res.bytes_planned, "ranks": len(cfg.nodes), "mode": args.m,
+                       "engine": args.engine, "pack": args.pack, "plan_ms": res.plan_ms,
+                       "nacks": res.nacks, "redispatched": res.redispatched}
+            if res.engine_stats:
+                summary["engine"] = {"name": args.engine, **res.engine_stats}
+            print(json.dumps(summary), flush=True)
     if not res.ok:
         print(json.dumps({"level": "error", "node": my_id, "error": res.error, "message": f"{role} failed"}),
               file=sys.stderr)

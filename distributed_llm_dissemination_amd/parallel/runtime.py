@@ -50,6 +50,8 @@ class SessionResult:
     plan_ms: float = 0.0
     flow_T: float = 0.0
     error: str = ""
+    nacks: int = 0  # leader: chunk re-sends after CRC mismatches
+    redispatched: int = 0  # leader: jobs re-sent from another owner after a deadline
     engine_stats: Dict[str, float] = field(default_factory=dict)
 
 
@@ -72,6 +74,14 @@ class Runtime:
         listen_addr: Optional[str] = None,
         poison: bool = True,
         sim_key: str = "sim",
+        pack: str = "none",
+        pack_block: int = 128,
+        inject_corrupt: float = 0.0,
+        inject_seed: int = 1,
+        max_retries: int = 4,
+        group_timeout_s: float = 300.0,
+        host_link_rate: Optional[Dict[int, int]] = None,
+        group_peers: int = 1,
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -80,6 +90,13 @@ class Runtime:
         self.engine_kind = engine
         self.storage_path = storage_path
         self.chunk_bytes = cfg.chunk_bytes or chunk_bytes
+        if pack not in ("none", "fp8"):
+            raise ValueError(f"unknown pack format {pack!r}")
+        if pack != "none" and engine not in ("rccl", "sim"):
+            raise ValueError("--pack needs the planned (rccl/sim) data engine")
+        self.pack = pack
+        self.pack_block = pack_block
+        self.host_link_rate = dict(host_link_rate or {})
         self.verify = verify
         self.payload_seed = payload_seed
         self._barrier = barrier or (lambda: None)
@@ -107,6 +124,13 @@ class Runtime:
             pcfg.chunk_bytes = self.chunk_bytes
             pcfg.verify = verify
             pcfg.poison = poison
+            pcfg.pack = 1 if pack == "fp8" else 0
+            pcfg.pack_block = pack_block
+            pcfg.inject_corrupt = inject_corrupt
+            pcfg.inject_seed = inject_seed
+            pcfg.max_retries = max_retries
+            pcfg.group_timeout_s = group_timeout_s
+            pcfg.group_peers = group_peers
             if engine == "rccl":
                 dev = device if device is not None else (self.me.device if self.me.device is not None else 0)
                 if self.world > 1 and nccl_uid is None:
@@ -121,6 +145,14 @@ class Runtime:
             self.engine = None  # host engines are per session (they bind to one node)
         else:
             raise ValueError(f"unknown engine {engine}")
+        # Bytes of each layer in the target tier and on the wire (packed with --pack fp8),
+        # and the chunk grid transfers/CRCs run on.
+        if self.engine is not None:
+            self.slot_sizes = {l: self.engine.slot_size(s) for l, s in self.sizes.items()}
+            self.grid = self.engine.chunk_grid
+        else:
+            self.slot_sizes = dict(self.sizes)
+            self.grid = self.chunk_bytes
         self.layers = self._materialize()
 
     # ---- "device" memory helpers: HIP kernels for rccl, host code for the simulator
@@ -133,8 +165,38 @@ class Runtime:
 
     def _dev_crc(self, ptr: int, size: int) -> List[int]:
         if self.engine_kind == "rccl":
-            return _core.crc32c_chunks(ptr, size, self.chunk_bytes)
-        return _core.host_crc32c_chunks(ptr, size, self.chunk_bytes)
+            return _core.crc32c_chunks(ptr, size, self.grid)
+        return _core.host_crc32c_chunks(ptr, size, self.grid)
+
+    def _gen_layer(self, layer: int, size: int, seed: int, host_buf=None) -> None:
+        """Generate a layer's source bytes (random bf16 bit patterns when packing),
+        optionally copy them to `host_buf`, put the target-tier image (packed with
+        --pack fp8) into the layer's HBM slot and record its CRC manifest."""
+        slot = self.engine.device_ptr(layer)
+        ssz = self.slot_sizes[layer]
+        if self.engine_kind == "rccl":
+            if self.pack == "fp8":
+                tmp = _core.device_malloc(size)
+                try:
+                    _core.fill_random(tmp, size, seed)
+                    if host_buf is not None:
+                        _core.memcpy(host_buf.ptr, tmp, size)
+                    _core.fp8_pack_chunks(tmp, size, self.chunk_bytes, self.pack_block, slot)
+                    _core.device_synchronize()
+                finally:
+                    _core.device_free(tmp)
+            else:
+                self._dev_fill(slot, size, seed)
+                if host_buf is not None:
+                    _core.memcpy(host_buf.ptr, slot, size)
+        else:
+            data = _core.fill_random_host(size, seed)
+            if host_buf is not None:
+                _core.sim_write(host_buf.ptr, data)
+            if self.pack == "fp8":
+                data = _core.fp8_pack_layer_host(data, self.chunk_bytes, self.pack_block)
+            _core.sim_write(slot, data)
+        self.engine.set_manifest(layer, _core.CrcManifest(self.grid, self._dev_crc(slot, ssz)))
 
     def _dev_to_host(self, dst: int, src: int, size: int) -> None:
         if self.engine_kind == "rccl":
@@ -153,7 +215,7 @@ class Runtime:
             for per in self.me.initial_layers.values():
                 want |= set(per)
             for l in sorted(want):
-                self.engine.provision(l, self.sizes[l])
+                self.engine.provision(l, self.slot_sizes[l])
         for st, per in sorted(self.me.initial_layers.items()):
             rate = self.me.sources.get(st, 0)
             for l, size in sorted(per.items()):
@@ -162,19 +224,25 @@ class Runtime:
                     layers[l] = _core.LayerSrc.client(size, rate)
                 elif st == SOURCE_DISK or (self.storage_path and st != SOURCE_DEVICE):
                     path = self._disk_layer(l, size, seed)
-                    layers[l] = _core.LayerSrc.disk(path, size, rate, _core.SourceType(st))
+                    # the file holds the source bytes; the layer's size is its slot size
+                    layers[l] = _core.LayerSrc.disk(path, self.slot_sizes[l], rate, _core.SourceType(st))
                     if gpu:
-                        self._gpu_manifest_from_host(l, size, seed)
+                        self._gen_layer(l, size, seed)
                 elif st == SOURCE_DEVICE and gpu:
                     ptr = self.engine.device_ptr(l)
-                    self._dev_fill(ptr, size, seed)
-                    self.engine.set_manifest(l, _core.CrcManifest(self.chunk_bytes, self._dev_crc(ptr, size)))
+                    self._gen_layer(l, size, seed)
                     self.engine.set_seeded(l, True)
-                    layers[l] = _core.layer_src_device(ptr, size)
+                    layers[l] = _core.layer_src_device(ptr, self.slot_sizes[l])
                 elif gpu:
                     buf = _core.HostBuffer.pinned(size) if self.engine_kind == "rccl" else _core.HostBuffer.malloc(size)
-                    self._gpu_fill_host(l, buf, size, seed)
-                    layers[l] = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
+                    self._gen_layer(l, size, seed, host_buf=buf)
+                    src = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
+                    if self.slot_sizes[l] != size:  # packed: bf16 source, fp8 slot
+                        src.data_size = self.slot_sizes[l]
+                        meta = src.meta
+                        meta.size = self.slot_sizes[l]
+                        src.meta = meta
+                    layers[l] = src
                 else:
                     data = _core.fill_random_host(size, seed)
                     layers[l] = _core.LayerSrc.inmem(data, rate, _core.SourceType(st))
@@ -201,19 +269,6 @@ class Runtime:
             os.replace(tmp, path)
         return path
 
-    def _gpu_fill_host(self, layer: int, buf, size: int, seed: int) -> None:
-        """Random payload generated on the GPU, checksummed, then copied into pinned host memory."""
-        ptr = self.engine.device_ptr(layer)
-        self._dev_fill(ptr, size, seed)
-        crc = self._dev_crc(ptr, size)
-        self._dev_to_host(buf.ptr, ptr, size)
-        self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, crc))
-
-    def _gpu_manifest_from_host(self, layer: int, size: int, seed: int) -> None:
-        ptr = self.engine.device_ptr(layer)
-        self._dev_fill(ptr, size, seed)
-        self.engine.set_manifest(layer, _core.CrcManifest(self.chunk_bytes, self._dev_crc(ptr, size)))
-
     # ---------------------------------------------------------- sessions
     def run(self, mode: int, *, timeout: float = 600.0, **policy) -> SessionResult:
         """prepare() + barrier + execute(): one full dissemination session."""
@@ -230,6 +285,8 @@ class Runtime:
         pull_window: int = 1,
         relay: bool = True,
         integer_seconds: bool = False,
+        job_timeout_s: float = 0.0,
+        job_min_rate: float = 0.0,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed)."""
         self.epoch += 1
@@ -248,8 +305,10 @@ class Runtime:
         nc.network_bw = {k: v for k, v in self.cfg.network_bw().items()}
         nc.link_bw = {(s, d): bw for s, per in self.cfg.links.items() for d, bw in per.items()}
         nc.integer_seconds = integer_seconds
-        nc.align = self.chunk_bytes if self.engine is not None else 1
-        eng = self.engine if self.engine is not None else _core.host_engine()
+        nc.job_timeout_s = job_timeout_s
+        nc.job_min_rate = job_min_rate
+        nc.align = self.grid if self.engine is not None else 1
+        eng = self.engine if self.engine is not None else _core.host_engine(self.host_link_rate)
         assign = {k: v for k, v in self.cfg.assignment.items()} if self.is_leader else {}
         node = _core.Node(nc, self.transport, eng, self.layers, assign, self.is_leader)
         node.start()
@@ -290,6 +349,8 @@ class Runtime:
             plan_ms=st.plan_ms,
             flow_T=st.flow_T,
             error=err if err else ("" if ok else "timeout waiting for Ready()"),
+            nacks=st.nacks,
+            redispatched=st.redispatched,
         )
         if self.engine is not None and ok:
             self.engine.quiesce()  # trailing verifications of chunks nobody waited for
@@ -305,20 +366,51 @@ class Runtime:
         return {
             k: getattr(es, k)
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
-                      "verify_failures", "unverified_pieces", "issue_ms")
+                      "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms")
         }
 
+    def link_bytes(self) -> Dict[str, Dict[int, int]]:
+        """Cumulative bytes this rank sent to / received from each peer rank (per-link counters)."""
+        es = self.engine.stats()
+        return {"sent": dict(es.peer_sent), "recv": dict(es.peer_recv)}
+
     def layer_bytes(self, layer: int) -> bytes:
-        """Bytes of a layer in this rank's target tier (tests / verification)."""
+        """Bytes of a layer in this rank's target tier (packed with --pack fp8)."""
         if self.engine is not None:
             ptr = self.engine.device_ptr(layer)
+            n = self.slot_sizes[layer]
             if self.engine_kind == "sim":
-                return _core.sim_read(ptr, self.sizes[layer])
-            buf = _core.HostBuffer.malloc(self.sizes[layer])
-            _core.memcpy(buf.ptr, ptr, self.sizes[layer])
+                return _core.sim_read(ptr, n)
+            buf = _core.HostBuffer.malloc(n)
+            _core.memcpy(buf.ptr, ptr, n)
             return buf.bytes()
         src = self._last_node.layer(layer)
         return src.host_bytes() if src is not None else b""
+
+    def unpacked_layer_bytes(self, layer: int) -> bytes:
+        """A packed layer dequantized back to bf16 after checking every packed chunk
+        against the manifest (rccl: the fused verify+unpack kernel, one pass over HBM)."""
+        if self.pack != "fp8":
+            return self.layer_bytes(layer)
+        size = self.sizes[layer]
+        ptr = self.engine.device_ptr(layer)
+        if self.engine_kind == "sim":
+            packed = _core.sim_read(ptr, self.slot_sizes[layer])
+            got = _core.host_crc32c_chunks(ptr, self.slot_sizes[layer], self.grid)
+            out = _core.fp8_unpack_layer_host(packed, size, self.chunk_bytes, self.pack_block)
+        else:
+            dev = _core.device_malloc(size)
+            try:
+                got = _core.fp8_verify_unpack(ptr, size, self.chunk_bytes, self.pack_block, dev)
+                buf = _core.HostBuffer.malloc(size)
+                _core.memcpy(buf.ptr, dev, size)
+                out = buf.bytes()
+            finally:
+                _core.device_free(dev)
+        want = self.engine.manifest().get(layer)
+        if want is not None and list(got) != list(want.crc):
+            raise RuntimeError(f"layer {layer}: packed chunks do not match the CRC manifest")
+        return out
 
     def close(self) -> None:
         if self.engine is not None:

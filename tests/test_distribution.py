@@ -52,6 +52,14 @@ def mock_layers(core, ids, size):
     return {l: core.LayerSrc.inmem(os.urandom(size)) for l in ids}
 
 
+def wait_status(leader, node_id, timeout=5.0):
+    """Block until the leader has processed `node_id`'s announce."""
+    deadline = time.monotonic() + timeout
+    while node_id not in leader.status():
+        assert time.monotonic() < deadline, f"leader never saw node {node_id}'s announce"
+        time.sleep(0.01)
+
+
 def exec_distribution(leader, receivers, assignment, timeout=5.0):
     """node_test.go:107-145 execDistribution: announce, wait for start and ready."""
     for r in receivers:
@@ -223,7 +231,12 @@ def test_external_client_pipe(core, kind):
         leader = c.node(0, 1, {}, assignment)
         holder = c.node(1, 1, {5: core.LayerSrc.client(size, 0)})
         dest = c.node(2, 1, {})
-        exec_distribution(leader, [holder, dest], assignment)
+        # The holder is not an assignment key: the leader starts as soon as node 2
+        # announces, so node 1's announce must be in first (separate connections
+        # race otherwise; the reference has the same start rule, node.go:295-324).
+        holder.announce()
+        wait_status(leader, 1)
+        exec_distribution(leader, [dest], assignment)
         assert dest.layer(5).host_bytes() == data
         client.stop()
         ct.close()
@@ -259,3 +272,34 @@ def test_mode1_random_owner_is_seeded(core):
         finally:
             c.close()
     assert dest is not None
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_dead_sender_jobs_are_redispatched(core, mode):
+    """the reference waits forever for a dead sender's ack. With a
+    job deadline the leader re-sends the layer from another owner, suspects the
+    silent sender and finishes."""
+    L = 8
+    layers = mock_layers(core, range(L), 256 << 10)
+    assignment = {3: list(range(L))}
+    c = Cluster(core, "tcp", 4)
+    try:
+        leader = c.node(0, mode, {}, assignment, job_timeout_s=0.3, pull_window=2)
+        n1 = c.node(1, mode, layers)
+        n2 = c.node(2, mode, layers)
+        n3 = c.node(3, mode, {})
+        n1.announce()
+        n2.announce()
+        wait_status(leader, 1)
+        wait_status(leader, 2)
+        n1.stop()  # node 1 dies after announcing: its jobs never complete
+        c.ts[1].close()
+        n3.announce()
+        assert leader.wait_ready(15), "leader never satisfied"
+        assert n3.wait_ready(5)
+        for l in range(L):
+            assert n3.layer(l).host_bytes() == layers[l].host_bytes()
+        st = leader.stats()
+        assert st.redispatched >= 1 and st.suspects == 1
+    finally:
+        c.close()

@@ -23,10 +23,19 @@ MiB = 1 << 20
 _keys = itertools.count()
 
 
-def run_cluster(cfg, mode, sessions=1, chunk=MiB, **policy):
+def expected_image(rt, layer, size):
+    """The layer's bytes in the target tier: the source, or its fp8-packed form."""
+    data = _core.fill_random_host(size, layer_seed(0, layer))
+    if rt.pack == "fp8":
+        return _core.fp8_pack_layer_host(data, rt.chunk_bytes, rt.pack_block)
+    return data
+
+
+def run_cluster(cfg, mode, sessions=1, chunk=MiB, rt_kw=None, **policy):
     key = f"sim{next(_keys)}"
     n = len(cfg.nodes)
-    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=chunk, sim_key=key) for i in range(n)]
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=chunk, sim_key=key,
+                   **(rt_kw or {})) for i in range(n)]
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
         r.transport.set_registry(reg)
@@ -49,7 +58,7 @@ def run_cluster(cfg, mode, sessions=1, chunk=MiB, **policy):
             sizes = cfg.layer_sizes()
             for i, r in enumerate(rts):
                 for l in cfg.assignment.get(i, []):
-                    assert r.layer_bytes(l) == _core.fill_random_host(sizes[l], layer_seed(0, l)), (i, l)
+                    assert r.layer_bytes(l) == expected_image(r, l, sizes[l]), (i, l)
             out.append(res)
         return out, key
     finally:
@@ -122,6 +131,104 @@ def test_disk_tier_staging_through_bounce_ring(tmp_path):
             for i, r in enumerate(rts):
                 for l in range(6):
                     assert r.layer_bytes(l) == _core.fill_random_host(3 * MiB + 8192, layer_seed(0, l))
+    finally:
+        for r in rts:
+            r.close()
+
+
+# ---------------------------------------------------------------- fp8 wire/storage format
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("tier", ["host", "device"])
+def test_fp8_packed_replication(mode, tier):
+    """BASELINE config #5 shape: bf16 sources are packed to fp8 at staging; HBM
+    slots, P2P transfers and CRCs all run on the packed chunk grid, so the wire
+    carries ~0.53x the bf16 bytes."""
+    n, L, size = 4, 6, 3 * MiB + 4096
+    cfg = make_workload(n, L, size, tier=tier, seeding="random", chunk_bytes=MiB)
+    (res,), key = run_cluster(cfg, mode, rt_kw={"pack": "fp8"}, pull_window=n - 1)
+    packed = _core.fp8_packed_size(size, MiB, 128)
+    assert packed == 3 * (MiB // 2 + MiB // 64) + 2048 + 64
+    need = sum(1 for r in range(n) for l in range(L) if r not in _owners(cfg, l))
+    assert _core.sim_fabric_bytes(key) == need * packed  # every remote copy moved packed
+    assert res[0].engine_stats["verify_failures"] == 0
+
+
+def _owners(cfg, layer):
+    return {nd.id for nd in cfg.nodes for per in nd.initial_layers.values() if layer in per}
+
+
+def test_fp8_unpacked_layer_roundtrip_disk(tmp_path):
+    cfg = make_workload(3, 4, 2 * MiB, tier="disk", seeding="random", chunk_bytes=MiB)
+    key = f"sim{next(_keys)}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+                   storage_path=str(tmp_path), pack="fp8") for i in range(3)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for r in rts:
+            r.prepare(1)
+        res = [None] * 3
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        for r in rts:
+            for l in range(4):
+                src = _core.fill_random_host(2 * MiB, layer_seed(0, l))
+                packed = _core.fp8_pack_layer_host(src, MiB, 128)
+                assert r.layer_bytes(l) == packed
+                assert r.unpacked_layer_bytes(l) == _core.fp8_unpack_layer_host(packed, 2 * MiB, MiB, 128)
+    finally:
+        for r in rts:
+            r.close()
+
+
+# ------------------------------------------------------------- fault injection / NACK
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_corrupted_chunks_are_nacked_and_resent(mode):
+    """--inject drop-chunk=P: received chunks are damaged behind their P2P group;
+    the CRC check catches each one, the receiver NACKs it, the leader re-sends
+    it from a pre-session holder, and the session still delivers exact bytes."""
+    n = 4
+    seeding = "leader" if mode == 0 else "random"
+    cfg = make_workload(n, 6, 3 * MiB, tier="host", seeding=seeding, chunk_bytes=MiB)
+    (res,), key = run_cluster(cfg, mode, rt_kw={"inject_corrupt": 0.25, "inject_seed": 7, "max_retries": 8},
+                              pull_window=2)
+    injected = sum(r.engine_stats["injected"] for r in res)
+    assert injected > 0
+    failures = sum(r.engine_stats["verify_failures"] for r in res)
+    # A damaged chunk may already have been forwarded (relays cut through before
+    # the check), so its downstream receivers detect and NACK it as well.
+    assert failures >= injected
+    assert res[0].nacks == failures
+
+
+def test_corruption_beyond_retry_budget_fails_loudly():
+    cfg = make_workload(2, 1, 2 * MiB, tier="host", seeding="leader", chunk_bytes=MiB)
+    key = f"sim{next(_keys)}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+                   inject_corrupt=1.0, max_retries=2) for i in range(2)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for r in rts:
+            r.prepare(1)
+        res = [None] * 2
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(4))) for i in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert not res[1].ok and "retries exhausted" in res[1].error
+        assert not res[0].ok
     finally:
         for r in rts:
             r.close()
