@@ -50,7 +50,17 @@ def parse_args(argv=None):
     p.add_argument("--timeout", type=float, default=300.0)
     p.add_argument("--pull-window", type=int, default=0, help="mode 2 jobs in flight per sender (0 = peers)")
     p.add_argument("--storage", default="", help="disk tier directory")
-    return p.parse_args(argv)
+    p.add_argument("--pack", default="none", choices=["none", "fp8"],
+                   help="fp8: layers are bf16 sources packed to block-scaled e4m3fn while staging "
+                        "(HBM + wire format; BASELINE config #5)")
+    p.add_argument("--preset", default="", choices=["", "llama70b", "llama405b-fp8"],
+                   help="llama70b = 80 x 1 GiB (default); llama405b-fp8 = 126 x 3 GiB with --pack fp8")
+    args = p.parse_args(argv)
+    if args.preset == "llama405b-fp8":
+        args.layers, args.layer_mib, args.pack = 126, 3072, "fp8"
+    elif args.preset == "llama70b":
+        args.layers, args.layer_mib = 80, 1024
+    return args
 
 
 def relaunch_with_torchrun(args) -> int:
@@ -117,7 +127,11 @@ def main(argv=None) -> int:
     t_setup = time.time()
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
-                 barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage)
+                 barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack)
+    if args.pack != "none":
+        # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
+        src_bytes = total_bytes
+        total_bytes = src_bytes * rt.slot_sizes[0] // rt.sizes[0]
     if world > 1:
         addrs = [None] * world
         dist.all_gather_object(addrs, rt.transport.address())
@@ -184,10 +198,19 @@ def main(argv=None) -> int:
                 "time_to_full_placement_s": round(ms_per_step / 1e3, 6),
                 "leader_time_to_deliver_s": round(last.time_to_deliver_s, 6) if last else None,
                 "engine": "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)",
+                "pack": args.pack,
             },
         }
+        if args.pack != "none":
+            out["dtype"] = "fp8 e4m3fn (block-scaled, packed from bf16 on the GPU)"
+            out["config"]["model"] = f"{args.layers}x{args.layer_mib}MiB bf16 layers (Llama-3.1-405B-sized shards), fp8 in HBM"
+            out["config"]["bf16_source_bytes_per_step"] = src_bytes
+            out["config"]["bf16_equivalent_GBps"] = round(src_bytes * args.steps / total / 1e9, 3)
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
+        if world > 1:
+            out["config"]["link_bytes_rank0_cumulative"] = {k: {str(p): b for p, b in v.items()}
+                                                            for k, v in rt.link_bytes().items()}
         print(json.dumps(out), flush=True)
     rt.close()
     if world > 1:

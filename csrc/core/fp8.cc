@@ -49,7 +49,7 @@ uint8_t f32_to_e4m3(float x) {
 float e4m3_to_f32(uint8_t q) {
   const float s = (q & 0x80) ? -1.0f : 1.0f;
   const int e = (q >> 3) & 15, m = q & 7;
-  if (e == 15 && m == 7) return NAN;
+  if (e == 15 && m == 7) return std::copysign(NAN, s);
   if (e == 0) return s * std::ldexp(float(m), -9);
   return s * std::ldexp(1.0f + float(m) / 8.0f, e - 7);
 }

@@ -176,6 +176,13 @@ void register_gpu_bindings(PyObject* module) {
           "fp8_pack_chunks");
   }, py::arg("src"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("dst"),
         py::arg("stream") = 0);
+  m.def("fp8_verify_unpack_async", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block,
+                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream) {
+    check(kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
+                                  reinterpret_cast<uint16_t*>(out), reinterpret_cast<uint32_t*>(crc_out_dev),
+                                  reinterpret_cast<void*>(ws), as_stream(stream)),
+          "fp8_verify_unpack");
+  });
   // Fused verify + unpack (synchronous): writes the bf16 layer to `out`, returns
   // the CRC32C of every packed chunk.
   m.def("fp8_verify_unpack", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block, uint64_t out,

@@ -53,6 +53,20 @@ def main():
     out["fp8_pack_GBps"] = (2 * ne + ne + ne // 32) / t / 1e9
     t = timed(lambda: _core.fp8_unpack(q.data_ptr(), sc.data_ptr(), ne, y.data_ptr(), 128))
     out["fp8_unpack_GBps"] = (ne + ne // 32 + 2 * ne) / t / 1e9
+    # fp8 wire format: whole-layer pack into the chunked layout, and the fused
+    # verify (CRC32C per packed chunk) + unpack (bf16) pass a consumer runs.
+    src = n // 2  # 512 MiB of bf16
+    pbytes = _core.fp8_packed_size(src, chunk, 128)
+    packed = torch.empty(pbytes, dtype=torch.uint8, device="cuda")
+    unpacked = torch.empty(src, dtype=torch.uint8, device="cuda")
+    t = timed(lambda: _core.fp8_pack_chunks(buf.data_ptr(), src, chunk, 128, packed.data_ptr()))
+    out["fp8_pack_chunks_GBps"] = (src + pbytes) / t / 1e9
+    pchunk = chunk // 2 + chunk // 2 // 128 * 4
+    ws2 = torch.empty(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device="cuda")
+    t = timed(lambda: _core.fp8_verify_unpack_async(packed.data_ptr(), src, chunk, 128, unpacked.data_ptr(),
+                                                    res.data_ptr(), ws2.data_ptr(), 0))
+    out["fp8_verify_unpack_GBps"] = (pbytes + src) / t / 1e9
+    out["fp8_verify_unpack_ms_per_GiB_bf16"] = t * 1e3 * (1 << 30) / src
     t = timed(lambda: buf[: n // 2].copy_(buf[n // 2 :]))
     out["torch_copy_GBps"] = n / t / 1e9
     print(json.dumps({k: round(v, 2) for k, v in out.items()}))

@@ -51,3 +51,26 @@ def test_corrupt_manifest_is_detected(gpu):
         assert "CRC32C mismatch" in res.error
     finally:
         rt.close()
+
+
+@pytest.mark.parametrize("tier", ["host", "device", "disk"])
+def test_fp8_packed_session(gpu, tier, tmp_path):
+    """--pack fp8 on one GPU: bf16 sources are packed on the copy stream while
+    staging; the HBM slot holds the packed image the manifest was computed on,
+    and the fused verify+unpack kernel restores the bf16 layer."""
+    size = 3 * MiB + 4096
+    cfg = make_workload(1, 3, size, tier=tier, chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"}, pack="fp8",
+                 storage_path=str(tmp_path) if tier == "disk" else "")
+    try:
+        images = {l: rt.layer_bytes(l) for l in range(3)}  # after materialize: the packed image
+        for _ in range(2):
+            res = rt.run(1, timeout=60)
+            assert res.ok, res.error
+            assert res.engine_stats["verify_failures"] == 0
+            for l in range(3):
+                assert rt.layer_bytes(l) == images[l]
+                out = rt.unpacked_layer_bytes(l)
+                assert out == gpu.fp8_unpack_layer_host(images[l], size, MiB, 128)
+    finally:
+        rt.close()

@@ -112,3 +112,74 @@ def test_fp8_roundtrip_random_bit_patterns(gpu):
     assert ok.all()
     inf = torch.isinf(xf)
     assert torch.equal(yf[inf].sign(), xf[inf].sign())
+
+
+def _host_fp8_codes_close(got: bytes, want: bytes, n_q_per_chunk, pchunk):
+    """q codes may differ by one near rounding ties (gfx950 double rounding); scales must match."""
+    g = np.frombuffer(got, dtype=np.uint8)
+    w = np.frombuffer(want, dtype=np.uint8)
+    assert g.shape == w.shape
+    diff = np.nonzero(g != w)[0]
+    in_q = (diff % pchunk) < n_q_per_chunk(diff // pchunk)
+    assert in_q.all(), "scale bytes differ"
+    assert (np.abs(g[diff].astype(int) - w[diff].astype(int)) == 1).all()
+    assert len(diff) < g.size * 0.002
+
+
+@pytest.mark.parametrize("size,chunk,block", [(3 * (1 << 20) + 4096, 1 << 20, 128), (2 << 20, 1 << 20, 32),
+                                              ((1 << 20) + 1024, 64 << 10, 512)])
+def test_fp8_pack_chunks_matches_host_layout(gpu, size, chunk, block):
+    x = (torch.randn(size // 2, device="cuda") * 2).to(torch.bfloat16)
+    packed_n = gpu.fp8_packed_size(size, chunk, block)
+    out = _dev_bytes(packed_n)
+    gpu.fp8_pack_chunks(x.data_ptr(), size, chunk, block, out.data_ptr())
+    torch.cuda.synchronize()
+    want = gpu.fp8_pack_layer_host(x.view(torch.uint8).cpu().numpy().tobytes(), chunk, block)
+    pchunk = chunk // 2 + chunk // 2 // block * 4
+    last_q = (size % chunk) // 2 if size % chunk else chunk // 2
+
+    def n_q(c):
+        return np.where(c == (packed_n - 1) // pchunk, last_q, chunk // 2)
+
+    _host_fp8_codes_close(out.cpu().numpy().tobytes(), want, n_q, pchunk)
+
+
+@pytest.mark.parametrize("size,chunk,block", [(3 * (1 << 20) + 4096, 1 << 20, 128), (2 << 20, 1 << 20, 64),
+                                              ((1 << 20) + 1024, 64 << 10, 512), (64 << 20, 64 << 20, 128)])
+def test_fp8_fused_verify_unpack(gpu, size, chunk, block):
+    """One pass: CRC32C of every packed chunk + bf16 dequantization; compared with
+    the CRC kernel, the host CRC and the standalone unpack kernel (same math)."""
+    raw = _dev_bytes(size)
+    gpu.fill_random(raw.data_ptr(), size, 11)  # random bf16 bit patterns, NaN/Inf included
+    packed_n = gpu.fp8_packed_size(size, chunk, block)
+    packed = _dev_bytes(packed_n)
+    gpu.fp8_pack_chunks(raw.data_ptr(), size, chunk, block, packed.data_ptr())
+    out = _dev_bytes(size)
+    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr())
+    pchunk = chunk // 2 + chunk // 2 // block * 4
+    assert crcs == gpu.crc32c_chunks(packed.data_ptr(), packed_n, pchunk)
+    host = packed.cpu().numpy().tobytes()
+    assert crcs == [gpu.crc32c(host[o : o + pchunk]) for o in range(0, packed_n, pchunk)]
+    ref = _dev_bytes(size)
+    for c, off in enumerate(range(0, size, chunk)):
+        n = min(chunk, size - off) // 2
+        base = packed.data_ptr() + c * pchunk
+        gpu.fp8_unpack(base, base + n, n, ref.data_ptr() + off, block)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert out.cpu().numpy().tobytes() == gpu.fp8_unpack_layer_host(host, size, chunk, block)
+
+
+def test_fp8_fused_verify_unpack_detects_corruption(gpu):
+    size, chunk = 4 << 20, 1 << 20
+    raw = _dev_bytes(size)
+    gpu.fill_random(raw.data_ptr(), size, 5)
+    packed_n = gpu.fp8_packed_size(size, chunk, 128)
+    packed = _dev_bytes(packed_n)
+    gpu.fp8_pack_chunks(raw.data_ptr(), size, chunk, 128, packed.data_ptr())
+    out = _dev_bytes(size)
+    good = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, 128, out.data_ptr())
+    pchunk = chunk // 2 + chunk // 2 // 128 * 4
+    packed[2 * pchunk + chunk // 2 + 3] ^= 0x10  # a scale byte of chunk 2
+    bad = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, 128, out.data_ptr())
+    assert [i for i in range(4) if good[i] != bad[i]] == [2]
