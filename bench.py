@@ -50,6 +50,8 @@ def parse_args(argv=None):
     p.add_argument("--timeout", type=float, default=300.0)
     p.add_argument("--pull-window", type=int, default=0, help="mode 2 jobs in flight per sender (0 = peers)")
     p.add_argument("--storage", default="", help="disk tier directory")
+    p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
+                   help="mode 0: scatter+relay P2P, ncclBroadcast, or leader fan-out")
     p.add_argument("--pack", default="none", choices=["none", "fp8"],
                    help="fp8: layers are bf16 sources packed to block-scaled e4m3fn while staging "
                         "(HBM + wire format; BASELINE config #5)")
@@ -138,7 +140,8 @@ def main(argv=None) -> int:
         rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
     log(f"setup done in {time.time() - t_setup:.1f}s")
 
-    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1))
+    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1),
+                  relay=args.bcast == "relay", collective=args.bcast == "collective")
 
     def step(timed: bool):
         rt.prepare(args.mode, **policy)

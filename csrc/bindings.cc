@@ -350,6 +350,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("align", &NodeConfig::align)
       .def_readwrite("storage_path", &NodeConfig::storage_path)
       .def_readwrite("relay", &NodeConfig::relay)
+      .def_readwrite("collective", &NodeConfig::collective)
       .def_readwrite("job_timeout_s", &NodeConfig::job_timeout_s)
       .def_readwrite("job_min_rate", &NodeConfig::job_min_rate)
       .def_readwrite("max_redispatch", &NodeConfig::max_redispatch);

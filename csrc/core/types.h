@@ -17,6 +17,9 @@ namespace dissem {
 using NodeID = uint64_t;
 using LayerID = uint64_t;
 constexpr NodeID kClientID = ~uint64_t(0);  // client.go:10
+// XferJob destination meaning "every rank of the data-plane communicator": a
+// collective broadcast from the job's src (ncclBroadcast on the GPU).
+constexpr NodeID kAllRanks = ~uint64_t(0) - 1;
 
 enum class Location : uint8_t {
   Inmem = 0,   // host RAM (reference InmemLayer)

@@ -24,9 +24,10 @@ using Ev = uint64_t;  // 0 = no event
 
 struct XOp {
   bool send;
-  int peer;
+  int peer;  // partner rank; the root rank when bcast
   uint8_t* ptr;
   int64_t len;
+  bool bcast = false;  // collective broadcast of [ptr, ptr+len) from rank `peer` to every rank (in place)
 };
 
 class Backend {

@@ -440,7 +440,11 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
   for (auto& j : jobs) {
     Kind kind;
     int peer;
-    if (j.src == self_node_ && j.dst == self_node_) {
+    const bool bcast = j.dst == kAllRanks;
+    if (bcast) {
+      kind = j.src == self_node_ ? Kind::Send : Kind::Recv;
+      peer = rank_of(j.src);
+    } else if (j.src == self_node_ && j.dst == self_node_) {
       kind = Kind::Local;
       peer = cfg_.rank;
     } else if (j.src == self_node_) {
@@ -470,6 +474,7 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       const int64_t e = std::min(cend, end);
       Piece p{kind, j.seq, pidx, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
       p.src_node = j.src;
+      p.bcast = bcast;
       const int64_t ci = c - first_chunk;
       if (p.full && ci < int64_t(j.crc.size())) {
         p.has_crc = true;
@@ -503,6 +508,15 @@ bool PlannedEngine::issue_some() {
     size_t take = 0;
     for (; take < ops_.size(); ++take) {
       Piece& p = ops_[take];
+      if (p.bcast) {
+        // A collective runs in a group of its own (every rank reaches it at the
+        // same key, so the ordering argument above covers it too).
+        if (!group.empty()) break;
+        if (p.kind == Kind::Send && ensure_chunk(layer(p.layer), p.layer, p.chunk, false) <= 0) break;
+        group.push_back(p);
+        ++take;
+        break;
+      }
       if (p.kind == Kind::Send) {
         if (nsend[p.peer] >= cfg_.group_peers) break;
         if (recv_chunks.count({p.layer, p.chunk})) break;  // forward only after its recv is posted
@@ -534,7 +548,7 @@ bool PlannedEngine::issue_some() {
       } else {
         recvd += p.len;
       }
-      xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len});
+      xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len, p.bcast});
     }
     Ev g = backend_->group(xops, waits);
     groups_inflight_.push_back({g, std::chrono::steady_clock::now()});

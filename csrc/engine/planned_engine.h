@@ -114,6 +114,7 @@ class PlannedEngine : public DataEngine {
     bool has_crc = false;
     uint32_t crc = 0;
     NodeID src_node = 0;
+    bool bcast = false;  // collective from rank `peer` (root: Send with peer == own rank; others: Recv)
   };
   struct Layer {
     int64_t size = 0;

@@ -216,6 +216,21 @@ class SimBackend : public Backend {
         }
       std::vector<std::unique_ptr<Posted>> posted;
       for (auto& o : ops) {
+        if (o.bcast) {
+          // Broadcast = the root sends to every other rank, each of which receives
+          // from the root: same matching (and deadlock) semantics as a collective.
+          if (o.peer == rank) {
+            for (int r = 0; r < world_; ++r)
+              if (r != rank) {
+                posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
+                fab->post(rank, r, true, posted.back().get());
+              }
+          } else {
+            posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
+            fab->post(o.peer, rank, false, posted.back().get());
+          }
+          continue;
+        }
         if (o.peer < 0 || o.peer >= world_ || o.peer == rank) {
           set_error("bad peer");
           ev->state = -1;

@@ -105,7 +105,8 @@ class HipBackend : public Backend {
       if (!nccl_) throw std::runtime_error("P2P group on a single-rank engine");
       NCCL_OK(ncclGroupStart());
       for (auto& o : ops) {
-        if (o.send) NCCL_OK(ncclSend(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
+        if (o.bcast) NCCL_OK(ncclBroadcast(o.ptr, o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
+        else if (o.send) NCCL_OK(ncclSend(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
         else NCCL_OK(ncclRecv(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
       }
       NCCL_OK(ncclGroupEnd());

@@ -667,7 +667,12 @@ void Node::flush_batch() {
         XferJob j = pr.second[round];
         j.seq = next_seq_++;
         per_rank[j.src].jobs.push_back(j);
-        if (j.dst != j.src) per_rank[j.dst].jobs.push_back(j);
+        if (j.dst == kAllRanks) {
+          for (auto& st : status_)
+            if (st.first != j.src) per_rank[st.first].jobs.push_back(j);
+        } else if (j.dst != j.src) {
+          per_rank[j.dst].jobs.push_back(j);
+        }
       }
       if (!any) break;
     }
@@ -735,7 +740,12 @@ void Node::schedule_mode0() {
     if (e_->planned()) {
       const int64_t total = src.data_size;
       const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1);
-      if (cfg_.relay && remote.size() >= 2 && total >= int64_t(remote.size()) * cb) {
+      bool everyone = cfg_.collective && remote.size() >= 2 && remote.size() + 1 == status_.size();
+      if (everyone) {
+        // Collective: one ncclBroadcast per layer (chunk-pipelined) rooted at the
+        // leader; every rank of the communicator takes part.
+        add_job(cfg_.id, kAllRanks, kv.first, 0, total, 0);
+      } else if (cfg_.relay && remote.size() >= 2 && total >= int64_t(remote.size()) * cb) {
         // Bandwidth-optimal broadcast on a fully connected xGMI mesh: scatter
         // 1/k of the layer to each of k dests, then every dest relays its share
         // to the other k-1 (per-link load 2/k of the layer instead of 1).

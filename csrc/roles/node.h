@@ -38,6 +38,7 @@ struct NodeConfig {
   int64_t align = 1;                // mode 3: byte alignment of ranges
   std::string storage_path;         // receiver persist dir ("" = none)
   bool relay = true;                // planned mode 0: scatter + peer relay instead of leader fan-out
+  bool collective = false;          // planned mode 0: ncclBroadcast when every other rank needs the layer
   // Failure handling (the reference waits forever for a dead
   // sender's ack). Leader, host engines: a job not acked within
   // job_timeout_s + bytes/job_min_rate is re-dispatched from another owner and

@@ -80,6 +80,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--owner-policy", default="random", choices=["random", "balanced"])
     p.add_argument("--pull-window", type=int, default=1)
     p.add_argument("--no-relay", action="store_true", help="mode 0 on rccl: leader fan-out instead of relay")
+    p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
+                   help="mode 0 on rccl: relay = scatter + peer relay over all xGMI links; collective = "
+                        "ncclBroadcast per layer; fanout = leader sends every copy")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--timeout", type=float, default=3600.0)
     p.add_argument("--json-summary", action="store_true")
@@ -181,7 +184,8 @@ def main(argv=None) -> int:
               file=sys.stderr)
         return 1
     policy = dict(seed=args.seed, owner_policy=args.owner_policy, pull_window=args.pull_window,
-                  relay=not args.no_relay, job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate)
+                  relay=not args.no_relay and args.bcast != "fanout", collective=args.bcast == "collective",
+                  job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate)
     rt.prepare(args.m, **policy)
     if barrier:
         barrier()

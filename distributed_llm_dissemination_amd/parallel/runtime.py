@@ -284,6 +284,7 @@ class Runtime:
         owner_policy: str = "random",
         pull_window: int = 1,
         relay: bool = True,
+        collective: bool = False,
         integer_seconds: bool = False,
         job_timeout_s: float = 0.0,
         job_min_rate: float = 0.0,
@@ -302,6 +303,7 @@ class Runtime:
         nc.owner_policy = owner_policy
         nc.pull_window = pull_window
         nc.relay = relay
+        nc.collective = collective
         nc.network_bw = {k: v for k, v in self.cfg.network_bw().items()}
         nc.link_bw = {(s, d): bw for s, per in self.cfg.links.items() for d, bw in per.items()}
         nc.integer_seconds = integer_seconds

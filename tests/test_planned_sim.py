@@ -85,6 +85,24 @@ def test_mode0_broadcast_relay(n, relay):
     assert moved == (n - 1) * 4 * 4 * MiB  # relay moves the same bytes, spread over all links
 
 
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("tier", ["host", "device"])
+def test_mode0_collective_broadcast(n, tier):
+    """--bcast collective: one ncclBroadcast per chunk rooted at the leader; every
+    rank takes part and the receivers verify each chunk."""
+    cfg = make_workload(n, 3, 3 * MiB + 4096, tier=tier, seeding="leader", chunk_bytes=MiB)
+    (res,), key = run_cluster(cfg, 0, collective=True)
+    assert _core.sim_fabric_bytes(key) == (n - 1) * 3 * (3 * MiB + 4096)
+    assert sum(r.engine_stats["bytes_verified"] for r in res[1:]) > 0
+    if n >= 3:  # one collective piece per chunk of each layer on every rank
+        assert all(r.engine_stats["pieces"] == 3 * 4 for r in res)
+
+
+def test_mode0_collective_falls_back_when_not_everyone_needs_it():
+    cfg = make_workload(4, 4, 2 * MiB, tier="host", seeding="leader", assignment="pipeline", chunk_bytes=MiB)
+    run_cluster(cfg, 0, collective=True)
+
+
 def test_device_seeded_uneven_copies_mode1():
     cfg = make_workload(4, 12, 2 * MiB, tier="device", seeding="uniform", copies=2, seed=3, chunk_bytes=MiB)
     run_cluster(cfg, 1)
