@@ -272,6 +272,7 @@ PYBIND11_MODULE(_core, m) {
       .def("device_ptr", [](PlannedEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.device_ptr(l)); })
       .def("set_manifest", &PlannedEngine::set_manifest)
       .def("manifest", &PlannedEngine::manifest)
+      .def("set_source_packed", &PlannedEngine::set_source_packed)
       .def("set_seeded", &PlannedEngine::set_seeded)
       .def("reset_session", [](PlannedEngine& e) {
         py::gil_scoped_release nogil;

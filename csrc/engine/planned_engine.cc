@@ -89,7 +89,7 @@ int64_t PlannedEngine::slot_size(int64_t src_bytes) const {
 }
 
 int64_t PlannedEngine::src_len(const Layer& L, int64_t c) const {
-  if (cfg_.pack == 1) {
+  if (cfg_.pack == 1 && !L.src_packed) {
     const int64_t src = fp8::source_size(L.size, cfg_.chunk_bytes, cfg_.pack_block);
     return std::min(cfg_.chunk_bytes, src - c * cfg_.chunk_bytes);
   }
@@ -135,6 +135,11 @@ void PlannedEngine::set_seeded(LayerID id, bool resident) {
   Layer& L = layers_[id];
   L.seeded = resident;
   for (auto& s : L.st) s = resident ? 2 : 0;
+}
+
+void PlannedEngine::set_source_packed(LayerID id, bool packed) {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  layers_[id].src_packed = packed;
 }
 
 std::map<LayerID, CrcManifest> PlannedEngine::manifest() {
@@ -288,7 +293,7 @@ void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
     }
   }
   if (L.host) {
-    stage_from(L, id, c, L.host + c * cfg_.chunk_bytes, nullptr);  // source grid (== grid_ unless packing)
+    stage_from(L, id, c, L.host + c * src_grid(L), nullptr);
   } else {
     submit_disk(L, id, c);
   }
@@ -307,7 +312,7 @@ void PlannedEngine::submit_disk(Layer& L, LayerID id, int64_t c) {
   DiskRead d;
   d.layer = id;
   d.chunk = c;
-  d.file_off = L.path_off + c * cfg_.chunk_bytes;
+  d.file_off = L.path_off + c * src_grid(L);
   d.len = src_len(L, c);
   d.path = L.path;
   disk_wait_.push_back(std::move(d));
@@ -385,8 +390,8 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   const int64_t len = std::min(grid_, L.size - off);
   const int64_t slen = src_len(L, c);
   if (!L.dev) L.dev = backend_->alloc(L.size);
-  Ev e = cfg_.pack == 1 ? backend_->stage_pack(L.dev + off, src, slen, cfg_.pack_block)
-                        : backend_->stage(L.dev + off, src, len);
+  Ev e = cfg_.pack == 1 && !L.src_packed ? backend_->stage_pack(L.dev + off, src, slen, cfg_.pack_block)
+                                         : backend_->stage(L.dev + off, src, len);
   L.st[size_t(c)] = 1;
   L.ev[size_t(c)] = e;
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};

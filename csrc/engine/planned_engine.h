@@ -79,6 +79,9 @@ class PlannedEngine : public DataEngine {
   uint8_t* device_ptr(LayerID layer);
   void set_manifest(LayerID layer, const CrcManifest& m);
   void set_seeded(LayerID layer, bool device_resident);
+  // The layer's host/disk source is already in the slot format (e.g. a layer
+  // persisted by an earlier run): stage it byte for byte, without packing.
+  void set_source_packed(LayerID layer, bool packed);
   void reset_session();  // wait idle, forget landed chunks, poison non-seeded slots
   PlannedStats stats();
   std::string error();
@@ -124,6 +127,7 @@ class PlannedEngine : public DataEngine {
     const uint8_t* host = nullptr;   // host-tier source (set at first staging)
     std::string path;                // disk-tier source
     int64_t path_off = 0;
+    bool src_packed = false;         // the source already holds the packed image (persisted layers)
     // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk,
     // 4 failed its CRC and awaits the leader's re-send (still forwardable: a
     // later receiver detects it and NACKs too)
@@ -173,6 +177,7 @@ class PlannedEngine : public DataEngine {
   uint32_t crc_slot();
   void fail(const std::string& what);
   int64_t src_len(const Layer& L, int64_t c) const;  // source bytes of chunk c
+  int64_t src_grid(const Layer& L) const { return cfg_.pack == 1 && !L.src_packed ? cfg_.chunk_bytes : grid_; }
 
   PlannedConfig cfg_;
   int64_t grid_ = 0;  // chunk grid of HBM slots and transfers (packed chunk with pack=fp8)

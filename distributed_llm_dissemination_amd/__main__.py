@@ -76,6 +76,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="leader: re-dispatch a job not acked within this many seconds (+ bytes/--job-min-rate)")
     p.add_argument("--job-min-rate", type=float, default=0.0)
     p.add_argument("--max-retries", type=int, default=4, help="CRC failures of one chunk before giving up")
+    p.add_argument("--persist-dir", default="",
+                   help="after delivery, write this node's layers + CRC manifest here; on start, announce "
+                        "layers found here as disk-tier copies (resume without re-transfer)")
     p.add_argument("--seed", type=int, default=0, help="mode-1 owner RNG seed")
     p.add_argument("--owner-policy", default="random", choices=["random", "balanced"])
     p.add_argument("--pull-window", type=int, default=1)
@@ -171,7 +174,8 @@ def main(argv=None) -> int:
                  verify=not args.no_verify and args.verify != "none", registry=registry, barrier=barrier,
                  nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block,
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
-                 host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer)
+                 host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
+                 persist_dir=args.persist_dir)
     if args.l:
         print(json.dumps({"level": "info", "node": my_id, "message": "layer set up"}), file=sys.stderr)
         rt.close()
@@ -205,6 +209,10 @@ def main(argv=None) -> int:
     if not res.ok:
         print(json.dumps({"level": "error", "node": my_id, "error": res.error, "message": f"{role} failed"}),
               file=sys.stderr)
+    elif args.persist_dir and cfg.assignment.get(my_id):
+        done = rt.persist()
+        print(json.dumps({"level": "info", "node": my_id, "layers": done, "dir": args.persist_dir,
+                          "message": "layers persisted"}), file=sys.stderr)
     if barrier:
         barrier()
     time.sleep(0.05)  # let startup messages flush before sockets close

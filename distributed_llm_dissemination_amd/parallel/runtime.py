@@ -18,6 +18,7 @@ new epoch so stray messages from an earlier session are dropped.
 from __future__ import annotations
 
 import hashlib
+import json
 import os
 import time
 from dataclasses import dataclass, field
@@ -82,6 +83,7 @@ class Runtime:
         group_timeout_s: float = 300.0,
         host_link_rate: Optional[Dict[int, int]] = None,
         group_peers: int = 1,
+        persist_dir: str = "",
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -97,6 +99,7 @@ class Runtime:
         self.pack = pack
         self.pack_block = pack_block
         self.host_link_rate = dict(host_link_rate or {})
+        self.persist_dir = persist_dir
         self.verify = verify
         self.payload_seed = payload_seed
         self._barrier = barrier or (lambda: None)
@@ -251,7 +254,90 @@ class Runtime:
             for l, rate in client.layers.items():
                 if l not in layers:
                     layers[l] = _core.LayerSrc.client(self.cfg.layer_size, rate)
+        for l, (path, entry) in self._resumable().items():
+            if l in layers:
+                continue
+            # A layer this node received in an earlier run: announce it as a disk-tier
+            # copy, so the leader promotes it locally instead of moving it again.
+            layers[l] = _core.LayerSrc.disk(path, self.slot_sizes[l], 0, _core.SourceType.Disk)
+            if gpu:
+                self.engine.set_manifest(l, _core.CrcManifest(self.grid, entry["crc"]))
+                self.engine.set_source_packed(l, True)
+            self.resumed.append(l)
         return layers
+
+    # ------------------------------------------------------ persist / resume
+    PERSIST_MANIFEST = "manifest.json"
+
+    def _persist_root(self) -> str:
+        return os.path.join(self.persist_dir, str(self.node_id))
+
+    def _resumable(self) -> Dict[int, tuple]:
+        """Persisted layers whose file and manifest entry match this run's layout."""
+        self.resumed: List[int] = []
+        if not self.persist_dir:
+            return {}
+        root = self._persist_root()
+        try:
+            with open(os.path.join(root, self.PERSIST_MANIFEST)) as f:
+                man = json.load(f)
+        except (OSError, ValueError):
+            return {}
+        out = {}
+        for lid, e in man.get("layers", {}).items():
+            l = int(lid)
+            path = os.path.join(root, f"{l}.layer")
+            if (l not in self.sizes or e.get("size") != self.sizes[l] or e.get("stored") != self.slot_sizes[l]
+                    or e.get("pack") != self.pack or e.get("grid") != self.grid or not os.path.exists(path)
+                    or os.path.getsize(path) != e["stored"]):
+                continue
+            out[l] = (path, e)
+        return out
+
+    def persist(self, layers: Optional[List[int]] = None) -> List[int]:
+        """Write this node's target-tier layers (default: its assignment) to
+        <persist_dir>/<node>/<layer>.layer plus a manifest (size, slot size,
+        packing, chunk grid, CRC32C per chunk). SURVEY §5.4; a later run with
+        the same --persist-dir announces them as disk-tier layers."""
+        if not self.persist_dir:
+            raise ValueError("no persist_dir configured")
+        root = self._persist_root()
+        os.makedirs(root, exist_ok=True)
+        mpath = os.path.join(root, self.PERSIST_MANIFEST)
+        try:
+            with open(mpath) as f:
+                man = json.load(f)
+        except (OSError, ValueError):
+            man = {"layers": {}}
+        todo = layers if layers is not None else list(self.cfg.assignment.get(self.node_id, []))
+        done = []
+        for l in todo:
+            stored = self.slot_sizes[l]
+            path = os.path.join(root, f"{l}.layer")
+            tmp = path + ".tmp"
+            if self.engine is not None:
+                ptr = self.engine.device_ptr(l)
+                crc = self._dev_crc(ptr, stored)
+                step = max(self.grid, 64 * MiB // self.grid * self.grid)
+                buf = (_core.HostBuffer.pinned(step) if self.engine_kind == "rccl" else _core.HostBuffer.malloc(step))
+                with open(tmp, "wb") as f:
+                    for off in range(0, stored, step):
+                        n = min(step, stored - off)
+                        self._dev_to_host(buf.ptr, ptr + off, n)
+                        f.write(buf.view()[:n])
+            else:
+                data = self._last_node.layer(l).host_bytes()
+                crc = [_core.crc32c(data[o : o + self.grid]) for o in range(0, len(data), self.grid)]
+                with open(tmp, "wb") as f:
+                    f.write(data)
+            os.replace(tmp, path)
+            man["layers"][str(l)] = {"size": self.sizes[l], "stored": stored, "pack": self.pack,
+                                     "grid": self.grid, "crc": crc}
+            done.append(l)
+        with open(mpath + ".tmp", "w") as f:
+            json.dump(man, f)
+        os.replace(mpath + ".tmp", mpath)
+        return done
 
     def _disk_layer(self, layer: int, size: int, seed: int) -> str:
         """<s>/layers/<id>/<layer>.layer, written only if missing (config.go:133-157)."""

@@ -89,3 +89,52 @@ def test_go_duration_format():
     assert go_duration(62.5) == "1m2.5s"
     assert go_duration(12e-6) == "12µs"
     assert go_duration(0) == "0s"
+
+
+def write_config_rates(tmp_path, ports, size, holders, assign, rates):
+    nodes = []
+    for i, p in enumerate(ports):
+        nodes.append({
+            "Id": i, "Addr": f"127.0.0.1:{p}", "NetworkBW": 1562500000, "IsLeader": i == 0,
+            "Sources": {"2": rates.get(i, 0)},
+            "InitialLayers": {"2": {str(l): {"LayerSize": size} for l in holders.get(i, [])}},
+        })
+    cfg = {"Nodes": nodes, "Assignment": {str(k): {str(l): {} for l in v} for k, v in assign.items()}}
+    path = tmp_path / "config.json"
+    path.write_text(json.dumps(cfg))
+    return str(path)
+
+
+@pytest.mark.slow
+def test_kill_rank_injection_recovers_via_job_deadline(tmp_path):
+    """--inject kill-rank=1@T: node 1 (a rate-limited owner) dies mid-transfer;
+    the leader's job deadline re-dispatches its layers to node 2."""
+    ports = free_ports(4)
+    size = 2 << 20
+    holders = {1: [0, 1, 2, 3], 2: [0, 1, 2, 3]}
+    assign = {1: [0], 2: [0], 3: [0, 1, 2, 3]}  # 1 and 2 are keys so the leader waits for their announce
+    cfg = write_config_rates(tmp_path, ports, size, holders, assign, rates={1: 2 << 20})
+    extra = ["--inject", "kill-rank=1@0.5", "--job-timeout", "1.5", "--owner-policy", "balanced"]
+    (rc0, out0, err0), (rc1, _, err1), (rc2, _, err2), (rc3, _, err3) = run_nodes(cfg, [0, 1, 2, 3], 1, extra)
+    assert rc1 == 86, err1  # killed by the injection
+    assert rc0 == 0, err0[-3000:]
+    assert rc3 == 0, err3[-3000:]
+    summary = json.loads(out0.strip().splitlines()[-1])
+    assert summary["redispatched"] >= 1
+    assert "job deadline expired" in err0
+
+
+@pytest.mark.slow
+def test_persist_dir_resume_skips_network(tmp_path):
+    ports = free_ports(2)
+    cfg = write_config(tmp_path, ports)
+    pdir = str(tmp_path / "persist")
+    outs = run_nodes(cfg, [0, 1], 1, ["--persist-dir", pdir])
+    assert all(rc == 0 for rc, _, _ in outs), [e[-2000:] for _, _, e in outs]
+    assert "layers persisted" in outs[1][2]
+    assert "start receiving layer" in outs[1][2]
+    ports2 = free_ports(2)
+    cfg = write_config(tmp_path, ports2)
+    outs = run_nodes(cfg, [0, 1], 1, ["--persist-dir", pdir])
+    assert all(rc == 0 for rc, _, _ in outs), [e[-2000:] for _, _, e in outs]
+    assert "start receiving layer" not in outs[1][2]  # promoted from the persisted copies

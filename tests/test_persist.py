@@ -1,0 +1,111 @@
+"""--persist-dir checkpoint/resume (the reference only skips layers
+a node already announces, node.go:578-580, and keeps disk layers between runs).
+
+Run 1 disseminates and every rank persists its received layers with a CRC
+manifest. Run 2 (fresh processes' worth of state, same directory) announces them
+as disk-tier copies, so the leader only schedules local promotions: nothing
+crosses the fabric, and the staged bytes are still CRC-checked.
+"""
+
+import itertools
+import os
+import threading
+
+import pytest
+
+from distributed_llm_dissemination_amd import _core
+from distributed_llm_dissemination_amd.models.catalog import make_workload
+from distributed_llm_dissemination_amd.parallel.runtime import Runtime, layer_seed
+
+MiB = 1 << 20
+_keys = itertools.count()
+
+
+def _cluster(cfg, persist, **kw):
+    key = f"persist{next(_keys)}"
+    n = len(cfg.nodes)
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+                   persist_dir=str(persist), **kw) for i in range(n)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    return rts, key
+
+
+def _session(rts, mode=1, timeout=30):
+    for r in rts:
+        r.prepare(mode)
+    res = [None] * len(rts)
+    ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(timeout))) for i in range(len(rts))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return res
+
+
+@pytest.mark.parametrize("pack", ["none", "fp8"])
+def test_persist_then_resume_moves_nothing(tmp_path, pack):
+    size = 2 * MiB + 4096
+    cfg = make_workload(3, 6, size, tier="host", seeding="random", chunk_bytes=MiB)
+    rts, key = _cluster(cfg, tmp_path, pack=pack)
+    try:
+        res = _session(rts)
+        assert all(x.ok for x in res), [x.error for x in res]
+        assert _core.sim_fabric_bytes(key) > 0
+        images = {l: rts[1].layer_bytes(l) for l in range(6)}
+        for r in rts:
+            assert sorted(r.persist()) == list(range(6))
+    finally:
+        for r in rts:
+            r.close()
+    rts, key = _cluster(cfg, tmp_path, pack=pack)
+    try:
+        for r in rts:  # layers each node did not seed come back from the persist dir
+            seeded = {l for per in r.me.initial_layers.values() for l in per}
+            assert sorted(r.resumed) == sorted(set(range(6)) - seeded)
+        res = _session(rts)
+        assert all(x.ok for x in res), [x.error for x in res]
+        assert _core.sim_fabric_bytes(key) == 0  # everything promoted locally
+        for r in rts:
+            for l in range(6):
+                assert r.layer_bytes(l) == images[l]
+            assert r.engine.stats().bytes_verified > 0
+    finally:
+        for r in rts:
+            r.close()
+
+
+def test_resume_ignores_mismatched_layout_and_detects_corruption(tmp_path):
+    cfg = make_workload(2, 2, 2 * MiB, tier="host", seeding="random", chunk_bytes=MiB)
+    rts, _ = _cluster(cfg, tmp_path)
+    try:
+        assert all(x.ok for x in _session(rts))
+        for r in rts:
+            r.persist()
+    finally:
+        for r in rts:
+            r.close()
+    # a different packing/grid: nothing is resumed
+    rts, _ = _cluster(cfg, tmp_path, pack="fp8")
+    try:
+        assert all(r.resumed == [] for r in rts)
+    finally:
+        for r in rts:
+            r.close()
+    # flip a byte in a persisted file: staging catches it against the manifest
+    seeded0 = {l for per in cfg.node(0).initial_layers.values() for l in per}
+    lost = next(l for l in range(2) if l not in seeded0)  # node 0 resumes this one from disk
+    victim = os.path.join(tmp_path, "0", f"{lost}.layer")
+    with open(victim, "r+b") as f:
+        f.seek(100)
+        b = f.read(1)
+        f.seek(100)
+        f.write(bytes([b[0] ^ 0xFF]))
+    rts, _ = _cluster(cfg, tmp_path, max_retries=1)
+    try:
+        res = _session(rts, timeout=4)
+        assert not res[0].ok and "CRC32C mismatch" in res[0].error
+    finally:
+        for r in rts:
+            r.close()
