@@ -147,11 +147,13 @@ def main(argv=None) -> int:
         rt.prepare(args.mode, **policy)
         barrier()
         torch.cuda.synchronize()
+        _core.trace_push("bench.step" if timed else "bench.warmup")
         t0 = time.perf_counter()
         res = rt.execute(args.timeout)
         torch.cuda.synchronize()
         barrier()
         dt = time.perf_counter() - t0
+        _core.trace_pop()
         if not res.ok:
             log(f"session failed: {res.error}")
             raise SystemExit(1)

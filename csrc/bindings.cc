@@ -9,6 +9,7 @@
 #include "core/crc32c.h"
 #include "core/fp8.h"
 #include "core/log.h"
+#include "core/trace.h"
 #include "core/wire.h"
 #include "engine/engine.h"
 #include "engine/planned_engine.h"
@@ -57,6 +58,11 @@ PYBIND11_MODULE(_core, m) {
   // ---- logging
   m.def("set_log_level", &log::set_level);
   m.def("set_log_file", &log::set_file);
+  // ---- roctx (rocprofv3 --marker-trace)
+  m.def("trace_available", &trace::available);
+  m.def("trace_mark", [](const std::string& s) { trace::mark(s.c_str()); });
+  m.def("trace_push", [](const std::string& s) { trace::push(s.c_str()); });
+  m.def("trace_pop", &trace::pop);
 
   // ---- enums
   py::enum_<Location>(m, "Location")

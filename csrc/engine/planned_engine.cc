@@ -25,6 +25,7 @@
 #include "core/fp8.h"
 #include "core/log.h"
 #include "core/queue.h"
+#include "core/trace.h"
 #include "roles/node.h"
 
 namespace dissem {
@@ -261,6 +262,7 @@ void PlannedEngine::nack(const Piece& p, Layer& L, uint32_t got) {
     return;
   }
   log::warn(int64_t(self_node_)).msg(std::string(buf) + "; requesting a re-send");
+  trace::mark("dissem.crc_mismatch");
   L.st[c] = 4;
   if (p.kind == Kind::Local) {
     // The source bytes did not match their manifest on the way in: stage again
@@ -389,6 +391,7 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   const int64_t off = c * grid_;
   const int64_t len = std::min(grid_, L.size - off);
   const int64_t slen = src_len(L, c);
+  trace::Scoped tr("dissem.stage");
   if (!L.dev) L.dev = backend_->alloc(L.size);
   Ev e = cfg_.pack == 1 && !L.src_packed ? backend_->stage_pack(L.dev + off, src, slen, cfg_.pack_block)
                                          : backend_->stage(L.dev + off, src, len);
@@ -537,6 +540,7 @@ bool PlannedEngine::issue_some() {
     }
     if (group.empty()) break;
     ops_.erase(ops_.begin(), ops_.begin() + int64_t(take));
+    trace::Scoped tr(group.front().bcast ? "dissem.bcast" : "dissem.p2p_group");
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<Ev> waits;
     std::vector<XOp> xops;

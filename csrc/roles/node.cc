@@ -6,6 +6,7 @@
 #include <tuple>
 
 #include "core/log.h"
+#include "core/trace.h"
 #include "sched/maxflow.h"
 
 namespace dissem {
@@ -125,6 +126,7 @@ void Node::announce() {
   m.layers = store_.inventory();
   if (e_->planned()) m.manifest = e_->manifest();
   NodeID hop = next_hop(cfg_.leader);
+  trace::mark("dissem.announce");
   if (!send_msg(hop, m)) throw std::runtime_error("announce failed");
 }
 
@@ -292,6 +294,7 @@ void Node::on_flow_retransmit(const MessagePtr& m) {
 
 void Node::on_startup(const MessagePtr&) {
   // node.go:1387-1389: tell the application the layers are ready.
+  trace::mark("dissem.startup");
   std::lock_guard<std::mutex> lk(sig_mu_);
   ready_ = true;
   sig_cv_.notify_all();
@@ -394,15 +397,19 @@ void Node::start_distribution() {
   }
   initial_status_ = status_;
   log::info(int64_t(cfg_.id)).i("mode", cfg_.mode).i("bytes_planned", planned).msg("timer start");
+  session_range_ = trace::start("dissem.session");
   int64_t t0 = log::now_us();
-  switch (cfg_.mode) {
-    case 0: schedule_mode0(); break;
-    case 1: schedule_mode1(); break;
-    case 2: schedule_mode2(); break;
-    case 3: schedule_mode3(); break;
-    default: log::error(int64_t(cfg_.id)).msg("unknown mode");
+  {
+    trace::Scoped plan("dissem.plan");
+    switch (cfg_.mode) {
+      case 0: schedule_mode0(); break;
+      case 1: schedule_mode1(); break;
+      case 2: schedule_mode2(); break;
+      case 3: schedule_mode3(); break;
+      default: log::error(int64_t(cfg_.id)).msg("unknown mode");
+    }
+    flush_batch();
   }
-  flush_batch();
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     stats_.plan_ms = double(log::now_us() - t0) / 1e3;
@@ -416,6 +423,7 @@ void Node::start_distribution() {
       stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
     }
     log::info(int64_t(cfg_.id)).msg("timer stop: startup");
+    trace::stop(session_range_);
     send_startup();
     std::lock_guard<std::mutex> lk(sig_mu_);
     sig_cv_.notify_all();
@@ -460,6 +468,7 @@ void Node::on_ack(const MessagePtr& m) {
       stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
     }
     log::info(int64_t(cfg_.id)).f("time_to_deliver_s", stats_.time_to_deliver_s).msg("timer stop: startup");
+    trace::stop(session_range_);
     send_startup();
     std::lock_guard<std::mutex> lk(sig_mu_);
     sig_cv_.notify_all();
@@ -654,6 +663,7 @@ void Node::flush_batch() {
   // feed them), then round-robin over (src, dst) pairs so that consecutive
   // sequence numbers spread over distinct xGMI links.
   if (pending_jobs_.empty()) return;
+  trace::Scoped tr("dissem.flush_batch");
   std::map<int, std::map<std::pair<NodeID, NodeID>, std::vector<XferJob>>> by_phase;
   for (auto& pj : pending_jobs_) by_phase[pj.phase][{pj.job.src, pj.job.dst}].push_back(pj.job);
   pending_jobs_.clear();

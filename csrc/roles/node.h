@@ -190,6 +190,7 @@ class Node {
   std::condition_variable sig_cv_;
   bool started_ = false, satisfied_ = false, ready_ = false;
   int64_t t_start_us_ = 0, t_ready_us_ = 0;
+  uint64_t session_range_ = 0;  // roctx range: timer start -> assignment satisfied
   NodeStats stats_;
   std::set<LayerID> acked_;
 };

@@ -6,6 +6,8 @@
 #include <queue>
 #include <tuple>
 
+#include "core/trace.h"
+
 namespace dissem {
 
 namespace {
@@ -185,6 +187,7 @@ int64_t max_flow_at(const FlowProblem& p, double T) {
 }
 
 FlowPlan solve_flow(const FlowProblem& p) {
+  trace::Scoped tr("dissem.maxflow");
   FlowPlan plan;
   plan.required = required_bytes(p);
   if (plan.required == 0) {
