@@ -27,7 +27,7 @@ CXXFLAGS  := -O2 -g1 -std=c++17 -fPIC -Wall -Wno-sign-compare -Wno-unused-result
              -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -I$(ROCM)/include/rccl -fvisibility=hidden
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Icsrc -I$(ROCM)/include -Wno-unused-result \
              -fvisibility=hidden
-LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -lpthread -ldl
+LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx -lpthread
 
 CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/core/fp8.cc csrc/core/trace.cc csrc/transport/inproc.cc \
              csrc/transport/tcp.cc csrc/store/store.cc csrc/sched/maxflow.cc csrc/roles/node.cc \
@@ -65,11 +65,11 @@ sanitize: $(BUILD)/tests/core_selftest_tsan $(BUILD)/tests/core_selftest_asan
 
 $(BUILD)/tests/core_selftest_tsan: $(SAN_SRC)
 	@mkdir -p $(dir $@)
-	$(CXX) -O1 -g -std=c++17 -Icsrc -fsanitize=thread -o $@ $(SAN_SRC) -lpthread -ldl
+	$(CXX) -O1 -g -std=c++17 -Icsrc -fsanitize=thread -I/opt/rocm/include -o $@ $(SAN_SRC) -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx -lpthread
 
 $(BUILD)/tests/core_selftest_asan: $(SAN_SRC)
 	@mkdir -p $(dir $@)
-	$(CXX) -O1 -g -std=c++17 -Icsrc -fsanitize=address,undefined -fno-omit-frame-pointer -o $@ $(SAN_SRC) -lpthread -ldl
+	$(CXX) -O1 -g -std=c++17 -Icsrc -fsanitize=address,undefined -fno-omit-frame-pointer -I/opt/rocm/include -o $@ $(SAN_SRC) -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx -lpthread
 
 clean:
 	rm -rf $(BUILD) $(PKG)/_core*.so bin/diskspeed

@@ -4,9 +4,8 @@
 // failures) are annotated so host-side scheduling lines up with the kernel and
 // copy timeline.
 //
-// libroctx is loaded with dlopen on first use, so the core has no link-time
-// dependency on it (host-only sanitizer builds included); without a profiler
-// attached the calls are no-ops inside libroctx.
+// The core links librocprofiler-sdk-roctx (host-only; also in the sanitizer
+// builds); without a profiler attached the calls return immediately.
 #pragma once
 
 #include <cstdint>
