@@ -268,7 +268,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("injected", &PlannedStats::injected)
       .def_readonly("issue_ms", &PlannedStats::issue_ms)
       .def_readonly("peer_sent", &PlannedStats::peer_sent)
-      .def_readonly("peer_recv", &PlannedStats::peer_recv);
+      .def_readonly("peer_recv", &PlannedStats::peer_recv)
+      .def_readonly("group_us_hist", &PlannedStats::group_us_hist)
+      .def_readonly("land_us_hist", &PlannedStats::land_us_hist);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
         return reinterpret_cast<uint64_t>(e.provision(l, n));

@@ -30,6 +30,16 @@
 
 namespace dissem {
 
+namespace {
+size_t log2_bucket(std::chrono::steady_clock::time_point since) {
+  const int64_t us =
+      std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - since).count();
+  size_t b = 0;
+  while (b < 31 && (int64_t(1) << (b + 1)) <= us) ++b;
+  return b;
+}
+}  // namespace
+
 PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> backend)
     : cfg_(cfg), backend_(std::move(backend)) {
   if (cfg_.world < 1 || cfg_.rank < 0 || cfg_.rank >= cfg_.world) throw std::runtime_error("bad rank/world");
@@ -630,6 +640,10 @@ void PlannedEngine::poll() {
       fail("P2P group failed: " + backend_->async_error());
       return;
     }
+    {
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.group_us_hist[log2_bucket(groups_inflight_.front().second)]++;
+    }
     backend_->release(groups_inflight_.front().first);
     groups_inflight_.pop_front();
   }
@@ -670,6 +684,10 @@ void PlannedEngine::poll() {
         landed(p);
         L.want[size_t(p.chunk)] = 0;
       }
+    }
+    {
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.land_us_hist[log2_bucket(it->t0)] += int64_t(it->pieces.size());
     }
     backend_->release(it->ev);
     if (it->bounce) bounce_free_.push_back(it->bounce);

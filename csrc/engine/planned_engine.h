@@ -67,6 +67,9 @@ struct PlannedStats {
   int64_t nacks = 0, injected = 0;
   double issue_ms = 0;  // host time spent enqueueing groups
   std::map<int, int64_t> peer_sent, peer_recv;  // bytes per peer rank (per-link counters)
+  // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
+  std::vector<int64_t> group_us_hist = std::vector<int64_t>(32, 0);  // P2P group issue -> complete
+  std::vector<int64_t> land_us_hist = std::vector<int64_t>(32, 0);   // chunk issue -> landed + verified
 };
 
 class PlannedEngine : public DataEngine {
@@ -138,6 +141,7 @@ class PlannedEngine : public DataEngine {
   };
   struct Verify {  // landing (recv group or staging copy) awaiting its check
     Ev ev = 0;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     std::vector<Piece> pieces;
     std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
     uint8_t* bounce = nullptr;    // disk staging buffer to recycle once landed

@@ -41,6 +41,19 @@ def layer_seed(base: int, layer: int) -> int:
     return int.from_bytes(h, "little")
 
 
+def hist_quantile(hist: List[int], q: float) -> int:
+    """Upper edge (us) of the log2 bucket holding quantile q (0 if the histogram is empty)."""
+    total = sum(hist)
+    if total <= 0:
+        return 0
+    acc = 0
+    for b, n in enumerate(hist):
+        acc += n
+        if acc >= q * total:
+            return 1 << (b + 1)
+    return 1 << len(hist)
+
+
 @dataclass
 class SessionResult:
     ok: bool
@@ -443,7 +456,11 @@ class Runtime:
         if self.engine is not None and ok:
             self.engine.quiesce()  # trailing verifications of chunks nobody waited for
             now = self._engine_stats()
-            res.engine_stats = {k: now[k] - self._stats0.get(k, 0) for k in now}
+            res.engine_stats = {k: now[k] - self._stats0.get(k, 0) for k in now if not k.endswith("_hist")}
+            for h in ("group_us_hist", "land_us_hist"):
+                delta = [a - b for a, b in zip(now[h], self._stats0[h])]
+                for q in (0.5, 0.99):
+                    res.engine_stats[f"{h[:-8]}_p{int(q * 100)}_us"] = hist_quantile(delta, q)
         if ok:
             node.stop()
         self._last_node = node  # on failure keep it alive for inspection
@@ -454,7 +471,8 @@ class Runtime:
         return {
             k: getattr(es, k)
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
-                      "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms")
+                      "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
+                      "group_us_hist", "land_us_hist")
         }
 
     def link_bytes(self) -> Dict[str, Dict[int, int]]:
