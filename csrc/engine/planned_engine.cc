@@ -444,9 +444,23 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   if (s == 3) return 0;  // disk read in flight
   if (s == 4 && !want_landed) return 1;  // forward the bad copy; its receiver NACKs it as well
   LayerSrc src;
-  if (L.host || !L.path.empty() || (node_ && node_->store().get(id, &src) && (src.host || !src.path.empty()))) {
+  const bool have = node_ && node_->store().get(id, &src);
+  // A client layer's host buffer exists while its stream is still landing; it
+  // becomes a source only once the node re-tags it Inmem (Node::on_layer).
+  const bool client = have && src.meta.location == Location::Client;
+  if (L.host || !L.path.empty() || (have && !client && (src.host || !src.path.empty()))) {
     stage_chunk(L, id, c);
     return L.st[size_t(c)] == 1 ? 1 : 0;
+  }
+  if (client) {
+    // Held by this node's external client (client.go): ask for the layer once.
+    // It arrives over TCP into host memory; the node then calls load_range,
+    // and this chunk (and any send waiting on it) stages from that copy.
+    if (!L.client_requested) {
+      L.client_requested = true;
+      node_->request_client_layer(id);
+    }
+    return 0;
   }
   return -1;
 }
@@ -737,6 +751,7 @@ void PlannedEngine::take_requests(bool block) {
             L.fails[c] = 0;
           }
           L.host = nullptr;  // re-read the source from the next session's store
+          L.client_requested = false;
           if (cfg_.poison && !L.seeded && L.dev) backend_->zero_sync(L.dev, L.size);
         }
         std::lock_guard<std::mutex> lk(req_mu_);

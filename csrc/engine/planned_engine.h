@@ -131,6 +131,7 @@ class PlannedEngine : public DataEngine {
     std::string path;                // disk-tier source
     int64_t path_off = 0;
     bool src_packed = false;         // the source already holds the packed image (persisted layers)
+    bool client_requested = false;   // ClientReq sent for this session
     // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk,
     // 4 failed its CRC and awaits the leader's re-send (still forwardable: a
     // later receiver detects it and NACKs too)

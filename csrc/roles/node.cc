@@ -331,6 +331,14 @@ void Node::send_layer(NodeID dest, LayerID layer, int64_t offset, int64_t size, 
   e_->send_range(dest, layer, offset, size, total, rate);
 }
 
+void Node::request_client_layer(LayerID layer) {
+  log::info(int64_t(cfg_.id)).u("layerID", layer).msg("ask the client to send the layer (device staging)");
+  Message r;
+  r.type = MsgType::ClientReq;
+  r.layer = layer;
+  send_msg(kClientID, r);
+}
+
 void Node::fetch_from_client(LayerID layer, NodeID dest) {
   log::debug(int64_t(cfg_.id)).u("layerID", layer).msg("ask the client to send the layer");
   if (dest != cfg_.id) {

@@ -95,6 +95,9 @@ class Node {
   void inject(MessagePtr m) { t_->inject(std::move(m)); }
   // Safe send from any thread (logs on failure).
   bool send_msg(NodeID dest, Message m);
+  // Ask this node's external client to stream `layer` here (any thread): the
+  // planned engine's way to obtain a client-held layer before it can stage it.
+  void request_client_layer(LayerID layer);
   bool is_leader() const { return is_leader_; }
 
  private:

@@ -236,7 +236,7 @@ class Runtime:
             rate = self.me.sources.get(st, 0)
             for l, size in sorted(per.items()):
                 seed = layer_seed(self.payload_seed, l)
-                if st == SOURCE_CLIENT and not gpu:
+                if st == SOURCE_CLIENT:  # metadata only: the node's external client holds the bytes
                     layers[l] = _core.LayerSrc.client(size, rate)
                 elif st == SOURCE_DISK or (self.storage_path and st != SOURCE_DEVICE):
                     path = self._disk_layer(l, size, seed)

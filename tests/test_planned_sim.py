@@ -250,3 +250,45 @@ def test_corruption_beyond_retry_budget_fails_loudly():
     finally:
         for r in rts:
             r.close()
+
+
+def test_client_held_layer_on_planned_engine():
+    """C17 on the GPU data plane: node 1's external client holds layer 9. The
+    leader plans node 1 as its sender; node 1's engine asks the client
+    (ClientReq), stages the streamed bytes into its HBM slot, then forwards."""
+    from distributed_llm_dissemination_amd.utils.config import ClientConf
+
+    size = 2 * MiB + 4096
+    cfg = make_workload(3, 3, size, tier="host", seeding="random", chunk_bytes=MiB)
+    cfg.clients.append(ClientConf(id=1, addr="", layers={9: 0}))
+    for r in range(3):
+        cfg.assignment[r].append(9)
+    key = f"sim{next(_keys)}"
+    data = _core.fill_random_host(size, layer_seed(0, 9))
+    ct = _core.tcp_transport("127.0.0.1:0", {}, True)
+    client = _core.ClientNode(1, ct, {9: _core.LayerSrc.inmem(data, 0)})
+    client.start()
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key) for i in range(3)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for i, r in enumerate(rts):
+        r.transport.set_registry({**reg, _core.CLIENT_ID: ct.address()} if i == 1 else reg)
+    ct.set_registry({1: reg[1]})
+    try:
+        for r in rts:
+            r.prepare(1)
+        res = [None] * 3
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        for r in rts:
+            assert r.layer_bytes(9) == data
+            for l in range(3):
+                assert r.layer_bytes(l) == _core.fill_random_host(size, layer_seed(0, l))
+    finally:
+        for r in rts:
+            r.close()
+        client.stop()
+        ct.close()
