@@ -124,6 +124,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("rate", &Message::rate)
       .def_readwrite("total_size", &Message::total_size)
       .def_readwrite("location", &Message::location)
+      .def_readwrite("partial", &Message::partial)
       .def_readwrite("save_disk", &Message::save_disk)
       .def_readwrite("chunk_bytes", &Message::chunk_bytes)
       .def_readwrite("crc", &Message::crc)
@@ -360,6 +361,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("storage_path", &NodeConfig::storage_path)
       .def_readwrite("relay", &NodeConfig::relay)
       .def_readwrite("collective", &NodeConfig::collective)
+      .def_readwrite("pull_job_bytes", &NodeConfig::pull_job_bytes)
+      .def_readwrite("range_acks", &NodeConfig::range_acks)
       .def_readwrite("job_timeout_s", &NodeConfig::job_timeout_s)
       .def_readwrite("job_min_rate", &NodeConfig::job_min_rate)
       .def_readwrite("max_redispatch", &NodeConfig::max_redispatch);

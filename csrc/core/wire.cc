@@ -190,6 +190,11 @@ Json encode_payload(const Message& m) {
       src_id();
       p["LayerID"] = Json(uint64_t(m.layer));
       p["Location"] = Json(unsigned(m.location));  // extension (unexported in reference)
+      if (m.partial) {  // extension: a range of the layer landed (mode-2 range jobs)
+        p["Partial"] = Json(true);
+        p["Offset"] = Json(m.offset);
+        p["DataSize"] = Json(m.data_size);
+      }
       break;
     case MsgType::Retransmit:
       src_id();
@@ -301,6 +306,11 @@ MessagePtr decode_envelope(const Json& env) {
     case MsgType::Ack:
       m->layer = p.get_u64("LayerID");
       m->location = Location(p.get_u64("Location", 0));
+      m->partial = p.get_bool("Partial", false);
+      if (m->partial) {
+        m->offset = p.get_i64("Offset", 0);
+        m->data_size = p.get_i64("DataSize", 0);
+      }
       break;
     case MsgType::Retransmit:
       m->layer = p.get_u64("LayerID");

@@ -75,6 +75,7 @@ struct Message {
   int64_t rate = 0;
   int64_t total_size = 0;  // full layer size
   Location location = Location::Inmem;
+  bool partial = false;    // Ack extension: [offset, offset+data_size) landed (mode-2 range jobs)
   bool save_disk = false;
   // Layer header extensions (GPU data plane)
   int64_t chunk_bytes = 0;

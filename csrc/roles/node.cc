@@ -179,7 +179,7 @@ void Node::handle(const MessagePtr& m) {
       if (is_leader_) on_announce(m);
       break;
     case MsgType::Ack:
-      if (is_leader_) on_ack(m);
+      if (is_leader_) m->partial ? on_range_ack(m) : on_ack(m);
       break;
     case MsgType::Layer:
       on_layer(m);
@@ -253,6 +253,16 @@ void Node::on_landed(LayerID layer, int64_t off, int64_t size, int64_t total, No
     log::info(int64_t(cfg_.id)).msg("l" + std::to_string(layer) + " downloaded (" +
                                     std::to_string(store_.landed_bytes(layer)) + " B / " + std::to_string(total) +
                                     " B)");
+    if (cfg_.range_acks && cfg_.id != kClientID) {  // mode-2 range jobs retire on these
+      Message a;
+      a.type = MsgType::Ack;
+      a.layer = layer;
+      a.location = e_->target();
+      a.partial = true;
+      a.offset = off;
+      a.data_size = size;
+      send_msg(cfg_.leader, a);
+    }
   }
   if (complete) {
     log::info(int64_t(cfg_.id)).u("layer", layer).i("total_bytes", total).u("from", from).f("duration[ms]", dur_ms)
@@ -482,10 +492,43 @@ void Node::on_ack(const MessagePtr& m) {
     sig_cv_.notify_all();
   }
   if (cfg_.mode != 2) return;
-  // Mode 2 pull loop (node.go:764-807): retire the job, pull the next one.
+  // Mode 2 pull loop (node.go:764-807): the whole layer is at the dest, so every
+  // job of (layer, dest) is done; retire them and pull the next ones.
+  auto lj = jobs_.find(m->layer);
+  if (lj != jobs_.end()) {
+    std::vector<JobKey> done;
+    for (auto& kv : lj->second)
+      if (kv.first.first == m->src) done.push_back(kv.first);
+    for (auto& k : done) retire_job(m->layer, k);
+  }
+  // The destination now owns a copy it can serve (status grew above): let it pull too.
+  while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
+  }
+  flush_batch();
+}
+
+void Node::on_range_ack(const MessagePtr& m) {
+  // A range of a layer landed at m->src: range jobs it completes are retired.
+  if (cfg_.mode != 2) return;
   auto lj = jobs_.find(m->layer);
   if (lj == jobs_.end()) return;
-  auto jt = lj->second.find(m->src);
+  std::vector<JobKey> done;
+  for (auto& kv : lj->second) {
+    if (kv.first.first != m->src) continue;
+    Job& j = kv.second;
+    const int64_t a = std::max(kv.first.second, m->offset);
+    const int64_t b = std::min(kv.first.second + j.size, m->offset + m->data_size);
+    if (a < b) j.got.add(a, b);
+    if (j.got.covered() >= j.size) done.push_back(kv.first);
+  }
+  for (auto& k : done) retire_job(m->layer, k);
+  if (!done.empty()) flush_batch();
+}
+
+void Node::retire_job(LayerID layer, const JobKey& key) {
+  auto lj = jobs_.find(layer);
+  if (lj == jobs_.end()) return;
+  auto jt = lj->second.find(key);
   if (jt == lj->second.end()) return;
   Job job = jt->second;
   lj->second.erase(jt);
@@ -495,18 +538,13 @@ void Node::on_ack(const MessagePtr& m) {
     pf.first = pf.second == 0 ? dur : 0.5 * pf.first + 0.5 * dur;  // EWMA (quirk Q9)
     pf.second++;
     inflight_[job.sender] = std::max(0, inflight_[job.sender] - 1);
-    log::info(int64_t(cfg_.id)).u("node", job.sender).u("layerID", m->layer).f("duration[ms]", dur / 1e3)
-        .msg("job completed");
+    log::info(int64_t(cfg_.id)).u("node", job.sender).u("layerID", layer).i("offset", key.second)
+        .f("duration[ms]", dur / 1e3).msg("job completed");
   } else {
     load_[job.sender] = std::max<int64_t>(0, load_[job.sender] - 1);
   }
   while (inflight_[job.sender] < cfg_.pull_window && assign_new_job(job.sender)) {
   }
-  // The destination now owns a copy it can serve (status grew above): let it pull too.
-  if (m->src != job.sender)
-    while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
-    }
-  flush_batch();
 }
 
 // ------------------------------------------------------- failure handling
@@ -581,7 +619,7 @@ void Node::on_tick() {
       // Keep the pull scheduler's books: the job now belongs to `alt`.
       auto lj = jobs_.find(e.layer);
       if (lj != jobs_.end()) {
-        auto jt = lj->second.find(e.dest);
+        auto jt = lj->second.find({e.dest, e.o.off});
         if (jt != lj->second.end()) {
           if (jt->second.state == JobState::Sending) inflight_[jt->second.sender] = std::max(0, inflight_[jt->second.sender] - 1);
           jt->second.sender = alt;
@@ -868,8 +906,8 @@ NodeID Node::min_loaded_sender(LayerID layer) {
   return found ? best : kClientID;
 }
 
-bool Node::rarest_own_job(NodeID node, LayerID* layer, NodeID* dest) {
-  // node.go:981-1010
+bool Node::rarest_own_job(NodeID node, LayerID* layer, JobKey* key) {
+  // node.go:981-1010 (ties: lowest layer id, then lowest (dest, offset))
   bool ok = false;
   size_t min_owners = SIZE_MAX;
   auto st = status_.find(node);
@@ -883,7 +921,7 @@ bool Node::rarest_own_job(NodeID node, LayerID* layer, NodeID* dest) {
       if (!ok || cnt < min_owners || (cnt == min_owners && l.first < *layer)) {
         min_owners = cnt;
         *layer = l.first;
-        *dest = jd.first;
+        *key = jd.first;
         ok = true;
       }
     }
@@ -891,11 +929,12 @@ bool Node::rarest_own_job(NodeID node, LayerID* layer, NodeID* dest) {
   return ok;
 }
 
-bool Node::rarest_stealable_job(NodeID node, LayerID* layer, NodeID* dest, NodeID* victim) {
+bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID* victim) {
   // node.go:1012-1073
   struct Cand {
     LayerID layer;
-    NodeID dest, sender;
+    JobKey dest;
+    NodeID sender;
     size_t owners;
     double ttf;
   };
@@ -926,36 +965,65 @@ bool Node::rarest_stealable_job(NodeID node, LayerID* layer, NodeID* dest, NodeI
   }
   if (!have) return false;
   *layer = best.layer;
-  *dest = best.dest;
+  *key = best.dest;
   *victim = best.sender;
   return true;
+}
+
+void Node::dispatch_range(LayerID layer, NodeID sender, NodeID dest, int64_t off, int64_t size) {
+  if (off == 0 && size >= layer_size(layer)) {
+    retransmit(layer, sender, dest);  // whole layer: the reference's Retransmit
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.jobs_dispatched++;
+  }
+  if (e_->planned()) {
+    add_job(sender, dest, layer, off, size);
+    return;
+  }
+  track(sender, dest, layer, off, size);
+  if (sender == cfg_.id) {
+    send_layer(dest, layer, off, size, 0);
+    return;
+  }
+  Message f;  // a byte range: FlowRetransmit carries offset + size
+  f.type = MsgType::FlowRetransmit;
+  f.layer = layer;
+  f.dest = dest;
+  f.offset = off;
+  f.data_size = size;
+  send_msg(sender, f);
 }
 
 bool Node::assign_new_job(NodeID node) {
   // node.go:909-945
   LayerID layer = 0;
-  NodeID dest = 0, victim = 0;
+  JobKey key{0, 0};
+  NodeID victim = 0;
   if (suspects_.count(node)) return false;
-  if (rarest_own_job(node, &layer, &dest)) {
-    Job& j = jobs_[layer][dest];
+  if (rarest_own_job(node, &layer, &key)) {
+    Job& j = jobs_[layer][key];
     j.state = JobState::Sending;
     j.t_us = log::now_us();
     load_[node] = std::max<int64_t>(0, load_[node] - 1);
     inflight_[node]++;
-    log::debug(int64_t(cfg_.id)).u("node", node).u("layer", layer).msg("pass a job initially assigned");
-    retransmit(layer, node, dest);
+    log::debug(int64_t(cfg_.id)).u("node", node).u("layer", layer).i("offset", key.second)
+        .msg("pass a job initially assigned");
+    dispatch_range(layer, node, key.first, key.second, j.size);
     return true;
   }
-  if (rarest_stealable_job(node, &layer, &dest, &victim)) {
+  if (rarest_stealable_job(node, &layer, &key, &victim)) {
     log::debug(int64_t(cfg_.id)).u("layer", layer)
         .msg("steal a job from the most loaded node (" + std::to_string(victim) + ") to node " + std::to_string(node));
     load_[victim] = std::max<int64_t>(0, load_[victim] - 1);
-    Job& j = jobs_[layer][dest];
+    Job& j = jobs_[layer][key];
     j.sender = node;
     j.state = JobState::Sending;
     j.t_us = log::now_us();
     inflight_[node]++;
-    retransmit(layer, node, dest);
+    dispatch_range(layer, node, key.first, key.second, j.size);
     return true;
   }
   log::debug(int64_t(cfg_.id)).u("node", node).msg("there is no job left to assign");
@@ -972,9 +1040,23 @@ void Node::schedule_mode2() {
     if (owners_[a].size() != owners_[b].size()) return owners_[a].size() < owners_[b].size();
     return a < b;  // rarest first, tiebreak by id
   });
+  // Jobs are (layer, dest, range). With pull_job_bytes the layer is cut into
+  // ranges (chunk-aligned on planned engines) so stealing can rebalance inside
+  // a layer; 0 keeps the reference's one job per (layer, dest).
+  int64_t jb = cfg_.pull_job_bytes;
+  if (jb > 0 && e_->planned() && e_->chunk_bytes() > 0)
+    jb = std::max<int64_t>(1, (jb + e_->chunk_bytes() - 1) / e_->chunk_bytes()) * e_->chunk_bytes();
   for (auto& kv : assignment_)
-    for (auto& l : kv.second)
-      if (!at(status_[kv.first], l.first, e_->target())) jobs_[l.first][kv.first] = Job{};
+    for (auto& l : kv.second) {
+      if (at(status_[kv.first], l.first, e_->target())) continue;
+      const int64_t size = layer_size(l.first);
+      const int64_t step = jb > 0 ? jb : std::max<int64_t>(size, 1);
+      for (int64_t off = 0; off < std::max<int64_t>(size, 1); off += step) {
+        Job j;
+        j.size = std::min(step, size - off);
+        jobs_[l.first][{kv.first, off}] = j;
+      }
+    }
   for (auto& kv : status_) load_.emplace(kv.first, 0);
   for (LayerID layer : sorted) {
     auto lj = jobs_.find(layer);
@@ -985,7 +1067,8 @@ void Node::schedule_mode2() {
         log::error(int64_t(cfg_.id)).u("layer", layer).msg("no owner holds the layer");
         continue;
       }
-      jd.second = Job{sender, JobState::Pending, 0};
+      jd.second.sender = sender;
+      jd.second.state = JobState::Pending;
       load_[sender]++;
       log::info(int64_t(cfg_.id)).msg("job assignment: layer: " + std::to_string(layer) +
                                       ", sender: " + std::to_string(sender));

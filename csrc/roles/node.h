@@ -32,6 +32,8 @@ struct NodeConfig {
   uint64_t seed = 0;                // mode-1 owner RNG (quirk Q5: seeded uniform choice)
   std::string owner_policy = "random";  // mode 1: "random" (reference) or "balanced"
   int pull_window = 1;              // mode 2: concurrent jobs per sender (reference: 1)
+  int64_t pull_job_bytes = 0;       // mode 2: job = this many bytes of a layer (0 = whole layer, reference)
+  bool range_acks = false;          // receiver: also ack each landed range (needed by mode-2 range jobs)
   std::map<NodeID, int64_t> network_bw;  // mode 3: NetworkBW per node (B/s, 0 = unlimited)
   std::map<std::pair<NodeID, NodeID>, int64_t> link_bw;  // mode 3 topology: per directed link
   bool integer_seconds = false;     // mode 3: reference T search over integer seconds
@@ -133,11 +135,15 @@ class Node {
   void schedule_mode1();
   void schedule_mode2();
   void schedule_mode3();
-  // mode 2 (node.go:628-1073)
+  // mode 2 (node.go:628-1073); a job is (layer, dest, byte range)
+  using JobKey = std::pair<NodeID, int64_t>;  // (dest, offset) within jobs_[layer]
   bool assign_new_job(NodeID node);
   NodeID min_loaded_sender(LayerID layer);
-  bool rarest_own_job(NodeID node, LayerID* layer, NodeID* dest);
-  bool rarest_stealable_job(NodeID node, LayerID* layer, NodeID* dest, NodeID* victim);
+  bool rarest_own_job(NodeID node, LayerID* layer, JobKey* key);
+  bool rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID* victim);
+  void dispatch_range(LayerID layer, NodeID sender, NodeID dest, int64_t off, int64_t size);
+  void retire_job(LayerID layer, const JobKey& key);
+  void on_range_ack(const MessagePtr& m);
 
   NodeConfig cfg_;
   std::shared_ptr<Transport> t_;
@@ -161,8 +167,10 @@ class Node {
     NodeID sender = 0;
     JobState state = JobState::Pending;
     int64_t t_us = 0;
+    int64_t size = 0;  // range [key.second, key.second + size)
+    RangeSet got;      // bytes the dest reported landed (range acks)
   };
-  std::map<LayerID, std::map<NodeID, Job>> jobs_;
+  std::map<LayerID, std::map<JobKey, Job>> jobs_;
   std::map<NodeID, int64_t> load_;        // senderLoadCounter
   std::map<NodeID, int> inflight_;        // jobs currently sending per sender
   std::map<NodeID, std::pair<double, uint64_t>> perf_;  // sender -> (EWMA job us, count) (quirk Q9)

@@ -82,6 +82,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0, help="mode-1 owner RNG seed")
     p.add_argument("--owner-policy", default="random", choices=["random", "balanced"])
     p.add_argument("--pull-window", type=int, default=1)
+    p.add_argument("--pull-job-mib", type=int, default=0,
+                   help="mode 2: split layers into jobs of this many MiB (0 = one job per layer, reference)")
     p.add_argument("--no-relay", action="store_true", help="mode 0 on rccl: leader fan-out instead of relay")
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0 on rccl: relay = scatter + peer relay over all xGMI links; collective = "
@@ -189,7 +191,8 @@ def main(argv=None) -> int:
         return 1
     policy = dict(seed=args.seed, owner_policy=args.owner_policy, pull_window=args.pull_window,
                   relay=not args.no_relay and args.bcast != "fanout", collective=args.bcast == "collective",
-                  job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate)
+                  job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate,
+                  pull_job_bytes=args.pull_job_mib << 20)
     rt.prepare(args.m, **policy)
     if barrier:
         barrier()

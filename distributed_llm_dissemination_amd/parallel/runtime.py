@@ -387,6 +387,7 @@ class Runtime:
         integer_seconds: bool = False,
         job_timeout_s: float = 0.0,
         job_min_rate: float = 0.0,
+        pull_job_bytes: int = 0,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed)."""
         self.epoch += 1
@@ -408,6 +409,8 @@ class Runtime:
         nc.integer_seconds = integer_seconds
         nc.job_timeout_s = job_timeout_s
         nc.job_min_rate = job_min_rate
+        nc.pull_job_bytes = pull_job_bytes
+        nc.range_acks = mode == 2 and pull_job_bytes > 0
         nc.align = self.grid if self.engine is not None else 1
         eng = self.engine if self.engine is not None else _core.host_engine(self.host_link_rate)
         assign = {k: v for k, v in self.cfg.assignment.items()} if self.is_leader else {}

@@ -274,6 +274,42 @@ def test_mode1_random_owner_is_seeded(core):
     assert dest is not None
 
 
+def test_mode2_range_jobs_balance_the_reference_experiment(core):
+    """The reference experiment's shape (conf/config.json): 7 rate-limited senders
+    hold all 8 layers, node 7 needs them. One job per layer leaves a sender with
+    2 layers (T ~ 2 layer-times); 256 KiB range jobs spread the bytes evenly
+    (T ~ 8/7 layer-times)."""
+    size, rate = 2 << 20, 2 << 20
+
+    def run(job_bytes):
+        layers = {l: core.LayerSrc.inmem(os.urandom(size), rate, core.SourceType.Disk) for l in range(8)}
+        assignment = {7: list(range(8))}
+        c = Cluster(core, "tcp", 8)
+        try:
+            kw = dict(pull_job_bytes=job_bytes, range_acks=job_bytes > 0, pull_window=1)
+            leader = c.node(0, 2, layers, assignment, **kw)
+            senders = [c.node(i, 2, layers, **kw) for i in range(1, 7)]
+            dest = c.node(7, 2, {}, **kw)
+            for s in senders:
+                s.announce()
+            for i in range(1, 7):
+                wait_status(leader, i)
+            t0 = time.perf_counter()
+            dest.announce()
+            assert leader.wait_ready(30)
+            dt = time.perf_counter() - t0
+            for l in range(8):
+                assert dest.layer(l).host_bytes() == layers[l].host_bytes()
+            return dt, leader.stats()
+        finally:
+            c.close()
+
+    t_layer, st_layer = run(0)
+    t_range, st_range = run(256 << 10)
+    assert st_layer.jobs_dispatched == 8 and st_range.jobs_dispatched == 8 * 8
+    assert t_range < 0.8 * t_layer, (t_range, t_layer)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 def test_dead_sender_jobs_are_redispatched(core, mode):
     """the reference waits forever for a dead sender's ack. With a

@@ -113,6 +113,15 @@ def test_pipeline_assignment_mode2_dynamic_batches():
     run_cluster(cfg, 2, pull_window=1)
 
 
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_mode2_range_jobs(n):
+    """Mode-2 jobs of one chunk each (--pull-job-mib): stealing works inside a
+    layer; receivers' range acks retire the jobs."""
+    cfg = make_workload(n, 5, 4 * MiB + 4096, tier="host", seeding="random", copies=2, chunk_bytes=MiB)
+    (res,), _ = run_cluster(cfg, 2, pull_window=2, pull_job_bytes=MiB)
+    assert res[0].jobs > 5 * (n - 2)  # more jobs than (layer, dest) pairs: layers were split
+
+
 def test_repeated_sessions_reset_state():
     cfg = make_workload(4, 6, 2 * MiB, tier="host", chunk_bytes=MiB)
     outs, _ = run_cluster(cfg, 1, sessions=3)
