@@ -9,6 +9,7 @@
 #include "core/crc32c.h"
 #include "core/fp8.h"
 #include "core/log.h"
+#include "core/ratelimit.h"
 #include "core/trace.h"
 #include "core/wire.h"
 #include "engine/engine.h"
@@ -313,6 +314,20 @@ PYBIND11_MODULE(_core, m) {
       out.push_back(crc32c(reinterpret_cast<const void*>(ptr + uint64_t(off)), size_t(std::min(chunk, n - off))));
     return out;
   });
+  // token bucket (core/ratelimit.h): pace `total` bytes at `rate` B/s; returns
+  // (seconds elapsed, piece sizes) - unit-test hook
+  m.def("token_bucket_pace", [](int64_t total, int64_t rate, int64_t burst) {
+    std::vector<int64_t> pieces;
+    double secs;
+    {
+      py::gil_scoped_release nogil;
+      TokenBucket tb(rate, burst);
+      auto t0 = std::chrono::steady_clock::now();
+      tb.paced(total, [&](int64_t, int64_t n) { pieces.push_back(n); });
+      secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return py::make_tuple(secs, pieces);
+  }, py::arg("total"), py::arg("rate"), py::arg("burst") = TokenBucket::kDefaultBurst);
   // fp8 wire/storage format (core/fp8.h), host reference
   m.def("fp8_packed_size", &fp8::packed_size, py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block") = 128);
   m.def("fp8_source_size", &fp8::source_size, py::arg("packed"), py::arg("src_chunk"), py::arg("block") = 128);

@@ -178,6 +178,15 @@ def main(argv=None) -> int:
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
                  host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
                  persist_dir=args.persist_dir)
+    if barrier is not None:
+        # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
+        import torch.distributed as dist
+
+        pairs = [None] * dist.get_world_size()
+        dist.all_gather_object(pairs, (my_id, rt.transport.address()))
+        reg = dict(registry)
+        reg.update({nid: addr for nid, addr in pairs})
+        rt.transport.set_registry(reg)
     if args.l:
         print(json.dumps({"level": "info", "node": my_id, "message": "layer set up"}), file=sys.stderr)
         rt.close()
