@@ -153,19 +153,22 @@ def main(argv=None) -> int:
     barrier = None
     uid = None
     device = me.device
-    if args.engine == "rccl":
+    world = int(os.environ.get("WORLD_SIZE", "1")) if torchrun_rank is not None else 1
+    if args.engine == "rccl" or world > 1:
         import torch
         import torch.distributed as dist
 
-        world = int(os.environ.get("WORLD_SIZE", "1"))
-        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        device = me.device if me.device is not None else local_rank
-        torch.cuda.set_device(device)
+        if args.engine == "rccl":
+            local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+            device = me.device if me.device is not None else local_rank
+            torch.cuda.set_device(device)
         if world > 1:
+            # Bootstrap only (gloo over TCP): barriers, the ncclUniqueId, addresses.
             dist.init_process_group("gloo")
-            box = [_core.nccl_unique_id() if dist.get_rank() == 0 else None]
-            dist.broadcast_object_list(box, src=0)
-            uid = box[0]
+            if args.engine == "rccl":
+                box = [_core.nccl_unique_id() if dist.get_rank() == 0 else None]
+                dist.broadcast_object_list(box, src=0)
+                uid = box[0]
             barrier = dist.barrier
     registry = cfg.registry()
     client = cfg.client(my_id)

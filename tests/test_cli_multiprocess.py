@@ -74,6 +74,27 @@ def test_two_process_loopback_mode(tmp_path, mode):
     assert summary["bytes_moved"] == 4 << 20 and summary["mode"] == mode
 
 
+@pytest.mark.slow
+def test_torchrun_launch_host_engine(tmp_path):
+    """torchrun (3 ranks, gloo bootstrap on CPU): -id comes from RANK, nodes have
+    no fixed Addr and exchange their ephemeral ports through the process group."""
+    from distributed_llm_dissemination_amd.models.catalog import make_workload
+
+    cfg = make_workload(3, 6, 512 << 10, tier="host", seeding="random")
+    path = tmp_path / "cfg.json"
+    path.write_text(json.dumps(cfg.to_json()))
+    port = free_ports(1)[0]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        "-m", "distributed_llm_dissemination_amd", "-f", str(path), "-m", "1", "--engine", "host",
+                        "--json-summary"], capture_output=True, text=True, env=env, cwd=ROOT, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Time to deliver:" in r.stdout
+    summary = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert summary["bytes_moved"] == 2 * 6 * (512 << 10)
+
+
 def test_usage_without_flags():
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-m", "distributed_llm_dissemination_amd"], capture_output=True, text=True,
