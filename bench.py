@@ -47,6 +47,8 @@ def parse_args(argv=None):
     p.add_argument("--assignment", default="replicate", choices=["replicate", "pipeline"])
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--owner-policy", default="random", choices=["random", "balanced", "links"],
+                   help="mode 1 owner choice when a layer has several holders (--copies > 1)")
     p.add_argument("--timeout", type=float, default=300.0)
     p.add_argument("--pull-window", type=int, default=0, help="mode 2 jobs in flight per sender (0 = peers)")
     p.add_argument("--storage", default="", help="disk tier directory")
@@ -140,7 +142,7 @@ def main(argv=None) -> int:
         rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
     log(f"setup done in {time.time() - t_setup:.1f}s")
 
-    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1),
+    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1), owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective")
 
     def step(timed: bool):

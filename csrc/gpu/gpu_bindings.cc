@@ -87,6 +87,27 @@ void register_gpu_bindings(PyObject* module) {
     return n;
   });
   m.def("set_device", [](int d) { check(hipSetDevice(d), "hipSetDevice"); });
+  // Pairwise GPU links (SURVEY C4's topology map): (i, j, link, hops, p2p) with
+  // link "xgmi" / "pcie" / "other" from hipExtGetLinkTypeAndHopCount.
+  m.def("gpu_topology", [] {
+    int n = 0;
+    check(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    py::list out;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        uint32_t type = 0, hops = 0;
+        const char* link = "other";
+        if (hipExtGetLinkTypeAndHopCount(i, j, &type, &hops) == hipSuccess) {
+          if (type == 4) link = "xgmi";       // HSA_AMD_LINK_INFO_TYPE_XGMI
+          else if (type == 2) link = "pcie";  // HSA_AMD_LINK_INFO_TYPE_PCIE
+        }
+        int p2p = 0;
+        (void)hipDeviceCanAccessPeer(&p2p, i, j);
+        out.append(py::make_tuple(i, j, std::string(link), hops, bool(p2p)));
+      }
+    return out;
+  });
   m.def("device_synchronize", [] {
     py::gil_scoped_release nogil;
     check(hipDeviceSynchronize(), "hipDeviceSynchronize");

@@ -849,7 +849,21 @@ void Node::schedule_mode1() {
         }
         std::vector<NodeID> cand(oit->second.begin(), oit->second.end());
         NodeID owner;
-        if (cfg_.owner_policy == "balanced") {
+        if (cfg_.owner_policy == "links") {
+          // xGMI-aware: every GPU pair has its own link, so spread each dest's
+          // inbound bytes over distinct links (least-loaded owner->dest link,
+          // then least total egress, then lowest id).
+          owner = cand[0];
+          std::pair<int64_t, int64_t> best{INT64_MAX, INT64_MAX};
+          for (NodeID c : cand) {
+            std::pair<int64_t, int64_t> k{link_bytes_[{c, dest}], owner_bytes_[c]};
+            if (k < best) {
+              best = k;
+              owner = c;
+            }
+          }
+          link_bytes_[{owner, dest}] += layer_size(layer);
+        } else if (cfg_.owner_policy == "balanced") {
           int64_t best = INT64_MAX;
           std::vector<NodeID> ties;
           for (NodeID c : cand) {

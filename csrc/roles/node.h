@@ -30,7 +30,7 @@ struct NodeConfig {
   int mode = 0;                     // 0 naive, 1 retransmit, 2 pull, 3 flow
   uint64_t epoch = 0;               // session id carried in messages (0 = none)
   uint64_t seed = 0;                // mode-1 owner RNG (quirk Q5: seeded uniform choice)
-  std::string owner_policy = "random";  // mode 1: "random" (reference) or "balanced"
+  std::string owner_policy = "random";  // mode 1: "random" (reference), "balanced" (egress), "links" (per-link)
   int pull_window = 1;              // mode 2: concurrent jobs per sender (reference: 1)
   int64_t pull_job_bytes = 0;       // mode 2: job = this many bytes of a layer (0 = whole layer, reference)
   bool range_acks = false;          // receiver: also ack each landed range (needed by mode-2 range jobs)
@@ -162,6 +162,7 @@ class Node {
   std::map<LayerID, NodeIDs> owners_;
   std::mt19937_64 rng_;
   std::map<NodeID, int64_t> owner_bytes_;  // balanced owner policy
+  std::map<std::pair<NodeID, NodeID>, int64_t> link_bytes_;  // "links" owner policy: bytes per (src, dst)
   enum class JobState { Pending, Sending };
   struct Job {
     NodeID sender = 0;

@@ -388,6 +388,7 @@ class Runtime:
         job_timeout_s: float = 0.0,
         job_min_rate: float = 0.0,
         pull_job_bytes: int = 0,
+        xgmi_link_gbps: float = 0.0,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed)."""
         self.epoch += 1
@@ -406,6 +407,8 @@ class Runtime:
         nc.collective = collective
         nc.network_bw = {k: v for k, v in self.cfg.network_bw().items()}
         nc.link_bw = {(s, d): bw for s, per in self.cfg.links.items() for d, bw in per.items()}
+        if not nc.link_bw and xgmi_link_gbps > 0 and self.engine_kind == "rccl":
+            nc.link_bw = self.topology_link_bw(xgmi_link_gbps)
         nc.integer_seconds = integer_seconds
         nc.job_timeout_s = job_timeout_s
         nc.job_min_rate = job_min_rate
@@ -477,6 +480,23 @@ class Runtime:
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
                       "group_us_hist", "land_us_hist")
         }
+
+    def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0) -> Dict[tuple, int]:
+        """Per directed (node, node) link capacity for the mode-3 planner from the
+        GPU topology (SURVEY C4/C13'): xGMI links at `xgmi_gbps` divided by their
+        hop count, anything else at `pcie_gbps`. Node i runs on device `device`
+        from the config, else its rank (one process per GPU of this node)."""
+        dev = {n.id: (n.device if n.device is not None else self.node_ids.index(n.id)) for n in self.cfg.nodes}
+        links = {(i, j): (kind, hops) for i, j, kind, hops, _ in _core.gpu_topology()}
+        out = {}
+        for a in self.node_ids:
+            for b in self.node_ids:
+                if a == b:
+                    continue
+                kind, hops = links.get((dev[a], dev[b]), ("other", 1))
+                gbps = xgmi_gbps / max(1, hops) if kind == "xgmi" else pcie_gbps
+                out[(a, b)] = int(gbps * 1e9)
+        return out
 
     def link_bytes(self) -> Dict[str, Dict[int, int]]:
         """Cumulative bytes this rank sent to / received from each peer rank (per-link counters)."""

@@ -53,6 +53,18 @@ def test_corrupt_manifest_is_detected(gpu):
         rt.close()
 
 
+def test_gpu_topology_probe(gpu):
+    import torch
+
+    n = torch.cuda.device_count()
+    topo = gpu.gpu_topology()
+    assert len(topo) == n * (n - 1)
+    for i, j, kind, hops, p2p in topo:
+        assert i != j and kind in ("xgmi", "pcie", "other") and hops >= 0
+    if n > 1:  # an MI355X node: fully connected xGMI
+        assert all(kind == "xgmi" and p2p for _, _, kind, _, p2p in topo)
+
+
 @pytest.mark.parametrize("tier", ["host", "device", "disk"])
 def test_fp8_packed_session(gpu, tier, tmp_path):
     """--pack fp8 on one GPU: bf16 sources are packed on the copy stream while

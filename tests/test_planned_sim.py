@@ -103,6 +103,14 @@ def test_mode0_collective_falls_back_when_not_everyone_needs_it():
     run_cluster(cfg, 0, collective=True)
 
 
+@pytest.mark.parametrize("policy", ["random", "balanced", "links"])
+def test_mode1_owner_policies_with_copies(policy):
+    cfg = make_workload(6, 12, 2 * MiB, tier="host", seeding="uniform", copies=3, seed=5, chunk_bytes=MiB)
+    (res,), key = run_cluster(cfg, 1, owner_policy=policy)
+    need = sum(1 for r in range(6) for l in range(12) if r not in _owners(cfg, l))
+    assert _core.sim_fabric_bytes(key) == need * 2 * MiB
+
+
 def test_device_seeded_uneven_copies_mode1():
     cfg = make_workload(4, 12, 2 * MiB, tier="device", seeding="uniform", copies=2, seed=3, chunk_bytes=MiB)
     run_cluster(cfg, 1)
