@@ -6,6 +6,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
+#include <tuple>
 
 #include "core/crc32c.h"
 #include "core/fp8.h"
@@ -228,6 +230,53 @@ void register_gpu_bindings(PyObject* module) {
     return crc;
   }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
         py::arg("stream") = 0);
+
+  // ---- RCCL path on one GPU: a one-rank communicator driven through the same
+  // Backend::group / crc calls the planned engine issues. `rounds` groups of
+  // {send chunk k to self, recv into dst chunk k}, then an in-place broadcast
+  // from rank 0; returns (src CRCs, dst CRCs after P2P, CRCs after broadcast).
+  m.def("rccl_selftest", [](int device, int64_t bytes, int64_t chunk) {
+    py::gil_scoped_release nogil;
+    if (bytes <= 0 || chunk <= 0 || chunk % 16) throw std::invalid_argument("bytes > 0, chunk % 16 == 0");
+    HipBackendConfig hc;
+    hc.device = device;
+    hc.max_crc_bytes = bytes;
+    hc.self_comm = true;
+    auto be = make_hip_backend(hc);
+    be->init_thread();
+    uint8_t* src = be->alloc(bytes);
+    uint8_t* dst = be->alloc(bytes);
+    check(kern::fill_random(src, bytes, 0x5e1f, nullptr), "fill_random");
+    check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    be->zero_sync(dst, bytes);
+    Ev last = 0;
+    for (int64_t off = 0; off < bytes; off += chunk) {
+      const int64_t n = std::min(chunk, bytes - off);
+      std::vector<XOp> ops{XOp{true, 0, src + off, n}, XOp{false, 0, dst + off, n}};
+      std::vector<Ev> waits;
+      if (last) waits.push_back(last);
+      last = be->group(ops, waits);
+    }
+    auto wait = [&](Ev e) {
+      int q;
+      while ((q = be->query(e)) == 0) std::this_thread::yield();
+      if (q < 0) throw std::runtime_error("rccl_selftest: " + be->async_error());
+    };
+    wait(last);
+    std::vector<uint32_t> a = crc_chunks_sync(reinterpret_cast<uint64_t>(src), bytes, chunk, 0);
+    std::vector<uint32_t> b = crc_chunks_sync(reinterpret_cast<uint64_t>(dst), bytes, chunk, 0);
+    XOp bc{false, 0, dst, bytes};
+    bc.bcast = true;
+    Ev e = be->group({bc}, {last});
+    wait(e);
+    std::vector<uint32_t> c = crc_chunks_sync(reinterpret_cast<uint64_t>(dst), bytes, chunk, 0);
+    std::string err = be->async_error();
+    be->free(src);
+    be->free(dst);
+    be->destroy(false);
+    if (!err.empty()) throw std::runtime_error("rccl_selftest: " + err);
+    return std::make_tuple(a, b, c);
+  }, py::arg("device"), py::arg("bytes"), py::arg("chunk"));
 
   // ---- RCCL engine = planned engine on the HIP backend
   m.def("nccl_unique_id", [] { return py::bytes(nccl_unique_id()); });

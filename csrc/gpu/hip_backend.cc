@@ -37,10 +37,14 @@ class HipBackend : public Backend {
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&crc_dev_), crc_host_, 0));
-    if (cfg_.world > 1) {
-      if (cfg_.nccl_uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("nccl_uid must be ncclUniqueId bytes");
+    if (cfg_.world > 1 || cfg_.self_comm) {
       ncclUniqueId id;
-      memcpy(&id, cfg_.nccl_uid.data(), sizeof id);
+      if (cfg_.world == 1 && cfg_.nccl_uid.empty()) {
+        NCCL_OK(ncclGetUniqueId(&id));
+      } else {
+        if (cfg_.nccl_uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("nccl_uid must be ncclUniqueId bytes");
+        memcpy(&id, cfg_.nccl_uid.data(), sizeof id);
+      }
       auto t0 = log::now_us();
       NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
       log::info(cfg_.rank).i("world", cfg_.world).f("init_ms", double(log::now_us() - t0) / 1e3)

@@ -20,6 +20,9 @@ struct HipBackendConfig {
   int world = 1;
   std::string nccl_uid;  // ncclUniqueId bytes (world > 1)
   int64_t max_crc_bytes = 64ll << 20;  // largest chunk the verify workspace must hold
+  // world == 1: still build a one-rank communicator, so P2P groups to self
+  // exercise the RCCL path on a single-GPU box (rccl_selftest)
+  bool self_comm = false;
 };
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg);

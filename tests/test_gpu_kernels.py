@@ -183,3 +183,13 @@ def test_fp8_fused_verify_unpack_detects_corruption(gpu):
     packed[2 * pchunk + chunk // 2 + 3] ^= 0x10  # a scale byte of chunk 2
     bad = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, 128, out.data_ptr())
     assert [i for i in range(4) if good[i] != bad[i]] == [2]
+
+
+@pytest.mark.parametrize("n,chunk", [(8 << 20, 2 << 20), ((64 << 20) + 16, 16 << 20)])
+def test_rccl_selftest_p2p_and_broadcast(gpu, n, chunk):
+    # One-rank communicator: ncclSend/ncclRecv to self in groups and an
+    # in-place ncclBroadcast, issued through the engine's Backend::group.
+    src, p2p, bcast = gpu.rccl_selftest(0, n, chunk)
+    assert len(src) == (n + chunk - 1) // chunk
+    assert p2p == src
+    assert bcast == src
