@@ -90,9 +90,10 @@ def main(argv=None) -> int:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-
     sys.path.insert(0, HERE)
+    from distributed_llm_dissemination_amd.utils.launch import rank_device, shared_gpu
+
+    local_rank = rank_device(rank, int(os.environ.get("LOCAL_RANK", str(rank))))
     import torch
     import torch.distributed as dist
 
@@ -204,7 +205,9 @@ def main(argv=None) -> int:
                 "bytes_per_step": total_bytes,
                 "time_to_full_placement_s": round(ms_per_step / 1e3, 6),
                 "leader_time_to_deliver_s": round(last.time_to_deliver_s, 6) if last else None,
-                "engine": "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)",
+                "engine": ("rccl-socket, all ranks on one GPU (schedule rehearsal; bandwidth not meaningful)"
+                           if world > 1 and shared_gpu() else
+                           "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)"),
                 "pack": args.pack,
             },
         }

@@ -163,8 +163,10 @@ def main(argv=None) -> int:
         import torch.distributed as dist
 
         if args.engine == "rccl":
+            from .utils.launch import rank_device
+
             local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-            device = me.device if me.device is not None else local_rank
+            device = rank_device(int(os.environ.get("RANK", "0")), local_rank, me.device)
             torch.cuda.set_device(device)
         if world > 1:
             # Bootstrap only (gloo over TCP): barriers, the ncclUniqueId, addresses.

@@ -28,19 +28,24 @@ def _port():
         return s.getsockname()[1]
 
 
-def _torchrun(n, args, timeout=600):
+def _torchrun(n, args, timeout=300):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     env = dict(os.environ, PYTHONPATH=ROOT)
+    if _ngpus() < n:
+        # one-GPU box: every rank on device 0, RCCL over loopback sockets (utils/launch.py)
+        env["DISSEM_SHARED_GPU"] = "1"
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
 
 
 @pytest.fixture(scope="module")
 def n():
+    """Ranks: every GPU (at most 8), or 3 ranks sharing one GPU on a one-GPU box
+    (odd on purpose: relay/scatter schedules with an uneven split)."""
     k = _ngpus()
-    if k < 2:
-        pytest.skip("needs >= 2 GPUs")
-    return min(k, 8)
+    if k < 1:
+        pytest.skip("needs a GPU")
+    return min(k, 8) if k >= 2 else 3
 
 
 @pytest.mark.parametrize("mode,extra", [(1, []), (2, ["--pull-window", "2"]), (3, []), (0, ["--seeding", "leader"]),
