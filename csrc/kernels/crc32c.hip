@@ -7,18 +7,31 @@
 //  * a chunk is cut into 16 KiB segments; one wave owns a segment;
 //  * lane l of the wave reads 16-B words l, l+64, l+128, ... (each wave
 //    instruction reads 1 KiB contiguous: fully coalesced) and keeps the raw CRC
-//    of its strided sub-message: s = shift_1024B(s) xor crc16(word), i.e. 4 + 16
-//    table lookups from LDS-resident slice-by-16 and shift tables;
-//  * lanes are aligned to the segment end with one GF(2) multiply by a per-lane
-//    constant x^(8*16*m) and XOR-reduced with cross-lane shuffles;
-//  * a second, tiny kernel folds the segments of each chunk (one wave per
-//    chunk) and applies the init/xorout term, writing the standard CRC32C.
+//    of its strided sub-message: s = shift_1KiB(s) xor crc16(word). Both maps
+//    are GF(2)-linear, so one step is the XOR of 40 nibble-table lookups (32 for
+//    the word's nibbles, 8 for the register's);
+//  * each lane's CRC is shifted to the END OF ITS CHUNK with one GF(2)
+//    multiply by a host-computed constant (per segment and lane: the lane's
+//    distance to its segment end plus the segment's distance to the chunk
+//    end), then the lanes are XOR-reduced with cross-lane shuffles, so
+//  * a chunk's raw CRC is the plain XOR of its segments' values: a second,
+//    small kernel XOR-reduces them (one 256-thread block per chunk) and adds
+//    the init/xorout term, writing the standard CRC32C.
 // The result is the exact CRC32C of each chunk for any chunk length that is a
-// multiple of 16 (the final chunk may have any length).
+// multiple of 16 (the buffer's final chunk may have any length).
+//
+// LDS layout (MI355X_MICROARCH.md, LDS): a ds_read_b32 is served in two groups
+// of 32 lanes over 32 banks; with data-dependent indices a plain 256-entry table
+// averages ~3 LDS cycles per group (bank conflicts measured at 2x the useful
+// cycles in round 1, profiles/r1_counters). Each nibble table entry is stored
+// 32 times, replica r in bank r, and lane l reads replica l & 31: conflict-free
+// by construction (profiles/r1_crc_ab: SQ_LDS_BANK_CONFLICT = 0).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "core/crc32c.h"
@@ -29,17 +42,18 @@ namespace kern {
 
 namespace {
 
-// 16 KiB per wave: 16 strided words per lane. Small enough that one 64 MiB
-// landing chunk spreads over 4096 waves (16 per CU), large enough that the
-// per-wave lane-alignment multiply is amortized.
+// 16 KiB per wave: 16 strided words per lane. One 64 MiB landing chunk spreads
+// over 4096 waves (16 per CU).
 constexpr int kSegBytes = 16 * 1024;
-constexpr int kT16 = 16 * 256;   // slice-by-16 tables
-constexpr int kA = 4 * 256;      // shift-by-1024-bytes map
-constexpr int kLanePow = 64;     // x^(8*16*m), m = 0..63
-constexpr int kAS = 4 * 256;     // shift-by-one-segment map
-constexpr int kX2N = 64;         // x^(2^k)
-constexpr int kConstWords = kT16 + kA + kLanePow + kAS + kX2N;
-constexpr int kSegKernelLds = kT16 + kA + kLanePow;
+constexpr int kWordsPerLane = kSegBytes / 16 / 64;
+constexpr int kNibTables = 40;  // 32 for a 16-B word, 8 for the register shifted by 1 KiB
+// Global constants: [T0: 256][lanepow: 64][nibble tables: 40 x 16].
+constexpr int kOffT0 = 0;
+constexpr int kOffLanePow = 256;
+constexpr int kOffNib = 256 + 64;
+constexpr int kConstWords = kOffNib + kNibTables * 16;
+// 40 tables x 16 entries x 32 replicas x 4 B = 80 KiB: two workgroups per CU.
+constexpr int kNibLds = kNibTables * 16 * 32;
 
 __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   uint32_t p = 0;
@@ -54,51 +68,49 @@ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
-__device__ inline uint32_t xpow8n(const uint32_t* x2n, uint64_t n) {
-  uint32_t p = 1u << 31;
-  int k = 3;
-#pragma unroll 1
-  while (n) {
-    if (n & 1) p = multmodp(x2n[k & 63], p);
-    n >>= 1;
-    ++k;
-  }
-  return p;
-}
-
-__device__ inline uint32_t shift_map(const uint32_t* A, uint32_t s) {
-  return A[s & 255] ^ A[256 + ((s >> 8) & 255)] ^ A[512 + ((s >> 16) & 255)] ^ A[768 + (s >> 24)];
-}
-
-__device__ inline uint32_t crc16raw(const uint32_t* T, uint4 w) {
-  return T[15 * 256 + (w.x & 255)] ^ T[14 * 256 + ((w.x >> 8) & 255)] ^ T[13 * 256 + ((w.x >> 16) & 255)] ^
-         T[12 * 256 + (w.x >> 24)] ^ T[11 * 256 + (w.y & 255)] ^ T[10 * 256 + ((w.y >> 8) & 255)] ^
-         T[9 * 256 + ((w.y >> 16) & 255)] ^ T[8 * 256 + (w.y >> 24)] ^ T[7 * 256 + (w.z & 255)] ^
-         T[6 * 256 + ((w.z >> 8) & 255)] ^ T[5 * 256 + ((w.z >> 16) & 255)] ^ T[4 * 256 + (w.z >> 24)] ^
-         T[3 * 256 + (w.w & 255)] ^ T[2 * 256 + ((w.w >> 8) & 255)] ^ T[1 * 256 + ((w.w >> 16) & 255)] ^
-         T[0 * 256 + (w.w >> 24)];
-}
-
 __device__ inline uint32_t wave_xor(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
   return v;
 }
 
-// One wave per 16 KiB segment; writes the segment's raw CRC to seg_out[g].
-__global__ void __launch_bounds__(256) crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes,
-                                                              int64_t chunk_bytes, int64_t spc,
-                                                              int64_t total_segs,
-                                                              const uint32_t* __restrict__ consts,
-                                                              uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t lds[kSegKernelLds];
-  for (int i = threadIdx.x; i < kSegKernelLds; i += blockDim.x) lds[i] = consts[i];
-  __syncthreads();
-  const uint32_t* T = lds;
-  const uint32_t* A = lds + kT16;
-  const uint32_t* lanepow = lds + kT16 + kA;
+// XOR of the 8 nibble tables t0..t0+7, indexed by the 8 nibbles of x.
+// L = lds + (lane & 31): entry (t, v) of this lane's bank-private replica.
+__device__ inline uint32_t nib8(const uint32_t* L, int t0, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) r ^= L[(t0 + n) * 512 + ((x >> (4 * n)) & 15) * 32];
+  return r;
+}
 
+// One strided step of a lane: s = shift_1KiB(s) xor crc16raw(w).
+__device__ inline uint32_t nib_step(const uint32_t* L, uint32_t s, uint4 w) {
+  return nib8(L, 32, s) ^ nib8(L, 0, w.x) ^ nib8(L, 8, w.y) ^ nib8(L, 16, w.z) ^ nib8(L, 24, w.w);
+}
+
+__device__ inline void load_nib_lds(uint32_t* lds, const uint32_t* __restrict__ consts) {
+  // 32 identical replicas per entry, written 4 at a time (16-B stores).
+  const uint32_t* nib = consts + kOffNib;
+  for (int i = threadIdx.x; i < kNibLds / 4; i += blockDim.x) {
+    const uint32_t v = nib[i >> 3];
+    reinterpret_cast<uint4*>(lds)[i] = make_uint4(v, v, v, v);
+  }
+  __syncthreads();
+}
+
+// Segment walk shared by the plain and the fused kernels. Each wave owns 16 KiB
+// segments; Visit sees every 16-B word with its byte offset in the chunk
+// (visit.begin(c, chunk_start, chunk_len) once per segment). seg_out[g] gets
+// the segment's raw CRC shifted to the end of its chunk: lane l of full segment
+// k multiplies by shift[k * 64 + l] (shift_last for a shorter final chunk). A
+// partial segment is always its chunk's last, so its lanes only align to it.
+template <int DEPTH, class Visit>
+__device__ inline void segment_crcs(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
+                                    int64_t spc, int64_t total_segs, const uint32_t* __restrict__ consts,
+                                    const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
+                                    uint32_t* __restrict__ seg_out, const uint32_t* lds, Visit& visit) {
   const int lane = threadIdx.x & 63;
+  const uint32_t* L = lds + (lane & 31);
   const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
   const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
   for (int64_t g = wave; g < total_segs; g += nwaves) {
@@ -109,36 +121,49 @@ __global__ void __launch_bounds__(256) crc32c_segments_kernel(const uint8_t* __r
     const int64_t seg_len = min(int64_t(kSegBytes), chunk_len - seg_start);
     const int64_t nw = seg_len >> 4;
     const uint4* words = reinterpret_cast<const uint4*>(src + chunk_start + seg_start);
+    visit.begin(c, chunk_start, chunk_len);
     uint32_t s = 0;
-    int64_t j = lane;
     if (nw == kSegBytes / 16) {
-      // Full segment: 64 words per lane, loads issued 8 ahead.
-#pragma unroll 8
-      for (int it = 0; it < kSegBytes / 16 / 64; ++it) {
-        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-        const u32x4 wv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * it));
-        const uint4 w = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        s = shift_map(A, s) ^ crc16raw(T, w);
+      // Full segment: 16 strided words per lane, DEPTH loads in flight per batch.
+      using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int b = 0; b < kWordsPerLane; b += DEPTH) {
+        u32x4 wv[DEPTH];
+#pragma unroll
+        for (int i = 0; i < DEPTH; ++i)
+          wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * (b + i)));
+#pragma unroll
+        for (int i = 0; i < DEPTH; ++i) {
+          const uint4 w = make_uint4(wv[i][0], wv[i][1], wv[i][2], wv[i][3]);
+          s = nib_step(L, s, w);
+          visit(w, seg_start + 16 * (lane + 64 * (b + i)));
+        }
       }
-      s = multmodp(lanepow[63 - lane], s);
+      s = multmodp((chunk_len == chunk_bytes ? shift : shift_last)[k * 64 + lane], s);
     } else {
       int64_t last = -1;
-      for (; j < nw; j += 64) {
-        uint4 w = words[j];
-        s = shift_map(A, s) ^ crc16raw(T, w);
+      for (int64_t j = lane; j < nw; j += 64) {
+        const uint4 w = words[j];
+        s = nib_step(L, s, w);
+        visit(w, seg_start + 16 * j);
         last = j;
       }
-      if (last >= 0) s = multmodp(lanepow[nw - 1 - last], s);
+      if (last >= 0) s = multmodp(consts[kOffLanePow + nw - 1 - last], s);
     }
     s = wave_xor(s);
     if (lane == 0) {
       // Byte tail (only the buffer's final segment can have one).
       const uint8_t* tail = src + chunk_start + seg_start + (nw << 4);
-      for (int64_t b = 0; b < (seg_len & 15); ++b) s = T[(s ^ tail[b]) & 255] ^ (s >> 8);
+      for (int64_t b = 0; b < (seg_len & 15); ++b) s = consts[kOffT0 + ((s ^ tail[b]) & 255)] ^ (s >> 8);
       seg_out[g] = s;
     }
   }
 }
+
+struct NoVisit {
+  __device__ void begin(int64_t, int64_t, int64_t) {}
+  __device__ void operator()(const uint4&, int64_t) {}
+};
 
 __device__ inline uint16_t f32_to_bf16_rne(float f) {
   uint32_t u = __float_as_uint(f);
@@ -163,122 +188,110 @@ __device__ inline void unpack16(uint4 w, float s, uint4* __restrict__ dst) {
 }
 
 // Fused verify + unpack of fp8-packed chunks (core/fp8.h layout
-// [q: n bytes][scales: n/BLOCK f32] per chunk): one pass over the packed bytes
-// computes each segment's raw CRC exactly like crc32c_segments_kernel and, for
-// words in the q region, writes the dequantized bf16 values. Every packed byte
-// is read once from HBM; the scales (1/32 of the traffic) are re-read from L2.
+// [q: n bytes][scales: n/BLOCK f32] per chunk): while computing each segment's
+// CRC, words in the q region are dequantized and written as bf16. Every packed
+// byte is read once from HBM; the scales (1/32 of the traffic) come from L2.
 template <int BLOCK>
-__global__ void __launch_bounds__(256) verify_unpack_segments_kernel(
-    const uint8_t* __restrict__ src, int64_t bytes, int64_t pchunk, int64_t spc, int64_t total_segs,
-    int64_t out_chunk_elems, const uint32_t* __restrict__ consts, uint32_t* __restrict__ seg_out,
-    uint16_t* __restrict__ out) {
-  __shared__ uint32_t lds[kSegKernelLds];
-  for (int i = threadIdx.x; i < kSegKernelLds; i += blockDim.x) lds[i] = consts[i];
-  __syncthreads();
-  const uint32_t* T = lds;
-  const uint32_t* A = lds + kT16;
-  const uint32_t* lanepow = lds + kT16 + kA;
-
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
-  for (int64_t g = wave; g < total_segs; g += nwaves) {
-    const int64_t c = g / spc, k = g % spc;
-    const int64_t chunk_start = c * pchunk;
-    const int64_t chunk_len = min(pchunk, bytes - chunk_start);
-    const int64_t n_q = chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
-    const float* scales = reinterpret_cast<const float*>(src + chunk_start + n_q);
-    uint16_t* obase = out + c * out_chunk_elems;
-    const int64_t seg_start = k * kSegBytes;
-    const int64_t seg_len = min(int64_t(kSegBytes), chunk_len - seg_start);
-    const int64_t nw = seg_len >> 4;
-    const uint4* words = reinterpret_cast<const uint4*>(src + chunk_start + seg_start);
-    uint32_t s = 0;
-    auto consume = [&](const uint4 w, int64_t j) {
-      s = shift_map(A, s) ^ crc16raw(T, w);
-      const int64_t e = seg_start + 16 * j;  // byte offset in chunk = element index in the q region
-      if (e < n_q) unpack16(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
-    };
-    if (nw == kSegBytes / 16) {
-#pragma unroll 8
-      for (int it = 0; it < kSegBytes / 16 / 64; ++it) {
-        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-        const u32x4 wv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * it));
-        consume(make_uint4(wv[0], wv[1], wv[2], wv[3]), lane + 64 * it);
-      }
-      s = multmodp(lanepow[63 - lane], s);
-    } else {
-      int64_t last = -1;
-      for (int64_t j = lane; j < nw; j += 64) {
-        consume(words[j], j);
-        last = j;
-      }
-      if (last >= 0) s = multmodp(lanepow[nw - 1 - last], s);
-    }
-    s = wave_xor(s);
-    if (lane == 0) {
-      const uint8_t* tail = src + chunk_start + seg_start + (nw << 4);
-      for (int64_t b = 0; b < (seg_len & 15); ++b) s = T[(s ^ tail[b]) & 255] ^ (s >> 8);
-      seg_out[g] = s;
-    }
+struct UnpackVisit {
+  int64_t out_chunk_elems;
+  uint16_t* out;
+  const uint8_t* src;
+  int64_t n_q = 0;
+  const float* scales = nullptr;
+  uint16_t* obase = nullptr;
+  __device__ void begin(int64_t c, int64_t chunk_start, int64_t chunk_len) {
+    n_q = chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
+    scales = reinterpret_cast<const float*>(src + chunk_start + n_q);
+    obase = out + c * out_chunk_elems;
   }
+  __device__ void operator()(const uint4& w, int64_t e) {  // e: byte offset in chunk = element index in q
+    if (e < n_q) unpack16(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
+  }
+};
+
+// Launch shape: 512 threads (8 waves), two workgroups per CU (LDS-bound at
+// 80 KiB each); waves_per_eu(4) keeps VGPRs <= 128 so both fit.
+constexpr int kSegThreads = 512;
+
+__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
+                       int64_t total_segs, const uint32_t* __restrict__ consts, const uint32_t* __restrict__ shift,
+                       const uint32_t* __restrict__ shift_last, uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t lds[kNibLds];
+  load_nib_lds(lds, consts);
+  NoVisit v;
+  segment_crcs<16>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
 }
 
-// One wave per chunk: fold the chunk's segment CRCs and finalize. `fold` holds
-// host-computed constants for full chunks: per lane x^(8*bytes after its run)
-// and the init/xorout term; only a short final chunk computes them here.
-__global__ void __launch_bounds__(64) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
-                                                         int64_t chunk_bytes, int64_t spc,
-                                                         const uint32_t* __restrict__ consts,
-                                                         const uint32_t* __restrict__ fold,
-                                                         uint32_t* __restrict__ out) {
-  __shared__ uint32_t AS[kAS];
-  __shared__ uint32_t X2N[kX2N];
-  for (int i = threadIdx.x; i < kAS; i += 64) AS[i] = consts[kT16 + kA + kLanePow + i];
-  for (int i = threadIdx.x; i < kX2N; i += 64) X2N[i] = consts[kT16 + kA + kLanePow + kAS + i];
-  __syncthreads();
-  const int lane = threadIdx.x;
+template <int BLOCK>
+__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
+verify_unpack_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t pchunk, int64_t spc,
+                              int64_t total_segs, int64_t out_chunk_elems, const uint32_t* __restrict__ consts,
+                              const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
+                              uint32_t* __restrict__ seg_out, uint16_t* __restrict__ out) {
+  __shared__ uint32_t lds[kNibLds];
+  load_nib_lds(lds, consts);
+  UnpackVisit<BLOCK> v{out_chunk_elems, out, src};
+  segment_crcs<4>(src, bytes, pchunk, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
+}
+
+// One 256-thread block per chunk: XOR of the chunk's (pre-shifted) segment
+// values plus the init/xorout term. init[0]: full chunks, init[1]: short last chunk.
+__global__ void __launch_bounds__(256) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
+                                                          int64_t chunk_bytes, int64_t spc,
+                                                          const uint32_t* __restrict__ init,
+                                                          uint32_t* __restrict__ out) {
+  __shared__ uint32_t part[4];
   const int64_t c = blockIdx.x;
-  const int64_t chunk_start = c * chunk_bytes;
-  const int64_t chunk_len = min(chunk_bytes, bytes - chunk_start);
+  const int64_t chunk_len = min(chunk_bytes, bytes - c * chunk_bytes);
   const int64_t n = (chunk_len + kSegBytes - 1) / kSegBytes;
-  const int64_t q = (n + 63) / 64;
-  const int64_t b = min(n, int64_t(lane) * q), e = min(n, int64_t(lane + 1) * q);
+  const uint32_t* seg = seg_out + c * spc;
   uint32_t r = 0;
-  for (int64_t k = b; k < e; ++k) {
-    const int64_t len = min(int64_t(kSegBytes), chunk_len - k * kSegBytes);
-    r = (len == kSegBytes ? shift_map(AS, r) : multmodp(xpow8n(X2N, uint64_t(len)), r)) ^ seg_out[c * spc + k];
-  }
-  const bool full = chunk_len == chunk_bytes;
-  const int64_t end_byte = min(e * kSegBytes, chunk_len);
-  if (r && e > b) r = multmodp(full ? fold[lane] : xpow8n(X2N, uint64_t(chunk_len - end_byte)), r);
-  r = wave_xor(e > b ? r : 0u);
-  if (lane == 0)
-    out[c] = r ^ (full ? fold[64] : (multmodp(xpow8n(X2N, uint64_t(chunk_len)), 0xFFFFFFFFu) ^ 0xFFFFFFFFu));
+  for (int64_t k = threadIdx.x; k < n; k += 256) r ^= seg[k];
+  r = wave_xor(r);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
+  __syncthreads();
+  if (threadIdx.x == 0) out[c] = part[0] ^ part[1] ^ part[2] ^ part[3] ^ init[chunk_len == chunk_bytes ? 0 : 1];
 }
 
+// Per-device constant tables and per-(chunk, last chunk) fold tables.
 struct DeviceConsts {
   std::mutex mu;
   std::map<int, uint32_t*> by_device;
-  std::map<std::pair<int, int64_t>, uint32_t*> fold;  // (device, chunk_bytes) -> 65 fold constants
+  // (device, chunk_bytes, last_len) -> [shift: spc x 64][shift_last: spc x 64][init: 2]
+  std::map<std::tuple<int, int64_t, int64_t>, uint32_t*> fold;
 };
 DeviceConsts g_consts;
 
-uint32_t* fold_consts(int64_t chunk_bytes) {
+// Per full segment k of a `len`-byte chunk and lane l: x^(8 * (bytes from the
+// end of lane l's last word to the chunk end)) = x^(8*16*(63 - l)) * x^(8 * (len - end of k)).
+void lane_shifts(int64_t len, int64_t spc, uint32_t* out) {
+  const int64_t nfull = len / kSegBytes;
+  std::fill(out, out + spc * 64, 0u);  // partial / absent segments: unused
+  if (nfull == 0) return;
+  uint32_t lanepow[64];
+  for (int m = 0; m < 64; ++m) lanepow[m] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
+  const uint32_t xs = crc32c_xpow8n(kSegBytes);
+  uint32_t seg = crc32c_xpow8n(uint64_t(len - nfull * kSegBytes));  // last full segment
+  for (int64_t k = nfull - 1; k >= 0; --k) {
+    for (int l = 0; l < 64; ++l) out[k * 64 + l] = crc32c_multmodp(lanepow[63 - l], seg);
+    seg = crc32c_multmodp(xs, seg);
+  }
+}
+
+uint32_t* fold_consts(int64_t chunk_bytes, int64_t last_len) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_consts.mu);
-  auto key = std::make_pair(dev, chunk_bytes);
+  auto key = std::make_tuple(dev, chunk_bytes, last_len);
   auto it = g_consts.fold.find(key);
   if (it != g_consts.fold.end()) return it->second;
-  const int64_t n = (chunk_bytes + kSegBytes - 1) / kSegBytes, q = (n + 63) / 64;
-  std::vector<uint32_t> h(65);
-  for (int l = 0; l < 64; ++l) {
-    int64_t e = std::min(n, int64_t(l + 1) * q);
-    int64_t end_byte = std::min(e * kSegBytes, chunk_bytes);
-    h[size_t(l)] = crc32c_xpow8n(uint64_t(chunk_bytes - end_byte));
-  }
-  h[64] = crc32c_init_term(uint64_t(chunk_bytes));
+  const int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
+  std::vector<uint32_t> h(size_t(2 * spc * 64 + 2));
+  lane_shifts(chunk_bytes, spc, h.data());
+  lane_shifts(last_len, spc, h.data() + spc * 64);
+  h[size_t(2 * spc * 64)] = crc32c_init_term(uint64_t(chunk_bytes));
+  h[size_t(2 * spc * 64 + 1)] = crc32c_init_term(uint64_t(last_len));
   uint32_t* d = nullptr;
   if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
   if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
@@ -292,21 +305,45 @@ uint32_t* device_consts() {
   std::lock_guard<std::mutex> lk(g_consts.mu);
   auto it = g_consts.by_device.find(dev);
   if (it != g_consts.by_device.end()) return it->second;
-  std::vector<uint32_t> h(kConstWords);
-  crc32c_slice16_tables(h.data());
-  crc32c_shift_tables(1024, h.data() + kT16);
-  for (int m = 0; m < 64; ++m) h[size_t(kT16 + kA + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
-  crc32c_shift_tables(kSegBytes, h.data() + kT16 + kA + kLanePow);
-  uint32_t p = 1u << 30;
-  for (int k = 0; k < 64; ++k) {
-    h[size_t(kT16 + kA + kLanePow + kAS + k)] = p;
-    p = crc32c_multmodp(p, p);
-  }
+  std::vector<uint32_t> T(16 * 256), A(4 * 256), h(kConstWords);
+  crc32c_slice16_tables(T.data());
+  crc32c_shift_tables(1024, A.data());
+  for (int i = 0; i < 256; ++i) h[size_t(kOffT0 + i)] = T[size_t(i)];
+  for (int m = 0; m < 64; ++m) h[size_t(kOffLanePow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
+  // Nibble tables: t = 2k + hi for data byte k (slice-by-16 table 15 - k),
+  // t = 32 + 2i + hi for byte i of the register (1 KiB shift map).
+  for (int t = 0; t < kNibTables; ++t)
+    for (uint32_t v = 0; v < 16; ++v) {
+      const uint32_t byte = v << (4 * (t & 1));
+      h[size_t(kOffNib + t * 16 + int(v))] =
+          t < 32 ? T[size_t((15 - t / 2) * 256) + byte] : A[size_t(((t - 32) / 2) * 256) + byte];
+    }
   uint32_t* d = nullptr;
   if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
   if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
   g_consts.by_device[dev] = d;
   return d;
+}
+
+// Two workgroups per CU, one 16 KiB segment per wave (grid-stride beyond that).
+dim3 seg_grid(int64_t total_segs) {
+  const int64_t waves = kSegThreads / 64;
+  return dim3(unsigned(std::min<int64_t>((total_segs + waves - 1) / waves, 2 * 256)));
+}
+
+struct Plan {
+  int64_t spc, nchunks, total_segs;
+  uint32_t *consts, *fold;
+};
+
+hipError_t plan(int64_t bytes, int64_t chunk_bytes, Plan* p) {
+  p->spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
+  p->nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
+  const int64_t last_len = bytes - (p->nchunks - 1) * chunk_bytes;
+  p->total_segs = (p->nchunks - 1) * p->spc + (last_len + kSegBytes - 1) / kSegBytes;
+  p->consts = device_consts();
+  p->fold = fold_consts(chunk_bytes, last_len);
+  return p->consts && p->fold ? hipSuccess : hipErrorOutOfMemory;
 }
 
 }  // namespace
@@ -322,19 +359,14 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
                          hipStream_t s) {
   if (bytes <= 0) return hipSuccess;
   if (chunk_bytes <= 0 || chunk_bytes % 16 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
-  uint32_t* consts = device_consts();
-  uint32_t* fold = fold_consts(chunk_bytes);
-  if (!consts || !fold) return hipErrorOutOfMemory;
-  const int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
-  const int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
-  const int64_t last_len = bytes - (nchunks - 1) * chunk_bytes;
-  const int64_t total_segs = (nchunks - 1) * spc + (last_len + kSegBytes - 1) / kSegBytes;
-  int64_t blocks = (total_segs + 3) / 4;
-  if (blocks > 256 * 6) blocks = 256 * 6;
+  Plan p;
+  if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  crc32c_segments_kernel<<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(static_cast<const uint8_t*>(src), bytes,
-                                                                      chunk_bytes, spc, total_segs, consts, seg);
-  crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, chunk_bytes, spc, consts, fold, out);
+  crc32c_segments_kernel<<<seg_grid(p.total_segs), dim3(kSegThreads), 0, s>>>(
+      static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold, p.fold + p.spc * 64,
+      seg);
+  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, chunk_bytes, p.spc,
+                                                                     p.fold + 2 * p.spc * 64, out);
   return hipGetLastError();
 }
 
@@ -347,27 +379,23 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   const int64_t pchunk = src_chunk / 2 + src_chunk / 2 / block * 4;
   const int64_t full = src_bytes / src_chunk, tail = src_bytes % src_chunk;
   const int64_t bytes = full * pchunk + (tail ? tail / 2 + tail / 2 / block * 4 : 0);
-  uint32_t* consts = device_consts();
-  uint32_t* fold = fold_consts(pchunk);
-  if (!consts || !fold) return hipErrorOutOfMemory;
-  const int64_t spc = (pchunk + kSegBytes - 1) / kSegBytes;
-  const int64_t nchunks = (bytes + pchunk - 1) / pchunk;
-  const int64_t last_len = bytes - (nchunks - 1) * pchunk;
-  const int64_t total_segs = (nchunks - 1) * spc + (last_len + kSegBytes - 1) / kSegBytes;
-  int64_t blocks = (total_segs + 3) / 4;
-  if (blocks > 256 * 6) blocks = 256 * 6;
+  Plan p;
+  if (hipError_t e = plan(bytes, pchunk, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  auto* p = static_cast<const uint8_t*>(packed);
-  const dim3 grid{unsigned(blocks)}, tpb{256};
+  auto* src = static_cast<const uint8_t*>(packed);
+  const int64_t oc = src_chunk / 2;
+  const dim3 grid = seg_grid(p.total_segs), tpb{kSegThreads};
+  const uint32_t *sp = p.fold, *sl = p.fold + p.spc * 64;
   switch (block) {
-    case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
-    case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
-    case 128: verify_unpack_segments_kernel<128><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
-    case 256: verify_unpack_segments_kernel<256><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
-    case 512: verify_unpack_segments_kernel<512><<<grid, tpb, 0, s>>>(p, bytes, pchunk, spc, total_segs, src_chunk / 2, consts, seg, out); break;
+    case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
+    case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
+    case 128: verify_unpack_segments_kernel<128><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
+    case 256: verify_unpack_segments_kernel<256><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
+    case 512: verify_unpack_segments_kernel<512><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
     default: return hipErrorInvalidValue;
   }
-  crc32c_fold_kernel<<<dim3(unsigned(nchunks)), dim3(64), 0, s>>>(seg, bytes, pchunk, spc, consts, fold, crc_out);
+  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, pchunk, p.spc,
+                                                                     p.fold + 2 * p.spc * 64, crc_out);
   return hipGetLastError();
 }
 

@@ -28,6 +28,8 @@ def test_fill_random_matches_host(gpu, n):
         (5 << 20, (1 << 20) + 4096),  # chunk not a multiple of the 64 KiB segment
         (7 << 20, 48 << 10),  # chunks smaller than a segment
         (64 << 20, 64 << 20),
+        ((64 << 20) + (5 << 10) + 3, 64 << 20),  # short last chunk: its own segment shifts and init term
+        (100 << 10, 100 << 10),  # a partial 16 KiB segment inside one chunk
     ],
 )
 def test_crc32c_chunks_match_host(gpu, n, chunk):
@@ -35,9 +37,8 @@ def test_crc32c_chunks_match_host(gpu, n, chunk):
     gpu.fill_random(t.data_ptr(), n, 7 + n)
     torch.cuda.synchronize()
     host = t.cpu().numpy().tobytes()
-    got = gpu.crc32c_chunks(t.data_ptr(), n, chunk)
     want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
-    assert got == want
+    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk) == want
 
 
 def test_crc32c_detects_single_bit_flip(gpu):
