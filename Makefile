@@ -54,7 +54,11 @@ $(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h) Makefile
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-tools: bin/diskspeed
+tools: bin/diskspeed bin/h2dbench
+
+bin/h2dbench: csrc/tools/h2dbench.hip
+	@mkdir -p bin
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
 
 bin/diskspeed: csrc/tools/diskspeed.cc
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Icsrc -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lpthread
@@ -72,6 +76,6 @@ $(BUILD)/tests/core_selftest_asan: $(SAN_SRC)
 	$(CXX) -O1 -g -std=c++17 -Icsrc -fsanitize=address,undefined -fno-omit-frame-pointer -I/opt/rocm/include -o $@ $(SAN_SRC) -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx -lpthread
 
 clean:
-	rm -rf $(BUILD) $(PKG)/_core*.so bin/diskspeed
+	rm -rf $(BUILD) $(PKG)/_core*.so bin/diskspeed bin/h2dbench
 
 .PHONY: all tools sanitize clean
