@@ -256,7 +256,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("max_retries", &PlannedConfig::max_retries)
       .def_readwrite("inject_corrupt", &PlannedConfig::inject_corrupt)
       .def_readwrite("inject_seed", &PlannedConfig::inject_seed)
-      .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s);
+      .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s)
+      .def_readwrite("reserve_cus", &PlannedConfig::reserve_cus);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)

@@ -59,6 +59,11 @@ struct PlannedConfig {
   double inject_corrupt = 0;
   uint64_t inject_seed = 1;
   double group_timeout_s = 300;    // a P2P group pending longer than this fails the engine (dead peer)
+  // CUs the verify/copy-stream kernels (CRC, fp8 pack) may never occupy, so an
+  // RCCL group kernel always finds free CUs to launch on instead of queueing
+  // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
+  // -1: 32 when world > 1 (one XCD's worth), 0 on one rank (no RCCL traffic).
+  int reserve_cus = -1;
 };
 
 struct PlannedStats {

@@ -287,6 +287,7 @@ void register_gpu_bindings(PyObject* module) {
     hc.world = cfg.world;
     hc.nccl_uid = std::string(uid);
     hc.max_crc_bytes = cfg.chunk_bytes;
+    hc.reserve_cus = cfg.reserve_cus >= 0 ? cfg.reserve_cus : (cfg.world > 1 ? 32 : 0);
     py::gil_scoped_release nogil;
     return std::make_shared<PlannedEngine>(cfg, make_hip_backend(hc));
   }, py::arg("cfg"), py::arg("device") = 0, py::arg("nccl_uid") = py::bytes(""));

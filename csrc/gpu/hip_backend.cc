@@ -31,8 +31,8 @@ class HipBackend : public Backend {
   explicit HipBackend(const HipBackendConfig& cfg) : cfg_(cfg) {
     HIP_OK(hipSetDevice(cfg_.device));
     HIP_OK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&verify_, hipStreamNonBlocking));
+    copy_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
+    verify_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     HIP_OK(hipMalloc(&ws_, kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes)));
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
                          hipHostMallocMapped | hipHostMallocCoherent));
@@ -207,6 +207,21 @@ class HipBackend : public Backend {
 }  // namespace
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg) { return std::make_unique<HipBackend>(cfg); }
+
+hipStream_t create_stream_reserving(int device, int reserve) {
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  int cus = 0;
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  if (reserve <= 0 || reserve >= cus) {
+    HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+  }
+  std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0u);
+  for (int cu = 0; cu < cus - reserve; ++cu) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+  HIP_OK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  return s;
+}
 
 std::shared_ptr<HostBuffer> alloc_pinned(int64_t size) {
   void* p = nullptr;

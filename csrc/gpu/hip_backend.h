@@ -6,6 +6,8 @@
 // two of our queues serialize behind each other.
 #pragma once
 
+#include <hip/hip_runtime_api.h>
+
 #include <memory>
 #include <string>
 
@@ -23,7 +25,14 @@ struct HipBackendConfig {
   // world == 1: still build a one-rank communicator, so P2P groups to self
   // exercise the RCCL path on a single-GPU box (rccl_selftest)
   bool self_comm = false;
+  // > 0: the verify and copy streams get a CU mask that leaves this many CUs
+  // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
+  int reserve_cus = 0;
 };
+
+// A non-default stream whose kernels may use every CU but the last `reserve`
+// (reserve <= 0: a plain non-blocking stream).
+hipStream_t create_stream_reserving(int device, int reserve);
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg);
 std::shared_ptr<HostBuffer> alloc_pinned(int64_t size);

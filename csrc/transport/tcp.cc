@@ -230,7 +230,10 @@ class TcpTransport : public Transport {
     TokenBucket tb(m.rate);
     if (payload && payload->host) {
       const uint8_t* base = payload->host->ptr + payload->host_off;
-      tb.paced(m.data_size, [&](int64_t off, int64_t n) { write_all(fd, base + off, size_t(n)); });
+      tb.paced(m.data_size, [&](int64_t off, int64_t n) {
+        write_all(fd, base + off, size_t(n));
+        bytes_sent += n;  // counted as it goes: progress is visible mid-layer
+      });
     } else if (payload && !payload->path.empty()) {
       int ffd = ::open(payload->path.c_str(), O_RDONLY | O_CLOEXEC);
       if (ffd < 0) throw std::runtime_error("open " + payload->path + ": " + strerror(errno));
@@ -244,6 +247,7 @@ class TcpTransport : public Transport {
             throw std::runtime_error("short read from " + payload->path);
           }
           write_all(fd, buf.data(), size_t(r));
+          bytes_sent += r;
           off += r;
           n -= r;
         }
@@ -252,7 +256,6 @@ class TcpTransport : public Transport {
     } else if (m.data_size > 0) {
       throw std::runtime_error("no data source specified for layer " + std::to_string(m.layer));
     }
-    bytes_sent += m.data_size;
   }
 
   void accept_loop() {

@@ -214,7 +214,9 @@ def main(argv=None) -> int:
     rt.prepare(args.m, **policy)
     if barrier:
         barrier()
-    arm_kill(faults, my_id)
+    # The kill clock starts once this node is sending layer bytes (not at process start).
+    arm_kill(faults, my_id, started=lambda: rt.transport.bytes_sent > (64 << 10)
+             or (rt.engine is not None and rt.engine.stats().bytes_sent > 0))
     res = rt.execute(args.timeout, announce_retry_s=30.0)
     if role == "leader" and res.ok:
         print(f"Time to deliver: {go_duration(res.time_to_deliver_s)}", flush=True)

@@ -5,8 +5,8 @@
     drop-chunk=P         every received chunk is damaged with probability P
                          behind its P2P group (planned engines); the CRC check
                          catches it, the receiver NACKs, the leader re-sends
-    kill-rank=R@T        node R exits abruptly T seconds after its session
-                         starts (host engines: the leader's job deadline
+    kill-rank=R@T        node R exits abruptly T seconds after it starts
+                         sending layer bytes (host engines: the leader's job deadline
                          re-dispatches its jobs; planned engines: the group
                          watchdog fails the session and aborts the communicator)
     slow-link=S:D:RATE   sender S paces layer bytes to D at RATE B/s (host
@@ -20,8 +20,9 @@ from __future__ import annotations
 import os
 import sys
 import threading
+import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 _SUFFIX = {"": 1, "K": 10**3, "M": 10**6, "G": 10**9}
 
@@ -70,17 +71,26 @@ def parse_inject(specs: Optional[List[str]]) -> FaultPlan:
     return plan
 
 
-def arm_kill(plan: FaultPlan, node_id: int) -> Optional[threading.Timer]:
-    """Start the kill timer for this node if the plan names it (call at session start)."""
+def arm_kill(plan: FaultPlan, node_id: int, started: Optional[Callable[[], bool]] = None) -> Optional[threading.Thread]:
+    """Start the kill timer for this node if the plan names it (call at session start).
+
+    With `started`, the T seconds count from the moment it first returns True
+    (e.g. the node has begun sending layer bytes) rather than from the call, so
+    the fault lands mid-transfer however long the other processes take to start.
+    """
     if node_id not in plan.kill:
         return None
+    delay = plan.kill[node_id]
 
     def die() -> None:
+        if started is not None:
+            while not started():
+                time.sleep(0.005)
+        time.sleep(delay)
         print(f'{{"level":"warn","node":{node_id},"message":"fault injection: kill-rank fired"}}',
               file=sys.stderr, flush=True)
         os._exit(86)  # abrupt: no goodbye to peers, sockets reset
 
-    t = threading.Timer(plan.kill[node_id], die)
-    t.daemon = True
+    t = threading.Thread(target=die, daemon=True)
     t.start()
     return t
