@@ -57,6 +57,9 @@ def parse_args(argv=None):
     p.add_argument("--pack", default="none", choices=["none", "fp8"],
                    help="fp8: layers are bf16 sources packed to block-scaled e4m3fn while staging "
                         "(HBM + wire format; BASELINE config #5)")
+    p.add_argument("--reserve-cus", type=int, default=-1,
+                   help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
+    p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
     p.add_argument("--preset", default="", choices=["", "llama70b", "llama405b-fp8"],
                    help="llama70b = 80 x 1 GiB (default); llama405b-fp8 = 126 x 3 GiB with --pack fp8")
     args = p.parse_args(argv)
@@ -100,6 +103,7 @@ def main(argv=None) -> int:
     import distributed_llm_dissemination_amd as dl
     from distributed_llm_dissemination_amd import _core
     from distributed_llm_dissemination_amd.models.catalog import delivered_bytes, make_workload
+    from distributed_llm_dissemination_amd.__main__ import engine_opts
     from distributed_llm_dissemination_amd.parallel.runtime import Runtime
 
     _core.set_log_level(2)
@@ -132,7 +136,8 @@ def main(argv=None) -> int:
     t_setup = time.time()
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
-                 barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack)
+                 barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
+                 engine_opts=engine_opts(args))
     if args.pack != "none":
         # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
         src_bytes = total_bytes

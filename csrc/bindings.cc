@@ -257,7 +257,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("inject_corrupt", &PlannedConfig::inject_corrupt)
       .def_readwrite("inject_seed", &PlannedConfig::inject_seed)
       .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s)
-      .def_readwrite("reserve_cus", &PlannedConfig::reserve_cus);
+      .def_readwrite("reserve_cus", &PlannedConfig::reserve_cus)
+      .def_readwrite("nccl_min_ctas", &PlannedConfig::nccl_min_ctas)
+      .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)

@@ -64,6 +64,10 @@ struct PlannedConfig {
   // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
   // -1: 32 when world > 1 (one XCD's worth), 0 on one rank (no RCCL traffic).
   int reserve_cus = -1;
+  // RCCL communicator CTA (workgroup/channel) bounds via ncclCommInitRankConfig;
+  // 0 keeps RCCL's own choice. More CTAs = more channels per P2P peer.
+  int nccl_min_ctas = 0;
+  int nccl_max_ctas = 0;
 };
 
 struct PlannedStats {

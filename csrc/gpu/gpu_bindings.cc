@@ -288,6 +288,8 @@ void register_gpu_bindings(PyObject* module) {
     hc.nccl_uid = std::string(uid);
     hc.max_crc_bytes = cfg.chunk_bytes;
     hc.reserve_cus = cfg.reserve_cus >= 0 ? cfg.reserve_cus : (cfg.world > 1 ? 32 : 0);
+    hc.nccl_min_ctas = cfg.nccl_min_ctas;
+    hc.nccl_max_ctas = cfg.nccl_max_ctas;
     py::gil_scoped_release nogil;
     return std::make_shared<PlannedEngine>(cfg, make_hip_backend(hc));
   }, py::arg("cfg"), py::arg("device") = 0, py::arg("nccl_uid") = py::bytes(""));

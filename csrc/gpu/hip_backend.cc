@@ -46,7 +46,14 @@ class HipBackend : public Backend {
         memcpy(&id, cfg_.nccl_uid.data(), sizeof id);
       }
       auto t0 = log::now_us();
-      NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
+      if (cfg_.nccl_min_ctas > 0 || cfg_.nccl_max_ctas > 0) {
+        ncclConfig_t nc = NCCL_CONFIG_INITIALIZER;
+        if (cfg_.nccl_min_ctas > 0) nc.minCTAs = cfg_.nccl_min_ctas;
+        if (cfg_.nccl_max_ctas > 0) nc.maxCTAs = cfg_.nccl_max_ctas;
+        NCCL_OK(ncclCommInitRankConfig(&nccl_, cfg_.world, id, cfg_.rank, &nc));
+      } else {
+        NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
+      }
       log::info(cfg_.rank).i("world", cfg_.world).f("init_ms", double(log::now_us() - t0) / 1e3)
           .msg("rccl communicator ready");
     }

@@ -28,6 +28,7 @@ struct HipBackendConfig {
   // > 0: the verify and copy streams get a CU mask that leaves this many CUs
   // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
   int reserve_cus = 0;
+  int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
 };
 
 // A non-default stream whose kernels may use every CU but the last `reserve`

@@ -70,6 +70,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--verify", default="crc32c", choices=["none", "crc32c"])
     p.add_argument("--streams-per-peer", type=int, default=1,
                    help="P2P ops per peer and direction in one RCCL group")
+    p.add_argument("--reserve-cus", type=int, default=-1,
+                   help="rccl: CUs the verify/copy kernels leave free for RCCL (-1: 32 with peers, else 0)")
+    p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX",
+                   help="rccl: communicator CTA bounds (ncclConfig minCTAs/maxCTAs; channels per P2P peer)")
     p.add_argument("--inject", action="append", default=[], metavar="SPEC",
                    help="fault injection: drop-chunk=P | kill-rank=R@T | slow-link=S:D:RATE")
     p.add_argument("--job-timeout", type=float, default=0.0,
@@ -98,6 +102,15 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--example-config", action="store_true")
     p.add_argument("--log-file", default="")
     return p
+
+
+def engine_opts(args) -> dict:
+    """Planned-engine (rccl) knobs from the CLI."""
+    opts = {"reserve_cus": args.reserve_cus}
+    if args.nccl_ctas:
+        lo, _, hi = args.nccl_ctas.partition(":")
+        opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)
+    return opts
 
 
 def main(argv=None) -> int:
@@ -186,7 +199,7 @@ def main(argv=None) -> int:
                  nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block,
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
                  host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
-                 persist_dir=args.persist_dir)
+                 persist_dir=args.persist_dir, engine_opts=engine_opts(args))
     if barrier is not None:
         # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
         import torch.distributed as dist

@@ -97,6 +97,7 @@ class Runtime:
         host_link_rate: Optional[Dict[int, int]] = None,
         group_peers: int = 1,
         persist_dir: str = "",
+        engine_opts: Optional[Dict[str, object]] = None,
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -147,6 +148,11 @@ class Runtime:
             pcfg.max_retries = max_retries
             pcfg.group_timeout_s = group_timeout_s
             pcfg.group_peers = group_peers
+            # Extra PlannedConfig fields (reserve_cus, nccl_min_ctas, max_inflight_groups, ...).
+            for k, v in (engine_opts or {}).items():
+                if not hasattr(pcfg, k):
+                    raise ValueError(f"unknown planned-engine option {k!r}")
+                setattr(pcfg, k, v)
             if engine == "rccl":
                 dev = device if device is not None else (self.me.device if self.me.device is not None else 0)
                 if self.world > 1 and nccl_uid is None:
