@@ -258,6 +258,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("inject_seed", &PlannedConfig::inject_seed)
       .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s)
       .def_readwrite("reserve_cus", &PlannedConfig::reserve_cus)
+      .def_readwrite("suspect_s", &PlannedConfig::suspect_s)
+      .def_readwrite("inject_die_after_groups", &PlannedConfig::inject_die_after_groups)
       .def_readwrite("nccl_min_ctas", &PlannedConfig::nccl_min_ctas)
       .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas);
   py::class_<PlannedStats>(m, "PlannedStats")
@@ -275,7 +277,10 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("peer_sent", &PlannedStats::peer_sent)
       .def_readonly("peer_recv", &PlannedStats::peer_recv)
       .def_readonly("group_us_hist", &PlannedStats::group_us_hist)
-      .def_readonly("land_us_hist", &PlannedStats::land_us_hist);
+      .def_readonly("land_us_hist", &PlannedStats::land_us_hist)
+      .def_readonly("suspects", &PlannedStats::suspects)
+      .def_readonly("shrinks", &PlannedStats::shrinks)
+      .def_readonly("aborted_pieces", &PlannedStats::aborted_pieces);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
         return reinterpret_cast<uint64_t>(e.provision(l, n));
@@ -394,7 +399,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("plan_ms", &NodeStats::plan_ms)
       .def_readonly("nacks", &NodeStats::nacks)
       .def_readonly("redispatched", &NodeStats::redispatched)
-      .def_readonly("suspects", &NodeStats::suspects);
+      .def_readonly("suspects", &NodeStats::suspects)
+      .def_readonly("recoveries", &NodeStats::recoveries)
+      .def_readonly("dropped", &NodeStats::dropped);
   py::class_<Node, std::shared_ptr<Node>>(m, "Node")
       .def(py::init([](const NodeConfig& cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEngine> e,
                        const LayersSrc& layers, const py::dict& assignment, bool is_leader) {

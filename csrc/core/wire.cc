@@ -49,6 +49,9 @@ const char* msg_type_name(MsgType t) {
     case MsgType::Nack: return "nack";
     case MsgType::Bcast: return "bcast";
     case MsgType::XferBatch: return "xfer_batch";
+    case MsgType::Suspect: return "suspect";
+    case MsgType::Shrink: return "shrink";
+    case MsgType::ShrinkDone: return "shrink_done";
     case MsgType::Landed: return "landed";
     case MsgType::SendDone: return "send_done";
     case MsgType::Tick: return "tick";
@@ -58,6 +61,25 @@ const char* msg_type_name(MsgType t) {
 }
 
 std::string node_str(NodeID id) { return std::to_string(id); }
+
+namespace {
+std::string to_hex(const std::string& b) {
+  static const char* d = "0123456789abcdef";
+  std::string out;
+  out.reserve(b.size() * 2);
+  for (unsigned char c : b) {
+    out.push_back(d[c >> 4]);
+    out.push_back(d[c & 15]);
+  }
+  return out;
+}
+std::string from_hex(const std::string& h) {
+  auto v = [](char c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; };
+  std::string out;
+  for (size_t i = 0; i + 1 < h.size(); i += 2) out.push_back(char((v(h[i]) << 4) | v(h[i + 1])));
+  return out;
+}
+}  // namespace
 
 NodeID parse_node_id(const std::string& s) {
   char* end = nullptr;
@@ -246,6 +268,17 @@ Json encode_payload(const Message& m) {
       }
       break;
     }
+    case MsgType::Suspect:
+    case MsgType::Shrink:
+    case MsgType::ShrinkDone: {
+      src_id();
+      p["Seq"] = Json(uint64_t(m.seq));
+      Json arr = Json::array();
+      for (auto n : m.peers) arr.push_back(Json(uint64_t(n)));
+      p["Peers"] = arr;
+      if (!m.payload_str.empty()) p["CommId"] = Json(to_hex(m.payload_str));
+      break;
+    }
     default:
       throw std::runtime_error(std::string("cannot serialize internal message ") + msg_type_name(m.type));
   }
@@ -357,6 +390,14 @@ MessagePtr decode_envelope(const Json& env) {
         for (auto& x : c->as_array()) m->crc.push_back(uint32_t(x.as_u64()));
       break;
     }
+    case MsgType::Suspect:
+    case MsgType::Shrink:
+    case MsgType::ShrinkDone:
+      m->seq = p.get_u64("Seq", 0);
+      if (auto* a = p.find("Peers"); a && a->is_array())
+        for (auto& x : a->as_array()) m->peers.push_back(x.as_u64());
+      m->payload_str = from_hex(p.get_str("CommId"));
+      break;
     default:
       throw std::runtime_error("unknown MsgType: " + std::to_string(unsigned(m->type)));
   }

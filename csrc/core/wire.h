@@ -31,6 +31,10 @@ enum class MsgType : uint8_t {
   Nack = 9,        // receiver -> sender: chunk CRC mismatch, resend range
   Bcast = 10,      // leader -> participants: collective broadcast descriptor (GPU mode 0)
   XferBatch = 11,  // leader -> ranks: sequence-numbered transfer jobs (GPU planned data plane)
+  // Elastic recovery of the planned (RCCL) data plane:
+  Suspect = 12,     // rank -> leader: a P2P group with these peers is stuck or failed
+  Shrink = 13,      // leader -> survivors: drop these dead nodes from the communicator (Seq = generation)
+  ShrinkDone = 14,  // rank -> leader: communicator shrunk, in-flight state reset (Seq = generation)
   // ---- node-internal events (never serialized) ----
   Landed = 32,     // a byte range of a layer is now resident in the target tier
   SendDone = 33,   // a sender finished pushing a range
@@ -81,7 +85,7 @@ struct Message {
   int64_t chunk_bytes = 0;
   std::vector<uint32_t> crc;    // expected CRC32C per chunk of the range
   uint64_t seq = 0;             // per (src,dest) stream sequence number
-  std::vector<NodeID> peers;    // Bcast participants
+  std::vector<NodeID> peers;    // Bcast participants; Suspect / Shrink node lists
   // XferBatch / Announce extensions
   uint64_t batch = 0;
   std::vector<XferJob> jobs;

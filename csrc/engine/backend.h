@@ -15,6 +15,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -58,6 +59,18 @@ class Backend {
   virtual void release(Ev e) = 0;
   virtual uint32_t crc_result(uint32_t slot) = 0;
   virtual std::string async_error() { return ""; }
+  // Elastic recovery: abort every in-flight comm-queue operation, then continue
+  // on a communicator of the surviving ranks (the same call on every survivor,
+  // with the same `dead` ranks, `generation` and `comm_id`). Returns this
+  // rank's new index. RCCL: ncclCommAbort, then ncclCommInitRank of the
+  // survivors with the leader's fresh unique id (comm_id).
+  virtual std::string new_comm_id() { return ""; }
+  virtual int shrink(const std::vector<int>& dead, uint64_t generation, const std::string& comm_id) {
+    (void)dead;
+    (void)generation;
+    (void)comm_id;
+    throw std::runtime_error(name() + " backend cannot shrink its communicator");
+  }
   virtual void sync_all() = 0;
   virtual void destroy(bool abort) = 0;
 };

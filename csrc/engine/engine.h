@@ -51,6 +51,9 @@ class DataEngine {
   virtual int64_t chunk_bytes() const { return 0; }
   // Per-layer CRC manifests of layers this rank can serve (sent with Announce).
   virtual std::map<LayerID, CrcManifest> manifest() { return {}; }
+  // Elastic recovery (leader): a fresh communicator id the survivors re-form
+  // around (RCCL: ncclGetUniqueId bytes); "" when the engine needs none.
+  virtual std::string new_comm_id() { return ""; }
   // Wait until every transfer this engine started for its node has finished.
   virtual void quiesce() {}
   virtual void shutdown() {}

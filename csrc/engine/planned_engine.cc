@@ -184,10 +184,18 @@ void PlannedEngine::fail(const std::string& what) {
 // ------------------------------------------------------------ DataEngine
 
 bool PlannedEngine::on_message(const MessagePtr& m) {
-  if (m->type != MsgType::XferBatch) return false;
+  if (m->type != MsgType::XferBatch && m->type != MsgType::Shrink) return false;
   {
     std::lock_guard<std::mutex> lk(req_mu_);
-    reqs_.push_back(Req{Req::Batch, m->jobs, 0, 0, 0});
+    if (m->type == MsgType::Shrink) {
+      Req r{Req::Shrink, {}, 0, 0, 0};
+      r.dead = m->peers;
+      r.generation = m->seq;
+      r.comm_id = m->payload_str;
+      reqs_.push_back(std::move(r));
+    } else {
+      reqs_.push_back(Req{Req::Batch, m->jobs, 0, 0, 0});
+    }
     busy_ = true;
   }
   req_cv_.notify_all();
@@ -533,6 +541,7 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
 
 bool PlannedEngine::issue_some() {
   bool progress = false;
+  if (recovering_ || dead_) return false;
   while (!ops_.empty() && int(groups_inflight_.size()) < cfg_.max_inflight_groups && !failed_) {
     std::vector<Piece> group;
     std::map<int, int> nsend, nrecv;
@@ -584,7 +593,10 @@ bool PlannedEngine::issue_some() {
       xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len, p.bcast});
     }
     Ev g = backend_->group(xops, waits);
-    groups_inflight_.push_back({g, std::chrono::steady_clock::now()});
+    Inflight inf{g, std::chrono::steady_clock::now(), {}};
+    for (auto& p : group)
+      if (std::find(inf.peers.begin(), inf.peers.end(), p.peer) == inf.peers.end()) inf.peers.push_back(p.peer);
+    groups_inflight_.push_back(std::move(inf));
     // Fault injection: damage some received chunks behind the group, before their check.
     Ev landed_ev = g;
     int64_t injected = 0;
@@ -634,31 +646,149 @@ bool PlannedEngine::issue_some() {
       stats_.issue_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     progress = true;
+    if (cfg_.inject_die_after_groups > 0 && ++groups_issued_ >= cfg_.inject_die_after_groups) {
+      die();
+      break;
+    }
   }
   return progress;
 }
 
+void PlannedEngine::die() {
+  // Fault injection: this rank stops cold - no more posts, no acks, and its
+  // control endpoint disappears (the leader's liveness probe sees it dead).
+  log::warn(int64_t(self_node_)).i("groups", groups_issued_).msg("fault injection: rank dies");
+  dead_ = true;
+  if (node_) node_->transport()->close();
+}
+
+std::vector<int> PlannedEngine::inflight_peers() const {
+  std::vector<int> peers;
+  for (auto& g : groups_inflight_)
+    for (int p : g.peers)
+      if (std::find(peers.begin(), peers.end(), p) == peers.end()) peers.push_back(p);
+  return peers;
+}
+
+void PlannedEngine::suspect(const std::vector<int>& peers, const std::string& why, bool broken) {
+  if (broken && !recovering_) {
+    recovering_ = true;  // the communicator is unusable until the Shrink
+    recover_since_ = std::chrono::steady_clock::now();
+  }
+  Message m;
+  m.type = MsgType::Suspect;
+  for (int r : peers)
+    if (r != cfg_.rank) m.peers.push_back(cfg_.rank_nodes[size_t(r)]);
+  log::warn(int64_t(self_node_)).s("why", why).i("peers", int64_t(m.peers.size()))
+      .msg("data plane stalled: reporting suspect peers to the leader");
+  trace::mark("dissem.suspect");
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.suspects++;
+  }
+  if (node_) node_->send_msg(node_->leader(), m);
+}
+
+void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t generation,
+                              const std::string& comm_id) {
+  // Every survivor runs this for the same generation: abort what is in flight,
+  // continue on a communicator without the dead ranks, forget every chunk that
+  // was not verified resident (the leader re-plans whole layers that were not acked).
+  trace::Scoped tr("dissem.shrink");
+  std::vector<int> dead;
+  for (NodeID n : dead_nodes) {
+    auto it = node_rank_.find(n);
+    if (it != node_rank_.end()) dead.push_back(it->second);
+  }
+  std::sort(dead.begin(), dead.end());
+  const int old_rank = cfg_.rank;
+  int64_t aborted = int64_t(ops_.size());
+  const int new_rank = backend_->shrink(dead, generation, comm_id);
+  for (auto& g : groups_inflight_) backend_->release(g.ev);
+  groups_inflight_.clear();
+  for (auto& v : verifies_) {
+    aborted += int64_t(v.pieces.size());
+    backend_->release(v.ev);
+    if (v.bounce) bounce_free_.push_back(v.bounce);
+  }
+  verifies_.clear();
+  ops_.clear();
+  restage_.clear();
+  for (auto& kv : layers_) {
+    Layer& L = kv.second;
+    for (size_t c = 0; c < L.st.size(); ++c) {
+      if (L.st[c] == 1 || L.st[c] == 4) L.st[c] = 0;  // pending or bad: gone (st 3: its disk read still lands)
+      if (L.ev[c]) backend_->release(L.ev[c]);
+      L.ev[c] = 0;
+      L.fails[c] = 0;
+    }
+  }
+  std::vector<NodeID> nodes;
+  for (int r = 0; r < cfg_.world; ++r)
+    if (!std::binary_search(dead.begin(), dead.end(), r)) nodes.push_back(cfg_.rank_nodes[size_t(r)]);
+  cfg_.rank_nodes = nodes;
+  cfg_.world = int(nodes.size());
+  cfg_.rank = new_rank;
+  node_rank_.clear();
+  for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
+  recovering_ = false;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.shrinks++;
+    stats_.aborted_pieces += aborted;
+  }
+  log::warn(int64_t(self_node_)).i("dead", int64_t(dead.size())).i("old_rank", old_rank).i("new_rank", new_rank)
+      .i("world", cfg_.world).i("aborted_pieces", aborted).msg("communicator shrunk: continuing without dead ranks");
+  if (node_) {
+    // Through the node's inbox, so acks for chunks that landed before the
+    // shrink reach the leader first.
+    auto d = std::make_shared<Message>();
+    d->type = MsgType::ShrinkDone;
+    d->seq = generation;
+    d->src = self_node_;
+    d->epoch = node_->epoch();
+    node_->inject(d);
+  }
+}
+
 void PlannedEngine::poll() {
   while (!groups_inflight_.empty()) {
-    int r = backend_->query(groups_inflight_.front().first);
+    Inflight& head = groups_inflight_.front();
+    int r = backend_->query(head.ev);
     if (r == 0) {
       // Watchdog: a group whose partner never posts (dead or hung peer) would
-      // block the comm queue forever. Fail; shutdown aborts the communicator.
-      double age = std::chrono::duration<double>(std::chrono::steady_clock::now() - groups_inflight_.front().second)
-                       .count();
+      // block the comm queue forever. Report its peers to the leader (which
+      // probes them and shrinks the communicator around a dead one); fail if
+      // nothing resolves it.
+      const auto now = std::chrono::steady_clock::now();
+      double age = std::chrono::duration<double>(now - head.t0).count();
+      if (node_ && cfg_.suspect_s > 0 && age > cfg_.suspect_s &&
+          now - last_suspect_ > std::chrono::duration<double>(cfg_.suspect_s)) {
+        // Not (yet) a failure: if the peers are alive the group may still
+        // complete. Name every in-flight peer: the group at the head may be
+        // waiting on a live rank that itself waits on the dead one.
+        last_suspect_ = now;
+        suspect(inflight_peers(), "P2P group pending for " + std::to_string(int(age)) + " s", false);
+      }
       if (cfg_.group_timeout_s > 0 && age > cfg_.group_timeout_s)
         fail("P2P group pending for " + std::to_string(int(age)) + " s: a peer rank is dead or stuck");
       break;
     }
     if (r < 0) {
-      fail("P2P group failed: " + backend_->async_error());
-      return;
+      if (!node_) {
+        fail("P2P group failed: " + backend_->async_error());
+        return;
+      }
+      // The communicator is broken (e.g. a peer's connection died): stop and
+      // let the leader decide; its Shrink resets everything in flight.
+      if (!recovering_) suspect(inflight_peers(), "P2P group failed: " + backend_->async_error(), true);
+      break;
     }
     {
       std::lock_guard<std::mutex> lk(stats_mu_);
-      stats_.group_us_hist[log2_bucket(groups_inflight_.front().second)]++;
+      stats_.group_us_hist[log2_bucket(head.t0)]++;
     }
-    backend_->release(groups_inflight_.front().first);
+    backend_->release(head.ev);
     groups_inflight_.pop_front();
   }
   for (auto it = verifies_.begin(); it != verifies_.end();) {
@@ -668,6 +798,10 @@ void PlannedEngine::poll() {
       continue;
     }
     if (r < 0) {
+      if (node_) {  // behind a failed group: the leader's Shrink resets it
+        if (!recovering_) suspect(inflight_peers(), "landing failed: " + backend_->async_error(), true);
+        break;
+      }
       fail("landing failed: " + backend_->async_error());
       return;
     }
@@ -759,6 +893,9 @@ void PlannedEngine::take_requests(bool block) {
         idle_cv_.notify_all();
         break;
       }
+      case Req::Shrink:
+        do_shrink(r.dead, r.generation, r.comm_id);
+        break;
       case Req::Stop:
         break;
     }
@@ -782,9 +919,21 @@ void PlannedEngine::run() {
         idle_cv_.notify_all();
         continue;
       }
+      if (dead_) {
+        // Fault injection: a crashed rank does nothing until shutdown.
+        std::lock_guard<std::mutex> lk(req_mu_);
+        reqs_.clear();
+        busy_ = false;
+        idle_cv_.notify_all();
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        continue;
+      }
       pump_disk();
       bool progress = issue_some();
       poll();
+      if (recovering_ && cfg_.group_timeout_s > 0 &&
+          std::chrono::steady_clock::now() - recover_since_ > std::chrono::duration<double>(cfg_.group_timeout_s))
+        fail("data plane stalled and the leader did not shrink the communicator");
       {
         std::lock_guard<std::mutex> lk(req_mu_);
         busy_ = !idle() || !reqs_.empty();
@@ -794,7 +943,13 @@ void PlannedEngine::run() {
       if (now - last_async_check > std::chrono::milliseconds(100)) {
         last_async_check = now;
         std::string e = backend_->async_error();
-        if (!e.empty()) fail("async error: " + e);
+        if (!e.empty() && !recovering_) {
+          if (node_) {
+            suspect(inflight_peers(), "async error: " + e, true);
+          } else {
+            fail("async error: " + e);
+          }
+        }
       }
       if (!progress && !idle()) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }

@@ -59,6 +59,12 @@ struct PlannedConfig {
   double inject_corrupt = 0;
   uint64_t inject_seed = 1;
   double group_timeout_s = 300;    // a P2P group pending longer than this fails the engine (dead peer)
+  // Elastic recovery (node-bound engines): a group pending longer than
+  // suspect_s, or failing, is reported to the leader (Suspect); the leader
+  // probes the peers and, if one is dead, has every survivor shrink the
+  // communicator (Shrink) and re-plans the rest. 0 = report only on failure.
+  double suspect_s = 10;
+  int inject_die_after_groups = 0;  // fault injection: stop dead after this many groups (tests)
   // CUs the verify/copy-stream kernels (CRC, fp8 pack) may never occupy, so an
   // RCCL group kernel always finds free CUs to launch on instead of queueing
   // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
@@ -74,6 +80,7 @@ struct PlannedStats {
   int64_t bytes_sent = 0, bytes_recv = 0, bytes_staged = 0, bytes_verified = 0;
   int64_t groups = 0, pieces = 0, verify_failures = 0, unverified_pieces = 0;
   int64_t nacks = 0, injected = 0;
+  int64_t suspects = 0, shrinks = 0, aborted_pieces = 0;  // elastic recovery
   double issue_ms = 0;  // host time spent enqueueing groups
   std::map<int, int64_t> peer_sent, peer_recv;  // bytes per peer rank (per-link counters)
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
@@ -108,6 +115,7 @@ class PlannedEngine : public DataEngine {
   int64_t slot_size(int64_t src_bytes) const;
   const PlannedConfig& config() const { return cfg_; }
   std::map<LayerID, CrcManifest> manifest() override;
+  std::string new_comm_id() override { return backend_->new_comm_id(); }
   bool on_message(const MessagePtr& m) override;
   void send_range(NodeID dest, LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
   void load_range(LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
@@ -164,10 +172,18 @@ class PlannedEngine : public DataEngine {
     bool ok = true;
   };
   struct Req {
-    enum Type { Batch, Load, Reset, Stop } type;
+    enum Type { Batch, Load, Reset, Stop, Shrink } type;
     std::vector<XferJob> jobs;
     LayerID layer = 0;
     int64_t off = 0, len = 0;
+    std::vector<NodeID> dead;  // Shrink
+    uint64_t generation = 0;   // Shrink
+    std::string comm_id;       // Shrink: the survivors' new communicator id
+  };
+  struct Inflight {  // a P2P group on the comm queue
+    Ev ev;
+    std::chrono::steady_clock::time_point t0;
+    std::vector<int> peers;  // partner ranks
   };
 
   void run();
@@ -178,6 +194,13 @@ class PlannedEngine : public DataEngine {
   bool idle() const {
     return ops_.empty() && verifies_.empty() && groups_inflight_.empty() && disk_inflight_ == 0 && disk_wait_.empty();
   }
+  // Elastic recovery: stop issuing, tell the leader which peers look dead, and
+  // wait for its Shrink (or fail after group_timeout_s).
+  // broken: the communicator failed (stop issuing) rather than merely stalled.
+  void suspect(const std::vector<int>& peers, const std::string& why, bool broken);
+  std::vector<int> inflight_peers() const;
+  void do_shrink(const std::vector<NodeID>& dead, uint64_t generation, const std::string& comm_id);
+  void die();  // fault injection
   Layer& layer(LayerID id, int64_t size_hint = 0);
   // 1: resident or in flight on a device queue, 0: still reading from disk, -1: no source
   int ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed);
@@ -212,7 +235,11 @@ class PlannedEngine : public DataEngine {
   std::deque<Piece> ops_;
   std::deque<Verify> verifies_;
   std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
-  std::deque<std::pair<Ev, std::chrono::steady_clock::time_point>> groups_inflight_;
+  std::deque<Inflight> groups_inflight_;
+  bool recovering_ = false;  // issue thread: waiting for the leader's Shrink
+  std::chrono::steady_clock::time_point recover_since_, last_suspect_;
+  int64_t groups_issued_ = 0;
+  std::atomic<bool> dead_{false};  // fault injection: this rank "crashed"
 
   // disk tier: issue thread owns bounce_free_/disk_wait_; readers exchange via disk_mu_
   std::vector<uint8_t*> bounce_all_, bounce_free_;

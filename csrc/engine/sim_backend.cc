@@ -6,6 +6,7 @@
 // rank's comm queue until every op in it has been matched and copied, so a
 // schedule that could deadlock on GPUs deadlocks here too; a bounded wait turns
 // that into a reported failure instead of a hang.
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -40,6 +41,7 @@ struct Posted {
 struct Fabric {
   std::mutex mu;
   std::condition_variable cv;
+  bool aborted = false;  // a survivor shrank this communicator: every wait fails now
   std::map<std::pair<int, int>, std::pair<std::deque<Posted*>, std::deque<Posted*>>> ch;  // (src,dst) -> sends, recvs
   SimFabricStats stats;
 
@@ -67,11 +69,12 @@ struct Fabric {
   bool wait_all(const std::vector<std::unique_ptr<Posted>>& ops, double timeout_s) {
     std::unique_lock<std::mutex> lk(mu);
     bool ok = cv_wait_for(cv, lk, timeout_s, [&] {
+      if (aborted) return true;
       for (auto& o : ops)
         if (!o->done) return false;
       return true;
     });
-    if (!ok) return false;
+    if (!ok || aborted) return false;
     for (auto& o : ops)
       if (o->bad) return false;
     return true;
@@ -278,6 +281,26 @@ class SimBackend : public Backend {
     std::lock_guard<std::mutex> lk(ev_mu_);
     return error_;
   }
+  int shrink(const std::vector<int>& dead, uint64_t generation, const std::string&) override {
+    {
+      std::lock_guard<std::mutex> lk(fab_->mu);
+      fab_->aborted = true;  // like NCCL_SHRINK_ABORT: in-flight groups fail now
+    }
+    fab_->cv.notify_all();
+    sync_all();
+    int new_rank = 0;
+    for (int r = 0; r < rank_; ++r)
+      if (std::find(dead.begin(), dead.end(), r) == dead.end()) ++new_rank;
+    world_ -= int(dead.size());
+    rank_ = new_rank;
+    {
+      std::lock_guard<std::mutex> lk(ev_mu_);
+      error_.clear();
+    }
+    fab_ = fabric(key_ + "/shrink" + std::to_string(generation));
+    return rank_;
+  }
+
   void sync_all() override {
     comm_.drain();
     copy_.drain();

@@ -3,7 +3,10 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl.h>
 
+#include <chrono>
+#include <algorithm>
 #include <cstring>
+#include <thread>
 #include <mutex>
 #include <vector>
 
@@ -45,18 +48,23 @@ class HipBackend : public Backend {
         if (cfg_.nccl_uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("nccl_uid must be ncclUniqueId bytes");
         memcpy(&id, cfg_.nccl_uid.data(), sizeof id);
       }
-      auto t0 = log::now_us();
-      if (cfg_.nccl_min_ctas > 0 || cfg_.nccl_max_ctas > 0) {
-        ncclConfig_t nc = NCCL_CONFIG_INITIALIZER;
-        if (cfg_.nccl_min_ctas > 0) nc.minCTAs = cfg_.nccl_min_ctas;
-        if (cfg_.nccl_max_ctas > 0) nc.maxCTAs = cfg_.nccl_max_ctas;
-        NCCL_OK(ncclCommInitRankConfig(&nccl_, cfg_.world, id, cfg_.rank, &nc));
-      } else {
-        NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
-      }
-      log::info(cfg_.rank).i("world", cfg_.world).f("init_ms", double(log::now_us() - t0) / 1e3)
-          .msg("rccl communicator ready");
+      init_comm(id);
     }
+  }
+
+  void init_comm(const ncclUniqueId& id_in) {
+    ncclUniqueId id = id_in;
+    auto t0 = log::now_us();
+    if (cfg_.nccl_min_ctas > 0 || cfg_.nccl_max_ctas > 0) {
+      ncclConfig_t nc = NCCL_CONFIG_INITIALIZER;
+      if (cfg_.nccl_min_ctas > 0) nc.minCTAs = cfg_.nccl_min_ctas;
+      if (cfg_.nccl_max_ctas > 0) nc.maxCTAs = cfg_.nccl_max_ctas;
+      NCCL_OK(ncclCommInitRankConfig(&nccl_, cfg_.world, id, cfg_.rank, &nc));
+    } else {
+      NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
+    }
+    log::info(cfg_.rank).i("world", cfg_.world).f("init_ms", double(log::now_us() - t0) / 1e3)
+        .msg("rccl communicator ready");
   }
   ~HipBackend() override { destroy(false); }
   std::string name() const override { return "rccl"; }
@@ -157,6 +165,48 @@ class HipBackend : public Backend {
       return ncclGetErrorString(ar);
     return "";
   }
+  std::string new_comm_id() override { return nccl_unique_id(); }
+
+  int shrink(const std::vector<int>& dead, uint64_t, const std::string& comm_id) override {
+    if (!nccl_) throw std::runtime_error("shrink without a communicator");
+    if (comm_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("shrink: bad communicator id");
+    // Abort first: P2P groups waiting on the dead rank are terminated, so the
+    // comm stream drains. (ncclCommShrink would keep the bootstrap, but the RCCL
+    // PyTorch loads into the process predates it; abort + re-init of the
+    // survivors works with any RCCL.)
+    (void)ncclCommAbort(nccl_);
+    nccl_ = nullptr;
+    int new_rank = 0;
+    for (int r = 0; r < cfg_.rank; ++r)
+      if (std::find(dead.begin(), dead.end(), r) == dead.end()) ++new_rank;
+    cfg_.world -= int(dead.size());
+    cfg_.rank = new_rank;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      err_.clear();
+    }
+    // Bounded drain of the three queues (an aborted kernel must have exited).
+    for (hipStream_t s : {comm_, copy_, verify_}) {
+      hipEvent_t e;
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(e, s));
+      auto t0 = std::chrono::steady_clock::now();
+      hipError_t q;
+      while ((q = hipEventQuery(e)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+          (void)hipEventDestroy(e);
+          throw std::runtime_error("queues did not drain after ncclCommShrink");
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      (void)hipEventDestroy(e);
+    }
+    ncclUniqueId id;
+    memcpy(&id, comm_id.data(), sizeof id);
+    init_comm(id);
+    return new_rank;
+  }
+
   void sync_all() override {
     (void)hipSetDevice(cfg_.device);
     (void)hipStreamSynchronize(comm_);

@@ -202,6 +202,14 @@ void Node::handle(const MessagePtr& m) {
     case MsgType::Nack:
       if (is_leader_) on_nack(m);
       break;
+    case MsgType::Suspect:
+      if (is_leader_) on_suspect(m);
+      break;
+    case MsgType::ShrinkDone:
+      // From this node's engine (via the inbox, behind its earlier acks).
+      if (is_leader_) on_shrink_done(m);
+      else send_msg(cfg_.leader, *m);
+      break;
     case MsgType::Tick:
       if (is_leader_ && !started_) {
         bool all = true;
@@ -469,6 +477,7 @@ void Node::send_startup() {
 }
 
 void Node::on_ack(const MessagePtr& m) {
+  if (dead_nodes_.count(m->src)) return;  // sent before it died: it is out of the assignment
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     LayerMeta meta;
@@ -477,20 +486,7 @@ void Node::on_ack(const MessagePtr& m) {
     status_[m->src][m->layer] = meta;  // node.go:413-417
   }
   outstanding_.erase({m->src, m->layer});
-  if (!satisfied_ && assignment_satisfied()) {
-    // Fire exactly once (quirk Q13).
-    {
-      std::lock_guard<std::mutex> lk(sig_mu_);
-      satisfied_ = true;
-      t_ready_us_ = log::now_us();
-      stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
-    }
-    log::info(int64_t(cfg_.id)).f("time_to_deliver_s", stats_.time_to_deliver_s).msg("timer stop: startup");
-    trace::stop(session_range_);
-    send_startup();
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    sig_cv_.notify_all();
-  }
+  finish_if_satisfied();
   if (cfg_.mode != 2) return;
   // Mode 2 pull loop (node.go:764-807): the whole layer is at the dest, so every
   // job of (layer, dest) is done; retire them and pull the next ones.
@@ -505,6 +501,128 @@ void Node::on_ack(const MessagePtr& m) {
   while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
   }
   flush_batch();
+}
+
+void Node::finish_if_satisfied() {
+  if (satisfied_ || !assignment_satisfied()) return;
+  // Fire exactly once (quirk Q13).
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    satisfied_ = true;
+    t_ready_us_ = log::now_us();
+    stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
+  }
+  log::info(int64_t(cfg_.id)).f("time_to_deliver_s", stats_.time_to_deliver_s).msg("timer stop: startup");
+  trace::stop(session_range_);
+  send_startup();
+  std::lock_guard<std::mutex> lk(sig_mu_);
+  sig_cv_.notify_all();
+}
+
+// ------------------------------------------- elastic recovery (planned data plane)
+//
+// A rank whose P2P group stalls or fails reports the group's peers (Suspect).
+// The leader probes them over the control plane; for peers that are gone it
+// starts a recovery generation: the dead nodes leave the status and the
+// assignment, every survivor shrinks the RCCL communicator around them
+// (ncclCommShrink with NCCL_SHRINK_ABORT: in-flight groups are aborted) and
+// resets what was in flight, and once all survivors have confirmed
+// (ShrinkDone) the leader re-plans every unacked (dest, layer) from a live
+// holder. Pairs without a live holder are dropped (logged, counted).
+void Node::on_suspect(const MessagePtr& m) {
+  if (!started_ || satisfied_) return;
+  std::vector<NodeID> gone;
+  for (NodeID p : m->peers) {
+    if (p == cfg_.id || dead_nodes_.count(p) || !status_.count(p)) continue;
+    if (!t_->alive(p)) gone.push_back(p);
+  }
+  if (gone.empty()) {
+    log::info(int64_t(cfg_.id)).u("from", m->src).i("peers", int64_t(m->peers.size()))
+        .msg("suspect report: every named peer answers; waiting");
+    return;
+  }
+  shrink_gen_++;
+  for (NodeID d : gone) dead_nodes_.insert(d);
+  int64_t dropped = 0;
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    for (NodeID d : gone) {
+      status_.erase(d);
+      auto a = assignment_.find(d);
+      if (a != assignment_.end()) {
+        dropped += int64_t(a->second.size());
+        assignment_.erase(a);
+      }
+    }
+    stats_.recoveries++;
+    stats_.dropped += dropped;
+  }
+  for (NodeID d : gone) initial_status_.erase(d);
+  // Planning state of the interrupted schedule: re-planned from scratch.
+  pending_jobs_.clear();
+  jobs_.clear();
+  load_.clear();
+  inflight_.clear();
+  outstanding_.clear();
+  shrink_wait_.clear();
+  for (auto& kv : status_) shrink_wait_.insert(kv.first);
+  log::warn(int64_t(cfg_.id)).u("generation", shrink_gen_).i("dead", int64_t(gone.size()))
+      .i("survivors", int64_t(shrink_wait_.size())).i("dropped_assignments", dropped)
+      .msg("rank(s) dead: shrinking the communicator and re-planning");
+  trace::mark("dissem.recovery");
+  Message s;
+  s.type = MsgType::Shrink;
+  s.seq = shrink_gen_;
+  s.peers.assign(dead_nodes_.begin(), dead_nodes_.end());
+  s.payload_str = e_->new_comm_id();  // the survivors' new communicator (RCCL unique id)
+  for (NodeID n : std::set<NodeID>(shrink_wait_)) send_msg(n, s);
+}
+
+void Node::on_shrink_done(const MessagePtr& m) {
+  if (m->seq != shrink_gen_ || !shrink_wait_.erase(m->src)) return;
+  if (shrink_wait_.empty()) replan_after_shrink();
+}
+
+void Node::replan_after_shrink() {
+  const Location target = e_->target();
+  std::map<NodeID, int64_t> planned;  // bytes per sender in this re-plan (spread the load)
+  std::vector<std::pair<NodeID, LayerID>> lost;
+  int64_t jobs = 0;
+  for (auto& kv : assignment_) {
+    const NodeID dest = kv.first;
+    for (auto& l : kv.second) {
+      const LayerID layer = l.first;
+      auto st = status_.find(dest);
+      if (st != status_.end() && at(st->second, layer, target)) continue;
+      if (st != status_.end() && st->second.count(layer)) {
+        add_job(dest, dest, layer, 0, -1);  // its own copy in another tier: promote it
+        ++jobs;
+        continue;
+      }
+      NodeID best = kClientID;
+      for (auto& o : status_) {
+        if (o.first == dest || !o.second.count(layer)) continue;
+        if (best == kClientID || planned[o.first] < planned[best]) best = o.first;
+      }
+      if (best == kClientID) {
+        lost.push_back({dest, layer});
+        continue;
+      }
+      planned[best] += layer_size(layer);
+      add_job(best, dest, layer, 0, -1);
+      ++jobs;
+    }
+  }
+  for (auto& dl : lost) {
+    log::error(int64_t(cfg_.id)).u("dest", dl.first).u("layer", dl.second)
+        .msg("no live holder of the layer: dropping it from the assignment");
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    assignment_[dl.first].erase(dl.second);
+    stats_.dropped++;
+  }
+  log::info(int64_t(cfg_.id)).u("generation", shrink_gen_).i("jobs", jobs).msg("re-planned after recovery");
+  flush_batch();
+  finish_if_satisfied();
 }
 
 void Node::on_range_ack(const MessagePtr& m) {

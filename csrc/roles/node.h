@@ -61,6 +61,8 @@ struct NodeStats {
   int64_t nacks = 0;             // leader: chunk re-sends requested by receivers (CRC mismatch)
   int64_t redispatched = 0;      // leader: jobs re-sent from another owner after their deadline
   int64_t suspects = 0;          // leader: senders that missed a deadline
+  int64_t recoveries = 0;        // leader: communicator shrinks after a rank died (planned engines)
+  int64_t dropped = 0;           // leader: (dest, layer) pairs given up (dead dest or no live owner)
 };
 
 class Node {
@@ -123,6 +125,11 @@ class Node {
   void start_distribution();
   // failure handling (leader)
   void on_nack(const MessagePtr& m);
+  // elastic recovery of the planned data plane (leader)
+  void on_suspect(const MessagePtr& m);
+  void on_shrink_done(const MessagePtr& m);
+  void replan_after_shrink();
+  void finish_if_satisfied();
   void on_tick();
   void track(NodeID sender, NodeID dest, LayerID layer, int64_t off, int64_t size);
   NodeID alternative_owner(LayerID layer, NodeID dest, NodeID avoid);
@@ -192,6 +199,9 @@ class Node {
   std::map<std::tuple<NodeID, LayerID, int64_t>, int> redispatches_;
   std::set<NodeID> suspects_;
   Status initial_status_;  // inventories at start (re-send sources for NACKs)
+  uint64_t shrink_gen_ = 0;         // recovery generation
+  std::set<NodeID> dead_nodes_;     // confirmed dead (liveness probe failed)
+  std::set<NodeID> shrink_wait_;    // survivors whose ShrinkDone is outstanding
   std::thread tick_th_;
   std::mutex tick_mu_;
   std::condition_variable tick_cv_;

@@ -77,6 +77,14 @@ class InprocTransport : public Transport, public std::enable_shared_from_this<In
 
   std::string address() const override { return addr_; }
 
+  bool alive(NodeID id) override {
+    std::string daddr;
+    if (!lookup(id, &daddr)) daddr = std::to_string(id);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_registry.find(daddr);
+    return it != g_registry.end() && it->second.lock() != nullptr;
+  }
+
   void close() override {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_registry.find(addr_);

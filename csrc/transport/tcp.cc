@@ -171,6 +171,19 @@ class TcpTransport : public Transport {
 
   std::string address() const override { return addr_; }
 
+  bool alive(NodeID id) override {
+    std::string daddr;
+    if (!lookup(id, &daddr)) return false;
+    if (is_self(daddr)) return !closed_.load();
+    try {
+      int fd = dial(daddr);  // a dead process's port refuses the connection
+      ::close(fd);
+      return true;
+    } catch (const std::exception&) {
+      return false;
+    }
+  }
+
   void close() override {
     if (closed_.exchange(true)) return;
     if (lfd_ >= 0) {

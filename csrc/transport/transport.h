@@ -42,6 +42,9 @@ class Transport {
   virtual void broadcast(const Message& m) = 0;
   virtual std::string address() const = 0;
   virtual void close() = 0;
+  // Liveness probe used by the leader's failure detector: can `id` still be
+  // reached (TCP: a fresh connect succeeds; in-process: its endpoint exists)?
+  virtual bool alive(NodeID id) { return true; }
 
   BlockingQueue<MessagePtr>& deliver() { return inbox_; }
   // Node-internal events (engine completions) enter the same inbox.

@@ -13,6 +13,7 @@ and ``Time to deliver: <Go duration>``.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import signal
@@ -74,6 +75,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="rccl: CUs the verify/copy kernels leave free for RCCL (-1: 32 with peers, else 0)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX",
                    help="rccl: communicator CTA bounds (ncclConfig minCTAs/maxCTAs; channels per P2P peer)")
+    p.add_argument("--suspect-timeout", type=float, default=10.0,
+                   help="rccl: report a P2P group stalled this long to the leader, which probes the peers and "
+                        "shrinks the communicator around dead ranks (elastic recovery; 0 = only on failure)")
     p.add_argument("--inject", action="append", default=[], metavar="SPEC",
                    help="fault injection: drop-chunk=P | kill-rank=R@T | slow-link=S:D:RATE")
     p.add_argument("--job-timeout", type=float, default=0.0,
@@ -106,7 +110,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
-    opts = {"reserve_cus": args.reserve_cus}
+    opts = {"reserve_cus": args.reserve_cus, "suspect_s": getattr(args, "suspect_timeout", 10.0)}
     if args.nccl_ctas:
         lo, _, hi = args.nccl_ctas.partition(":")
         opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)
@@ -238,7 +242,8 @@ def main(argv=None) -> int:
             summary = {"time_to_full_placement_s": res.time_to_deliver_s, "aggregate_GBps": gbps,
                        "bytes_moved": res.bytes_planned, "ranks": len(cfg.nodes), "mode": args.m,
                        "engine": args.engine, "pack": args.pack, "plan_ms": res.plan_ms,
-                       "nacks": res.nacks, "redispatched": res.redispatched}
+                       "nacks": res.nacks, "redispatched": res.redispatched, "recoveries": res.recoveries,
+                       "dropped": res.dropped}
             if res.engine_stats:
                 summary["engine"] = {"name": args.engine, **res.engine_stats}
             print(json.dumps(summary), flush=True)
@@ -250,7 +255,15 @@ def main(argv=None) -> int:
         print(json.dumps({"level": "info", "node": my_id, "layers": done, "dir": args.persist_dir,
                           "message": "layers persisted"}), file=sys.stderr)
     if barrier:
-        barrier()
+        # A rank may have died during the session (elastic recovery): do not
+        # wait for it forever.
+        try:
+            import torch.distributed as dist
+
+            dist.monitored_barrier(timeout=datetime.timedelta(seconds=15))
+        except Exception as e:  # noqa: BLE001
+            print(json.dumps({"level": "warn", "node": my_id, "error": str(e)[:200],
+                              "message": "final barrier incomplete (a rank is gone)"}), file=sys.stderr)
     time.sleep(0.05)  # let startup messages flush before sockets close
     rt.close()
     return 0 if res.ok else 1

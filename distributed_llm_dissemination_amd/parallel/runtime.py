@@ -66,6 +66,8 @@ class SessionResult:
     error: str = ""
     nacks: int = 0  # leader: chunk re-sends after CRC mismatches
     redispatched: int = 0  # leader: jobs re-sent from another owner after a deadline
+    recoveries: int = 0  # leader: communicator shrinks after a rank died (planned engines)
+    dropped: int = 0  # leader: (dest, layer) pairs given up (dead dest / no live holder)
     engine_stats: Dict[str, float] = field(default_factory=dict)
 
 
@@ -464,6 +466,8 @@ class Runtime:
             error=err if err else ("" if ok else "timeout waiting for Ready()"),
             nacks=st.nacks,
             redispatched=st.redispatched,
+            recoveries=st.recoveries,
+            dropped=st.dropped,
         )
         if self.engine is not None and ok:
             self.engine.quiesce()  # trailing verifications of chunks nobody waited for
@@ -484,7 +488,7 @@ class Runtime:
             k: getattr(es, k)
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
-                      "group_us_hist", "land_us_hist")
+                      "suspects", "shrinks", "aborted_pieces", "group_us_hist", "land_us_hist")
         }
 
     def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0) -> Dict[tuple, int]:

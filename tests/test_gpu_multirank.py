@@ -72,3 +72,44 @@ def test_cli_torchrun_rccl(n, tmp_path):
                       "--json-summary"])
     assert r.returncode == 0, r.stderr[-4000:]
     assert "Time to deliver:" in r.stdout
+
+
+def test_cli_rank_death_elastic_recovery(n, tmp_path):
+    """A rank process dies mid-session (--inject kill-rank, os._exit): the
+    survivors' RCCL groups with it fail or stall, the leader's probe finds it
+    gone, the survivors abort the communicator and re-form one without it
+    (fresh unique id from the leader), and the leader re-plans the unacked
+    layers from live holders. Plain processes, not torchrun: its agent would
+    tear every worker down when one exits."""
+    from distributed_llm_dissemination_amd.models.catalog import make_workload
+
+    cfg = make_workload(n, 24, 64 << 20, tier="host", seeding="uniform", copies=2, seed=7, chunk_bytes=8 << 20)
+    path = tmp_path / "cfg.json"
+    path.write_text(json.dumps(cfg.to_json()))
+    victim = n - 1
+    port = _port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, PYTHONPATH=ROOT, RANK=str(r), LOCAL_RANK=str(r if _ngpus() >= n else 0),
+                   WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if _ngpus() < n:
+            env["DISSEM_SHARED_GPU"] = "1"
+        procs.append(subprocess.Popen(
+            [sys.executable, "-m", "distributed_llm_dissemination_amd", "-f", str(path), "-m", "1", "--engine", "rccl",
+             "--json-summary", "--suspect-timeout", "2", "--timeout", "120", "--inject", f"kill-rank={victim}@0"],
+            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT, env=env))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=200))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    rcs = [p.returncode for p in procs]
+    assert rcs[victim] == 86, outs[victim][1][-3000:]
+    for r in range(n):
+        if r != victim:
+            assert rcs[r] == 0, (r, outs[r][1][-4000:])
+    summary = json.loads(outs[0][0].strip().splitlines()[-1])
+    assert summary["recoveries"] >= 1, summary
