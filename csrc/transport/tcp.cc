@@ -16,6 +16,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -62,7 +63,9 @@ void write_all(int fd, const void* data, size_t n) {
   }
 }
 
-int dial(const std::string& addr) {
+// Connect with a bounded wait (liveness probes must not hang the leader's event
+// loop on an unreachable host). timeout_ms <= 0: blocking connect.
+int dial(const std::string& addr, int timeout_ms = 0) {
   HostPort hp = split_addr(addr);
   std::string host = hp.host.empty() ? "127.0.0.1" : hp.host;
   addrinfo hints{};
@@ -75,7 +78,26 @@ int dial(const std::string& addr) {
   for (addrinfo* ai = res; ai; ai = ai->ai_next) {
     fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC, ai->ai_protocol);
     if (fd < 0) continue;
-    if (::connect(fd, ai->ai_addr, ai->ai_addrlen) == 0) break;
+    if (timeout_ms > 0) {
+      const int fl = fcntl(fd, F_GETFL, 0);
+      fcntl(fd, F_SETFL, fl | O_NONBLOCK);
+      int rc2 = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+      if (rc2 != 0 && errno == EINPROGRESS) {
+        pollfd pf{fd, POLLOUT, 0};
+        int err = 0;
+        socklen_t el = sizeof err;
+        if (::poll(&pf, 1, timeout_ms) == 1 && getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &el) == 0 && err == 0)
+          rc2 = 0;
+        else
+          errno = err ? err : ETIMEDOUT;
+      }
+      if (rc2 == 0) {
+        fcntl(fd, F_SETFL, fl);
+        break;
+      }
+    } else if (::connect(fd, ai->ai_addr, ai->ai_addrlen) == 0) {
+      break;
+    }
     ::close(fd);
     fd = -1;
   }
@@ -176,7 +198,7 @@ class TcpTransport : public Transport {
     if (!lookup(id, &daddr)) return false;
     if (is_self(daddr)) return !closed_.load();
     try {
-      int fd = dial(daddr);  // a dead process's port refuses the connection
+      int fd = dial(daddr, 2000);  // a dead process's port refuses the connection
       ::close(fd);
       return true;
     } catch (const std::exception&) {

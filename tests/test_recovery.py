@@ -93,3 +93,31 @@ def test_layer_without_live_holder_is_dropped():
     assert res[0].recoveries == 1
     # the dead rank's own assignment + every survivor's copy of a lost layer
     assert res[0].dropped == len(cfg.assignment[2]) + 2 * len(lost)
+
+
+def test_false_alarm_does_not_shrink():
+    """A tiny suspect timeout makes ordinary groups look stalled: ranks report
+    suspects, the leader's probe finds every peer alive, nothing is shrunk and
+    the session completes normally."""
+    key = f"recov{next(_keys)}"
+    cfg = make_workload(3, 6, 4 * MiB, tier="host", seeding="random", chunk_bytes=MiB)
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+                   engine_opts={"suspect_s": 1e-4}) for i in range(3)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for r in rts:
+            r.prepare(1)
+        res = [None] * 3
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        assert res[0].recoveries == 0 and res[0].dropped == 0
+        assert all(x.engine_stats["shrinks"] == 0 for x in res)
+    finally:
+        for r in rts:
+            r.close()
