@@ -47,7 +47,7 @@ const char* msg_type_name(MsgType t);
 // One transfer of a byte range of a layer from `src` to `dst` (src == dst: a
 // local promotion into HBM). Jobs carry a leader-assigned global sequence
 // number; every rank executes its jobs in sequence order, which makes the
-// RCCL point-to-point schedule deadlock-free (csrc/gpu/gpu_engine.cc).
+// RCCL point-to-point schedule deadlock-free (csrc/engine/planned_engine.cc).
 struct XferJob {
   uint64_t seq = 0;
   NodeID src = 0, dst = 0;

@@ -5,7 +5,7 @@
 // fresh connection per layer payload, token-bucket pacing, cut-through "pipe")
 // and InprocTransport (a process-global registry of queues; the test fake).
 // On MI355X the layer bytes normally move on the RCCL data plane instead
-// (csrc/gpu/rccl_engine.cc); the TCP payload path is the CPU/loopback plane.
+// (csrc/engine/planned_engine.cc on csrc/gpu/hip_backend.cc); the TCP payload path is the CPU/loopback plane.
 #pragma once
 
 #include <atomic>
