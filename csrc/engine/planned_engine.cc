@@ -763,7 +763,7 @@ void PlannedEngine::poll() {
       const auto now = std::chrono::steady_clock::now();
       double age = std::chrono::duration<double>(now - head.t0).count();
       if (node_ && cfg_.suspect_s > 0 && age > cfg_.suspect_s &&
-          now - last_suspect_ > std::chrono::duration<double>(cfg_.suspect_s)) {
+          now - last_suspect_ > std::chrono::duration<double>(std::max(cfg_.suspect_s, 1.0))) {
         // Not (yet) a failure: if the peers are alive the group may still
         // complete. Name every in-flight peer: the group at the head may be
         // waiting on a live rank that itself waits on the dead one.
