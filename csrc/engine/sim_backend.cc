@@ -47,6 +47,11 @@ struct Fabric {
 
   void post(int src, int dst, bool send, Posted* op) {
     std::lock_guard<std::mutex> lk(mu);
+    if (aborted) {  // like an aborted communicator: nothing moves any more
+      op->done = op->bad = true;
+      cv.notify_all();
+      return;
+    }
     auto& c = ch[{src, dst}];
     (send ? c.first : c.second).push_back(op);
     while (!c.first.empty() && !c.second.empty()) {
@@ -64,6 +69,18 @@ struct Fabric {
       s->done = r->done = true;
     }
     cv.notify_all();
+  }
+  // Withdraw ops still queued (their group gave up): a later match must never
+  // copy into or out of a buffer whose owner has moved on.
+  void cancel(const std::vector<std::unique_ptr<Posted>>& ops) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& kv : ch)
+      for (auto* q : {&kv.second.first, &kv.second.second})
+        for (auto it = q->begin(); it != q->end();) {
+          bool mine = false;
+          for (auto& o : ops) mine = mine || o.get() == *it;
+          it = mine ? q->erase(it) : std::next(it);
+        }
   }
   // Returns false on timeout (deadlock) or a size mismatch.
   bool wait_all(const std::vector<std::unique_ptr<Posted>>& ops, double timeout_s) {
@@ -244,6 +261,7 @@ class SimBackend : public Backend {
         else fab->post(o.peer, rank, false, posted.back().get());
       }
       if (!fab->wait_all(posted, kTimeout)) {
+        fab->cancel(posted);
         set_error("P2P group did not complete (deadlock or size mismatch)");
         ev->state = -1;
         return;
