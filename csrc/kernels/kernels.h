@@ -1,5 +1,13 @@
 // Launchers for the gfx950 kernels. Callable from host C++ (g++ objects); the
 // kernels themselves are in csrc/kernels/*.hip, compiled for gfx950 only.
+//
+// All of them are single-pass streaming kernels: every input byte is read once
+// and every output byte written once, 16 B per lane, with no data shared
+// between workgroups. The hardware's round-robin of workgroups over the 8 XCDs
+// therefore needs no remapping (there is no L2 reuse to keep on one XCD); what
+// matters is enough bytes in flight per CU (HBM latency) and, for CRC32C, the
+// LDS table layout (crc32c.hip). Grids are sized to the CU count (256) times
+// the workgroups a CU holds, with grid-stride loops beyond that.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
