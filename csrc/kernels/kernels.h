@@ -6,8 +6,10 @@
 // between workgroups. The hardware's round-robin of workgroups over the 8 XCDs
 // therefore needs no remapping (there is no L2 reuse to keep on one XCD); what
 // matters is enough bytes in flight per CU (HBM latency) and, for CRC32C, the
-// LDS table layout (crc32c.hip). Grids are sized to the CU count (256) times
-// the workgroups a CU holds, with grid-stride loops beyond that.
+// LDS table layout (crc32c.hip). fill and CRC32C size their grids to the CU
+// count (256) times the workgroups a CU holds and grid-stride beyond that;
+// fp8 pack/unpack give every lane one 8-element group (a 64 MiB chunk is
+// 16k workgroups, far more than the chip holds at once).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
