@@ -298,5 +298,10 @@ def run_client(cfg, node_id: int) -> int:
     return 0
 
 
+def entry() -> None:
+    """Console script `dissem` (pyproject.toml)."""
+    sys.exit(main())
+
+
 if __name__ == "__main__":
     sys.exit(main())
