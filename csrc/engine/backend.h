@@ -55,6 +55,21 @@ class Backend {
   // verify queue: after `after`, CRC32C of [p, p+n) into result slot `slot`
   // (n == 0: just an ordering marker on the verify queue)
   virtual Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) = 0;
+  // verify queue: after `after`, CRC32C of several independent buffers (the
+  // chunks one P2P group landed) into their result slots; one event for all.
+  struct CrcReq {
+    const uint8_t* p;
+    int64_t n;
+    uint32_t slot;
+  };
+  virtual Ev crc_batch(const std::vector<CrcReq>& reqs, Ev after) {
+    Ev last = 0;
+    for (auto& r : reqs) {
+      if (last) release(last);
+      last = crc(r.p, r.n, r.slot, after);
+    }
+    return last ? last : crc(nullptr, 0, 0, after);
+  }
   virtual int query(Ev e) = 0;  // 1 done, 0 pending, -1 failed
   virtual void release(Ev e) = 0;
   virtual uint32_t crc_result(uint32_t slot) = 0;

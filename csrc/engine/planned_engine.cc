@@ -613,6 +613,7 @@ bool PlannedEngine::issue_some() {
     // Receivers: chunks are valid behind `g` on the comm queue; check them on the verify queue.
     Verify v;
     Ev last = 0;
+    std::vector<Backend::CrcReq> checks;
     for (auto& p : group) {
       if (p.kind != Kind::Recv) continue;
       Layer& L = layers_[p.layer];
@@ -621,13 +622,13 @@ bool PlannedEngine::issue_some() {
       uint32_t slot = ~0u;
       if (cfg_.verify && p.has_crc && p.full) {
         slot = crc_slot();
-        if (last) backend_->release(last);
-        last = backend_->crc(L.dev + p.off, p.len, slot, landed_ev);
+        checks.push_back(Backend::CrcReq{L.dev + p.off, p.len, slot});
       }
       v.pieces.push_back(p);
       v.slots.push_back(slot);
     }
-    if (!v.pieces.empty() && !last) last = backend_->crc(nullptr, 0, 0, landed_ev);
+    // Every chunk this group landed is checked by one batched launch.
+    if (!v.pieces.empty()) last = backend_->crc_batch(checks, landed_ev);
     if (landed_ev != g) backend_->release(landed_ev);
     if (!v.pieces.empty()) {
       v.ev = last;

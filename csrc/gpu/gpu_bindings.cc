@@ -182,6 +182,39 @@ void register_gpu_bindings(PyObject* module) {
           "crc32c_chunks");
   });
   m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
+  // Batched CRC of independent device buffers [(ptr, nbytes), ...] (synchronous).
+  m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream) {
+    py::gil_scoped_release nogil;
+    if (bufs.size() > size_t(kern::kCrcBatchMax)) throw std::invalid_argument("too many buffers for one batch");
+    int64_t mx = 0;
+    for (auto& b : bufs) mx = std::max(mx, b.second);
+    void* ws = nullptr;
+    uint32_t *host = nullptr, *dev = nullptr;
+    check(hipMalloc(&ws, kern::crc32c_batch_workspace_bytes(mx, int(bufs.size()))), "hipMalloc");
+    check(hipHostMalloc(reinterpret_cast<void**>(&host), std::max<size_t>(bufs.size(), 1) * 4, hipHostMallocMapped),
+          "hipHostMalloc");
+    check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
+    std::vector<kern::CrcItem> items;
+    for (size_t i = 0; i < bufs.size(); ++i)
+      items.push_back(kern::CrcItem{reinterpret_cast<const void*>(bufs[i].first), bufs[i].second, dev + i});
+    hipError_t e = kern::crc32c_batch(items.data(), int(items.size()), ws, as_stream(stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    std::vector<uint32_t> out(host, host + bufs.size());
+    (void)hipFree(ws);
+    (void)hipHostFree(host);
+    check(e, "crc32c_batch");
+    return out;
+  }, py::arg("buffers"), py::arg("stream") = 0);
+  m.def("crc32c_batch_async", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t out_dev, uint64_t ws,
+                                 uint64_t stream) {
+    std::vector<kern::CrcItem> items;
+    for (size_t i = 0; i < bufs.size(); ++i)
+      items.push_back(kern::CrcItem{reinterpret_cast<const void*>(bufs[i].first), bufs[i].second,
+                                    reinterpret_cast<uint32_t*>(out_dev) + i});
+    check(kern::crc32c_batch(items.data(), int(items.size()), reinterpret_cast<void*>(ws), as_stream(stream)),
+          "crc32c_batch");
+  });
+  m.def("crc32c_batch_workspace_bytes", &kern::crc32c_batch_workspace_bytes);
   m.def("fp8_pack", [](uint64_t bf16, int64_t n, uint64_t fp8, uint64_t scales, int block, uint64_t stream) {
     check(kern::fp8_pack(reinterpret_cast<const uint16_t*>(bf16), n, reinterpret_cast<uint8_t*>(fp8),
                          reinterpret_cast<float*>(scales), block, as_stream(stream)),

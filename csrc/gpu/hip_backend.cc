@@ -36,7 +36,8 @@ class HipBackend : public Backend {
     HIP_OK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
     copy_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     verify_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
-    HIP_OK(hipMalloc(&ws_, kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes)));
+    HIP_OK(hipMalloc(&ws_, std::max(kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes),
+                                     kern::crc32c_batch_workspace_bytes(cfg_.max_crc_bytes, kern::kCrcBatchMax))));
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&crc_dev_), crc_host_, 0));
@@ -138,6 +139,24 @@ class HipBackend : public Backend {
     if (n > 0) {
       if (n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
       HIP_OK(kern::crc32c_chunks(p, n, n, crc_dev_ + slot, ws_, verify_));
+    }
+    return record(verify_);
+  }
+
+  Ev crc_batch(const std::vector<CrcReq>& reqs, Ev after) override {
+    // One segments + one fold launch per kCrcBatchMax landed chunks (instead of
+    // two launches per chunk): fewer LDS table fills and partially empty grids.
+    if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
+    std::vector<kern::CrcItem> items;
+    for (size_t i = 0; i <= reqs.size(); ++i) {
+      if (i == reqs.size() || items.size() == size_t(kern::kCrcBatchMax)) {
+        if (!items.empty()) HIP_OK(kern::crc32c_batch(items.data(), int(items.size()), ws_, verify_));
+        items.clear();
+        if (i == reqs.size()) break;
+      }
+      const CrcReq& r = reqs[i];
+      if (r.n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
+      if (r.n > 0) items.push_back(kern::CrcItem{r.p, r.n, crc_dev_ + r.slot});
     }
     return record(verify_);
   }

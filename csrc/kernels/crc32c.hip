@@ -76,7 +76,7 @@ __device__ inline uint32_t wave_xor(uint32_t v) {
 
 // XOR of the 8 nibble tables t0..t0+7, indexed by the 8 nibbles of x.
 // L = lds + (lane & 31): entry (t, v) of this lane's bank-private replica.
-__device__ inline uint32_t nib8(const uint32_t* L, int t0, uint32_t x) {
+__device__ __forceinline__ uint32_t nib8(const uint32_t* L, int t0, uint32_t x) {
   uint32_t r = 0;
 #pragma unroll
   for (int n = 0; n < 8; ++n) r ^= L[(t0 + n) * 512 + ((x >> (4 * n)) & 15) * 32];
@@ -84,7 +84,7 @@ __device__ inline uint32_t nib8(const uint32_t* L, int t0, uint32_t x) {
 }
 
 // One strided step of a lane: s = shift_1KiB(s) xor crc16raw(w).
-__device__ inline uint32_t nib_step(const uint32_t* L, uint32_t s, uint4 w) {
+__device__ __forceinline__ uint32_t nib_step(const uint32_t* L, uint32_t s, uint4 w) {
   return nib8(L, 32, s) ^ nib8(L, 0, w.x) ^ nib8(L, 8, w.y) ^ nib8(L, 16, w.z) ^ nib8(L, 24, w.w);
 }
 
@@ -98,14 +98,61 @@ __device__ inline void load_nib_lds(uint32_t* lds, const uint32_t* __restrict__ 
   __syncthreads();
 }
 
-// Segment walk shared by the plain and the fused kernels. Each wave owns 16 KiB
-// segments; Visit sees every 16-B word with its byte offset in the chunk
-// (visit.begin(c, chunk_start, chunk_len) once per segment). seg_out[g] gets
-// the segment's raw CRC shifted to the end of its chunk: lane l of full segment
-// k multiplies by shift[k * 64 + l] (shift_last for a shorter final chunk). A
-// partial segment is always its chunk's last, so its lanes only align to it.
+// One 16 KiB segment on one wave: the raw CRC of [seg, seg + seg_len), shifted
+// to its chunk end (full segments: lane l multiplies by shift_row[l]; a partial
+// segment is always its chunk's last, so its lanes only align to it). The
+// result is valid in lane 0. Visit sees every 16-B word with its byte offset
+// in the chunk (seg_start + offset in the segment).
 template <int DEPTH, class Visit>
-__device__ inline void segment_crcs(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
+__device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg, int64_t seg_start, int64_t seg_len,
+                                       const uint32_t* __restrict__ shift_row,
+                                       const uint32_t* __restrict__ consts, const uint32_t* L, int lane,
+                                       Visit& visit) {
+  const int64_t nw = seg_len >> 4;
+  const uint4* words = reinterpret_cast<const uint4*>(seg);
+  uint32_t s = 0;
+  if (nw == kSegBytes / 16) {
+    // Full segment: 16 strided words per lane, DEPTH loads in flight per batch.
+    using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int b = 0; b < kWordsPerLane; b += DEPTH) {
+      u32x4 wv[DEPTH];
+#pragma unroll
+      for (int i = 0; i < DEPTH; ++i)
+        wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * (b + i)));
+#pragma unroll
+      for (int i = 0; i < DEPTH; ++i) {
+        const uint4 w = make_uint4(wv[i][0], wv[i][1], wv[i][2], wv[i][3]);
+        s = nib_step(L, s, w);
+        visit(w, seg_start + 16 * (lane + 64 * (b + i)));
+      }
+    }
+    s = multmodp(shift_row[lane], s);
+  } else {
+    int64_t last = -1;
+    for (int64_t j = lane; j < nw; j += 64) {
+      const uint4 w = words[j];
+      s = nib_step(L, s, w);
+      visit(w, seg_start + 16 * j);
+      last = j;
+    }
+    if (last >= 0) s = multmodp(consts[kOffLanePow + nw - 1 - last], s);
+  }
+  s = wave_xor(s);
+  if (lane == 0) {
+    // Byte tail (only a buffer's final segment can have one).
+    const uint8_t* tail = seg + (nw << 4);
+    for (int64_t b = 0; b < (seg_len & 15); ++b) s = consts[kOffT0 + ((s ^ tail[b]) & 255)] ^ (s >> 8);
+  }
+  return s;
+}
+
+// Segment walk of the plain and the fused kernels: `bytes` cut into chunks of
+// `chunk_bytes`, each wave owns 16 KiB segments (grid-stride). seg_out[g] gets
+// the segment's raw CRC shifted to the end of its chunk (shift: lane
+// constants of full chunks, shift_last: of a shorter final chunk).
+template <int DEPTH, class Visit>
+__device__ __forceinline__ void segment_crcs(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
                                     int64_t spc, int64_t total_segs, const uint32_t* __restrict__ consts,
                                     const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
                                     uint32_t* __restrict__ seg_out, const uint32_t* lds, Visit& visit) {
@@ -119,44 +166,11 @@ __device__ inline void segment_crcs(const uint8_t* __restrict__ src, int64_t byt
     const int64_t chunk_len = min(chunk_bytes, bytes - chunk_start);
     const int64_t seg_start = k * kSegBytes;
     const int64_t seg_len = min(int64_t(kSegBytes), chunk_len - seg_start);
-    const int64_t nw = seg_len >> 4;
-    const uint4* words = reinterpret_cast<const uint4*>(src + chunk_start + seg_start);
     visit.begin(c, chunk_start, chunk_len);
-    uint32_t s = 0;
-    if (nw == kSegBytes / 16) {
-      // Full segment: 16 strided words per lane, DEPTH loads in flight per batch.
-      using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-#pragma unroll
-      for (int b = 0; b < kWordsPerLane; b += DEPTH) {
-        u32x4 wv[DEPTH];
-#pragma unroll
-        for (int i = 0; i < DEPTH; ++i)
-          wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * (b + i)));
-#pragma unroll
-        for (int i = 0; i < DEPTH; ++i) {
-          const uint4 w = make_uint4(wv[i][0], wv[i][1], wv[i][2], wv[i][3]);
-          s = nib_step(L, s, w);
-          visit(w, seg_start + 16 * (lane + 64 * (b + i)));
-        }
-      }
-      s = multmodp((chunk_len == chunk_bytes ? shift : shift_last)[k * 64 + lane], s);
-    } else {
-      int64_t last = -1;
-      for (int64_t j = lane; j < nw; j += 64) {
-        const uint4 w = words[j];
-        s = nib_step(L, s, w);
-        visit(w, seg_start + 16 * j);
-        last = j;
-      }
-      if (last >= 0) s = multmodp(consts[kOffLanePow + nw - 1 - last], s);
-    }
-    s = wave_xor(s);
-    if (lane == 0) {
-      // Byte tail (only the buffer's final segment can have one).
-      const uint8_t* tail = src + chunk_start + seg_start + (nw << 4);
-      for (int64_t b = 0; b < (seg_len & 15); ++b) s = consts[kOffT0 + ((s ^ tail[b]) & 255)] ^ (s >> 8);
-      seg_out[g] = s;
-    }
+    const uint32_t* row = (chunk_len == chunk_bytes ? shift : shift_last) + k * 64;
+    const uint32_t s = one_segment<DEPTH>(src + chunk_start + seg_start, seg_start, seg_len, row, consts, L, lane,
+                                          visit);
+    if (lane == 0) seg_out[g] = s;
   }
 }
 
@@ -252,6 +266,51 @@ __global__ void __launch_bounds__(256) crc32c_fold_kernel(const uint32_t* __rest
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
   __syncthreads();
   if (threadIdx.x == 0) out[c] = part[0] ^ part[1] ^ part[2] ^ part[3] ^ init[chunk_len == chunk_bytes ? 0 : 1];
+}
+
+// ---- batched: up to kCrcBatchMax independent buffers (the chunks one P2P
+// group landed) in one segments launch + one fold launch.
+struct BatchArgs {
+  int n;
+  int64_t seg_base[kCrcBatchMax + 1];  // prefix sums of the items' segment counts
+  const uint8_t* src[kCrcBatchMax];
+  int64_t bytes[kCrcBatchMax];
+  const uint32_t* shift[kCrcBatchMax];  // lane shift table of a `bytes`-byte chunk
+  uint32_t init[kCrcBatchMax];
+  uint32_t* out[kCrcBatchMax];
+};
+
+__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_batch_segments_kernel(const BatchArgs a, const uint32_t* __restrict__ consts, uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t lds[kNibLds];
+  load_nib_lds(lds, consts);
+  const int lane = threadIdx.x & 63;
+  const uint32_t* L = lds + (lane & 31);
+  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
+  NoVisit v;
+  for (int64_t g = wave; g < a.seg_base[a.n]; g += nwaves) {
+    int j = 0;
+    while (g >= a.seg_base[j + 1]) ++j;
+    const int64_t k = g - a.seg_base[j];
+    const int64_t seg_start = k * kSegBytes;
+    const int64_t seg_len = min(int64_t(kSegBytes), a.bytes[j] - seg_start);
+    const uint32_t s = one_segment<16>(a.src[j] + seg_start, seg_start, seg_len, a.shift[j] + k * 64, consts, L,
+                                       lane, v);
+    if (lane == 0) seg_out[g] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256) crc32c_batch_fold_kernel(const BatchArgs a,
+                                                                const uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t part[4];
+  const int j = blockIdx.x;
+  uint32_t r = 0;
+  for (int64_t g = a.seg_base[j] + threadIdx.x; g < a.seg_base[j + 1]; g += 256) r ^= seg_out[g];
+  r = wave_xor(r);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
+  __syncthreads();
+  if (threadIdx.x == 0) *a.out[j] = part[0] ^ part[1] ^ part[2] ^ part[3] ^ a.init[j];
 }
 
 // Per-device constant tables and per-(chunk, last chunk) fold tables.
@@ -367,6 +426,41 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
       seg);
   crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, chunk_bytes, p.spc,
                                                                      p.fold + 2 * p.spc * 64, out);
+  return hipGetLastError();
+}
+
+size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n) {
+  const int64_t spc = (std::max<int64_t>(max_item_bytes, 1) + kSegBytes - 1) / kSegBytes;
+  return size_t(int64_t(std::max(n, 1)) * spc * 4 + 16);
+}
+
+hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n > kCrcBatchMax) return hipErrorInvalidValue;
+  BatchArgs a{};
+  a.n = 0;
+  a.seg_base[0] = 0;
+  uint32_t* consts = device_consts();
+  if (!consts) return hipErrorOutOfMemory;
+  for (int i = 0; i < n; ++i) {
+    const CrcItem& it = items[i];
+    if (it.bytes <= 0) continue;
+    if (it.bytes % 16 || (reinterpret_cast<uintptr_t>(it.src) & 15)) return hipErrorInvalidValue;
+    uint32_t* fold = fold_consts(it.bytes, it.bytes);
+    if (!fold) return hipErrorOutOfMemory;
+    const int64_t spc = (it.bytes + kSegBytes - 1) / kSegBytes;
+    const int j = a.n++;
+    a.src[j] = static_cast<const uint8_t*>(it.src);
+    a.bytes[j] = it.bytes;
+    a.shift[j] = fold;
+    a.init[j] = crc32c_init_term(uint64_t(it.bytes));
+    a.out[j] = it.out;
+    a.seg_base[j + 1] = a.seg_base[j] + spc;
+  }
+  if (a.n == 0) return hipSuccess;
+  auto* seg = static_cast<uint32_t*>(workspace);
+  crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n]), dim3(kSegThreads), 0, s>>>(a, consts, seg);
+  crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(256), 0, s>>>(a, seg);
   return hipGetLastError();
 }
 

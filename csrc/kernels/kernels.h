@@ -31,6 +31,17 @@ void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset = 
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes);
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                          hipStream_t s);
+// Batched: the standard CRC32C of each of up to kCrcBatchMax independent
+// buffers (bytes % 16 == 0, 16-B aligned) in one launch pair - the chunks a
+// P2P group landed. `workspace`: crc32c_batch_workspace_bytes(max bytes, n).
+constexpr int kCrcBatchMax = 16;
+struct CrcItem {
+  const void* src;
+  int64_t bytes;
+  uint32_t* out;
+};
+size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
+hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements
 // (scale = amax/448; non-finite inputs: +-inf saturate, NaN stays NaN), and back.

@@ -44,6 +44,19 @@ def main():
     ws1 = torch.empty(_core.crc32c_workspace_bytes(chunk, chunk), dtype=torch.uint8, device="cuda")
     t = timed(lambda: _core.crc32c_chunks_async(buf.data_ptr(), chunk, chunk, res.data_ptr(), ws1.data_ptr(), 0), 50)
     out["crc32c_one_64MiB_chunk_us"] = t * 1e6
+    # what a P2P group of 7 peers lands: 7 chunks, checked one by one or in one batch
+    outs7 = torch.empty(16, dtype=torch.int32, device="cuda")
+    bufs7 = [(buf.data_ptr() + i * chunk, chunk) for i in range(7)]
+
+    def seven_separate():
+        for i in range(7):
+            _core.crc32c_chunks_async(buf.data_ptr() + i * chunk, chunk, chunk, outs7.data_ptr() + 4 * i,
+                                      ws1.data_ptr(), 0)
+
+    wsb = torch.empty(_core.crc32c_batch_workspace_bytes(chunk, 7), dtype=torch.uint8, device="cuda")
+    out["crc32c_7x64MiB_separate_us"] = timed(seven_separate, 20) * 1e6
+    out["crc32c_7x64MiB_batched_us"] = timed(
+        lambda: _core.crc32c_batch_async(bufs7, outs7.data_ptr(), wsb.data_ptr(), 0), 20) * 1e6
     ne = n // 2
     x = buf.view(torch.bfloat16)[:ne]
     q = torch.empty(ne, dtype=torch.uint8, device="cuda")

@@ -41,6 +41,21 @@ def test_crc32c_chunks_match_host(gpu, n, chunk):
     assert gpu.crc32c_chunks(t.data_ptr(), n, chunk) == want
 
 
+def test_crc32c_batch_matches_host(gpu):
+    # the chunks one P2P group lands: independent buffers of mixed sizes
+    sizes = [64 << 20, (1 << 20) + 16, 100 << 10, 16, 48 << 10, 3 * (16 << 10) + 32]
+    bufs = []
+    for i, n in enumerate(sizes):
+        t = _dev_bytes(n)
+        gpu.fill_random(t.data_ptr(), n, 1000 + i)
+        bufs.append(t)
+    torch.cuda.synchronize()
+    got = gpu.crc32c_batch([(t.data_ptr(), t.numel()) for t in bufs])
+    assert got == [gpu.crc32c(t.cpu().numpy().tobytes()) for t in bufs]
+    # the batched and per-buffer kernels agree
+    assert got == [gpu.crc32c_chunks(t.data_ptr(), t.numel(), t.numel())[0] for t in bufs]
+
+
 def test_crc32c_detects_single_bit_flip(gpu):
     n = 4 << 20
     t = _dev_bytes(n)
