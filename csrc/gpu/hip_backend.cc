@@ -35,10 +35,13 @@ class HipBackend : public Backend {
     HIP_OK(hipSetDevice(cfg_.device));
     HIP_OK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
     copy_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
-    // Without peers the run is one long H2D stream: two SDMA queues in
-    // alternation keep the PCIe link busier across copy boundaries (h2dbench:
-    // 56.8 -> 57.4 GB/s). With RCCL in the process keep one copy queue.
-    if (cfg_.world == 1 && !cfg_.self_comm) copy2_ = create_stream_reserving(cfg_.device, 0);
+    // Two SDMA copy queues in alternation keep the PCIe link busier across copy
+    // boundaries (h2dbench: 56.8 -> 57.4 GB/s; bench 56.0 -> 56.9 GB/s). With
+    // RCCL in the process only when the copy queues are CU-masked: a masked
+    // stream gets a hardware queue of its own, so no copy can end up queued
+    // behind a comm-stream kernel that waits for a peer.
+    if ((cfg_.world == 1 && !cfg_.self_comm) || cfg_.reserve_cus > 0)
+      copy2_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     verify_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     HIP_OK(hipMalloc(&ws_, std::max(kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes),
                                      kern::crc32c_batch_workspace_bytes(cfg_.max_crc_bytes, kern::kCrcBatchMax))));
