@@ -105,21 +105,23 @@ class HipBackend : public Backend {
 
   Ev stage_pack(uint8_t* dst, const uint8_t* src, int64_t n_src, int block) override {
     // bf16 lands in a device scratch chunk, then the gfx950 pack kernel writes
-    // the packed chunk into the layer slot. One scratch suffices: both steps
-    // are ordered on the copy stream, and packing (~10 us per 64 MiB) is noise
-    // next to the PCIe copy (~1.2 ms).
-    if (n_src > scratch_bytes_) {
-      HIP_OK(hipStreamSynchronize(copy_));
-      if (scratch_) HIP_OK(hipFree(scratch_));
-      scratch_ = nullptr;
-      HIP_OK(hipMalloc(&scratch_, size_t(n_src)));
-      scratch_bytes_ = n_src;
+    // the packed chunk into the layer slot. One scratch per copy queue: both
+    // steps are ordered on that queue, and packing (~22 us per 64 MiB) is
+    // noise next to the PCIe copy (~1.2 ms).
+    const int q = copy2_ && (flip_ ^= true) ? 1 : 0;
+    hipStream_t s = q ? copy2_ : copy_;
+    if (n_src > scratch_bytes_[q]) {
+      HIP_OK(hipStreamSynchronize(s));
+      if (scratch_[q]) HIP_OK(hipFree(scratch_[q]));
+      scratch_[q] = nullptr;
+      HIP_OK(hipMalloc(&scratch_[q], size_t(n_src)));
+      scratch_bytes_[q] = n_src;
     }
-    HIP_OK(hipMemcpyAsync(scratch_, src, size_t(n_src), hipMemcpyHostToDevice, copy_));
+    HIP_OK(hipMemcpyAsync(scratch_[q], src, size_t(n_src), hipMemcpyHostToDevice, s));
     const int64_t n = n_src / 2;
-    HIP_OK(kern::fp8_pack(static_cast<const uint16_t*>(scratch_), n, dst, reinterpret_cast<float*>(dst + n), block,
-                          copy_));
-    return record(copy_);
+    HIP_OK(kern::fp8_pack(static_cast<const uint16_t*>(scratch_[q]), n, dst, reinterpret_cast<float*>(dst + n), block,
+                          s));
+    return record(s);
   }
 
   Ev corrupt(uint8_t* p) override {
@@ -255,7 +257,8 @@ class HipBackend : public Backend {
     for (auto e : pool_) (void)hipEventDestroy(e);
     pool_.clear();
     if (ws_) (void)hipFree(ws_);
-    if (scratch_) (void)hipFree(scratch_);
+    for (void* p : scratch_)
+      if (p) (void)hipFree(p);
     if (crc_host_) (void)hipHostFree(crc_host_);
     (void)hipStreamDestroy(comm_);
     (void)hipStreamDestroy(copy_);
@@ -283,8 +286,8 @@ class HipBackend : public Backend {
   bool flip_ = false;
   ncclComm_t nccl_ = nullptr;
   void* ws_ = nullptr;
-  void* scratch_ = nullptr;  // bf16 landing chunk for stage_pack
-  int64_t scratch_bytes_ = 0;
+  void* scratch_[2] = {nullptr, nullptr};  // bf16 landing chunk for stage_pack, per copy queue
+  int64_t scratch_bytes_[2] = {0, 0};
   uint32_t* crc_host_ = nullptr;
   uint32_t* crc_dev_ = nullptr;
   std::vector<hipEvent_t> pool_;  // issue-thread only
