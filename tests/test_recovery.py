@@ -121,3 +121,12 @@ def test_false_alarm_does_not_shrink():
     finally:
         for r in rts:
             r.close()
+
+
+def test_rank_death_eight_ranks_mode3_flow():
+    # mode 3 stripes layers over several senders in byte ranges; after the
+    # shrink the leader re-plans the unacked layers whole from live holders.
+    cfg = make_workload(8, 16, 4 * MiB, tier="host", seeding="uniform", copies=3, seed=3, chunk_bytes=MiB)
+    res, _ = _cluster(cfg, dead_rank=5, die_after=2, mode=3)
+    assert res[0].recoveries == 1
+    assert res[0].dropped == len(cfg.assignment[5])
