@@ -95,8 +95,10 @@ static void ring(bool tcp, int mode) {
   for (auto& t : ts) t->close();
 }
 
-// Planned engine on the simulated fabric: 4 ranks, full replication, mode 1.
-static void planned_sim(int mode, double corrupt = 0) {
+// Planned engine on the simulated fabric: 4 ranks, full replication.
+// die >= 0: that rank stops dead after two groups (elastic recovery path;
+// every layer then has two holders).
+static void planned_sim(int mode, double corrupt = 0, int die = -1) {
   const int n = 4, L = 6;
   const int64_t chunk = 1 << 16, size = 3 * chunk + 100;
   static int uniq = 0;
@@ -119,11 +121,15 @@ static void planned_sim(int mode, double corrupt = 0) {
     pc.chunk_bytes = chunk;
     pc.inject_corrupt = corrupt;
     pc.max_retries = 16;
+    if (die >= 0) {
+      pc.suspect_s = 0.2;
+      if (i == die) pc.inject_die_after_groups = 2;
+    }
     auto e = std::make_shared<PlannedEngine>(pc, make_sim_backend(key, i, n));
     LayersSrc mine;
     for (int l = 0; l < L; ++l) {
       e->provision(LayerID(l), size);
-      if (l % n == i) {
+      if (l % n == i || (die >= 0 && (l + 1) % n == i)) {
         mine[LayerID(l)] = inmem(data[size_t(l)]);
         CrcManifest m;
         m.chunk_bytes = chunk;
@@ -143,8 +149,11 @@ static void planned_sim(int mode, double corrupt = 0) {
   }
   for (auto& nd : nodes) nd->start();
   for (int i = 1; i < n; ++i) nodes[size_t(i)]->announce();
-  for (auto& nd : nodes) EXPECT(nd->wait_ready(20));
+  for (int i = 0; i < n; ++i)
+    if (i != die) EXPECT(nodes[size_t(i)]->wait_ready(20));
+  if (die >= 0) EXPECT(nodes[0]->stats().recoveries == 1);
   for (int i = 0; i < n; ++i) {
+    if (i == die) continue;
     engines[size_t(i)]->quiesce();
     for (int l = 0; l < L; ++l)
       EXPECT(memcmp(engines[size_t(i)]->device_ptr(LayerID(l)), data[size_t(l)]->ptr, size_t(size)) == 0);
@@ -164,6 +173,8 @@ int main() {
   }
   for (int mode = 1; mode <= 3; ++mode) planned_sim(mode);
   planned_sim(1, 0.3);  // NACK / re-send path under injected corruption
+  planned_sim(1, 0, 3);  // a rank dies: suspect -> probe -> shrink -> re-plan
+  planned_sim(2, 0, 2);
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;
