@@ -234,10 +234,12 @@ class Runtime:
         layers: Dict[int, _core.LayerSrc] = {}
         gpu = self.engine is not None
         if gpu:
-            # Every layer this rank may hold in HBM gets a slot up front (one arena per rank).
+            # Every layer this rank may hold in HBM gets its slot up front.
             want = set(self.cfg.assignment.get(self.node_id, []))
             for per in self.me.initial_layers.values():
                 want |= set(per)
+            if self.engine_kind == "rccl":
+                self._check_hbm_capacity(want)
             for l in sorted(want):
                 self.engine.provision(l, self.slot_sizes[l])
         for st, per in sorted(self.me.initial_layers.items()):
@@ -286,6 +288,22 @@ class Runtime:
                 self.engine.set_source_packed(l, True)
             self.resumed.append(l)
         return layers
+
+    # Headroom kept free of layer slots: CRC workspaces, fp8 staging scratch,
+    # RCCL's own buffers, PyTorch's context.
+    HBM_HEADROOM = 4 << 30
+
+    def _check_hbm_capacity(self, layers) -> None:
+        """refuse a placement that cannot fit before allocating any of it
+        (126 x 3 GiB bf16 = 378 GiB does not fit 288 GB; fp8 packing or a partitioned
+        assignment does)."""
+        need = sum(self.slot_sizes[l] for l in layers)
+        free, total = _core.mem_info()
+        if need + self.HBM_HEADROOM > free:
+            raise ValueError(
+                f"node {self.node_id}: its {len(layers)} layer slots need {need / 2**30:.1f} GiB of HBM but only "
+                f"{free / 2**30:.1f} of {total / 2**30:.1f} GiB are free (keeping {self.HBM_HEADROOM >> 30} GiB "
+                f"headroom); use --pack fp8 or an assignment that partitions the layers")
 
     # ------------------------------------------------------ persist / resume
     PERSIST_MANIFEST = "manifest.json"

@@ -86,3 +86,14 @@ def test_fp8_packed_session(gpu, tier, tmp_path):
                 assert out == gpu.fp8_unpack_layer_host(images[l], size, MiB, 128)
     finally:
         rt.close()
+
+
+def test_hbm_capacity_is_checked_before_allocating():
+    """A placement larger than the GPU's HBM is refused up front with a clear
+    message (no partial allocation): 80 x 4 GiB = 320 GiB > 288 GB."""
+    from distributed_llm_dissemination_amd.models.catalog import make_workload
+    from distributed_llm_dissemination_amd.parallel.runtime import Runtime
+
+    cfg = make_workload(1, 80, 4 << 30, tier="device", chunk_bytes=64 << 20)
+    with pytest.raises(ValueError, match="HBM"):
+        Runtime(cfg, 0, engine="rccl", chunk_bytes=64 << 20, registry={0: "127.0.0.1:0"})
