@@ -60,6 +60,7 @@ def parse_args(argv=None):
     p.add_argument("--reserve-cus", type=int, default=-1,
                    help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
+    p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
     p.add_argument("--preset", default="", choices=["", "llama70b", "llama405b-fp8"],
                    help="llama70b = 80 x 1 GiB (default); llama405b-fp8 = 126 x 3 GiB with --pack fp8")
     args = p.parse_args(argv)

@@ -261,7 +261,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("suspect_s", &PlannedConfig::suspect_s)
       .def_readwrite("inject_die_after_groups", &PlannedConfig::inject_die_after_groups)
       .def_readwrite("nccl_min_ctas", &PlannedConfig::nccl_min_ctas)
-      .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas);
+      .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas)
+      .def_readwrite("nccl_register", &PlannedConfig::nccl_register);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)

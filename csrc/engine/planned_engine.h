@@ -74,6 +74,7 @@ struct PlannedConfig {
   // 0 keeps RCCL's own choice. More CTAs = more channels per P2P peer.
   int nccl_min_ctas = 0;
   int nccl_max_ctas = 0;
+  bool nccl_register = false;  // register every HBM slot with the communicator (ncclCommRegister)
 };
 
 struct PlannedStats {

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstring>
 #include <thread>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -79,13 +80,37 @@ class HipBackend : public Backend {
 
   void init_thread() override { HIP_OK(hipSetDevice(cfg_.device)); }
 
+  // Layer slots are allocated once per session set-up; with nccl_register each
+  // is also registered with the communicator (ncclCommRegister), which lets
+  // RCCL use the user buffer directly where its transport supports it.
+  void register_slot(uint8_t* p, int64_t n) {
+    if (!cfg_.nccl_register || !nccl_) return;
+    void* h = nullptr;
+    ncclResult_t r = ncclCommRegister(nccl_, p, size_t(n), &h);
+    if (r != ncclSuccess) {
+      log::warn(cfg_.rank).s("error", ncclGetErrorString(r)).msg("ncclCommRegister failed; slot stays unregistered");
+      return;
+    }
+    regs_[p] = {n, h};
+  }
+  void deregister_slot(uint8_t* p) {
+    auto it = regs_.find(p);
+    if (it == regs_.end()) return;
+    if (nccl_ && it->second.second) (void)ncclCommDeregister(nccl_, it->second.second);
+    regs_.erase(it);
+  }
+
   uint8_t* alloc(int64_t n) override {
     HIP_OK(hipSetDevice(cfg_.device));
     void* p = nullptr;
     HIP_OK(hipMalloc(&p, size_t(std::max<int64_t>(n, 1))));
+    register_slot(static_cast<uint8_t*>(p), std::max<int64_t>(n, 1));
     return static_cast<uint8_t*>(p);
   }
-  void free(uint8_t* p) override { (void)hipFree(p); }
+  void free(uint8_t* p) override {
+    deregister_slot(p);
+    (void)hipFree(p);
+  }
   uint8_t* alloc_host(int64_t n) override {
     void* p = nullptr;
     HIP_OK(hipHostMalloc(&p, size_t(std::max<int64_t>(n, 4096)), hipHostMallocDefault));
@@ -205,6 +230,9 @@ class HipBackend : public Backend {
     // survivors works with any RCCL.)
     (void)ncclCommAbort(nccl_);
     nccl_ = nullptr;
+    std::vector<std::pair<uint8_t*, int64_t>> regd;  // re-register with the new communicator
+    for (auto& kv : regs_) regd.push_back({kv.first, kv.second.first});
+    regs_.clear();
     int new_rank = 0;
     for (int r = 0; r < cfg_.rank; ++r)
       if (std::find(dead.begin(), dead.end(), r) == dead.end()) ++new_rank;
@@ -234,6 +262,7 @@ class HipBackend : public Backend {
     ncclUniqueId id;
     memcpy(&id, comm_id.data(), sizeof id);
     init_comm(id);
+    for (auto& pr : regd) register_slot(pr.first, pr.second);
     return new_rank;
   }
 
@@ -283,6 +312,7 @@ class HipBackend : public Backend {
   HipBackendConfig cfg_;
   hipStream_t comm_ = nullptr, copy_ = nullptr, verify_ = nullptr;
   hipStream_t copy2_ = nullptr;  // second H2D queue (single-rank runs)
+  std::map<uint8_t*, std::pair<int64_t, void*>> regs_;  // registered slots: size, handle
   bool flip_ = false;
   ncclComm_t nccl_ = nullptr;
   void* ws_ = nullptr;

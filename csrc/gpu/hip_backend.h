@@ -29,6 +29,7 @@ struct HipBackendConfig {
   // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
   int reserve_cus = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
+  bool nccl_register = false;                  // ncclCommRegister every layer slot
 };
 
 // A non-default stream whose kernels may use every CU but the last `reserve`

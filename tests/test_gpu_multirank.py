@@ -51,7 +51,8 @@ def n():
 @pytest.mark.parametrize("mode,extra", [(1, []), (2, ["--pull-window", "2"]), (3, []), (0, ["--seeding", "leader"]),
                                         (0, ["--seeding", "leader", "--bcast", "collective"]),
                                         (1, ["--pack", "fp8", "--layer-mib", "96"]),
-                                        (1, ["--nccl-ctas", "4:16", "--reserve-cus", "64"])])
+                                        (1, ["--nccl-ctas", "4:16", "--reserve-cus", "64"]),
+                                        (1, ["--nccl-register"])])
 def test_bench_modes(n, mode, extra):
     r = _torchrun(n, ["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--layers", "16",
                       "--layer-mib", "64", "--chunk-mib", "16", "--mode", str(mode)] + extra)
