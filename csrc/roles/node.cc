@@ -521,6 +521,9 @@ void Node::finish_if_satisfied() {
 
 // ------------------------------------------- elastic recovery (planned data plane)
 //
+// The reference only sketches this (Leader interface TODOs `update(a)` and
+// `crash(n node)`, distributor/node.go:215-219; a dead sender hangs the run,
+// SURVEY §5.3).
 // A rank whose P2P group stalls or fails reports the group's peers (Suspect).
 // The leader probes them over the control plane; for peers that are gone it
 // starts a recovery generation: the dead nodes leave the status and the
