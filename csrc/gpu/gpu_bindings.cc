@@ -36,7 +36,7 @@ struct Scratch {
 std::mutex g_scratch_mu;
 std::map<int, Scratch> g_scratch;
 
-std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk, uint64_t stream) {
+std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk, uint64_t stream, int impl = 0) {
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   std::lock_guard<std::mutex> lk(g_scratch_mu);
@@ -55,7 +55,8 @@ std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk
   }
   uint32_t* dout = nullptr;
   check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dout), s.out, 0), "hipHostGetDevicePointer");
-  check(kern::crc32c_chunks(reinterpret_cast<const void*>(ptr), bytes, chunk, dout, s.ws, as_stream(stream)),
+  check(kern::crc32c_chunks_impl(reinterpret_cast<const void*>(ptr), bytes, chunk, dout, s.ws, as_stream(stream),
+                                 kern::CrcImpl(impl), 0),
         "crc32c_chunks");
   check(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize");
   return std::vector<uint32_t>(s.out, s.out + n);
@@ -171,16 +172,19 @@ void register_gpu_bindings(PyObject* module) {
   m.def("fill_random", [](uint64_t ptr, int64_t n, uint64_t seed, uint64_t stream) {
     check(kern::fill_random(reinterpret_cast<void*>(ptr), n, seed, as_stream(stream)), "fill_random");
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("seed"), py::arg("stream") = 0);
-  m.def("crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t stream) {
+  // impl: 0 auto, 1 LDS nibble tables, 2 MFMA (kern::CrcImpl).
+  m.def("crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t stream, int impl) {
     py::gil_scoped_release nogil;
-    return crc_chunks_sync(ptr, n, chunk, stream);
-  }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("stream") = 0);
+    return crc_chunks_sync(ptr, n, chunk, stream, impl);
+  }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("stream") = 0, py::arg("impl") = 0);
   m.def("crc32c_chunks_async", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t out_dev, uint64_t ws,
-                                  uint64_t stream) {
-    check(kern::crc32c_chunks(reinterpret_cast<const void*>(ptr), n, chunk, reinterpret_cast<uint32_t*>(out_dev),
-                              reinterpret_cast<void*>(ws), as_stream(stream)),
+                                  uint64_t stream, int impl, int max_blocks) {
+    check(kern::crc32c_chunks_impl(reinterpret_cast<const void*>(ptr), n, chunk, reinterpret_cast<uint32_t*>(out_dev),
+                                   reinterpret_cast<void*>(ws), as_stream(stream), kern::CrcImpl(impl), max_blocks),
           "crc32c_chunks");
-  });
+  }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("out"), py::arg("workspace"),
+     py::arg("stream") = 0, py::arg("impl") = 0, py::arg("max_blocks") = 0);
+  m.def("crc32c_mfma_applies", &kern::crc32c_mfma_applies);
   m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
   // Batched CRC of independent device buffers [(ptr, nbytes), ...] (synchronous).
   m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream) {

@@ -416,14 +416,25 @@ size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes) {
 
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                          hipStream_t s) {
+  return crc32c_chunks_impl(src, bytes, chunk_bytes, out, workspace, s, CrcImpl::kAuto, 0);
+}
+
+hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
+                              hipStream_t s, CrcImpl impl, int max_blocks) {
   if (bytes <= 0) return hipSuccess;
   if (chunk_bytes <= 0 || chunk_bytes % 16 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  crc32c_segments_kernel<<<seg_grid(p.total_segs), dim3(kSegThreads), 0, s>>>(
-      static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold, p.fold + p.spc * 64,
-      seg);
+  const bool mfma = impl == CrcImpl::kMfma || (impl == CrcImpl::kAuto && crc32c_mfma_default() &&
+                                               crc32c_mfma_applies(bytes, chunk_bytes));
+  if (mfma) {
+    if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks); e != hipSuccess) return e;
+  } else {
+    crc32c_segments_kernel<<<seg_grid(p.total_segs), dim3(kSegThreads), 0, s>>>(
+        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
+        p.fold + p.spc * 64, seg);
+  }
   crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, chunk_bytes, p.spc,
                                                                      p.fold + 2 * p.spc * 64, out);
   return hipGetLastError();

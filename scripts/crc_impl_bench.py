@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""A/B of the two CRC32C segment kernels on one MI355X.
+
+impl 1 = LDS nibble tables (crc32c.hip), impl 2 = GF(2) matrix product on the
+matrix cores (crc32c_mfma.hip), over a grid-cap sweep for the MFMA kernel.
+Shapes: 1 GiB in 64 MiB chunks (bulk throughput) and one 64 MiB chunk (the
+per-landing verify of the data engine). Prints one JSON object.
+"""
+
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+from distributed_llm_dissemination_amd import _core  # noqa: E402
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+
+
+def main():
+    n, chunk = 1 << 30, 64 << 20
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _core.fill_random(buf.data_ptr(), n, 3)
+    res = torch.empty(n // chunk, dtype=torch.int32, device="cuda")
+    ws = torch.empty(_core.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    out = {}
+    variants = [("nibble", 1, 0)] + [(f"mfma_cap{c}", 2, c) for c in (256, 512, 768, 1024, 2048, 4096)]
+    for name, impl, cap in variants:
+        def bulk():
+            _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)
+
+        def one():
+            _core.crc32c_chunks_async(buf.data_ptr(), chunk, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)
+
+        t = timed(bulk, 20)
+        out[f"{name}_1GiB_GBps"] = round(n / t / 1e9, 1)
+        out[f"{name}_one_64MiB_us"] = round(timed(one, 100) * 1e6, 1)
+        # results agree with the reference kernel
+        a = _core.crc32c_chunks(buf.data_ptr(), n, chunk, impl=impl)
+        out[f"{name}_match"] = a == _core.crc32c_chunks(buf.data_ptr(), n, chunk, impl=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -41,6 +41,41 @@ def test_crc32c_chunks_match_host(gpu, n, chunk):
     assert gpu.crc32c_chunks(t.data_ptr(), n, chunk) == want
 
 
+@pytest.mark.parametrize(
+    "n,chunk",
+    [
+        (16 << 10, 16 << 10),  # one segment
+        (64 << 20, 64 << 20),  # the data engine's landed chunk
+        ((3 << 20) + (48 << 10), 1 << 20),  # short last chunk of whole segments
+        (7 << 20, 48 << 10),  # 3-segment chunks
+        (33 << 20, 4 << 20),
+    ],
+)
+def test_crc32c_mfma_matches_host(gpu, n, chunk):
+    """The matrix-core CRC (impl=2) against the host CRC32C and the LDS-table kernel."""
+    assert gpu.crc32c_mfma_applies(n, chunk)
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 11 + n)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
+    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=2) == want
+    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=1) == want
+    # a single flipped bit anywhere changes exactly its chunk's CRC
+    for pos in (0, n // 2 + 5, n - 1):
+        t[pos] ^= 0x10
+        got = gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=2)
+        t[pos] ^= 0x10
+        assert [i for i, (a, b) in enumerate(zip(got, want)) if a != b] == [pos // chunk]
+
+
+def test_crc32c_mfma_refuses_partial_segments(gpu):
+    assert not gpu.crc32c_mfma_applies((1 << 20) + 16, 1 << 20)
+    t = _dev_bytes((1 << 20) + 16)
+    with pytest.raises(RuntimeError):
+        gpu.crc32c_chunks(t.data_ptr(), t.numel(), 1 << 20, impl=2)
+
+
 def test_crc32c_batch_matches_host(gpu):
     # the chunks one P2P group lands: independent buffers of mixed sizes
     sizes = [64 << 20, (1 << 20) + 16, 100 << 10, 16, 48 << 10, 3 * (16 << 10) + 32]
