@@ -56,7 +56,7 @@ $(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h) Makefile
 
 tools: bin/diskspeed bin/h2dbench bin/contention
 
-bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(BUILD)/kernels/fill.hip.o $(BUILD)/core/crc32c.o
+bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(BUILD)/kernels/crc32c_mfma.hip.o $(BUILD)/kernels/fill.hip.o $(BUILD)/core/crc32c.o
 	@mkdir -p bin
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
 
@@ -80,6 +80,6 @@ $(BUILD)/tests/core_selftest_asan: $(SAN_SRC)
 	$(CXX) -O1 -g -std=c++17 -Icsrc -fsanitize=address,undefined -fno-omit-frame-pointer -I/opt/rocm/include -o $@ $(SAN_SRC) -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx -lpthread
 
 clean:
-	rm -rf $(BUILD) $(PKG)/_core*.so bin/diskspeed bin/h2dbench bin/contention bin/contention
+	rm -rf $(BUILD) $(PKG)/_core*.so bin/diskspeed bin/h2dbench bin/contention
 
 .PHONY: all tools sanitize clean

@@ -61,6 +61,8 @@ def parse_args(argv=None):
                    help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
     p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
+    p.add_argument("--lanes", type=int, default=0,
+                   help="comm lanes (RCCL communicator + stream each); 0 = world-1 (one ring distance per lane)")
     p.add_argument("--preset", default="", choices=["", "llama70b", "llama405b-fp8"],
                    help="llama70b = 80 x 1 GiB (default); llama405b-fp8 = 126 x 3 GiB with --pack fp8")
     args = p.parse_args(argv)
@@ -94,6 +96,11 @@ def main(argv=None) -> int:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     rank = int(os.environ.get("RANK", "0"))
+    # stdout carries exactly one JSON line (rank 0): everything else any library
+    # prints there (RCCL's version banner, gloo) goes to stderr.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     sys.path.insert(0, HERE)
     from distributed_llm_dissemination_amd.utils.launch import rank_device, shared_gpu
 
@@ -149,6 +156,7 @@ def main(argv=None) -> int:
         rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
     log(f"setup done in {time.time() - t_setup:.1f}s")
 
+    engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
     policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1), owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective")
 
@@ -171,6 +179,7 @@ def main(argv=None) -> int:
     for i in range(args.warmup):
         dt, res = step(False)
         log(f"warmup {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s)")
+    links0 = rt.link_stats()
     times = []
     last = None
     for i in range(args.steps):
@@ -178,10 +187,18 @@ def main(argv=None) -> int:
         times.append(dt)
         log(f"step {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s) ttd={last.time_to_deliver_s * 1e3:.1f} ms")
     total = sum(times)
+    # Per directed link over the timed steps: bytes this rank sent to each peer,
+    # and the device time of the P2P groups that involved the peer.
+    links1 = rt.link_stats()
+    mine = {p: (links1["sent"].get(p, 0) - links0["sent"].get(p, 0),
+                links1["busy_ms"].get(p, 0.0) - links0["busy_ms"].get(p, 0.0)) for p in links1["sent"]}
+    all_links = [mine]
     if world > 1:
         t = torch.tensor([total], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         total = float(t.item())
+        all_links = [None] * world
+        dist.all_gather_object(all_links, mine)
     ms_per_step = total / max(1, args.steps) * 1e3
     value = total_bytes * args.steps / total / 1e9
     if rank == 0:
@@ -213,7 +230,8 @@ def main(argv=None) -> int:
                 "leader_time_to_deliver_s": round(last.time_to_deliver_s, 6) if last else None,
                 "engine": ("rccl-socket, all ranks on one GPU (schedule rehearsal; bandwidth not meaningful)"
                            if world > 1 and shared_gpu() else
-                           "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)"),
+                           "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)") + (
+                               f", {engine_note}" if engine_note else ""),
                 "pack": args.pack,
             },
         }
@@ -225,9 +243,21 @@ def main(argv=None) -> int:
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
         if world > 1:
-            out["config"]["link_bytes_rank0_cumulative"] = {k: {str(p): b for p, b in v.items()}
-                                                            for k, v in rt.link_bytes().items()}
-        print(json.dumps(out), flush=True)
+            es = rt.engine.stats()
+            out["config"]["comm_lanes"] = es.lanes
+            out["config"]["comm_init_ms_rank0"] = round(es.comm_init_ms, 1)
+        if world > 1:
+            # GB/s per directed link: averaged over the timed wall time, and while
+            # its P2P groups were on the device (busy).
+            wall, busy = {}, {}
+            for src, per in enumerate(all_links):
+                for p, (b, ms) in sorted(per.items()):
+                    wall[f"{src}->{p}"] = round(b / total / 1e9, 2)
+                    busy[f"{src}->{p}"] = round(b / (ms / 1e3) / 1e9, 2) if ms > 0 else None
+            out["config"]["per_link_GBps"] = wall
+            out["config"]["per_link_busy_GBps"] = busy
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
     rt.close()
     if world > 1:
         dist.destroy_process_group()

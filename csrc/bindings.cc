@@ -262,7 +262,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("inject_die_after_groups", &PlannedConfig::inject_die_after_groups)
       .def_readwrite("nccl_min_ctas", &PlannedConfig::nccl_min_ctas)
       .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas)
-      .def_readwrite("nccl_register", &PlannedConfig::nccl_register);
+      .def_readwrite("nccl_register", &PlannedConfig::nccl_register)
+      .def_readwrite("lanes", &PlannedConfig::lanes)
+      .def_readwrite("link_rate", &PlannedConfig::link_rate);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)
@@ -281,7 +283,12 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("land_us_hist", &PlannedStats::land_us_hist)
       .def_readonly("suspects", &PlannedStats::suspects)
       .def_readonly("shrinks", &PlannedStats::shrinks)
-      .def_readonly("aborted_pieces", &PlannedStats::aborted_pieces);
+      .def_readonly("aborted_pieces", &PlannedStats::aborted_pieces)
+      .def_readonly("peer_busy_ms", &PlannedStats::peer_busy_ms)
+      .def_readonly("lane_busy_ms", &PlannedStats::lane_busy_ms)
+      .def_readonly("lanes", &PlannedStats::lanes)
+      .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)
+      .def_readonly("paced", &PlannedStats::paced);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
         return reinterpret_cast<uint64_t>(e.provision(l, n));
@@ -307,8 +314,16 @@ PYBIND11_MODULE(_core, m) {
   // Simulated fabric (CPU): host "device" memory, RCCL P2P matching semantics between
   // in-process ranks that share `comm_key`.
   m.def("sim_engine", [](const PlannedConfig& cfg, const std::string& comm_key) {
-    return std::make_shared<PlannedEngine>(cfg, make_sim_backend(comm_key, cfg.rank, cfg.world));
+    return std::make_shared<PlannedEngine>(cfg, make_sim_backend(comm_key, cfg.rank, cfg.world, resolve_lanes(cfg)));
   });
+  py::class_<SimTiming>(m, "SimTiming")
+      .def(py::init<>())
+      .def_readwrite("link_bps", &SimTiming::link_bps)
+      .def_readwrite("link", &SimTiming::link)
+      .def_readwrite("stage_bps", &SimTiming::stage_bps)
+      .def_readwrite("copy_bytes", &SimTiming::copy_bytes)
+      .def_readwrite("p2p_rounds", &SimTiming::p2p_rounds);
+  m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
   m.def("sim_read", [](uint64_t ptr, int64_t n) {
     return py::bytes(reinterpret_cast<const char*>(ptr), size_t(n));

@@ -203,6 +203,7 @@ Json encode_payload(const Message& m) {
         Json c = Json::array();
         for (uint32_t x : j.crc) c.push_back(Json(unsigned(x)));
         e.push_back(c);
+        if (j.rate) e.push_back(Json(j.rate));
         arr.push_back(e);
       }
       p["Jobs"] = arr;
@@ -332,6 +333,7 @@ MessagePtr decode_envelope(const Json& env) {
           j.total = a.at(6).as_i64();
           j.chunk_bytes = a.at(7).as_i64();
           for (auto& x : a.at(8).as_array()) j.crc.push_back(uint32_t(x.as_u64()));
+          if (a.size() > 9) j.rate = a.at(9).as_i64();
           m->jobs.push_back(std::move(j));
         }
       }

@@ -55,6 +55,7 @@ struct XferJob {
   int64_t offset = 0, size = 0, total = 0;
   int64_t chunk_bytes = 0;     // CRC chunk grid of the layer
   std::vector<uint32_t> crc;   // expected CRC32C of the grid chunks the range covers
+  int64_t rate = 0;            // pacing of the sends (B/s, 0 = unlimited; mode 3: size/T)
 };
 
 // Per-layer integrity manifest announced by holders: CRC32C per chunk.

@@ -1,19 +1,26 @@
 // Device backend of the planned data engine. The engine (csrc/engine/
 // planned_engine.cc) owns scheduling: piece order, group formation, chunk
-// states, verification bookkeeping. A backend owns the device: memory, the
-// three ordered queues (comm, copy, verify) and completion events.
+// states, verification bookkeeping, pacing. A backend owns the device: memory,
+// the ordered queues and completion events:
+//   * `lanes()` comm lanes - each an independent communicator + in-order queue
+//     for grouped P2P (a directed pair a->b always uses lane_of(a, b), on both
+//     ends), so a peer that is slow to post stalls only its own lane;
+//   * copy queue(s) for host->device staging;
+//   * a verify queue for CRC checks.
 //
 //  * HipBackend (csrc/gpu/hip_backend.cc): HBM via hipMalloc, RCCL grouped
-//    P2P on one world communicator over xGMI, hipMemcpyAsync H2D staging,
-//    the gfx950 CRC32C kernel, hipEvents.
+//    P2P over xGMI (one communicator + stream per lane), hipMemcpyAsync H2D
+//    staging, the gfx950 CRC32C kernel, hipEvents.
 //  * SimBackend (csrc/engine/sim_backend.cc): host memory, worker threads as
 //    in-order queues, and an in-process "fabric" that matches sends and recvs
-//    between ranks FIFO per (src, dst) exactly like RCCL P2P (a group blocks its
-//    queue until every op in it is matched). Used to test multi-rank schedules,
-//    including deadlock freedom, without GPUs.
+//    between ranks FIFO per (lane, src, dst) exactly like RCCL P2P (a group
+//    blocks its lane until every op in it is matched). Optional timing model:
+//    per directed link bandwidth and per-rank staging bandwidth. Used to test
+//    multi-rank schedules, deadlock freedom and timing without GPUs.
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -47,11 +54,21 @@ class Backend {
   // copy queue: host -> device copy of `n_src` bytes of bf16, then fp8-pack them
   // into dst in the packed chunk layout of core/fp8.h
   virtual Ev stage_pack(uint8_t* dst, const uint8_t* src_host, int64_t n_src, int block) = 0;
-  // comm queue: wait for `waits`, then one grouped set of P2P sends/recvs
-  virtual Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) = 0;
-  // comm queue (fault injection): overwrite 4 bytes at p behind everything
-  // queued so far, e.g. a chunk a group just received
-  virtual Ev corrupt(uint8_t* p) = 0;
+  // Independent comm lanes (>= 1).
+  virtual int lanes() const { return 1; }
+  // comm lane `lane`: wait for `waits`, then one grouped set of P2P sends/recvs
+  virtual Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits, int lane = 0) = 0;
+  // An event that fires once everything queued so far on comm lane `lane` is done.
+  virtual Ev mark(int lane) = 0;
+  // Device time (ms) of a completed group, from the moment its lane reached it
+  // (waits satisfied) to its end; < 0 if unknown.
+  virtual double group_ms(Ev e) {
+    (void)e;
+    return -1;
+  }
+  // comm lane (fault injection): overwrite 4 bytes at p behind everything
+  // queued so far on the lane, e.g. a chunk a group just received
+  virtual Ev corrupt(uint8_t* p, int lane = 0) = 0;
   // verify queue: after `after`, CRC32C of [p, p+n) into result slot `slot`
   // (n == 0: just an ordering marker on the verify queue)
   virtual Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) = 0;
@@ -88,14 +105,39 @@ class Backend {
   }
   virtual void sync_all() = 0;
   virtual void destroy(bool abort) = 0;
+  virtual double comm_init_ms() const { return 0; }
 };
+
+// The lane a directed pair (src -> dst) uses, identical on both ends: by the
+// ring distance dst - src, so with world - 1 lanes every lane of a rank talks
+// to exactly one send peer and one recv peer.
+inline int lane_of(int src, int dst, int world, int lanes) {
+  if (lanes <= 1 || world <= 1) return 0;
+  const int delta = ((dst - src) % world + world) % world;  // 1 .. world-1
+  return (delta - 1) % lanes;
+}
 
 struct SimFabricStats {
   int64_t matched = 0, bytes = 0;
 };
 
+// Timing model of the simulated fabric (all rates in bytes/s, 0 = instant).
+struct SimTiming {
+  double link_bps = 0;                            // every directed rank->rank link
+  std::map<std::pair<int, int>, double> link;     // per directed link override
+  double stage_bps = 0;                           // host->device staging per rank (PCIe)
+  bool copy_bytes = true;                         // false: move no payload bytes (timing-only runs)
+  // Model RCCL's P2P schedule with few channels: a group's ops run in rounds of
+  // one ring distance each (send to rank+d, recv from rank-d), round d+1 only
+  // after round d completed. Irregular groups can then deadlock where
+  // independent ops would not; one-distance groups (lanes = world-1) cannot.
+  bool p2p_rounds = false;
+};
+
 // In-process simulated fabric: ranks of one "communicator" share `comm_key`.
-std::unique_ptr<Backend> make_sim_backend(const std::string& comm_key, int rank, int world);
+std::unique_ptr<Backend> make_sim_backend(const std::string& comm_key, int rank, int world, int lanes = 1);
 SimFabricStats sim_fabric_stats(const std::string& comm_key);
+// Set the timing model of a fabric (before its ranks start moving bytes).
+void sim_set_timing(const std::string& comm_key, const SimTiming& t);
 
 }  // namespace dissem

@@ -2,16 +2,23 @@
 //
 // Deadlock freedom. Every piece p has a global key k(p) = (batch, piece index
 // within its job, job sequence number), known identically to its sender and
-// receiver. Each rank posts its pieces in increasing key order, cut into
-// consecutive groups on one ordered comm queue. A group finishes once every one
-// of its pieces is posted by the partner rank. Suppose ranks were stuck: take
-// the unfinished piece with the smallest key k*. Its partner has already
-// finished every piece it owns with a key < k* (minimality), so it reaches k*
-// in its own order and posts it, and so does the owner of k* - a contradiction.
-// Hence no deadlock for any interleaving of batches, including mode 2's dynamic
-// dispatch. Host-side waits precede a post only for data that no earlier piece
-// can produce, which the leader never schedules. tests/test_planned_sim.py
-// checks this on the simulated fabric for every mode at up to 8 ranks.
+// receiver, and a lane (lane_of the directed pair, also identical on both
+// ends). Each rank posts the pieces of each lane in increasing key order, cut
+// into consecutive groups on that lane's ordered queue; a P2P op inside a group
+// progresses as soon as its partner's op is posted. Suppose ranks were stuck:
+// take the unfinished piece with the smallest key k*, on lane x. On both of its
+// ranks every earlier group of lane x holds only keys < k* (consecutive
+// segments of the key order), which finished by minimality, so both ranks
+// reach and post the group holding k* - unless a host- or device-side wait
+// holds it back. Waits point only at smaller keys: a send waits for staging
+// (no comm dependency) or, when it forwards a chunk this rank receives on
+// another lane, for a mark recorded after that recv's group; a group that
+// receives a chunk with a queued forward is closed right after that recv, so
+// the mark covers keys <= the recv's key < the forward's key. Those finished
+// too, so k* completes - a contradiction. Hence no deadlock for any
+// interleaving of batches (mode 2's dynamic dispatch included) and any number
+// of lanes. tests/test_planned_sim.py checks this on the simulated fabric for
+// every mode at up to 8 ranks, with one lane and with world-1 lanes.
 #include "engine/planned_engine.h"
 
 #include <fcntl.h>
@@ -57,6 +64,12 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
     throw std::runtime_error("unknown pack format " + std::to_string(cfg_.pack));
   }
   inject_rng_.seed(cfg_.inject_seed * 0x9E3779B97F4A7C15ull + uint64_t(cfg_.rank));
+  lanes_ = std::max(1, backend_->lanes());
+  ops_.resize(size_t(lanes_));
+  inflight_.resize(size_t(lanes_));
+  stats_.lanes = lanes_;
+  stats_.lane_busy_ms.assign(size_t(lanes_), 0.0);
+  stats_.comm_init_ms = backend_->comm_init_ms();
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
   self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
   th_ = std::thread([this] { run(); });
@@ -250,6 +263,72 @@ uint32_t PlannedEngine::crc_slot() {
   return s;
 }
 
+void PlannedEngine::ev_drop(Ev e) {
+  if (!e) return;
+  auto it = evref_.find(e);
+  if (it == evref_.end() || --it->second <= 0) {
+    if (it != evref_.end()) evref_.erase(it);
+    backend_->release(e);
+  }
+}
+
+void PlannedEngine::set_chunk_ev(Layer& L, int64_t c, Ev e) {
+  Ev& slot = L.ev[size_t(c)];
+  if (slot == e) return;
+  ev_hold(e);
+  ev_drop(slot);
+  slot = e;
+}
+
+// Non-blocking token bucket with one chunk of burst: a chunk may go when the
+// bucket is full enough for it; tokens may go negative, so the long-run rate
+// is exactly `rate`.
+bool PlannedEngine::pace_ready(uint64_t key, int64_t rate, int64_t n) {
+  if (rate <= 0) return true;
+  const auto now = std::chrono::steady_clock::now();
+  Pace& p = pace_[key];
+  if (p.rate <= 0) {
+    p.rate = double(rate);
+    p.burst = double(n);
+    p.tokens = double(n);
+    p.last = now;
+  }
+  p.rate = double(rate);
+  p.burst = std::max(p.burst, double(n));
+  p.tokens = std::min(p.burst, p.tokens + std::chrono::duration<double>(now - p.last).count() * p.rate);
+  p.last = now;
+  return p.tokens >= double(n) - 0.5;
+}
+
+void PlannedEngine::pace_take(uint64_t key, int64_t rate, int64_t n) {
+  if (rate > 0) pace_[key].tokens -= double(n);
+}
+
+namespace {
+constexpr uint64_t kPaceJob = 1ull << 62, kPacePeer = 2ull << 62, kPaceTier = 3ull << 62;
+}
+
+bool PlannedEngine::stage_paced(Layer& L, LayerID id, int64_t c) {
+  if (L.stage_rate < 0) {
+    LayerSrc src;
+    L.stage_rate = 0;
+    if (node_ && node_->store().get(id, &src)) {
+      L.stage_rate = std::max<int64_t>(0, src.meta.limit_rate);
+      L.stage_tier = int(src.meta.source_type);
+    }
+  }
+  if (L.stage_rate <= 0) return false;
+  const uint64_t key = kPaceTier | uint64_t(L.stage_tier);
+  const int64_t n = src_len(L, c);
+  if (!pace_ready(key, L.stage_rate, n)) {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.paced++;
+    return true;
+  }
+  pace_take(key, L.stage_rate, n);
+  return false;
+}
+
 void PlannedEngine::landed(const Piece& p) {
   if (!node_) return;
   auto m = std::make_shared<Message>();
@@ -271,10 +350,7 @@ void PlannedEngine::nack(const Piece& p, Layer& L, uint32_t got) {
     std::lock_guard<std::mutex> lk(stats_mu_);
     stats_.verify_failures++;
   }
-  if (L.ev[c]) {
-    backend_->release(L.ev[c]);
-    L.ev[c] = 0;
-  }
+  set_chunk_ev(L, int64_t(c), 0);
   if (++L.fails[c] > cfg_.max_retries || !node_) {
     fail(std::string(buf) + (node_ ? " (retries exhausted)" : ""));
     return;
@@ -414,7 +490,7 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   Ev e = cfg_.pack == 1 && !L.src_packed ? backend_->stage_pack(L.dev + off, src, slen, cfg_.pack_block)
                                          : backend_->stage(L.dev + off, src, len);
   L.st[size_t(c)] = 1;
-  L.ev[size_t(c)] = e;
+  set_chunk_ev(L, c, e);
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
   p.src_node = self_node_;
   Verify v;
@@ -457,6 +533,12 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   // becomes a source only once the node re-tags it Inmem (Node::on_layer).
   const bool client = have && src.meta.location == Location::Client;
   if (L.host || !L.path.empty() || (have && !client && (src.host || !src.path.empty()))) {
+    if (s == 0 && stage_paced(L, id, c)) {
+      // The source tier's LimitRate holds this chunk back; promotions retry from
+      // local_wait_, sends from their lane's next issue pass.
+      if (want_landed) local_wait_.push_back({id, c});
+      return 0;
+    }
     stage_chunk(L, id, c);
     return L.st[size_t(c)] == 1 ? 1 : 0;
   }
@@ -515,6 +597,9 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       Piece p{kind, j.seq, pidx, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
       p.src_node = j.src;
       p.bcast = bcast;
+      p.rate = j.rate;
+      // Collectives run on lane 0 (every rank's copy of the lane-0 communicator).
+      p.lane = bcast || kind == Kind::Local ? 0 : lane_for(peer, kind == Kind::Send);
       const int64_t ci = c - first_chunk;
       if (p.full && ci < int64_t(j.crc.size())) {
         p.has_crc = true;
@@ -535,20 +620,41 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       if (ensure_chunk(L, p.layer, p.chunk, true) < 0) fail("no source to load layer " + std::to_string(p.layer));
       continue;
     }
-    ops_.push_back(p);
+    if (p.kind == Kind::Send && !p.bcast) fwd_pending_[{p.layer, p.chunk}]++;
+    ops_[size_t(p.lane)].push_back(p);
   }
 }
 
 bool PlannedEngine::issue_some() {
-  bool progress = false;
   if (recovering_ || dead_) return false;
-  while (!ops_.empty() && int(groups_inflight_.size()) < cfg_.max_inflight_groups && !failed_) {
+  // Local promotions held back by tier pacing.
+  for (size_t n = local_wait_.size(); n > 0 && !failed_; --n) {
+    auto lc = local_wait_.front();
+    local_wait_.pop_front();
+    Layer& L = layers_[lc.first];
+    if (L.st[size_t(lc.second)] == 0 && ensure_chunk(L, lc.first, lc.second, true) < 0)
+      fail("no source to load layer " + std::to_string(lc.first));
+  }
+  // Lanes are independent: a lane whose next piece cannot go yet (data not
+  // staged or received, pacing, in-flight cap) does not hold the others.
+  bool progress = false;
+  for (int lane = 0; lane < lanes_; ++lane) progress |= issue_lane(lane);
+  return progress;
+}
+
+bool PlannedEngine::issue_lane(int lane) {
+  bool progress = false;
+  auto& q = ops_[size_t(lane)];
+  auto& infl = inflight_[size_t(lane)];
+  const auto now = std::chrono::steady_clock::now();
+  while (!q.empty() && int(infl.size()) < cfg_.max_inflight_groups && !failed_) {
     std::vector<Piece> group;
     std::map<int, int> nsend, nrecv;
     std::set<std::pair<LayerID, int64_t>> recv_chunks;
+    std::vector<std::pair<uint64_t, std::pair<int64_t, int64_t>>> takes;  // pacing: key, (rate, bytes)
     size_t take = 0;
-    for (; take < ops_.size(); ++take) {
-      Piece& p = ops_[take];
+    for (; take < q.size(); ++take) {
+      Piece& p = q[take];
       if (p.bcast) {
         // A collective runs in a group of its own (every rank reaches it at the
         // same key, so the ordering argument above covers it too).
@@ -562,17 +668,43 @@ bool PlannedEngine::issue_some() {
         if (nsend[p.peer] >= cfg_.group_peers) break;
         if (recv_chunks.count({p.layer, p.chunk})) break;  // forward only after its recv is posted
         Layer& L = layer(p.layer);
-        if (ensure_chunk(L, p.layer, p.chunk, false) <= 0) break;  // still reading from disk (or no source yet)
+        if (ensure_chunk(L, p.layer, p.chunk, false) <= 0) break;  // not staged / received yet (or paced)
+        // Pacing: the job's rate (mode 3) and the link cap to this peer.
+        int64_t link = 0;
+        if (!cfg_.link_rate.empty()) {
+          auto it = cfg_.link_rate.find(cfg_.rank_nodes[size_t(p.peer)]);
+          if (it != cfg_.link_rate.end()) link = it->second;
+        }
+        const uint64_t kj = kPaceJob | p.seq, kp = kPacePeer | uint64_t(p.peer);
+        if (!pace_ready(kj, p.rate, p.len) || !pace_ready(kp, link, p.len)) {
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          stats_.paced++;
+          break;
+        }
+        takes.push_back({kj, {p.rate, p.len}});
+        takes.push_back({kp, {link, p.len}});
         nsend[p.peer]++;
-      } else {
-        if (nrecv[p.peer] >= cfg_.group_peers) break;
-        nrecv[p.peer]++;
-        recv_chunks.insert({p.layer, p.chunk});
+        group.push_back(p);
+        continue;
       }
+      if (nrecv[p.peer] >= cfg_.group_peers) break;
+      nrecv[p.peer]++;
+      recv_chunks.insert({p.layer, p.chunk});
       group.push_back(p);
+      // Lanes: a chunk that this rank forwards on (possibly) another lane is
+      // released to that send by a mark behind this group - close the group
+      // here so the mark never waits on pieces with larger keys.
+      if (lanes_ > 1) {
+        auto f = fwd_pending_.find({p.layer, p.chunk});
+        if (f != fwd_pending_.end() && f->second > 0) {
+          ++take;
+          break;
+        }
+      }
     }
     if (group.empty()) break;
-    ops_.erase(ops_.begin(), ops_.begin() + int64_t(take));
+    for (auto& t : takes) pace_take(t.first, t.second.first, t.second.second);
+    q.erase(q.begin(), q.begin() + int64_t(take));
     trace::Scoped tr(group.front().bcast ? "dissem.bcast" : "dissem.p2p_group");
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<Ev> waits;
@@ -586,17 +718,21 @@ bool PlannedEngine::issue_some() {
           Ev e = L.ev[size_t(p.chunk)];
           if (std::find(waits.begin(), waits.end(), e) == waits.end()) waits.push_back(e);
         }
+        if (!p.bcast) {
+          auto f = fwd_pending_.find({p.layer, p.chunk});
+          if (f != fwd_pending_.end() && --f->second <= 0) fwd_pending_.erase(f);
+        }
         sent += p.len;
       } else {
         recvd += p.len;
       }
       xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len, p.bcast});
     }
-    Ev g = backend_->group(xops, waits);
-    Inflight inf{g, std::chrono::steady_clock::now(), {}};
+    Ev g = backend_->group(xops, waits, lane);
+    Inflight inf{g, now, {}};
     for (auto& p : group)
       if (std::find(inf.peers.begin(), inf.peers.end(), p.peer) == inf.peers.end()) inf.peers.push_back(p.peer);
-    groups_inflight_.push_back(std::move(inf));
+    infl.push_back(std::move(inf));
     // Fault injection: damage some received chunks behind the group, before their check.
     Ev landed_ev = g;
     int64_t injected = 0;
@@ -604,21 +740,28 @@ bool PlannedEngine::issue_some() {
       std::uniform_real_distribution<double> u(0.0, 1.0);
       for (auto& p : group) {
         if (p.kind != Kind::Recv || p.len < 4 || u(inject_rng_) >= cfg_.inject_corrupt) continue;
-        Ev c = backend_->corrupt(layers_[p.layer].dev + p.off);
+        Ev c = backend_->corrupt(layers_[p.layer].dev + p.off, lane);
         if (landed_ev != g) backend_->release(landed_ev);
         landed_ev = c;
         injected++;
       }
     }
-    // Receivers: chunks are valid behind `g` on the comm queue; check them on the verify queue.
+    // Receivers: chunks are valid behind `g` on this lane; check them on the
+    // verify queue. With one lane a later send of the chunk is ordered behind
+    // `g` on the same queue; with several, it waits for a mark on this lane.
     Verify v;
-    Ev last = 0;
+    Ev last = 0, mark = 0;
     std::vector<Backend::CrcReq> checks;
     for (auto& p : group) {
       if (p.kind != Kind::Recv) continue;
       Layer& L = layers_[p.layer];
       L.st[size_t(p.chunk)] = 1;
-      L.ev[size_t(p.chunk)] = 0;  // pending on the comm queue itself: later sends are ordered behind it
+      if (lanes_ > 1 && !p.bcast) {
+        if (!mark) mark = backend_->mark(lane);
+        set_chunk_ev(L, p.chunk, mark);
+      } else {
+        set_chunk_ev(L, p.chunk, 0);  // pending on the comm queue itself: later sends are ordered behind it
+      }
       uint32_t slot = ~0u;
       if (cfg_.verify && p.has_crc && p.full) {
         slot = crc_slot();
@@ -665,9 +808,10 @@ void PlannedEngine::die() {
 
 std::vector<int> PlannedEngine::inflight_peers() const {
   std::vector<int> peers;
-  for (auto& g : groups_inflight_)
-    for (int p : g.peers)
-      if (std::find(peers.begin(), peers.end(), p) == peers.end()) peers.push_back(p);
+  for (auto& lane : inflight_)
+    for (auto& g : lane)
+      for (int p : g.peers)
+        if (std::find(peers.begin(), peers.end(), p) == peers.end()) peers.push_back(p);
   return peers;
 }
 
@@ -703,24 +847,28 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
   }
   std::sort(dead.begin(), dead.end());
   const int old_rank = cfg_.rank;
-  int64_t aborted = int64_t(ops_.size());
+  int64_t aborted = 0;
+  for (auto& q : ops_) aborted += int64_t(q.size());
   const int new_rank = backend_->shrink(dead, generation, comm_id);
-  for (auto& g : groups_inflight_) backend_->release(g.ev);
-  groups_inflight_.clear();
+  for (auto& lane : inflight_) {
+    for (auto& g : lane) backend_->release(g.ev);
+    lane.clear();
+  }
   for (auto& v : verifies_) {
     aborted += int64_t(v.pieces.size());
     backend_->release(v.ev);
     if (v.bounce) bounce_free_.push_back(v.bounce);
   }
   verifies_.clear();
-  ops_.clear();
+  for (auto& q : ops_) q.clear();
   restage_.clear();
+  local_wait_.clear();
+  fwd_pending_.clear();
   for (auto& kv : layers_) {
     Layer& L = kv.second;
     for (size_t c = 0; c < L.st.size(); ++c) {
       if (L.st[c] == 1 || L.st[c] == 4) L.st[c] = 0;  // pending or bad: gone (st 3: its disk read still lands)
-      if (L.ev[c]) backend_->release(L.ev[c]);
-      L.ev[c] = 0;
+      set_chunk_ev(L, int64_t(c), 0);
       L.fails[c] = 0;
     }
   }
@@ -753,44 +901,53 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
 }
 
 void PlannedEngine::poll() {
-  while (!groups_inflight_.empty()) {
-    Inflight& head = groups_inflight_.front();
-    int r = backend_->query(head.ev);
-    if (r == 0) {
-      // Watchdog: a group whose partner never posts (dead or hung peer) would
-      // block the comm queue forever. Report its peers to the leader (which
-      // probes them and shrinks the communicator around a dead one); fail if
-      // nothing resolves it.
-      const auto now = std::chrono::steady_clock::now();
-      double age = std::chrono::duration<double>(now - head.t0).count();
-      if (node_ && cfg_.suspect_s > 0 && age > cfg_.suspect_s &&
-          now - last_suspect_ > std::chrono::duration<double>(std::max(cfg_.suspect_s, 1.0))) {
-        // Not (yet) a failure: if the peers are alive the group may still
-        // complete. Name every in-flight peer: the group at the head may be
-        // waiting on a live rank that itself waits on the dead one.
-        last_suspect_ = now;
-        suspect(inflight_peers(), "P2P group pending for " + std::to_string(int(age)) + " s", false);
+  const auto now = std::chrono::steady_clock::now();
+  for (int lane = 0; lane < lanes_; ++lane) {
+    auto& infl = inflight_[size_t(lane)];
+    while (!infl.empty()) {
+      Inflight& head = infl.front();
+      int r = backend_->query(head.ev);
+      if (r == 0) {
+        // Watchdog: a group whose partner never posts (dead or hung peer) would
+        // block its lane forever. Report the in-flight peers to the leader
+        // (which probes them and shrinks the communicator around a dead one);
+        // fail if nothing resolves it.
+        double age = std::chrono::duration<double>(now - head.t0).count();
+        if (node_ && cfg_.suspect_s > 0 && age > cfg_.suspect_s &&
+            now - last_suspect_ > std::chrono::duration<double>(std::max(cfg_.suspect_s, 1.0))) {
+          // Not (yet) a failure: if the peers are alive the group may still
+          // complete. Name every in-flight peer: the group at the head may be
+          // waiting on a live rank that itself waits on the dead one.
+          last_suspect_ = now;
+          suspect(inflight_peers(), "P2P group pending for " + std::to_string(int(age)) + " s", false);
+        }
+        if (cfg_.group_timeout_s > 0 && age > cfg_.group_timeout_s)
+          fail("P2P group pending for " + std::to_string(int(age)) + " s: a peer rank is dead or stuck");
+        break;
       }
-      if (cfg_.group_timeout_s > 0 && age > cfg_.group_timeout_s)
-        fail("P2P group pending for " + std::to_string(int(age)) + " s: a peer rank is dead or stuck");
-      break;
-    }
-    if (r < 0) {
-      if (!node_) {
-        fail("P2P group failed: " + backend_->async_error());
-        return;
+      if (r < 0) {
+        if (!node_) {
+          fail("P2P group failed: " + backend_->async_error());
+          return;
+        }
+        // The communicator is broken (e.g. a peer's connection died): stop and
+        // let the leader decide; its Shrink resets everything in flight.
+        if (!recovering_) suspect(inflight_peers(), "P2P group failed: " + backend_->async_error(), true);
+        break;
       }
-      // The communicator is broken (e.g. a peer's connection died): stop and
-      // let the leader decide; its Shrink resets everything in flight.
-      if (!recovering_) suspect(inflight_peers(), "P2P group failed: " + backend_->async_error(), true);
-      break;
+      const double ms = backend_->group_ms(head.ev);
+      {
+        std::lock_guard<std::mutex> lk(stats_mu_);
+        stats_.group_us_hist[log2_bucket(head.t0)]++;
+        if (ms >= 0) {
+          stats_.lane_busy_ms[size_t(lane)] += ms;
+          for (int p : head.peers) stats_.peer_busy_ms[p] += ms;
+        }
+      }
+      backend_->release(head.ev);
+      infl.pop_front();
     }
-    {
-      std::lock_guard<std::mutex> lk(stats_mu_);
-      stats_.group_us_hist[log2_bucket(head.t0)]++;
-    }
-    backend_->release(head.ev);
-    groups_inflight_.pop_front();
+    if (failed_ || recovering_) break;
   }
   for (auto it = verifies_.begin(); it != verifies_.end();) {
     int r = backend_->query(it->ev);
@@ -823,10 +980,7 @@ void PlannedEngine::poll() {
         stats_.unverified_pieces++;
       }
       if (p.full) L.st[size_t(p.chunk)] = 2;
-      if (L.ev[size_t(p.chunk)]) {
-        backend_->release(L.ev[size_t(p.chunk)]);
-        L.ev[size_t(p.chunk)] = 0;
-      }
+      set_chunk_ev(L, p.chunk, 0);
       if (p.kind == Kind::Recv) {
         landed(p);
       } else if (L.want[size_t(p.chunk)]) {
@@ -880,15 +1034,18 @@ void PlannedEngine::take_requests(bool block) {
           Layer& L = kv.second;
           for (size_t c = 0; c < L.st.size(); ++c) {
             L.st[c] = L.seeded ? 2 : 0;
-            if (L.ev[c]) backend_->release(L.ev[c]);
-            L.ev[c] = 0;
+            set_chunk_ev(L, int64_t(c), 0);
             L.want[c] = 0;
             L.fails[c] = 0;
           }
           L.host = nullptr;  // re-read the source from the next session's store
           L.client_requested = false;
+          L.stage_rate = -1;
           if (cfg_.poison && !L.seeded && L.dev) backend_->zero_sync(L.dev, L.size);
         }
+        pace_.clear();
+        local_wait_.clear();
+        fwd_pending_.clear();
         std::lock_guard<std::mutex> lk(req_mu_);
         resets_done_++;
         idle_cv_.notify_all();
@@ -912,9 +1069,10 @@ void PlannedEngine::run() {
       if (stop_req_) break;
       if (failed_) {
         // Drop queued work; in-flight P2P ops are aborted at shutdown.
-        ops_.clear();
+        for (auto& q : ops_) q.clear();
+        for (auto& q : inflight_) q.clear();
         verifies_.clear();
-        groups_inflight_.clear();
+        local_wait_.clear();
         std::lock_guard<std::mutex> lk(req_mu_);
         busy_ = false;
         idle_cv_.notify_all();

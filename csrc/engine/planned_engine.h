@@ -7,10 +7,19 @@
 //    with global sequence numbers and sends each rank its share.
 //  * Each job is cut into pieces on a fixed chunk grid. A rank orders its pieces
 //    by the key (batch, piece index within the job, sequence number) - a key its
-//    partner computes identically - and issues them as groups of at most one
-//    send and one recv per peer: each group is an all-to-all round that keeps
-//    every xGMI link of the GPU busy. Because every rank posts its pieces in one
-//    global key order, the schedule cannot deadlock (planned_engine.cc).
+//    partner computes identically. Pieces go to comm lanes (lane_of: by ring
+//    distance of the pair, the same lane on both ends; one RCCL communicator +
+//    HIP stream per lane) and each lane issues its pieces in key order as
+//    groups of at most one send and one recv per peer. With one lane a group is
+//    an all-to-all round over every xGMI link; with world-1 lanes every link
+//    pair progresses on its own, so a slow or late peer stalls only its lane.
+//    Because every lane posts in one global key order, the schedule cannot
+//    deadlock (planned_engine.cc).
+//  * Pacing (reference writeWithLimit, transport.go:407-424): sends of a job
+//    with a rate (mode 3: size/T, node.go:1281) and sends to a rate-capped
+//    peer (--inject slow-link) are issued no faster than their token bucket
+//    allows; staging from a tier with a LimitRate (Sources) is paced per tier
+//    (node.go:1615-1624).
 //  * Host-tier sources are staged chunk by chunk on the copy queue; a send
 //    waits on its chunk's staging event, so PCIe staging and xGMI transfer
 //    pipeline per chunk (the reference's pipe/tee, at chunk grain).
@@ -18,6 +27,7 @@
 //    holder's announced manifest before the node acks it.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -42,7 +52,15 @@ struct PlannedConfig {
   int64_t chunk_bytes = 64ll << 20;
   bool verify = true;
   bool poison = true;              // zero non-seeded slots between sessions
-  int max_inflight_groups = 64;
+  int max_inflight_groups = 64;   // per lane
+  // Independent comm lanes (communicator + stream each). 0 = auto: world - 1
+  // (at most 7), so each lane carries one send and one recv peer of one ring
+  // distance. That is also what keeps irregular groups (mode 2, relays) safe on
+  // RCCL: with few channels RCCL runs a group's ops in rounds of one distance
+  // each, so a multi-distance group can wait on itself across ranks
+  // (SimTiming::p2p_rounds reproduces it; tests/test_planned_sim.py).
+  int lanes = 0;
+  std::map<NodeID, int64_t> link_rate;  // cap this rank's sends to a node (B/s; slow-link injection)
   int group_peers = 1;             // ops per peer and direction per group
   int disk_readers = 4;            // NVMe reader threads (O_DIRECT pread into pinned bounce buffers)
   int disk_ring = 8;               // pinned bounce buffers of chunk_bytes each
@@ -77,6 +95,15 @@ struct PlannedConfig {
   bool nccl_register = false;  // register every HBM slot with the communicator (ncclCommRegister)
 };
 
+// Comm lanes an engine of this config runs: cfg.lanes clamped to [1, world-1];
+// 0 = auto = world - 1, at most 7 (one send + one recv peer per lane on an
+// 8-GPU node).
+inline int resolve_lanes(const PlannedConfig& c) {
+  const int most = std::max(1, c.world - 1);
+  if (c.lanes <= 0) return std::min(most, 7);
+  return std::min(c.lanes, most);
+}
+
 struct PlannedStats {
   int64_t bytes_sent = 0, bytes_recv = 0, bytes_staged = 0, bytes_verified = 0;
   int64_t groups = 0, pieces = 0, verify_failures = 0, unverified_pieces = 0;
@@ -84,6 +111,12 @@ struct PlannedStats {
   int64_t suspects = 0, shrinks = 0, aborted_pieces = 0;  // elastic recovery
   double issue_ms = 0;  // host time spent enqueueing groups
   std::map<int, int64_t> peer_sent, peer_recv;  // bytes per peer rank (per-link counters)
+  // device time of completed groups involving each peer / on each lane (ms)
+  std::map<int, double> peer_busy_ms;
+  std::vector<double> lane_busy_ms;
+  int lanes = 1;
+  double comm_init_ms = 0;
+  int64_t paced = 0;  // issue attempts a token bucket deferred
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
   std::vector<int64_t> group_us_hist = std::vector<int64_t>(32, 0);  // P2P group issue -> complete
   std::vector<int64_t> land_us_hist = std::vector<int64_t>(32, 0);   // chunk issue -> landed + verified
@@ -139,6 +172,8 @@ class PlannedEngine : public DataEngine {
     uint32_t crc = 0;
     NodeID src_node = 0;
     bool bcast = false;  // collective from rank `peer` (root: Send with peer == own rank; others: Recv)
+    int lane = 0;
+    int64_t rate = 0;    // job pacing (B/s, 0 = unlimited)
   };
   struct Layer {
     int64_t size = 0;
@@ -150,6 +185,8 @@ class PlannedEngine : public DataEngine {
     int64_t path_off = 0;
     bool src_packed = false;         // the source already holds the packed image (persisted layers)
     bool client_requested = false;   // ClientReq sent for this session
+    int64_t stage_rate = -1;         // source tier LimitRate (-1: not looked up yet)
+    int stage_tier = 0;
     // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk,
     // 4 failed its CRC and awaits the leader's re-send (still forwardable: a
     // later receiver detects it and NACKs too)
@@ -181,20 +218,41 @@ class PlannedEngine : public DataEngine {
     uint64_t generation = 0;   // Shrink
     std::string comm_id;       // Shrink: the survivors' new communicator id
   };
-  struct Inflight {  // a P2P group on the comm queue
+  struct Inflight {  // a P2P group on a comm lane
     Ev ev;
     std::chrono::steady_clock::time_point t0;
     std::vector<int> peers;  // partner ranks
+  };
+  struct Pace {  // token bucket, one chunk of burst (TokenBucket semantics, non-blocking)
+    double rate = 0, tokens = 0, burst = 0;
+    std::chrono::steady_clock::time_point last{};
   };
 
   void run();
   void take_requests(bool block);
   void add_batch(std::vector<XferJob>& jobs);
   bool issue_some();
+  bool issue_lane(int lane);
   void poll();
   bool idle() const {
-    return ops_.empty() && verifies_.empty() && groups_inflight_.empty() && disk_inflight_ == 0 && disk_wait_.empty();
+    for (auto& q : ops_)
+      if (!q.empty()) return false;
+    for (auto& q : inflight_)
+      if (!q.empty()) return false;
+    return verifies_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty();
   }
+  int lane_for(int peer, bool send) const {
+    return send ? lane_of(cfg_.rank, peer, cfg_.world, lanes_) : lane_of(peer, cfg_.rank, cfg_.world, lanes_);
+  }
+  // Events shared by several chunks (a lane mark after a recv group): refcounted.
+  void ev_hold(Ev e) {
+    if (e) evref_[e]++;
+  }
+  void ev_drop(Ev e);
+  void set_chunk_ev(Layer& L, int64_t c, Ev e);
+  bool pace_ready(uint64_t key, int64_t rate, int64_t n);
+  void pace_take(uint64_t key, int64_t rate, int64_t n);
+  bool stage_paced(Layer& L, LayerID id, int64_t c);  // true: the tier's bucket defers this chunk
   // Elastic recovery: stop issuing, tell the leader which peers look dead, and
   // wait for its Shrink (or fail after group_timeout_s).
   // broken: the communicator failed (stop issuing) rather than merely stalled.
@@ -233,10 +291,15 @@ class PlannedEngine : public DataEngine {
 
   // issue-thread state
   std::map<LayerID, Layer> layers_;
-  std::deque<Piece> ops_;
+  int lanes_ = 1;
+  std::vector<std::deque<Piece>> ops_;          // per lane, key order
+  std::vector<std::deque<Inflight>> inflight_;  // per lane
   std::deque<Verify> verifies_;
   std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
-  std::deque<Inflight> groups_inflight_;
+  std::deque<std::pair<LayerID, int64_t>> local_wait_;  // local promotions deferred by tier pacing
+  std::map<std::pair<LayerID, int64_t>, int> fwd_pending_;  // queued sends per chunk (relay cuts)
+  std::map<Ev, int> evref_;
+  std::map<uint64_t, Pace> pace_;
   bool recovering_ = false;  // issue thread: waiting for the leader's Shrink
   std::chrono::steady_clock::time_point recover_since_, last_suspect_;
   int64_t groups_issued_ = 0;

@@ -2,10 +2,17 @@
 // in-process fabric with RCCL point-to-point matching semantics.
 //
 // The fabric matches the i-th send from rank A to rank B with the i-th recv on
-// B from A (FIFO per directed pair, like NCCL/RCCL P2P). A group occupies its
-// rank's comm queue until every op in it has been matched and copied, so a
-// schedule that could deadlock on GPUs deadlocks here too; a bounded wait turns
-// that into a reported failure instead of a hang.
+// B from A (FIFO per lane and directed pair, like NCCL/RCCL P2P on one
+// communicator). A group occupies its rank's lane queue until every op in it
+// has been matched and copied, so a schedule that could deadlock on GPUs
+// deadlocks here too; a bounded wait turns that into a reported failure
+// instead of a hang.
+//
+// Timing model (SimTiming): a matched transfer occupies its directed link for
+// len / link_bps after the link's previous transfer (full duplex, links
+// independent); a staging copy occupies the rank's copy queue for
+// len / stage_bps. With copy_bytes = false no payload moves (timing-only runs
+// of full-size schedules in little memory).
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -16,6 +23,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <tuple>
 
 #include "core/crc32c.h"
 #include "core/fp8.h"
@@ -29,30 +37,42 @@ namespace {
 
 struct SimEvent {
   std::atomic<int> state{0};  // 0 pending, 1 done, -1 failed
+  double ms = -1;             // groups: time on the lane from dependencies met to completion
 };
+
+using Clock = std::chrono::steady_clock;
 
 struct Posted {
   uint8_t* ptr;
   int64_t len;
   bool done = false;
   bool bad = false;
+  Clock::time_point done_at{};  // timing model: when the link finishes this transfer
 };
 
 struct Fabric {
   std::mutex mu;
   std::condition_variable cv;
   bool aborted = false;  // a survivor shrank this communicator: every wait fails now
-  std::map<std::pair<int, int>, std::pair<std::deque<Posted*>, std::deque<Posted*>>> ch;  // (src,dst) -> sends, recvs
+  // (lane, src, dst) -> sends, recvs
+  std::map<std::tuple<int, int, int>, std::pair<std::deque<Posted*>, std::deque<Posted*>>> ch;
   SimFabricStats stats;
+  SimTiming timing;
+  std::map<std::pair<int, int>, Clock::time_point> link_free;  // timing model: directed link busy until
 
-  void post(int src, int dst, bool send, Posted* op) {
+  double link_rate(int src, int dst) const {
+    auto it = timing.link.find({src, dst});
+    return it != timing.link.end() ? it->second : timing.link_bps;
+  }
+
+  void post(int lane, int src, int dst, bool send, Posted* op) {
     std::lock_guard<std::mutex> lk(mu);
     if (aborted) {  // like an aborted communicator: nothing moves any more
       op->done = op->bad = true;
       cv.notify_all();
       return;
     }
-    auto& c = ch[{src, dst}];
+    auto& c = ch[{lane, src, dst}];
     (send ? c.first : c.second).push_back(op);
     while (!c.first.empty() && !c.second.empty()) {
       Posted* s = c.first.front();
@@ -62,9 +82,16 @@ struct Fabric {
       if (s->len != r->len) {
         s->bad = r->bad = true;
       } else {
-        memcpy(r->ptr, s->ptr, size_t(s->len));
+        if (timing.copy_bytes) memcpy(r->ptr, s->ptr, size_t(s->len));
         stats.matched++;
         stats.bytes += s->len;
+        const double bps = link_rate(src, dst);
+        if (bps > 0) {
+          auto& free_at = link_free[{src, dst}];
+          const auto start = std::max(Clock::now(), free_at);
+          free_at = start + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(s->len) / bps));
+          s->done_at = r->done_at = free_at;
+        }
       }
       s->done = r->done = true;
     }
@@ -92,8 +119,13 @@ struct Fabric {
       return true;
     });
     if (!ok || aborted) return false;
-    for (auto& o : ops)
+    Clock::time_point until{};
+    for (auto& o : ops) {
       if (o->bad) return false;
+      until = std::max(until, o->done_at);
+    }
+    lk.unlock();
+    std::this_thread::sleep_until(until);  // the links are still moving these bytes
     return true;
   }
 };
@@ -101,10 +133,13 @@ struct Fabric {
 std::mutex g_fab_mu;
 std::map<std::string, std::shared_ptr<Fabric>> g_fabrics;
 
-std::shared_ptr<Fabric> fabric(const std::string& key) {
+std::shared_ptr<Fabric> fabric(const std::string& key, const Fabric* inherit = nullptr) {
   std::lock_guard<std::mutex> lk(g_fab_mu);
   auto& f = g_fabrics[key];
-  if (!f) f = std::make_shared<Fabric>();
+  if (!f) {
+    f = std::make_shared<Fabric>();
+    if (inherit) f->timing = inherit->timing;  // a shrunk communicator runs over the same links
+  }
   return f;
 }
 
@@ -171,10 +206,13 @@ bool wait_event(const std::shared_ptr<SimEvent>& e, double timeout_s) {
 
 class SimBackend : public Backend {
  public:
-  SimBackend(const std::string& key, int rank, int world)
-      : key_(key), rank_(rank), world_(world), fab_(fabric(key)), results_(kCrcSlots, 0) {}
+  SimBackend(const std::string& key, int rank, int world, int lanes)
+      : key_(key), rank_(rank), world_(world), fab_(fabric(key)), results_(kCrcSlots, 0) {
+    for (int l = 0; l < std::max(1, lanes); ++l) comm_.push_back(std::make_unique<Queue>());
+  }
   ~SimBackend() override { destroy(false); }
   std::string name() const override { return "sim"; }
+  int lanes() const override { return int(comm_.size()); }
 
   uint8_t* alloc(int64_t n) override {
     auto* p = new uint8_t[size_t(std::max<int64_t>(n, 1))]();
@@ -192,10 +230,21 @@ class SimBackend : public Backend {
     memset(p, 0, size_t(n));
   }
 
+  // Staging occupies the copy queue for n / stage_bps (timing model).
+  void stage_delay(Clock::time_point t0, int64_t n) {
+    const double bps = fab_->timing.stage_bps;
+    if (bps > 0)
+      std::this_thread::sleep_until(
+          t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(n) / bps)));
+  }
+
   Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {
     auto [id, ev] = make_event();
+    const bool copy = fab_->timing.copy_bytes;
     copy_.push([=] {
-      memcpy(dst, src, size_t(n));
+      const auto t0 = Clock::now();
+      if (copy) memcpy(dst, src, size_t(n));
+      stage_delay(t0, n);
       ev->state = 1;
     });
     return id;
@@ -203,17 +252,20 @@ class SimBackend : public Backend {
 
   Ev stage_pack(uint8_t* dst, const uint8_t* src, int64_t n_src, int block) override {
     auto [id, ev] = make_event();
+    const bool copy = fab_->timing.copy_bytes;
     copy_.push([=] {
+      const auto t0 = Clock::now();
       const int64_t n = n_src / 2;
-      fp8::pack_host(reinterpret_cast<const uint16_t*>(src), n, dst, reinterpret_cast<float*>(dst + n), block);
+      if (copy) fp8::pack_host(reinterpret_cast<const uint16_t*>(src), n, dst, reinterpret_cast<float*>(dst + n), block);
+      stage_delay(t0, n_src);
       ev->state = 1;
     });
     return id;
   }
 
-  Ev corrupt(uint8_t* p) override {
+  Ev corrupt(uint8_t* p, int lane) override {
     auto [id, ev] = make_event();
-    comm_.push([=] {
+    comm_.at(size_t(lane))->push([=] {
       const uint32_t pat = 0xA5A5A5A5u;
       memcpy(p, &pat, 4);
       ev->state = 1;
@@ -221,21 +273,44 @@ class SimBackend : public Backend {
     return id;
   }
 
-  Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) override {
+  Ev mark(int lane) override {
+    auto [id, ev] = make_event();
+    comm_.at(size_t(lane))->push([=] { ev->state = 1; });
+    return id;
+  }
+
+  Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits, int lane) override {
     auto [id, ev] = make_event();
     std::vector<std::shared_ptr<SimEvent>> deps;
     for (Ev w : waits) deps.push_back(lookup(w));
     int rank = rank_;
     auto fab = fab_;
-    comm_.push([=] {
+    comm_.at(size_t(lane))->push([=] {
       for (auto& d : deps)
         if (!d || !wait_event(d, kTimeout)) {
           set_error("group dependency failed");
           ev->state = -1;
           return;
         }
+      const auto t0 = Clock::now();
       std::vector<std::unique_ptr<Posted>> posted;
-      for (auto& o : ops) {
+      // Optional RCCL round model: ops grouped by ring distance, each round
+      // waits for the previous one (collectives stay in round 0).
+      std::vector<std::vector<XOp>> rounds(1);
+      if (fab->timing.p2p_rounds) {
+        rounds.assign(size_t(std::max(1, world_)), {});
+        for (auto& o : ops) {
+          int d = 0;
+          if (!o.bcast) d = o.send ? (o.peer - rank + world_) % world_ : (rank - o.peer + world_) % world_;
+          rounds[size_t(d)].push_back(o);
+        }
+      } else {
+        rounds[0] = ops;
+      }
+      for (auto& round : rounds) {
+      if (round.empty()) continue;
+      const size_t first = posted.size();
+      for (auto& o : round) {
         if (o.bcast) {
           // Broadcast = the root sends to every other rank, each of which receives
           // from the root: same matching (and deadlock) semantics as a collective.
@@ -243,11 +318,11 @@ class SimBackend : public Backend {
             for (int r = 0; r < world_; ++r)
               if (r != rank) {
                 posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
-                fab->post(rank, r, true, posted.back().get());
+                fab->post(lane, rank, r, true, posted.back().get());
               }
           } else {
             posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
-            fab->post(o.peer, rank, false, posted.back().get());
+            fab->post(lane, o.peer, rank, false, posted.back().get());
           }
           continue;
         }
@@ -257,8 +332,17 @@ class SimBackend : public Backend {
           return;
         }
         posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
-        if (o.send) fab->post(rank, o.peer, true, posted.back().get());
-        else fab->post(o.peer, rank, false, posted.back().get());
+        if (o.send) fab->post(lane, rank, o.peer, true, posted.back().get());
+        else fab->post(lane, o.peer, rank, false, posted.back().get());
+      }
+      if (rounds.size() > 1) {
+        std::vector<std::unique_ptr<Posted>> cur;
+        for (size_t i = first; i < posted.size(); ++i) cur.push_back(std::move(posted[i]));
+        posted.resize(first);
+        const bool ok = fab->wait_all(cur, kTimeout);
+        for (auto& c : cur) posted.push_back(std::move(c));
+        if (!ok) break;
+      }
       }
       if (!fab->wait_all(posted, kTimeout)) {
         fab->cancel(posted);
@@ -266,9 +350,15 @@ class SimBackend : public Backend {
         ev->state = -1;
         return;
       }
+      ev->ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
       ev->state = 1;
     });
     return id;
+  }
+
+  double group_ms(Ev e) override {
+    auto ev = lookup(e);
+    return ev && ev->state.load() > 0 ? ev->ms : -1;
   }
 
   Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
@@ -315,17 +405,17 @@ class SimBackend : public Backend {
       std::lock_guard<std::mutex> lk(ev_mu_);
       error_.clear();
     }
-    fab_ = fabric(key_ + "/shrink" + std::to_string(generation));
+    fab_ = fabric(key_ + "/shrink" + std::to_string(generation), fab_.get());
     return rank_;
   }
 
   void sync_all() override {
-    comm_.drain();
+    for (auto& q : comm_) q->drain();
     copy_.drain();
     verify_.drain();
   }
   void destroy(bool) override {
-    comm_.stop();
+    for (auto& q : comm_) q->stop();
     copy_.stop();
     verify_.stop();
   }
@@ -358,13 +448,21 @@ class SimBackend : public Backend {
   std::map<Ev, std::shared_ptr<SimEvent>> events_;
   Ev next_ = 0;
   std::string error_;
-  Queue comm_, copy_, verify_;
+  std::vector<std::unique_ptr<Queue>> comm_;
+  Queue copy_, verify_;
 };
 
 }  // namespace
 
-std::unique_ptr<Backend> make_sim_backend(const std::string& comm_key, int rank, int world) {
-  return std::make_unique<SimBackend>(comm_key, rank, world);
+std::unique_ptr<Backend> make_sim_backend(const std::string& comm_key, int rank, int world, int lanes) {
+  return std::make_unique<SimBackend>(comm_key, rank, world, lanes);
+}
+
+void sim_set_timing(const std::string& comm_key, const SimTiming& t) {
+  auto f = fabric(comm_key);
+  std::lock_guard<std::mutex> lk(f->mu);
+  f->timing = t;
+  f->link_free.clear();
 }
 
 SimFabricStats sim_fabric_stats(const std::string& comm_key) {

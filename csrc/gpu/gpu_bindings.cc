@@ -328,6 +328,7 @@ void register_gpu_bindings(PyObject* module) {
     hc.nccl_min_ctas = cfg.nccl_min_ctas;
     hc.nccl_max_ctas = cfg.nccl_max_ctas;
     hc.nccl_register = cfg.nccl_register;
+    hc.lanes = resolve_lanes(cfg);
     py::gil_scoped_release nogil;
     return std::make_shared<PlannedEngine>(cfg, make_hip_backend(hc));
   }, py::arg("cfg"), py::arg("device") = 0, py::arg("nccl_uid") = py::bytes(""));

@@ -34,7 +34,23 @@ class HipBackend : public Backend {
  public:
   explicit HipBackend(const HipBackendConfig& cfg) : cfg_(cfg) {
     HIP_OK(hipSetDevice(cfg_.device));
-    HIP_OK(hipStreamCreateWithFlags(&comm_, hipStreamNonBlocking));
+    const int lanes = std::max(1, cfg_.lanes);
+    // One in-order stream per comm lane. With several lanes each must sit on a
+    // hardware queue of its own: two lanes sharing one would run their RCCL
+    // kernels in submission order, and a kernel waiting for a peer would hold
+    // back the other lane's kernel that peer may itself be waiting for. A
+    // CU-masked stream gets a dedicated queue, so extra lanes are created with
+    // a mask of every CU (profiles/: Queue_Id per lane).
+    for (int l = 0; l < lanes; ++l) {
+      hipStream_t s = nullptr;
+      if (lanes > 1) {
+        s = create_stream_reserving(cfg_.device, 0, /*dedicated=*/true);
+      } else {
+        HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      }
+      comm_.push_back(s);
+    }
+    nccl_.assign(size_t(lanes), nullptr);
     copy_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     // Two SDMA copy queues in alternation keep the PCIe link busier across copy
     // boundaries (h2dbench: 56.8 -> 57.4 GB/s; bench 56.0 -> 56.9 GB/s). With
@@ -64,19 +80,27 @@ class HipBackend : public Backend {
   void init_comm(const ncclUniqueId& id_in) {
     ncclUniqueId id = id_in;
     auto t0 = log::now_us();
-    if (cfg_.nccl_min_ctas > 0 || cfg_.nccl_max_ctas > 0) {
-      ncclConfig_t nc = NCCL_CONFIG_INITIALIZER;
-      if (cfg_.nccl_min_ctas > 0) nc.minCTAs = cfg_.nccl_min_ctas;
-      if (cfg_.nccl_max_ctas > 0) nc.maxCTAs = cfg_.nccl_max_ctas;
-      NCCL_OK(ncclCommInitRankConfig(&nccl_, cfg_.world, id, cfg_.rank, &nc));
-    } else {
-      NCCL_OK(ncclCommInitRank(&nccl_, cfg_.world, id, cfg_.rank));
+    ncclConfig_t nc = NCCL_CONFIG_INITIALIZER;
+    if (cfg_.nccl_min_ctas > 0) nc.minCTAs = cfg_.nccl_min_ctas;
+    if (cfg_.nccl_max_ctas > 0) nc.maxCTAs = cfg_.nccl_max_ctas;
+    NCCL_OK(ncclCommInitRankConfig(&nccl_[0], cfg_.world, id, cfg_.rank, &nc));
+    // Further lanes: independent communicators over the same ranks (own
+    // channels and connections; collective split, same order on every rank).
+    for (size_t l = 1; l < nccl_.size(); ++l) {
+      ncclConfig_t lc = NCCL_CONFIG_INITIALIZER;
+      if (cfg_.nccl_min_ctas > 0) lc.minCTAs = cfg_.nccl_min_ctas;
+      if (cfg_.nccl_max_ctas > 0) lc.maxCTAs = cfg_.nccl_max_ctas;
+      lc.splitShare = 0;
+      NCCL_OK(ncclCommSplit(nccl_[0], 0, cfg_.rank, &nccl_[l], &lc));
     }
-    log::info(cfg_.rank).i("world", cfg_.world).f("init_ms", double(log::now_us() - t0) / 1e3)
-        .msg("rccl communicator ready");
+    init_ms_ = double(log::now_us() - t0) / 1e3;
+    log::info(cfg_.rank).i("world", cfg_.world).i("lanes", int64_t(nccl_.size())).f("init_ms", init_ms_)
+        .msg("rccl communicators ready");
   }
   ~HipBackend() override { destroy(false); }
   std::string name() const override { return "rccl"; }
+  int lanes() const override { return int(comm_.size()); }
+  double comm_init_ms() const override { return init_ms_; }
 
   void init_thread() override { HIP_OK(hipSetDevice(cfg_.device)); }
 
@@ -84,19 +108,24 @@ class HipBackend : public Backend {
   // is also registered with the communicator (ncclCommRegister), which lets
   // RCCL use the user buffer directly where its transport supports it.
   void register_slot(uint8_t* p, int64_t n) {
-    if (!cfg_.nccl_register || !nccl_) return;
-    void* h = nullptr;
-    ncclResult_t r = ncclCommRegister(nccl_, p, size_t(n), &h);
-    if (r != ncclSuccess) {
-      log::warn(cfg_.rank).s("error", ncclGetErrorString(r)).msg("ncclCommRegister failed; slot stays unregistered");
-      return;
+    if (!cfg_.nccl_register || !nccl_[0]) return;
+    std::vector<void*> hs;
+    for (auto c : nccl_) {
+      void* h = nullptr;
+      ncclResult_t r = ncclCommRegister(c, p, size_t(n), &h);
+      if (r != ncclSuccess) {
+        log::warn(cfg_.rank).s("error", ncclGetErrorString(r)).msg("ncclCommRegister failed; slot stays unregistered");
+        h = nullptr;
+      }
+      hs.push_back(h);
     }
-    regs_[p] = {n, h};
+    regs_[p] = {n, hs};
   }
   void deregister_slot(uint8_t* p) {
     auto it = regs_.find(p);
     if (it == regs_.end()) return;
-    if (nccl_ && it->second.second) (void)ncclCommDeregister(nccl_, it->second.second);
+    for (size_t l = 0; l < it->second.second.size() && l < nccl_.size(); ++l)
+      if (nccl_[l] && it->second.second[l]) (void)ncclCommDeregister(nccl_[l], it->second.second[l]);
     regs_.erase(it);
   }
 
@@ -118,8 +147,8 @@ class HipBackend : public Backend {
   }
   void free_host(uint8_t* p) override { (void)hipHostFree(p); }
   void zero_sync(uint8_t* p, int64_t n) override {
-    HIP_OK(hipMemsetAsync(p, 0, size_t(n), comm_));
-    HIP_OK(hipStreamSynchronize(comm_));
+    HIP_OK(hipMemsetAsync(p, 0, size_t(n), comm_[0]));
+    HIP_OK(hipStreamSynchronize(comm_[0]));
   }
 
   Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {
@@ -149,24 +178,44 @@ class HipBackend : public Backend {
     return record(s);
   }
 
-  Ev corrupt(uint8_t* p) override {
-    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), 0xA5A5A5A5u, 1, comm_));
-    return record(comm_);
+  Ev corrupt(uint8_t* p, int lane) override {
+    hipStream_t s = comm_.at(size_t(lane));
+    HIP_OK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p), 0xA5A5A5A5u, 1, s));
+    return record(s);
   }
 
-  Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits) override {
-    for (Ev w : waits) HIP_OK(hipStreamWaitEvent(comm_, ev(w), 0));
+  Ev mark(int lane) override { return record(comm_.at(size_t(lane))); }
+
+  Ev group(const std::vector<XOp>& ops, const std::vector<Ev>& waits, int lane) override {
+    hipStream_t s = comm_.at(size_t(lane));
+    ncclComm_t c = nccl_.at(size_t(lane));
+    for (Ev w : waits) HIP_OK(hipStreamWaitEvent(s, ev(w), 0));
+    // Timed group: a timing event where the lane reaches the group (its waits
+    // met) and one at its end; group_ms() reads the device time between them.
+    hipEvent_t start = timed();
+    HIP_OK(hipEventRecord(start, s));
     if (!ops.empty()) {
-      if (!nccl_) throw std::runtime_error("P2P group on a single-rank engine");
+      if (!c) throw std::runtime_error("P2P group on a single-rank engine");
       NCCL_OK(ncclGroupStart());
       for (auto& o : ops) {
-        if (o.bcast) NCCL_OK(ncclBroadcast(o.ptr, o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
-        else if (o.send) NCCL_OK(ncclSend(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
-        else NCCL_OK(ncclRecv(o.ptr, size_t(o.len), ncclUint8, o.peer, nccl_, comm_));
+        if (o.bcast) NCCL_OK(ncclBroadcast(o.ptr, o.ptr, size_t(o.len), ncclUint8, o.peer, c, s));
+        else if (o.send) NCCL_OK(ncclSend(o.ptr, size_t(o.len), ncclUint8, o.peer, c, s));
+        else NCCL_OK(ncclRecv(o.ptr, size_t(o.len), ncclUint8, o.peer, c, s));
       }
       NCCL_OK(ncclGroupEnd());
     }
-    return record(comm_);
+    hipEvent_t end = timed();
+    HIP_OK(hipEventRecord(end, s));
+    const Ev e = reinterpret_cast<Ev>(end);
+    starts_[e] = start;
+    return e;
+  }
+
+  double group_ms(Ev e) override {
+    auto it = starts_.find(e);
+    if (it == starts_.end()) return -1;
+    float ms = 0;
+    return hipEventElapsedTime(&ms, it->second, ev(e)) == hipSuccess ? double(ms) : -1;
   }
 
   Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
@@ -205,7 +254,15 @@ class HipBackend : public Backend {
     return -1;
   }
   void release(Ev e) override {
-    if (e) pool_.push_back(ev(e));
+    if (!e) return;
+    auto it = starts_.find(e);
+    if (it != starts_.end()) {
+      timed_pool_.push_back(it->second);
+      timed_pool_.push_back(ev(e));
+      starts_.erase(it);
+      return;
+    }
+    pool_.push_back(ev(e));
   }
   uint32_t crc_result(uint32_t slot) override { return __atomic_load_n(&crc_host_[slot], __ATOMIC_ACQUIRE); }
   std::string async_error() override {
@@ -213,24 +270,28 @@ class HipBackend : public Backend {
       std::lock_guard<std::mutex> lk(mu_);
       if (!err_.empty()) return err_;
     }
-    if (!nccl_) return "";
-    ncclResult_t ar = ncclSuccess;
-    if (ncclCommGetAsyncError(nccl_, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress)
-      return ncclGetErrorString(ar);
+    for (auto c : nccl_) {
+      if (!c) continue;
+      ncclResult_t ar = ncclSuccess;
+      if (ncclCommGetAsyncError(c, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress)
+        return ncclGetErrorString(ar);
+    }
     return "";
   }
   std::string new_comm_id() override { return nccl_unique_id(); }
 
   int shrink(const std::vector<int>& dead, uint64_t, const std::string& comm_id) override {
-    if (!nccl_) throw std::runtime_error("shrink without a communicator");
+    if (!nccl_[0]) throw std::runtime_error("shrink without a communicator");
     if (comm_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("shrink: bad communicator id");
     // Abort first: P2P groups waiting on the dead rank are terminated, so the
-    // comm stream drains. (ncclCommShrink would keep the bootstrap, but the RCCL
+    // comm streams drain. (ncclCommShrink would keep the bootstrap, but the RCCL
     // PyTorch loads into the process predates it; abort + re-init of the
     // survivors works with any RCCL.)
-    (void)ncclCommAbort(nccl_);
-    nccl_ = nullptr;
-    std::vector<std::pair<uint8_t*, int64_t>> regd;  // re-register with the new communicator
+    for (auto& c : nccl_) {
+      if (c) (void)ncclCommAbort(c);
+      c = nullptr;
+    }
+    std::vector<std::pair<uint8_t*, int64_t>> regd;  // re-register with the new communicators
     for (auto& kv : regs_) regd.push_back({kv.first, kv.second.first});
     regs_.clear();
     int new_rank = 0;
@@ -242,8 +303,10 @@ class HipBackend : public Backend {
       std::lock_guard<std::mutex> lk(mu_);
       err_.clear();
     }
-    // Bounded drain of the three queues (an aborted kernel must have exited).
-    for (hipStream_t s : {comm_, copy_, verify_, copy2_}) {
+    // Bounded drain of every queue (an aborted kernel must have exited).
+    std::vector<hipStream_t> all(comm_);
+    for (hipStream_t s : {copy_, verify_, copy2_}) all.push_back(s);
+    for (hipStream_t s : all) {
       if (!s) continue;
       hipEvent_t e;
       HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -268,7 +331,7 @@ class HipBackend : public Backend {
 
   void sync_all() override {
     (void)hipSetDevice(cfg_.device);
-    (void)hipStreamSynchronize(comm_);
+    for (hipStream_t s : comm_) (void)hipStreamSynchronize(s);
     (void)hipStreamSynchronize(copy_);
     if (copy2_) (void)hipStreamSynchronize(copy2_);
     (void)hipStreamSynchronize(verify_);
@@ -278,18 +341,26 @@ class HipBackend : public Backend {
     destroyed_ = true;
     (void)hipSetDevice(cfg_.device);
     if (!abort) sync_all();
-    if (nccl_) {
-      if (abort) ncclCommAbort(nccl_);
-      else ncclCommDestroy(nccl_);
-      nccl_ = nullptr;
+    for (size_t l = nccl_.size(); l-- > 0;) {  // split lanes before the parent
+      if (!nccl_[l]) continue;
+      if (abort) ncclCommAbort(nccl_[l]);
+      else ncclCommDestroy(nccl_[l]);
+      nccl_[l] = nullptr;
     }
     for (auto e : pool_) (void)hipEventDestroy(e);
     pool_.clear();
+    for (auto& kv : starts_) {
+      timed_pool_.push_back(kv.second);
+      timed_pool_.push_back(ev(kv.first));
+    }
+    starts_.clear();
+    for (auto e : timed_pool_) (void)hipEventDestroy(e);
+    timed_pool_.clear();
     if (ws_) (void)hipFree(ws_);
     for (void* p : scratch_)
       if (p) (void)hipFree(p);
     if (crc_host_) (void)hipHostFree(crc_host_);
-    (void)hipStreamDestroy(comm_);
+    for (hipStream_t s : comm_) (void)hipStreamDestroy(s);
     (void)hipStreamDestroy(copy_);
     if (copy2_) (void)hipStreamDestroy(copy2_);
     (void)hipStreamDestroy(verify_);
@@ -308,13 +379,27 @@ class HipBackend : public Backend {
     HIP_OK(hipEventRecord(e, s));
     return reinterpret_cast<Ev>(e);
   }
+  hipEvent_t timed() {
+    hipEvent_t e;
+    if (!timed_pool_.empty()) {
+      e = timed_pool_.back();
+      timed_pool_.pop_back();
+    } else {
+      HIP_OK(hipEventCreate(&e));
+    }
+    return e;
+  }
 
   HipBackendConfig cfg_;
-  hipStream_t comm_ = nullptr, copy_ = nullptr, verify_ = nullptr;
-  hipStream_t copy2_ = nullptr;  // second H2D queue (single-rank runs)
-  std::map<uint8_t*, std::pair<int64_t, void*>> regs_;  // registered slots: size, handle
+  std::vector<hipStream_t> comm_;  // one per lane
+  hipStream_t copy_ = nullptr, verify_ = nullptr;
+  hipStream_t copy2_ = nullptr;  // second H2D queue
+  std::map<uint8_t*, std::pair<int64_t, std::vector<void*>>> regs_;  // registered slots: size, handle per lane
   bool flip_ = false;
-  ncclComm_t nccl_ = nullptr;
+  std::vector<ncclComm_t> nccl_;  // one per lane (lane 0: the world communicator, others split from it)
+  double init_ms_ = 0;
+  std::map<Ev, hipEvent_t> starts_;  // timed group end -> its start event
+  std::vector<hipEvent_t> timed_pool_;
   void* ws_ = nullptr;
   void* scratch_[2] = {nullptr, nullptr};  // bf16 landing chunk for stage_pack, per copy queue
   int64_t scratch_bytes_[2] = {0, 0};
@@ -330,12 +415,13 @@ class HipBackend : public Backend {
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg) { return std::make_unique<HipBackend>(cfg); }
 
-hipStream_t create_stream_reserving(int device, int reserve) {
+hipStream_t create_stream_reserving(int device, int reserve, bool dedicated) {
   HIP_OK(hipSetDevice(device));
   hipStream_t s = nullptr;
   int cus = 0;
   HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  if (reserve <= 0 || reserve >= cus) {
+  if (reserve >= cus) reserve = 0;
+  if (reserve <= 0 && !dedicated) {
     HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     return s;
   }

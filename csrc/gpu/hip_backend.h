@@ -1,9 +1,14 @@
 // MI355X backend of the planned engine: HBM slots (hipMalloc), RCCL grouped
-// point-to-point on one world communicator over xGMI (comm stream),
-// hipMemcpyAsync staging from pinned host memory (copy stream), and the gfx950
-// CRC32C kernel (verify stream). Three streams + PyTorch's default stream fit
-// the 4 hardware queues a process gets by default (GPU_MAX_HW_QUEUES), so no
-// two of our queues serialize behind each other.
+// point-to-point over xGMI on one communicator + stream per comm lane,
+// hipMemcpyAsync staging from pinned host memory (one or two copy streams), and
+// the gfx950 CRC32C kernel (verify stream).
+//
+// Hardware queues: HIP maps ordinary streams onto a pool of GPU_MAX_HW_QUEUES
+// (4) queues, so streams can share one; a CU-masked stream always gets a queue
+// of its own. The copy and verify streams are CU-masked whenever RCCL runs
+// (reserve_cus > 0, the default with peers) and extra comm lanes are created
+// with a mask of every CU, so no RCCL kernel waiting for a peer can hold back
+// a copy, a check or another lane (queue ids: profiles/r2_queues/).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -29,12 +34,14 @@ struct HipBackendConfig {
   // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
   int reserve_cus = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
+  int lanes = 1;                               // comm lanes (communicator + stream each)
   bool nccl_register = false;                  // ncclCommRegister every layer slot
 };
 
 // A non-default stream whose kernels may use every CU but the last `reserve`
-// (reserve <= 0: a plain non-blocking stream).
-hipStream_t create_stream_reserving(int device, int reserve);
+// (reserve <= 0: a plain non-blocking stream, or with `dedicated` a stream
+// masked to every CU, which gets a hardware queue of its own).
+hipStream_t create_stream_reserving(int device, int reserve, bool dedicated = false);
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg);
 std::shared_ptr<HostBuffer> alloc_pinned(int64_t size);

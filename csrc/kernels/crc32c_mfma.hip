@@ -22,9 +22,11 @@
 // of its chunk and the 32 lanes are XOR-reduced. The fold kernel is shared
 // with crc32c.hip (seg_out holds chunk-end-shifted segment CRCs).
 //
-// Used for chunk lengths that are whole 16 KiB segments (every chunk the data
-// engine checks: 64 MiB, packed fp8 chunks); other shapes take the nibble-table
-// kernel.
+// Applies to chunk lengths that are whole 16 KiB segments. Reached through
+// crc32c_chunks_impl (kMfma, or kAuto with DISSEM_CRC_IMPL=mfma): that is the
+// staging-side verify (HipBackend::crc) and the ops/bindings entry points.
+// The batched landing verify (crc32c_batch) and the fused fp8 verify+unpack
+// always use the nibble-table kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -806,8 +806,9 @@ void Node::on_nack(const MessagePtr& m) {
   flush_batch();
 }
 
-void Node::add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase) {
+void Node::add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase, int64_t rate) {
   XferJob j;
+  j.rate = rate;
   j.src = src;
   j.dst = dst;
   j.layer = layer;
@@ -1301,7 +1302,7 @@ void Node::schedule_mode3() {
       stats_.jobs_dispatched++;
     }
     if (e_->planned()) {
-      add_job(j.sender, j.dest, j.layer, j.offset, j.size);
+      add_job(j.sender, j.dest, j.layer, j.offset, j.size, 0, f.rate);
     } else {
       track(j.sender, j.dest, j.layer, j.offset, j.size);
       send_msg(j.sender, f);

@@ -136,7 +136,7 @@ class Node {
   void ticker();
   int64_t layer_size(LayerID l);
   void retransmit(LayerID layer, NodeID owner, NodeID dest);
-  void add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase = 0);
+  void add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase = 0, int64_t rate = 0);
   void flush_batch();
   void schedule_mode0();
   void schedule_mode1();

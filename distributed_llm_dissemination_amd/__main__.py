@@ -77,6 +77,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="rccl: communicator CTA bounds (ncclConfig minCTAs/maxCTAs; channels per P2P peer)")
     p.add_argument("--nccl-register", action="store_true",
                    help="rccl: register every HBM layer slot with the communicator (ncclCommRegister)")
+    p.add_argument("--lanes", type=int, default=0,
+                   help="rccl: independent comm lanes (RCCL communicator + HIP stream each); 0 = world-1, "
+                        "one ring distance per lane, so a slow peer stalls only its own lane")
     p.add_argument("--suspect-timeout", type=float, default=10.0,
                    help="rccl: report a P2P group stalled this long to the leader, which probes the peers and "
                         "shrinks the communicator around dead ranks (elastic recovery; 0 = only on failure)")
@@ -113,7 +116,7 @@ def build_parser() -> argparse.ArgumentParser:
 def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
     opts = {"reserve_cus": args.reserve_cus, "suspect_s": getattr(args, "suspect_timeout", 10.0),
-            "nccl_register": bool(getattr(args, "nccl_register", False))}
+            "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0))}
     if args.nccl_ctas:
         lo, _, hi = args.nccl_ctas.partition(":")
         opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)

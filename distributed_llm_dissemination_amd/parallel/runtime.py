@@ -506,7 +506,7 @@ class Runtime:
             k: getattr(es, k)
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
-                      "suspects", "shrinks", "aborted_pieces", "group_us_hist", "land_us_hist")
+                      "suspects", "shrinks", "aborted_pieces", "paced", "group_us_hist", "land_us_hist")
         }
 
     def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0) -> Dict[tuple, int]:
@@ -530,6 +530,13 @@ class Runtime:
         """Cumulative bytes this rank sent to / received from each peer rank (per-link counters)."""
         es = self.engine.stats()
         return {"sent": dict(es.peer_sent), "recv": dict(es.peer_recv)}
+
+    def link_stats(self) -> Dict[str, Dict[int, float]]:
+        """Cumulative per-peer counters: bytes sent/received and the device time (ms)
+        of the P2P groups that involved the peer; per-lane device time."""
+        es = self.engine.stats()
+        return {"sent": dict(es.peer_sent), "recv": dict(es.peer_recv), "busy_ms": dict(es.peer_busy_ms),
+                "lane_busy_ms": list(es.lane_busy_ms)}
 
     def layer_bytes(self, layer: int) -> bytes:
         """Bytes of a layer in this rank's target tier (packed with --pack fp8)."""

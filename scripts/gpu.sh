@@ -1,0 +1,101 @@
+#!/bin/bash
+# One entry point for every GPU-box recipe (run through gpurun):
+#
+#   gpurun --timeout 1200 -- bash scripts/gpu.sh <recipe> [out-subdir]
+#
+# Every GPU step runs under its own `timeout -k`, steps are chained with &&,
+# and output goes to gpurun_out/<out-subdir> (default: the recipe name).
+#
+# Recipes
+#   check      GPU tests, smoke(), 1-GPU headline bench
+#   multirank  multi-rank RCCL rehearsal on one GPU (ranks share device 0)
+#   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
+#   queues     per-rank rocprofv3 kernel traces of a shared-GPU 3-rank bench (HW queue ids)
+#   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
+#   profile    kernel trace of the headline bench and the fp8 subset
+#   disk       NVMe tier bench + diskspeed
+#   contention probe-kernel launch delay under a CRC burst (CU reservation)
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+RECIPE=${1:-check}
+OUT=gpurun_out/${2:-$RECIPE}
+mkdir -p "$OUT"
+PYTEST="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+
+shared_rank() {  # shared_rank <world> <rank> <port> <outfile> <bench args...>: one bench rank on device 0
+  local world=$1 rank=$2 port=$3 out=$4
+  shift 4
+  DISSEM_SHARED_GPU=1 RANK=$rank LOCAL_RANK=0 WORLD_SIZE=$world MASTER_ADDR=127.0.0.1 MASTER_PORT=$port \
+    timeout -k 10 300 python3 bench.py --gpus "$world" "$@" > "$out" 2> "${out%.json}.log"
+}
+
+case "$RECIPE" in
+  check)
+    timeout -k 10 900 $PYTEST tests -m gpu > $OUT/pytest_gpu.log 2>&1 &&
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 &&
+    timeout -k 10 600 python bench.py --steps 3 --warmup 1 > $OUT/bench.json 2> $OUT/bench.log
+    ;;
+  multirank)
+    timeout -k 10 1100 $PYTEST tests/test_gpu_multirank.py > $OUT/pytest.log 2>&1
+    ;;
+  shared8)
+    rc=0
+    for spec in "1" "1 --seeding uniform" "2 --pull-window 2" "3" "0 --seeding leader" \
+                "0 --seeding leader --bcast collective" "1 --pack fp8 --layer-mib 96"; do
+      set -- $spec
+      mode=$1; shift
+      tag=m${mode}$(echo "$*" | tr -c 'a-z0-9' '_')
+      DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
+        --layer-mib 64 --chunk-mib 16 --mode "$mode" "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
+    done
+    [ $rc -eq 0 ]
+    ;;
+  queues)
+    # Plain per-rank processes (no torchrun): rocprofv3 wraps the python program itself.
+    pids=()
+    for r in 0 1 2; do
+      DISSEM_SHARED_GPU=1 RANK=$r LOCAL_RANK=0 WORLD_SIZE=3 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+        timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/rank$r -o q -- \
+        python3 bench.py --gpus 3 --steps 1 --warmup 1 --layers 8 --layer-mib 64 --chunk-mib 16 \
+        > $OUT/rank$r.json 2> $OUT/rank$r.log &
+      pids+=($!)
+    done
+    rc=0
+    for p in "${pids[@]}"; do wait $p || rc=$?; done
+    [ $rc -eq 0 ] && python3 scripts/queue_summary.py $OUT > $OUT/queues.txt 2>&1
+    ;;
+  crc)
+    timeout -k 10 300 $PYTEST tests/test_gpu_kernels.py > $OUT/pytest.log 2>&1 &&
+    timeout -k 10 300 python scripts/kernel_bench.py > $OUT/kernel_bench.json 2> $OUT/kernel_bench.log &&
+    timeout -k 10 300 python scripts/crc_impl_bench.py > $OUT/crc_impl.json 2> $OUT/crc_impl.log &&
+    timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o ci -- \
+      python3 scripts/crc_impl_bench.py > $OUT/trace.log 2>&1 &&
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU \
+      SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc -o lds -- python3 scripts/kernel_bench.py \
+      > $OUT/pmc.log 2>&1
+    ;;
+  profile)
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench -o bench -- \
+      python3 bench.py --steps 2 --warmup 1 > $OUT/bench.log 2>&1 &&
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fp8 -o fp8 -- \
+      python3 bench.py --pack fp8 --layers 20 --layer-mib 3072 --steps 2 --warmup 1 > $OUT/fp8.log 2>&1
+    ;;
+  disk)
+    mkdir -p /tmp/dl_disk &&
+    timeout -k 10 900 python bench.py --tier disk --layers 16 --storage /tmp/dl_disk --steps 2 --warmup 1 \
+      > $OUT/bench_disk.json 2> $OUT/bench_disk.log &&
+    timeout -k 10 120 bin/diskspeed -path /tmp/dl_disk/layers/0/0.layer > $OUT/diskspeed.log 2>&1
+    ;;
+  contention)
+    timeout -k 10 120 bin/contention -trials 40 -reserve 32 > $OUT/contention.jsonl 2>&1 &&
+    timeout -k 10 120 bin/contention -trials 40 -reserve 64 > $OUT/contention64.jsonl 2>&1
+    ;;
+  *)
+    echo "unknown recipe $RECIPE" >&2
+    exit 2
+    ;;
+esac
+rc=$?
+echo "recipe $RECIPE exit $rc"
+exit $rc

@@ -69,6 +69,23 @@ def test_crc32c_mfma_matches_host(gpu, n, chunk):
         assert [i for i, (a, b) in enumerate(zip(got, want)) if a != b] == [pos // chunk]
 
 
+@pytest.mark.parametrize("max_blocks", [4, 64, 1024])
+def test_crc32c_mfma_capped_grid_matches_host(gpu, max_blocks):
+    """MFMA kernel, capped launch: every wave loops over many segments (grid-stride):
+    its per-iteration chain/accumulator reset must hold."""
+    n, chunk = 96 << 20, 64 << 20  # 6144 segments of 16 KiB: >= 24 per wave at 4 blocks
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 77)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
+    out = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ws = torch.empty(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, 2, max_blocks)
+    torch.cuda.synchronize()
+    assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
+
+
 def test_crc32c_mfma_refuses_partial_segments(gpu):
     assert not gpu.crc32c_mfma_applies((1 << 20) + 16, 1 << 20)
     t = _dev_bytes((1 << 20) + 16)

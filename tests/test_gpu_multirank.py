@@ -38,14 +38,20 @@ def _torchrun(n, args, timeout=300):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
 
 
-@pytest.fixture(scope="module")
-def n():
-    """Ranks: every GPU (at most 8), or 3 ranks sharing one GPU on a one-GPU box
-    (odd on purpose: relay/scatter schedules with an uneven split)."""
+@pytest.fixture(scope="module", params=["odd", "full"])
+def n(request):
+    """Ranks. With >= 2 GPUs: every GPU (at most 8). On a one-GPU box every rank
+    shares device 0: 3 ranks (odd on purpose: relay/scatter schedules with an
+    uneven split) and 8 ranks, the driver's `bench.py --gpus 8` world (8-way
+    communicator init, 7 peers in every group)."""
     k = _ngpus()
     if k < 1:
         pytest.skip("needs a GPU")
-    return min(k, 8) if k >= 2 else 3
+    if k >= 2:
+        if request.param == "odd":
+            pytest.skip("multi-GPU box: one run over every GPU")
+        return min(k, 8)
+    return 3 if request.param == "odd" else 8
 
 
 @pytest.mark.parametrize("mode,extra", [(1, []), (2, ["--pull-window", "2"]), (3, []), (0, ["--seeding", "leader"]),

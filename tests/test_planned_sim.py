@@ -312,15 +312,18 @@ def test_client_held_layer_on_planned_engine():
 
 
 @pytest.mark.parametrize("n", [4, 8])
-def test_mode1_balanced_seeding_forms_full_all_to_all_rounds(n):
+@pytest.mark.parametrize("lanes", [1, 0])
+def test_mode1_balanced_seeding_forms_full_all_to_all_rounds(n, lanes):
     """The headline bench's schedule: with every rank seeding the same number of
-    layers, each P2P group is a full all-to-all round - one chunk to and one
-    chunk from every peer (n - 1 sends + n - 1 recvs), so all xGMI links of
-    every GPU are busy in every round."""
+    layers, each round moves one chunk to and one chunk from every peer
+    (n - 1 sends + n - 1 recvs), so all xGMI links of every GPU are busy in
+    every round. One lane: each round is one P2P group; world-1 lanes (the
+    default): each round is one group per lane, one ring distance each."""
     layers, chunks = 2 * n, 4
     cfg = make_workload(n, layers, chunks * MiB, tier="host", seeding="random", chunk_bytes=MiB)
-    (res,), _ = run_cluster(cfg, 1)
+    (res,), _ = run_cluster(cfg, 1, rt_kw={"engine_opts": {"lanes": lanes}})
     per_rank_rounds = (layers // n) * chunks
+    nl = 1 if lanes == 1 else n - 1
     for r in res:
-        assert r.engine_stats["groups"] == per_rank_rounds
+        assert r.engine_stats["groups"] == per_rank_rounds * nl
         assert r.engine_stats["pieces"] == per_rank_rounds * 2 * (n - 1)
