@@ -1,7 +1,7 @@
 // Planned data engine (see planned_engine.h).
 //
-// Deadlock freedom. Every piece p has a global key k(p) = (batch, piece index
-// within its job, job sequence number), known identically to its sender and
+// Deadlock freedom. Every piece p has a global key k(p) = (batch, chunk index
+// within its layer, job sequence number), known identically to its sender and
 // receiver, and a lane (lane_of the directed pair, also identical on both
 // ends). Each rank posts the pieces of each lane in increasing key order, cut
 // into consecutive groups on that lane's ordered queue; a P2P op inside a group
@@ -589,12 +589,14 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
     }
     const int64_t end = j.offset + j.size;
     const int64_t first_chunk = j.offset / cb;
-    int64_t pidx = 0;
-    for (int64_t pos = j.offset; pos < end; ++pidx) {
+    for (int64_t pos = j.offset; pos < end;) {
       const int64_t c = pos / cb;
       const int64_t cend = std::min((c + 1) * cb, L.size);
       const int64_t e = std::min(cend, end);
-      Piece p{kind, j.seq, pidx, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
+      // Ordering key (batch, chunk index in the layer, seq): a relay of chunk c
+      // (a later phase, so a larger seq) always sorts after the recv of chunk c
+      // it forwards, whatever byte ranges the two jobs cover.
+      Piece p{kind, j.seq, c, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
       p.src_node = j.src;
       p.bcast = bcast;
       p.rate = j.rate;

@@ -6,7 +6,7 @@
 //  * The leader turns every scheduling decision (mode 0/1/2/3) into XferJobs
 //    with global sequence numbers and sends each rank its share.
 //  * Each job is cut into pieces on a fixed chunk grid. A rank orders its pieces
-//    by the key (batch, piece index within the job, sequence number) - a key its
+//    by the key (batch, chunk index within the layer, sequence number) - a key its
 //    partner computes identically. Pieces go to comm lanes (lane_of: by ring
 //    distance of the pair, the same lane on both ends; one RCCL communicator +
 //    HIP stream per lane) and each lane issues its pieces in key order as
@@ -162,7 +162,7 @@ class PlannedEngine : public DataEngine {
   struct Piece {
     Kind kind;
     uint64_t seq;
-    int64_t pidx;  // piece index inside its job (ordering key, major)
+    int64_t pidx;  // chunk index inside its layer (ordering key after the batch)
     int peer;      // rank
     LayerID layer;
     int64_t off, len, total;

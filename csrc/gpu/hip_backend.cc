@@ -93,9 +93,35 @@ class HipBackend : public Backend {
       lc.splitShare = 0;
       NCCL_OK(ncclCommSplit(nccl_[0], 0, cfg_.rank, &nccl_[l], &lc));
     }
+    connect_all();
     init_ms_ = double(log::now_us() - t0) / 1e3;
     log::info(cfg_.rank).i("world", cfg_.world).i("lanes", int64_t(nccl_.size())).f("init_ms", init_ms_)
         .msg("rccl communicators ready");
+  }
+
+  // RCCL connects a pair lazily inside the first ncclGroupEnd that uses it, and
+  // that call blocks the host thread until the peer runs the same setup. With
+  // several lanes, ranks reach their first groups on different lanes in
+  // different orders (mode 2's dynamic jobs), and two ranks each blocked in a
+  // setup the other has not reached yet would hang. So every lane connects
+  // every distance it serves (and lane 0 its broadcast ring) here, in one fixed
+  // order on every rank.
+  void connect_all() {
+    const int world = cfg_.world, lanes = int(nccl_.size());
+    if (world < 2) return;
+    if (!probe_) HIP_OK(hipMalloc(&probe_, 8192));
+    uint8_t* sbuf = static_cast<uint8_t*>(probe_);
+    uint8_t* rbuf = sbuf + 4096;
+    for (int d = 1; d < world; ++d) {
+      const int lane = lane_of(0, d, world, lanes);
+      const int to = (cfg_.rank + d) % world, from = (cfg_.rank - d + world) % world;
+      NCCL_OK(ncclGroupStart());
+      NCCL_OK(ncclSend(sbuf, 64, ncclUint8, to, nccl_[size_t(lane)], comm_[size_t(lane)]));
+      NCCL_OK(ncclRecv(rbuf, 64, ncclUint8, from, nccl_[size_t(lane)], comm_[size_t(lane)]));
+      NCCL_OK(ncclGroupEnd());
+    }
+    NCCL_OK(ncclBroadcast(sbuf, sbuf, 64, ncclUint8, 0, nccl_[0], comm_[0]));
+    for (hipStream_t s : comm_) HIP_OK(hipStreamSynchronize(s));
   }
   ~HipBackend() override { destroy(false); }
   std::string name() const override { return "rccl"; }
@@ -357,6 +383,7 @@ class HipBackend : public Backend {
     for (auto e : timed_pool_) (void)hipEventDestroy(e);
     timed_pool_.clear();
     if (ws_) (void)hipFree(ws_);
+    if (probe_) (void)hipFree(probe_);
     for (void* p : scratch_)
       if (p) (void)hipFree(p);
     if (crc_host_) (void)hipHostFree(crc_host_);
@@ -398,6 +425,7 @@ class HipBackend : public Backend {
   bool flip_ = false;
   std::vector<ncclComm_t> nccl_;  // one per lane (lane 0: the world communicator, others split from it)
   double init_ms_ = 0;
+  void* probe_ = nullptr;  // connect_all() scratch
   std::map<Ev, hipEvent_t> starts_;  // timed group end -> its start event
   std::vector<hipEvent_t> timed_pool_;
   void* ws_ = nullptr;

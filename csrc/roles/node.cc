@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <set>
 #include <tuple>
 
 #include "core/log.h"
@@ -957,6 +958,16 @@ void Node::schedule_mode1() {
   // node.go:554-608: a random current owner retransmits each missing layer.
   for (auto& kv : status_)
     for (auto& l : kv.second) owners_[l.first].insert(kv.first);  // initialized on demand (quirk Q3)
+  const bool links = cfg_.owner_policy == "links";
+  // Link capacities (config Links / probed topology); unknown links count as
+  // the fastest known one, and with none known every link is equal.
+  double cap_max = 0;
+  for (auto& kv : cfg_.link_bw) cap_max = std::max(cap_max, double(kv.second));
+  auto cap = [&](NodeID s, NodeID d) {
+    auto it = cfg_.link_bw.find({s, d});
+    return it != cfg_.link_bw.end() && it->second > 0 ? double(it->second) : (cap_max > 0 ? cap_max : 1.0);
+  };
+  RelayPlan plan;
   for (auto& kv : assignment_) {
     NodeID dest = kv.first;
     for (auto& l : kv.second) {
@@ -971,14 +982,15 @@ void Node::schedule_mode1() {
         }
         std::vector<NodeID> cand(oit->second.begin(), oit->second.end());
         NodeID owner;
-        if (cfg_.owner_policy == "links") {
+        if (links) {
           // xGMI-aware: every GPU pair has its own link, so spread each dest's
-          // inbound bytes over distinct links (least-loaded owner->dest link,
-          // then least total egress, then lowest id).
+          // inbound bytes over distinct links - least projected link time
+          // (bytes / capacity) first, then least total egress, then lowest id.
           owner = cand[0];
-          std::pair<int64_t, int64_t> best{INT64_MAX, INT64_MAX};
+          std::pair<double, int64_t> best{1e300, INT64_MAX};
           for (NodeID c : cand) {
-            std::pair<int64_t, int64_t> k{link_bytes_[{c, dest}], owner_bytes_[c]};
+            std::pair<double, int64_t> k{double(link_bytes_[{c, dest}] + layer_size(layer)) / cap(c, dest),
+                                         owner_bytes_[c]};
             if (k < best) {
               best = k;
               owner = c;
@@ -1002,7 +1014,11 @@ void Node::schedule_mode1() {
           owner = cand[size_t(rng_() % cand.size())];  // uniform (quirk Q5)
         }
         owner_bytes_[owner] += layer_size(layer);
-        retransmit(layer, owner, dest);
+        if (links && e_->planned()) {
+          plan[{dest, layer}].push_back(PlanPart{owner, 0, layer_size(layer), 0});
+        } else {
+          retransmit(layer, owner, dest);
+        }
       } else {
         LayerSrc src;
         if (!store_.get(layer, &src)) {
@@ -1013,6 +1029,79 @@ void Node::schedule_mode1() {
       }
     }
   }
+  if (plan.empty()) return;
+  if (cap_max > 0) relay_rebalance(plan, cap);
+  for (auto& kv : plan)
+    for (auto& p : kv.second) {
+      {
+        std::lock_guard<std::mutex> lk(sig_mu_);
+        stats_.jobs_dispatched++;
+      }
+      add_job(p.src, kv.first.first, kv.first.second, p.off, p.size, p.phase);
+    }
+}
+
+void Node::relay_rebalance(RelayPlan& plan, const std::function<double(NodeID, NodeID)>& cap) {
+  // A slow link (config Links / measured topology) must not set the session
+  // time: move chunk-sized slices of the layers it carries onto relays. A relay
+  // is a rank that receives the same layer straight from an owner in this plan
+  // (phase 0); it forwards the slice in phase 1, chunk-pipelined behind its own
+  // recv (the planned engine orders a relay after the recv it forwards). Each
+  // move takes one slice off the link with the longest projected time onto the
+  // relay->dest link whose time stays lowest, while that lowers the maximum.
+  const int64_t unit = std::max<int64_t>(cfg_.align, 1);
+  std::map<std::pair<NodeID, NodeID>, int64_t> bytes;
+  std::set<std::pair<NodeID, LayerID>> relayed_into, relays_from;
+  for (auto& kv : plan)
+    for (auto& p : kv.second) bytes[{p.src, kv.first.first}] += p.size;
+  auto t = [&](NodeID s, NodeID d, int64_t extra) { return double(bytes[{s, d}] + extra) / cap(s, d); };
+  int64_t moves = 0;
+  for (int iter = 0; iter < 1000000; ++iter) {
+    std::pair<NodeID, NodeID> worst{};
+    double tw = -1;
+    for (auto& kv : bytes)
+      if (kv.second > 0 && t(kv.first.first, kv.first.second, 0) > tw) {
+        tw = t(kv.first.first, kv.first.second, 0);
+        worst = kv.first;
+      }
+    if (tw <= 0) break;
+    const NodeID s = worst.first, d = worst.second;
+    bool moved = false;
+    for (auto& kv : plan) {
+      if (kv.first.first != d || relays_from.count(kv.first)) continue;
+      const LayerID layer = kv.first.second;
+      auto& parts = kv.second;
+      for (size_t i = 0; i < parts.size() && !moved; ++i) {
+        PlanPart& p = parts[i];
+        if (p.phase != 0 || p.src != s || p.size <= unit) continue;
+        // the best relay: receives this layer directly (phase 0 only) in this plan
+        NodeID best = 0;
+        double tb = 1e300;
+        for (auto& other : plan) {
+          const NodeID x = other.first.first;
+          if (other.first.second != layer || x == d || x == s || relayed_into.count(other.first)) continue;
+          const double tx = t(x, d, unit);
+          if (tx < tb) {
+            tb = tx;
+            best = x;
+          }
+        }
+        if (tb >= tw) continue;  // no relay improves on this link
+        p.size -= unit;
+        parts.push_back(PlanPart{best, p.off + p.size, unit, 1});
+        bytes[{s, d}] -= unit;
+        bytes[{best, d}] += unit;
+        relayed_into.insert(kv.first);
+        relays_from.insert({best, layer});
+        moved = true;
+        ++moves;
+      }
+      if (moved) break;
+    }
+    if (!moved) break;
+  }
+  if (moves)
+    log::info(int64_t(cfg_.id)).i("relayed_slices", moves).i("slice_bytes", unit).msg("mode 1: relays around slow links");
 }
 
 // ------------------------------------------------------------------- mode 2

@@ -12,6 +12,7 @@
 #pragma once
 
 #include <condition_variable>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <random>
@@ -140,6 +141,13 @@ class Node {
   void flush_batch();
   void schedule_mode0();
   void schedule_mode1();
+  struct PlanPart {
+    NodeID src;
+    int64_t off, size;
+    int phase;  // 0: from an owner, 1: relayed by a rank that receives the layer in phase 0
+  };
+  using RelayPlan = std::map<std::pair<NodeID, LayerID>, std::vector<PlanPart>>;  // (dest, layer) -> parts
+  void relay_rebalance(RelayPlan& plan, const std::function<double(NodeID, NodeID)>& cap);
   void schedule_mode2();
   void schedule_mode3();
   // mode 2 (node.go:628-1073); a job is (layer, dest, byte range)

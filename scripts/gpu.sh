@@ -46,7 +46,7 @@ case "$RECIPE" in
       set -- $spec
       mode=$1; shift
       tag=m${mode}$(echo "$*" | tr -c 'a-z0-9' '_')
-      DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
+      DISSEM_SHARED_GPU=1 timeout -k 10 150 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
         --layer-mib 64 --chunk-mib 16 --mode "$mode" "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
     done
     [ $rc -eq 0 ]

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Predict T(N) of the headline bench with the planned engine on the simulated
+fabric's timing model (CPU only, no payload bytes).
+
+The schedule is the real one - leader plan, sequence numbers, lanes, groups,
+staging waits - executed by the same engine code that drives RCCL; the sim
+backend charges every staging copy len / PCIe and every P2P transfer
+len / link on its directed link. Sizes are scaled down by --scale with the
+rates scaled by the same factor, so every chunk takes its full-size time and a
+session takes its full-size wall time in a fraction of the memory.
+
+    python scripts/predict_scaling.py --link-gbps 50 64 --ns 1 2 4 8
+
+Prints one JSON line per (link rate, N): predicted ms per step and the
+aggregate GB/s value bench.py would report (N x 80 GiB / T).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from distributed_llm_dissemination_amd import _core  # noqa: E402
+from distributed_llm_dissemination_amd.models.catalog import delivered_bytes, make_workload  # noqa: E402
+from distributed_llm_dissemination_amd.parallel.runtime import Runtime  # noqa: E402
+
+MiB = 1 << 20
+_n = [0]
+
+
+def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
+            link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
+            slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False) -> dict:
+    """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
+
+    slow_link=((s, d), frac): that directed link runs at frac of the others.
+    plan_links: the leader's plan knows every link's capacity (config Links),
+    so mode 1 with owner_policy "links" can relay around the slow one."""
+    key = f"predict{os.getpid()}_{_n[0]}"
+    _n[0] += 1
+    t = _core.SimTiming()
+    t.copy_bytes = False
+    t.stage_bps = pcie_gbps * 1e9 / scale
+    t.link_bps = link_gbps * 1e9 / scale
+    if slow_link is not None:
+        (s, d), frac = slow_link
+        t.link = {(s, d): link_gbps * 1e9 / scale * frac}
+    _core.sim_set_timing(key, t)
+    lb, cb = layer_bytes // scale, chunk // scale
+    cfg = make_workload(n, layers, lb, tier="host", seeding=seeding, chunk_bytes=cb)
+    if plan_links:
+        bw = int(link_gbps * 1e9)
+        cfg.links = {s: {d: bw for d in range(n) if d != s} for s in range(n)}
+        if slow_link is not None:
+            (s, d), frac = slow_link
+            cfg.links[s][d] = int(bw * frac)
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
+                   poison=False, engine_opts={"lanes": lanes}) for i in range(n)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    times = []
+    try:
+        for _ in range(steps):
+            for r in rts:
+                r.prepare(mode, pull_window=max(1, n - 1), **(policy or {}))
+            res = [None] * n
+
+            def go(i):
+                res[i] = rts[i].execute(600)
+
+            ths = [threading.Thread(target=go, args=(i,)) for i in range(n)]
+            t0 = time.perf_counter()
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            times.append(time.perf_counter() - t0)
+            if not all(x.ok for x in res):
+                raise RuntimeError([x.error for x in res if not x.ok])
+    finally:
+        for r in rts:
+            r.close()
+    sec = min(times)
+    total = delivered_bytes(cfg) * scale
+    return {"n": n, "link_GBps": link_gbps, "pcie_GBps": pcie_gbps, "mode": mode, "lanes": lanes or max(1, n - 1),
+            "ms_per_step": round(sec * 1e3, 1), "value_GBps": round(total / sec / 1e9, 1), "scale": scale}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--link-gbps", type=float, nargs="+", default=[50.0])
+    ap.add_argument("--pcie-gbps", type=float, default=57.5)
+    ap.add_argument("--scale", type=int, default=256)
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--mode", type=int, default=1)
+    args = ap.parse_args()
+    _core.set_log_level(3)
+    for lg in args.link_gbps:
+        for n in args.ns:
+            r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode)
+            # closed form: every GPU stages 80/N GiB over PCIe and gets
+            # 80/N GiB from each peer over its link; both overlap
+            bound = 85.899e9 / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)
+            r["closed_form_ms"] = round(bound * 1e3, 1)
+            print(json.dumps(r), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

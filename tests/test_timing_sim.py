@@ -1,0 +1,109 @@
+"""Schedules under the simulated fabric's timing and RCCL models (CPU).
+
+SimTiming gives the sim fabric per-link bandwidth, per-rank staging (PCIe)
+bandwidth and, optionally, RCCL's round-by-round P2P execution. These tests
+check what the byte-exact tests in test_planned_sim.py cannot: that lanes keep
+irregular groups safe under RCCL's round model, that token-bucket pacing holds
+configured rates (reference writeWithLimit, transport.go:407-424; mode-3
+size/T rates, node.go:1281; tier LimitRate on self loads, node.go:1615-1624),
+and what the headline schedule's T(N) is predicted to be.
+"""
+
+import itertools
+import os
+import sys
+import threading
+import time
+
+import pytest
+
+from distributed_llm_dissemination_amd import _core
+from distributed_llm_dissemination_amd.models.catalog import make_workload
+from distributed_llm_dissemination_amd.parallel.runtime import Runtime
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+import predict_scaling  # noqa: E402
+
+MiB = 1 << 20
+_keys = itertools.count()
+
+
+def run_timed(cfg, mode, timing=None, lanes=0, chunk=MiB, verify=True, **policy):
+    key = f"tsim{os.getpid()}_{next(_keys)}"
+    if timing is not None:
+        _core.sim_set_timing(key, timing)
+    n = len(cfg.nodes)
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=chunk, sim_key=key, verify=verify,
+                   engine_opts={"lanes": lanes}) for i in range(n)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for r in rts:
+            r.prepare(mode, **policy)
+        res = [None] * n
+
+        def go(i):
+            res[i] = rts[i].execute(60)
+
+        ths = [threading.Thread(target=go, args=(i,)) for i in range(n)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dt = time.perf_counter() - t0
+        assert all(x.ok for x in res), [x.error for x in res]
+        return dt, res
+    finally:
+        for r in rts:
+            r.close()
+
+
+def test_lanes_keep_irregular_groups_safe_under_rccl_rounds():
+    """Mode 2 at 8 ranks dispatches jobs as acks return, so ranks form
+    different groups. Under RCCL's round model (a group's ops run one ring
+    distance at a time) a multi-distance group can wait on itself across ranks
+    - the 8-rank hang first seen on the GPU box with one lane. With world-1
+    lanes every group holds one distance and the session completes."""
+    cfg = make_workload(8, 16, 4 * MiB, tier="host", seeding="random", chunk_bytes=MiB)
+    t = _core.SimTiming()
+    t.p2p_rounds = True
+    for _ in range(2):
+        _, res = run_timed(cfg, 2, t, lanes=0, pull_window=2)
+        assert res[0].engine_stats["verify_failures"] == 0
+
+
+def test_tier_rate_paces_staging():
+    """A host tier with a LimitRate (config Sources) is staged no faster than
+    that rate: 8 MiB at 40 MB/s takes ~0.18 s instead of ~0 (the bucket's
+    burst of one chunk goes at once, like x/time/rate's initial burst)."""
+    rate = 40_000_000
+    cfg = make_workload(1, 4, 2 * MiB, tier="host", tier_rate=rate, chunk_bytes=MiB)
+    dt, res = run_timed(cfg, 1)
+    want = 7 * MiB / rate
+    assert want * 0.9 <= dt <= want * 1.5 + 0.1, (dt, want)
+    assert res[0].engine_stats["paced"] > 0
+
+
+def test_mode3_jobs_finish_at_the_planned_T():
+    """Mode 3 paces every job at size/T (node.go:1281): with the leader's 50 MB/s
+    NetworkBW as the binding cut, the transfers end together close to T."""
+    cfg = make_workload(4, 4, 2 * MiB, tier="host", seeding="leader", network_bw=50_000_000, chunk_bytes=MiB // 4)
+    dt, res = run_timed(cfg, 3, chunk=MiB // 4)
+    T = res[0].flow_T
+    assert T == pytest.approx(3 * 4 * 2 * MiB / 50e6, rel=0.02)
+    assert abs(dt - T) <= 0.1 * T + 0.05, (dt, T)
+    assert res[0].engine_stats["paced"] > 0
+
+
+def test_predicted_scaling_follows_the_link_bound():
+    """The headline schedule on the timing model (scripts/predict_scaling.py)
+    at 1/1024 size: T(N) stays within 35 % of the closed form
+    85.9 GB / (N * min(PCIe, link)) - the schedule keeps every GPU's PCIe
+    copy and its N-1 links busy together (sim thread overhead included)."""
+    for n in (1, 2, 4):
+        r = predict_scaling.predict(n, scale=1024, link_gbps=50.0 / 4, pcie_gbps=57.5 / 4, steps=1)
+        bound = 85.899e9 / n / (min(57.5, 50.0 if n > 1 else 1e9) / 4 * 1e9)
+        assert r["ms_per_step"] / 1e3 <= bound * 1.35, (n, r, bound)
+        assert r["ms_per_step"] / 1e3 >= bound * 0.95, (n, r, bound)
