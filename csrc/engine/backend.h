@@ -108,13 +108,39 @@ class Backend {
   virtual double comm_init_ms() const { return 0; }
 };
 
-// The lane a directed pair (src -> dst) uses, identical on both ends: by the
-// ring distance dst - src, so with world - 1 lanes every lane of a rank talks
-// to exactly one send peer and one recv peer.
+// Lanes. Every directed pair (src -> dst) has one lane, computed identically
+// on both ends. Two schemes:
+//  * per distance (lanes <= world-1): lane = (d - 1) % lanes with d the ring
+//    distance dst - src; with world-1 lanes each lane of a rank carries one
+//    send peer (rank+d) and one recv peer (rank-d), one RCCL round each;
+//  * per directed link (lanes == directed_lanes(world), the default on up to 8
+//    ranks): the links of distance d form cycles r -> r+d -> ...; each link's
+//    lane is (d, color of its sender in a proper coloring of its cycle), so a
+//    rank's send to rank+d and its recv from rank-d sit on different lanes and
+//    every directed xGMI link progresses on its own - no lockstep along the
+//    ring. Cycles of even length need 2 colors, odd ones 3.
+inline int lane_gcd(int a, int b) { return b ? lane_gcd(b, a % b) : a; }
+inline int lane_colors(int world) {
+  for (int d = 1; d < world; ++d)
+    if ((world / lane_gcd(world, d)) % 2) return 3;
+  return 2;
+}
+inline int directed_lanes(int world) { return world > 1 ? (world - 1) * lane_colors(world) : 1; }
+inline int lane_color(int src, int d, int world, int colors) {
+  const int g = lane_gcd(world, d), len = world / g;
+  int k = 0;  // position of src on its cycle r0, r0+d, r0+2d, ...
+  for (int x = src % g; x != src; x = (x + d) % world) ++k;
+  if (colors == 3 && len % 2 == 1 && k == len - 1) return 2;
+  return k % 2;
+}
 inline int lane_of(int src, int dst, int world, int lanes) {
   if (lanes <= 1 || world <= 1) return 0;
-  const int delta = ((dst - src) % world + world) % world;  // 1 .. world-1
-  return (delta - 1) % lanes;
+  const int d = ((dst - src) % world + world) % world;  // 1 .. world-1
+  if (lanes == directed_lanes(world)) {
+    const int c = lane_colors(world);
+    return (d - 1) * c + lane_color(((src % world) + world) % world, d, world, c);
+  }
+  return (d - 1) % lanes;
 }
 
 struct SimFabricStats {

@@ -53,12 +53,12 @@ struct PlannedConfig {
   bool verify = true;
   bool poison = true;              // zero non-seeded slots between sessions
   int max_inflight_groups = 64;   // per lane
-  // Independent comm lanes (communicator + stream each). 0 = auto: world - 1
-  // (at most 7), so each lane carries one send and one recv peer of one ring
-  // distance. That is also what keeps irregular groups (mode 2, relays) safe on
-  // RCCL: with few channels RCCL runs a group's ops in rounds of one distance
-  // each, so a multi-distance group can wait on itself across ranks
-  // (SimTiming::p2p_rounds reproduces it; tests/test_planned_sim.py).
+  // Independent comm lanes (communicator + stream each; backend.h lane_of).
+  // 0 = auto: one lane per directed link, so every xGMI link of a GPU sends or
+  // receives on its own. One-distance lanes are also what keeps irregular
+  // groups (mode 2, relays) safe on RCCL: with few channels RCCL runs a
+  // group's ops in rounds of one distance each, so a multi-distance group can
+  // wait on itself across ranks (SimTiming::p2p_rounds reproduces it).
   int lanes = 0;
   std::map<NodeID, int64_t> link_rate;  // cap this rank's sends to a node (B/s; slow-link injection)
   int group_peers = 1;             // ops per peer and direction per group
@@ -95,13 +95,14 @@ struct PlannedConfig {
   bool nccl_register = false;  // register every HBM slot with the communicator (ncclCommRegister)
 };
 
-// Comm lanes an engine of this config runs: cfg.lanes clamped to [1, world-1];
-// 0 = auto = world - 1, at most 7 (one send + one recv peer per lane on an
-// 8-GPU node).
+// Comm lanes an engine of this config runs. 0 = auto: one lane per directed
+// link (directed_lanes: 14 on 8 ranks) up to 8 ranks, else world-1 (at most 7)
+// per-distance lanes; > 0: at most that many (per-distance scheme unless it
+// equals directed_lanes).
 inline int resolve_lanes(const PlannedConfig& c) {
-  const int most = std::max(1, c.world - 1);
-  if (c.lanes <= 0) return std::min(most, 7);
-  return std::min(c.lanes, most);
+  if (c.world <= 1) return 1;
+  if (c.lanes <= 0) return c.world <= 8 ? directed_lanes(c.world) : std::min(c.world - 1, 7);
+  return std::min(c.lanes, directed_lanes(c.world));
 }
 
 struct PlannedStats {

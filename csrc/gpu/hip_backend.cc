@@ -113,11 +113,11 @@ class HipBackend : public Backend {
     uint8_t* sbuf = static_cast<uint8_t*>(probe_);
     uint8_t* rbuf = sbuf + 4096;
     for (int d = 1; d < world; ++d) {
-      const int lane = lane_of(0, d, world, lanes);
       const int to = (cfg_.rank + d) % world, from = (cfg_.rank - d + world) % world;
+      const size_t ls = size_t(lane_of(cfg_.rank, to, world, lanes)), lr = size_t(lane_of(from, cfg_.rank, world, lanes));
       NCCL_OK(ncclGroupStart());
-      NCCL_OK(ncclSend(sbuf, 64, ncclUint8, to, nccl_[size_t(lane)], comm_[size_t(lane)]));
-      NCCL_OK(ncclRecv(rbuf, 64, ncclUint8, from, nccl_[size_t(lane)], comm_[size_t(lane)]));
+      NCCL_OK(ncclSend(sbuf, 64, ncclUint8, to, nccl_[ls], comm_[ls]));
+      NCCL_OK(ncclRecv(rbuf, 64, ncclUint8, from, nccl_[lr], comm_[lr]));
       NCCL_OK(ncclGroupEnd());
     }
     NCCL_OK(ncclBroadcast(sbuf, sbuf, 64, ncclUint8, 0, nccl_[0], comm_[0]));

@@ -312,18 +312,19 @@ def test_client_held_layer_on_planned_engine():
 
 
 @pytest.mark.parametrize("n", [4, 8])
-@pytest.mark.parametrize("lanes", [1, 0])
+@pytest.mark.parametrize("lanes", [1, -1, 0])
 def test_mode1_balanced_seeding_forms_full_all_to_all_rounds(n, lanes):
     """The headline bench's schedule: with every rank seeding the same number of
     layers, each round moves one chunk to and one chunk from every peer
     (n - 1 sends + n - 1 recvs), so all xGMI links of every GPU are busy in
-    every round. One lane: each round is one P2P group; world-1 lanes (the
-    default): each round is one group per lane, one ring distance each."""
+    every round. One lane: each round is one P2P group; world-1 lanes: one
+    group per ring distance (a send and a recv); the default, one lane per
+    directed link: one single-op group per link and direction."""
     layers, chunks = 2 * n, 4
     cfg = make_workload(n, layers, chunks * MiB, tier="host", seeding="random", chunk_bytes=MiB)
-    (res,), _ = run_cluster(cfg, 1, rt_kw={"engine_opts": {"lanes": lanes}})
+    (res,), _ = run_cluster(cfg, 1, rt_kw={"engine_opts": {"lanes": n - 1 if lanes == -1 else lanes}})
     per_rank_rounds = (layers // n) * chunks
-    nl = 1 if lanes == 1 else n - 1
+    nl = {1: 1, -1: n - 1, 0: 2 * (n - 1)}[lanes]
     for r in res:
         assert r.engine_stats["groups"] == per_rank_rounds * nl
         assert r.engine_stats["pieces"] == per_rank_rounds * 2 * (n - 1)

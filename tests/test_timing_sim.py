@@ -107,3 +107,20 @@ def test_predicted_scaling_follows_the_link_bound():
         bound = 85.899e9 / n / (min(57.5, 50.0 if n > 1 else 1e9) / 4 * 1e9)
         assert r["ms_per_step"] / 1e3 <= bound * 1.35, (n, r, bound)
         assert r["ms_per_step"] / 1e3 >= bound * 0.95, (n, r, bound)
+
+
+def test_slow_link_costs_at_most_a_seventh_with_the_link_aware_plan():
+    """One directed link at half speed (8 ranks, headline mode 1, 1/1024 size,
+    timing slowed 4x). Lanes are per directed link, so the slow link holds back
+    only its own transfers; the leader's link-aware plan (owner policy
+    "links" with the config's Links) then moves chunk slices of the layers it
+    carries onto relays - ranks that receive the same layer directly - until
+    the slowest link no longer sets the pace: <= 1/7 extra time, where a plan
+    that ignores the link takes ~2x."""
+    kw = dict(layers=32, scale=1024, link_gbps=50.0 / 4, pcie_gbps=57.5 / 4, mode=1, steps=1,
+              policy={"owner_policy": "links"})
+    base = predict_scaling.predict(8, **kw)["ms_per_step"]
+    slow = predict_scaling.predict(8, slow_link=((0, 1), 0.5), **kw)["ms_per_step"]
+    planned = predict_scaling.predict(8, slow_link=((0, 1), 0.5), plan_links=True, **kw)["ms_per_step"]
+    assert slow > 1.5 * base, (base, slow)
+    assert planned <= base * (1 + 1 / 7), (base, planned, slow)
