@@ -47,8 +47,9 @@ def parse_args(argv=None):
     p.add_argument("--assignment", default="replicate", choices=["replicate", "pipeline"])
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--owner-policy", default="random", choices=["random", "balanced", "links"],
-                   help="mode 1 owner choice when a layer has several holders (--copies > 1)")
+    p.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
+                   help="mode 1 owner choice when a layer has several holders (--copies > 1); links also "
+                        "relays around links the plan knows to be slow")
     p.add_argument("--timeout", type=float, default=300.0)
     p.add_argument("--pull-window", type=int, default=0, help="mode 2 jobs in flight per sender (0 = peers)")
     p.add_argument("--storage", default="", help="disk tier directory")

@@ -395,6 +395,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("pull_window", &NodeConfig::pull_window)
       .def_readwrite("network_bw", &NodeConfig::network_bw)
       .def_readwrite("link_bw", &NodeConfig::link_bw)
+      .def_readwrite("stage_bw", &NodeConfig::stage_bw)
       .def_readwrite("integer_seconds", &NodeConfig::integer_seconds)
       .def_readwrite("align", &NodeConfig::align)
       .def_readwrite("storage_path", &NodeConfig::storage_path)
@@ -490,8 +491,9 @@ PYBIND11_MODULE(_core, m) {
                          const std::vector<std::tuple<LayerID, NodeID, int64_t>>& demands,
                          const std::map<NodeID, int64_t>& egress, const std::map<NodeID, int64_t>& ingress,
                          const std::map<std::pair<NodeID, NodeID>, int64_t>& links, int64_t align,
-                         bool integer_seconds, bool allow_self) {
+                         bool integer_seconds, bool allow_self, const std::map<NodeID, int64_t>& stage) {
     FlowProblem p;
+    p.stage_bps = stage;
     p.holdings = holdings;
     for (auto& d : demands) p.demands.push_back({std::get<0>(d), std::get<1>(d), std::get<2>(d)});
     p.egress_bps = egress;
@@ -505,7 +507,8 @@ PYBIND11_MODULE(_core, m) {
   }, py::arg("holdings"), py::arg("demands"), py::arg("egress") = std::map<NodeID, int64_t>{},
      py::arg("ingress") = std::map<NodeID, int64_t>{},
      py::arg("links") = std::map<std::pair<NodeID, NodeID>, int64_t>{}, py::arg("align") = 1,
-     py::arg("integer_seconds") = false, py::arg("allow_self") = false);
+     py::arg("integer_seconds") = false, py::arg("allow_self") = false,
+     py::arg("stage") = std::map<NodeID, int64_t>{});
 
   py::class_<RangeSet>(m, "RangeSet")
       .def(py::init<>())

@@ -1365,6 +1365,7 @@ void Node::schedule_mode3() {
     p.ingress_bps[kv.first] = kv.second;
   }
   p.link_bps = cfg_.link_bw;
+  p.stage_bps = cfg_.stage_bw;
   p.align = cfg_.align;
   p.integer_seconds = cfg_.integer_seconds;
   log::info(int64_t(cfg_.id)).msg("assigning a job...");

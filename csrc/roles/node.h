@@ -36,7 +36,8 @@ struct NodeConfig {
   int64_t pull_job_bytes = 0;       // mode 2: job = this many bytes of a layer (0 = whole layer, reference)
   bool range_acks = false;          // receiver: also ack each landed range (needed by mode-2 range jobs)
   std::map<NodeID, int64_t> network_bw;  // mode 3: NetworkBW per node (B/s, 0 = unlimited)
-  std::map<std::pair<NodeID, NodeID>, int64_t> link_bw;  // mode 3 topology: per directed link
+  std::map<std::pair<NodeID, NodeID>, int64_t> link_bw;  // mode 1 links / mode 3 topology: per directed link
+  std::map<NodeID, int64_t> stage_bw;  // mode 3: per node host->HBM staging (PCIe) budget for non-HBM tiers
   bool integer_seconds = false;     // mode 3: reference T search over integer seconds
   int64_t align = 1;                // mode 3: byte alignment of ranges
   std::string storage_path;         // receiver persist dir ("" = none)

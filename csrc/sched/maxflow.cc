@@ -4,6 +4,7 @@
 #include <cmath>
 #include <limits>
 #include <queue>
+#include <set>
 #include <tuple>
 
 #include "core/trace.h"
@@ -91,41 +92,85 @@ struct Built {
 };
 
 Built build(const FlowProblem& p, double T) {
-  // Vertex numbering.
-  std::map<NodeID, int> vs;
-  std::map<std::pair<NodeID, int>, int> vst;
-  std::map<std::tuple<NodeID, int, NodeID>, int> vlink;
-  std::map<std::pair<LayerID, NodeID>, int> vd;
-  std::map<NodeID, int> vdest;
-  int n = 2;
   // demands indexed by layer
   std::map<LayerID, std::vector<const FlowDemand*>> by_layer;
-  for (auto& dm : p.demands) {
-    by_layer[dm.layer].push_back(&dm);
-    if (!vd.count({dm.layer, dm.dest})) vd[{dm.layer, dm.dest}] = n++;
-    if (!vdest.count(dm.dest)) vdest[dm.dest] = n++;
-  }
+  for (auto& dm : p.demands) by_layer[dm.layer].push_back(&dm);
+  std::map<std::pair<LayerID, NodeID>, int64_t> dsize;
+  for (auto& dm : p.demands) dsize[{dm.layer, dm.dest}] = std::max(dsize[{dm.layer, dm.dest}], dm.size);
   const bool topo = !p.link_bps.empty();
+  const int kDevice = int(SourceType::Device);
+  // Candidate (sender, tier, layer, dest) edges, and per (sender, dest) the
+  // demanded bytes by tier (to split a link shared by several tiers).
+  struct Cand {
+    NodeID s;
+    int t;
+    LayerID l;
+    NodeID d;
+  };
+  std::vector<Cand> cands;
+  std::map<std::pair<NodeID, NodeID>, std::map<int, int64_t>> sd_tiers;
+  std::set<std::tuple<NodeID, LayerID, NodeID>> seen;
   for (auto& hs : p.holdings) {
-    NodeID s = hs.first;
+    const NodeID s = hs.first;
     for (auto& lm : hs.second) {
       auto bl = by_layer.find(lm.first);
       if (bl == by_layer.end()) continue;
-      int t = int(lm.second.source_type);
+      const int t = int(lm.second.source_type);
       for (auto* dm : bl->second) {
         if (dm->dest == s && !p.allow_self) continue;
-        if (!vs.count(s)) vs[s] = n++;
-        if (!vst.count({s, t})) vst[{s, t}] = n++;
-        if (topo && !vlink.count({s, t, dm->dest})) vlink[{s, t, dm->dest}] = n++;
+        if (!seen.insert({s, lm.first, dm->dest}).second) continue;
+        cands.push_back({s, t, lm.first, dm->dest});
+        sd_tiers[{s, dm->dest}][t] += dsize[{lm.first, dm->dest}];
       }
     }
+  }
+  // Vertex numbering: 0 source, 1 sink.
+  int n = 2;
+  std::map<NodeID, int> vs, vstage, vdest;
+  std::map<std::pair<NodeID, int>, int> vst;
+  std::map<std::tuple<NodeID, int, NodeID>, int> vlink;  // (s, tier or -1 = shared, d)
+  std::map<std::pair<LayerID, NodeID>, int> vd;
+  for (auto& kv : dsize) {
+    vd[kv.first] = n++;
+    if (!vdest.count(kv.first.second)) vdest[kv.first.second] = n++;
+  }
+  auto link_key = [&](const Cand& c) {
+    return std::make_tuple(c.s, sd_tiers[{c.s, c.d}].size() > 1 ? c.t : -1, c.d);
+  };
+  for (auto& c : cands) {
+    if (!vs.count(c.s)) vs[c.s] = n++;
+    if (c.t != kDevice && !vstage.count(c.s)) vstage[c.s] = n++;
+    if (!vst.count({c.s, c.t})) vst[{c.s, c.t}] = n++;
+    if (topo && c.s != c.d && !vlink.count(link_key(c))) vlink[link_key(c)] = n++;
   }
   Built b;
   b.d = std::make_unique<Dinic>(n);
   Dinic& d = *b.d;
-  for (auto& kv : vs) {
-    auto eg = p.egress_bps.find(kv.first);
-    d.add(b.src, kv.second, cap_for(eg == p.egress_bps.end() ? 0 : eg->second, T));
+  auto rate_of = [](const std::map<NodeID, int64_t>& m, NodeID k) {
+    auto it = m.find(k);
+    return it == m.end() ? int64_t(0) : it->second;
+  };
+  for (auto& kv : vs) d.add(b.src, kv.second, cap_for(rate_of(p.egress_bps, kv.first), T));
+  // Staging is paid once per byte a sender loads into HBM, however many dests it
+  // then forwards it to over xGMI; a flow charges every transfer, so the
+  // budget is scaled by the sender's fan-out (its candidate bytes over the
+  // distinct layer bytes it could load) - exact when its layers share one
+  // fan-out.
+  std::map<NodeID, double> cand_bytes, layer_bytes;
+  std::set<std::pair<NodeID, LayerID>> counted;
+  for (auto& c : cands) {
+    if (c.t == kDevice) continue;
+    cand_bytes[c.s] += double(dsize[{c.l, c.d}]);
+    if (counted.insert({c.s, c.l}).second) {
+      int64_t mx = 0;
+      for (auto* dm : by_layer[c.l]) mx = std::max(mx, dm->size);
+      layer_bytes[c.s] += double(mx);
+    }
+  }
+  for (auto& kv : vstage) {
+    const int64_t r = rate_of(p.stage_bps, kv.first);
+    const double fan = layer_bytes[kv.first] > 0 ? std::max(1.0, cand_bytes[kv.first] / layer_bytes[kv.first]) : 1.0;
+    d.add(vs[kv.first], kv.second, r > 0 ? cap_for(int64_t(double(r) * fan), T) : kInf);
   }
   // Tier capacity: the tier's configured rate (all its layers share one device).
   std::map<std::pair<NodeID, int>, int64_t> tier_rate;
@@ -138,36 +183,38 @@ Built build(const FlowProblem& p, double T) {
       if (it == tier_rate.end()) tier_rate[key] = r;
       else if (it->second > 0 && (r <= 0 || r > it->second)) it->second = r;  // 0 = unlimited wins
     }
-  for (auto& kv : vst) d.add(vs[kv.first.first], kv.second, cap_for(tier_rate[kv.first], T));
-  for (auto& kv : vlink) {
-    NodeID s = std::get<0>(kv.first), dst = std::get<2>(kv.first);
-    auto lk = p.link_bps.find({s, dst});
-    int64_t rate = lk == p.link_bps.end() ? 0 : lk->second;
-    if (s == dst) rate = 0;  // a self-load does not use a network link
-    d.add(vst[{s, std::get<1>(kv.first)}], kv.second, cap_for(rate, T));
+  for (auto& kv : vst) {
+    const NodeID s = kv.first.first;
+    const int parent = kv.first.second == kDevice ? vs[s] : vstage[s];
+    d.add(parent, kv.second, cap_for(tier_rate[kv.first], T));
   }
-  for (auto& hs : p.holdings) {
-    NodeID s = hs.first;
-    for (auto& lm : hs.second) {
-      auto bl = by_layer.find(lm.first);
-      if (bl == by_layer.end()) continue;
-      int t = int(lm.second.source_type);
-      for (auto* dm : bl->second) {
-        if (dm->dest == s && !p.allow_self) continue;
-        auto key = std::make_tuple(s, lm.first, dm->dest);
-        if (b.job_edges.count(key)) continue;
-        int from = topo ? vlink[{s, t, dm->dest}] : vst[{s, t}];
-        b.job_edges[key] = d.add(from, vd[{dm->layer, dm->dest}], kInf);
-      }
+  for (auto& kv : vlink) {
+    const NodeID s = std::get<0>(kv.first), dst = std::get<2>(kv.first);
+    const int t = std::get<1>(kv.first);
+    auto lk = p.link_bps.find({s, dst});
+    int64_t cap = cap_for(lk == p.link_bps.end() ? 0 : lk->second, T);
+    const auto& tiers = sd_tiers[{s, dst}];
+    if (t >= 0 && cap < kInf) {
+      // several tiers share this link: each gets its share of the demanded bytes
+      int64_t tot = 0;
+      for (auto& x : tiers) tot += x.second;
+      cap = tot > 0 ? int64_t(double(cap) * double(tiers.at(t)) / double(tot)) : cap;
+    }
+    // a shared vertex is fed by every tier of the sender that serves this dest
+    if (t >= 0) {
+      d.add(vst[{s, t}], kv.second, cap);
+    } else {
+      const int only = tiers.begin()->first;
+      d.add(vst[{s, only}], kv.second, cap);
     }
   }
-  std::map<std::pair<LayerID, NodeID>, int64_t> dsize;
-  for (auto& dm : p.demands) dsize[{dm.layer, dm.dest}] = std::max(dsize[{dm.layer, dm.dest}], dm.size);
-  for (auto& kv : vd) d.add(kv.second, vdest[kv.first.second], dsize[kv.first]);
-  for (auto& kv : vdest) {
-    auto in = p.ingress_bps.find(kv.first);
-    d.add(kv.second, b.sink, cap_for(in == p.ingress_bps.end() ? 0 : in->second, T));
+  for (auto& c : cands) {
+    auto key = std::make_tuple(c.s, c.l, c.d);
+    const int from = (topo && c.s != c.d) ? vlink[link_key(c)] : vst[{c.s, c.t}];
+    b.job_edges[key] = d.add(from, vd[{c.l, c.d}], kInf);
   }
+  for (auto& kv : vd) d.add(kv.second, vdest[kv.first.second], dsize[kv.first]);
+  for (auto& kv : vdest) d.add(kv.second, b.sink, cap_for(rate_of(p.ingress_bps, kv.first), T));
   return b;
 }
 

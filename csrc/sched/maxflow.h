@@ -10,8 +10,17 @@
 //    from one edge (quirk Q8);
 //  * keeps one vertex per (sender, source tier) whose capacity is that tier's
 //    rate (quirk Q7: the reference collapses every tier to SourceType 0);
-//  * optionally adds a per directed link vertex (sender -> dest) with its own
-//    capacity: the xGMI topology mode, where each GPU pair has one link;
+//  * puts a per-sender staging vertex (host->HBM, PCIe) above its host, disk
+//    and client tiers - bytes from those tiers cross the GPU's PCIe link before
+//    any xGMI link, HBM-resident (Device) layers do not;
+//  * optionally adds one vertex per directed link (sender -> dest) with its
+//    capacity, shared by everything the sender sends to that dest: the xGMI
+//    topology mode, where each GPU pair has one link. A sender whose layers for
+//    one dest sit in several tiers gets one (tier, dest) vertex per tier instead,
+//    each with the link's capacity split by that tier's share of the demanded
+//    bytes (a link shared across tiers is a two-commodity constraint a single
+//    flow cannot state exactly; the split keeps the plan feasible, never
+//    optimistic - tests/test_maxflow.py checks both cases against an LP);
 //  * searches T continuously (seconds as double), or over integer seconds for
 //    reference parity;
 //  * rounds byte counts to a chunk alignment so ranges map onto whole chunks.
@@ -44,6 +53,7 @@ struct FlowProblem {
   std::map<NodeID, LayerIDs> holdings;    // what each potential sender holds (tier + rate)
   std::vector<FlowDemand> demands;
   std::map<std::pair<NodeID, NodeID>, int64_t> link_bps;  // optional per directed link caps
+  std::map<NodeID, int64_t> stage_bps;   // per sender host->HBM staging (PCIe) for non-Device tiers
   int64_t align = 1;
   bool integer_seconds = false;
   bool allow_self = false;  // may a dest source a demand from its own lower tier

@@ -93,8 +93,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="after delivery, write this node's layers + CRC manifest here; on start, announce "
                         "layers found here as disk-tier copies (resume without re-transfer)")
     p.add_argument("--seed", type=int, default=0, help="mode-1 owner RNG seed")
-    p.add_argument("--owner-policy", default="random", choices=["random", "balanced", "links"],
-                   help="mode 1 owner choice: random (reference), balanced (egress bytes), links (per-link bytes)")
+    p.add_argument("--owner-policy", default=None, choices=["random", "balanced", "links"],
+                   help="mode 1 owner choice: random (reference), balanced (egress bytes), links (per-link time, "
+                        "relays around slow links; default on the rccl engine)")
     p.add_argument("--pull-window", type=int, default=1)
     p.add_argument("--pull-job-mib", type=int, default=0,
                    help="mode 2: split layers into jobs of this many MiB (0 = one job per layer, reference)")
@@ -102,9 +103,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0 on rccl: relay = scatter + peer relay over all xGMI links; collective = "
                         "ncclBroadcast per layer; fanout = leader sends every copy")
-    p.add_argument("--xgmi-link-gbps", type=float, default=0.0,
-                   help="mode 3 on rccl: model each GPU pair's link (probed xGMI topology) at this GB/s "
-                        "when the config has no Links")
+    p.add_argument("--xgmi-link-gbps", type=float, default=None,
+                   help="rccl: plan each GPU pair's link (probed xGMI topology) at this GB/s when the config has "
+                        "no Links (default 50; 0 = no link tier)")
+    p.add_argument("--pcie-gbps", type=float, default=None,
+                   help="rccl: plan each GPU's host->HBM staging at this GB/s (mode 3; default 55; 0 = unlimited)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--timeout", type=float, default=3600.0)
     p.add_argument("--json-summary", action="store_true")
@@ -230,10 +233,13 @@ def main(argv=None) -> int:
         print(json.dumps({"level": "error", "node": my_id, "error": "unknown mode", "message": f"{role} failed"}),
               file=sys.stderr)
         return 1
+    if args.owner_policy is None:
+        args.owner_policy = "links" if args.engine == "rccl" else "random"
     policy = dict(seed=args.seed, owner_policy=args.owner_policy, pull_window=args.pull_window,
                   relay=not args.no_relay and args.bcast != "fanout", collective=args.bcast == "collective",
                   job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate,
-                  pull_job_bytes=args.pull_job_mib << 20, xgmi_link_gbps=args.xgmi_link_gbps)
+                  pull_job_bytes=args.pull_job_mib << 20, xgmi_link_gbps=args.xgmi_link_gbps,
+                  stage_gbps=args.pcie_gbps)
     rt.prepare(args.m, **policy)
     if barrier:
         barrier()

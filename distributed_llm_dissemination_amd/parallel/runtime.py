@@ -289,6 +289,12 @@ class Runtime:
             self.resumed.append(l)
         return layers
 
+    # Planning estimates for the GPU topology (per direction): one xGMI link as
+    # RCCL P2P drives it, and one GPU's PCIe host->HBM staging (57.5 GB/s
+    # measured, profiles/r1_h2d/).
+    XGMI_PLAN_GBPS = 50.0
+    PCIE_PLAN_GBPS = 55.0
+
     # Headroom kept free of layer slots: CRC workspaces, fp8 staging scratch,
     # RCCL's own buffers, PyTorch's context.
     HBM_HEADROOM = 4 << 30
@@ -414,9 +420,18 @@ class Runtime:
         job_timeout_s: float = 0.0,
         job_min_rate: float = 0.0,
         pull_job_bytes: int = 0,
-        xgmi_link_gbps: float = 0.0,
+        xgmi_link_gbps: Optional[float] = None,
+        stage_gbps: Optional[float] = None,
+        link_bw: Optional[Dict[tuple, int]] = None,
     ) -> None:
-        """Reset the data plane and start a fresh Node for the next epoch (untimed)."""
+        """Reset the data plane and start a fresh Node for the next epoch (untimed).
+
+        On the rccl engine the planners see the GPU topology by default: every
+        directed pair of GPUs as a link of ``xgmi_link_gbps`` (divided by its hop
+        count; default XGMI_PLAN_GBPS) and every GPU's host->HBM staging at
+        ``stage_gbps`` (default PCIE_PLAN_GBPS). ``link_bw`` overrides both the
+        config's Links and the probe (e.g. per-link rates measured in an earlier
+        session)."""
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()
@@ -433,8 +448,17 @@ class Runtime:
         nc.collective = collective
         nc.network_bw = {k: v for k, v in self.cfg.network_bw().items()}
         nc.link_bw = {(s, d): bw for s, per in self.cfg.links.items() for d, bw in per.items()}
-        if not nc.link_bw and xgmi_link_gbps > 0 and self.engine_kind == "rccl":
+        gpu = self.engine_kind == "rccl"
+        if xgmi_link_gbps is None:
+            xgmi_link_gbps = self.XGMI_PLAN_GBPS if gpu else 0.0
+        if stage_gbps is None:
+            stage_gbps = self.PCIE_PLAN_GBPS if gpu else 0.0
+        if not nc.link_bw and xgmi_link_gbps > 0 and gpu:
             nc.link_bw = self.topology_link_bw(xgmi_link_gbps)
+        if link_bw:
+            nc.link_bw = dict(link_bw)
+        if stage_gbps > 0:
+            nc.stage_bw = {n.id: int(stage_gbps * 1e9) for n in self.cfg.nodes}
         nc.integer_seconds = integer_seconds
         nc.job_timeout_s = job_timeout_s
         nc.job_min_rate = job_min_rate
