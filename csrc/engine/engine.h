@@ -40,6 +40,15 @@ class DataEngine {
                           int64_t rate) = 0;
   // Make [offset, offset+size) of `layer` resident in this node's target tier.
   virtual void load_range(LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) = 0;
+  // Host bytes of `layer` (a client stream landing in place at `base`) are
+  // present up to `prefix` of its `total` source bytes: cut-through engines
+  // may stage those chunks now.
+  virtual void host_prefix_ready(LayerID layer, const uint8_t* base, int64_t prefix, int64_t total) {
+    (void)layer;
+    (void)base;
+    (void)prefix;
+    (void)total;
+  }
   // Engine-specific control messages (GPU layer headers). Return true if consumed.
   virtual bool on_message(const MessagePtr&) { return false; }
   // Collective broadcast of a whole layer from this node to `dests` (GPU mode 0).

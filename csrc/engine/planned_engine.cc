@@ -229,6 +229,17 @@ void PlannedEngine::load_range(LayerID layer_id, int64_t offset, int64_t size, i
   req_cv_.notify_all();
 }
 
+void PlannedEngine::host_prefix_ready(LayerID layer_id, const uint8_t* base, int64_t prefix, int64_t total) {
+  {
+    std::lock_guard<std::mutex> lk(req_mu_);
+    Req r{Req::HostReady, {}, layer_id, prefix, total};
+    r.base = base;
+    reqs_.push_back(std::move(r));
+    busy_ = true;
+  }
+  req_cv_.notify_all();
+}
+
 void PlannedEngine::quiesce() {
   std::unique_lock<std::mutex> lk(req_mu_);
   // Bounded: a transfer whose peer died must not hang the caller forever.
@@ -527,6 +538,17 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   if (s == 1) return 1;
   if (s == 3) return 0;  // disk read in flight
   if (s == 4 && !want_landed) return 1;  // forward the bad copy; its receiver NACKs it as well
+  if (L.host && L.host_prefix >= 0) {
+    // A client stream still landing in host memory: its chunks stage as they
+    // complete (cut-through); a later one waits for host_prefix_ready.
+    if (c * src_grid(L) + src_len(L, c) > L.host_prefix) return 0;
+    if (s == 0 && stage_paced(L, id, c)) {
+      if (want_landed) local_wait_.push_back({id, c});
+      return 0;
+    }
+    stage_chunk(L, id, c);
+    return L.st[size_t(c)] == 1 ? 1 : 0;
+  }
   LayerSrc src;
   const bool have = node_ && node_->store().get(id, &src);
   // A client layer's host buffer exists while its stream is still landing; it
@@ -1041,6 +1063,7 @@ void PlannedEngine::take_requests(bool block) {
             L.fails[c] = 0;
           }
           L.host = nullptr;  // re-read the source from the next session's store
+          L.host_prefix = -1;
           L.client_requested = false;
           L.stage_rate = -1;
           if (cfg_.poison && !L.seeded && L.dev) backend_->zero_sync(L.dev, L.size);
@@ -1056,6 +1079,21 @@ void PlannedEngine::take_requests(bool block) {
       case Req::Shrink:
         do_shrink(r.dead, r.generation, r.comm_id);
         break;
+      case Req::HostReady: {
+        Layer& L = layer(r.layer);
+        if (!L.size || !r.base) break;
+        L.host = r.base;
+        L.path.clear();
+        const int64_t src_total = r.len;
+        L.host_prefix = r.off >= src_total ? -1 : r.off;
+        // Stage what this rank itself needs now; sends pick theirs up on their next pass.
+        for (int64_t c = 0; c < int64_t(L.st.size()); ++c) {
+          if (L.host_prefix >= 0 && c * src_grid(L) + src_len(L, c) > L.host_prefix) break;
+          if (L.want[size_t(c)] && L.st[size_t(c)] == 0 && ensure_chunk(L, r.layer, c, true) < 0)
+            fail("no source to load layer " + std::to_string(r.layer));
+        }
+        break;
+      }
       case Req::Stop:
         break;
     }

@@ -154,6 +154,7 @@ class PlannedEngine : public DataEngine {
   bool on_message(const MessagePtr& m) override;
   void send_range(NodeID dest, LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
   void load_range(LayerID layer, int64_t offset, int64_t size, int64_t total, int64_t rate) override;
+  void host_prefix_ready(LayerID layer, const uint8_t* base, int64_t prefix, int64_t total) override;
   void quiesce() override;
   void shutdown() override;
   int rank_of(NodeID n) const;
@@ -187,6 +188,7 @@ class PlannedEngine : public DataEngine {
     bool src_packed = false;         // the source already holds the packed image (persisted layers)
     bool client_requested = false;   // ClientReq sent for this session
     int64_t stage_rate = -1;         // source tier LimitRate (-1: not looked up yet)
+    int64_t host_prefix = -1;        // source bytes present at `host` (-1: all; a client stream still landing)
     int stage_tier = 0;
     // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk,
     // 4 failed its CRC and awaits the leader's re-send (still forwardable: a
@@ -211,13 +213,14 @@ class PlannedEngine : public DataEngine {
     bool ok = true;
   };
   struct Req {
-    enum Type { Batch, Load, Reset, Stop, Shrink } type;
+    enum Type { Batch, Load, Reset, Stop, Shrink, HostReady } type;
     std::vector<XferJob> jobs;
     LayerID layer = 0;
     int64_t off = 0, len = 0;
     std::vector<NodeID> dead;  // Shrink
     uint64_t generation = 0;   // Shrink
     std::string comm_id;       // Shrink: the survivors' new communicator id
+    const uint8_t* base = nullptr;  // HostReady: host copy; `off` = bytes present, `len` = total
   };
   struct Inflight {  // a P2P group on a comm lane
     Ev ev;

@@ -32,22 +32,47 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
   if (is_leader_) status_[cfg_.id] = store_.inventory();  // node.go:252-257
   e_->bind(this);
   if (is_leader_ && e_->planned()) manifests_ = e_->manifest();
-  if (e_->target() == Location::Inmem) {
-    // TCP payload bytes land directly in this node's store slot.
-    t_->set_landing([this](const Message& h) -> uint8_t* {
-      if (h.epoch && cfg_.epoch && h.epoch != cfg_.epoch) return nullptr;
-      try {
-        int64_t total = h.total_size ? h.total_size : h.data_size;
-        if (h.offset < 0 || h.offset + h.data_size > total) return nullptr;
-        return store_.host_landing(h.layer, total) + h.offset;
-      } catch (...) {
-        return nullptr;
+  // TCP payload bytes land directly in this node's host slot of the layer
+  // (host engines: the target itself; GPU engines: the staging source of a
+  // client-held layer, see on_layer).
+  LandingFn landing = [this](const Message& h) -> uint8_t* {
+    if (h.epoch && cfg_.epoch && h.epoch != cfg_.epoch) return nullptr;
+    try {
+      int64_t total = h.total_size ? h.total_size : h.data_size;
+      if (h.offset < 0 || h.offset + h.data_size > total) return nullptr;
+      return store_.host_landing(h.layer, total) + h.offset;
+    } catch (...) {
+      return nullptr;
+    }
+  };
+  ProgressFn progress;
+  if (e_->target() == Location::Device) {
+    // Cut-through (transport.go:144-196, at chunk grain): while a client
+    // stream is still arriving, every chunk that has fully landed in host
+    // memory is handed to the engine, which stages it into HBM and forwards it
+    // to the dests waiting on it before the rest of the layer is here.
+    progress = [this](const Message& h, int64_t got) {
+      if (h.epoch && cfg_.epoch && h.epoch != cfg_.epoch) return;
+      if (h.offset != 0) return;  // client streams carry whole layers from offset 0
+      const int64_t total = h.total_size ? h.total_size : h.data_size;
+      const int64_t step = std::max<int64_t>(e_->chunk_bytes(), 1);
+      const int64_t prefix = got >= total ? total : (got / step) * step;
+      {
+        std::lock_guard<std::mutex> lk(stream_mu_);
+        int64_t& done = stream_prefix_[h.layer];
+        if (prefix <= done) return;
+        done = prefix;
       }
-    });
+      e_->host_prefix_ready(h.layer, store_.host_landing(h.layer, total), prefix, total);
+    };
   }
+  t_->set_hooks(this, std::move(landing), std::move(progress));
 }
 
-Node::~Node() { stop(); }
+Node::~Node() {
+  stop();
+  t_->clear_hooks(this);
+}
 
 void Node::start() {
   if (running_.exchange(true)) return;
@@ -230,24 +255,26 @@ void Node::handle(const MessagePtr& m) {
 void Node::on_layer(const MessagePtr& m) {
   // A payload that arrived over the transport (node.go:1354-1384 / 1520-1567).
   int64_t total = m->total_size ? m->total_size : m->data_size;
-  if (!m->in_place && m->data) {
-    if (e_->target() == Location::Inmem) {
-      uint8_t* dst = store_.host_landing(m->layer, total);
-      if (m->offset < 0 || m->offset + m->data_size > total) throw std::runtime_error("layer range out of bounds");
-      memcpy(dst + m->offset, m->data->ptr + m->data_off, size_t(m->data_size));
-    } else {
-      // Device target: keep the host copy (e.g. from the external client), then
-      // stage it into HBM; the engine reports Landed when it is resident.
-      uint8_t* dst = store_.host_landing(m->layer, total);
-      memcpy(dst + m->offset, m->data->ptr + m->data_off, size_t(m->data_size));
-      LayerSrc src;
-      if (store_.get(m->layer, &src)) {
-        src.meta.location = Location::Inmem;
-        store_.put(m->layer, src);
-      }
-      e_->load_range(m->layer, m->offset, m->data_size, total, 0);
-      return;
+  if (e_->target() == Location::Device && (m->in_place || m->data)) {
+    // Device target: the host copy (e.g. from the external client) is the
+    // staging source; the engine reports Landed once the bytes are in HBM.
+    // Chunks that landed while the stream was arriving are already staged
+    // (set_progress above); this stages whatever is left.
+    uint8_t* dst = store_.host_landing(m->layer, total);
+    if (!m->in_place) memcpy(dst + m->offset, m->data->ptr + m->data_off, size_t(m->data_size));
+    LayerSrc src;
+    if (store_.get(m->layer, &src)) {
+      src.meta.location = Location::Inmem;
+      store_.put(m->layer, src);
     }
+    if (m->offset == 0 && m->data_size == total) e_->host_prefix_ready(m->layer, dst, total, total);
+    e_->load_range(m->layer, m->offset, m->data_size, total, 0);
+    return;
+  }
+  if (!m->in_place && m->data) {
+    uint8_t* dst = store_.host_landing(m->layer, total);
+    if (m->offset < 0 || m->offset + m->data_size > total) throw std::runtime_error("layer range out of bounds");
+    memcpy(dst + m->offset, m->data->ptr + m->data_off, size_t(m->data_size));
   }
   on_landed(m->layer, m->offset, m->data_size, total, m->src, m->dur_ms);
 }

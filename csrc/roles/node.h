@@ -224,6 +224,8 @@ class Node {
   uint64_t session_range_ = 0;  // roctx range: timer start -> assignment satisfied
   NodeStats stats_;
   std::set<LayerID> acked_;
+  std::mutex stream_mu_;  // reader threads of the transport
+  std::map<LayerID, int64_t> stream_prefix_;  // cut-through: host bytes of a client stream handed to the engine
 };
 
 // External client: a separate process holding rate-limited layers in memory

@@ -415,6 +415,9 @@ class TcpTransport : public Transport {
     }
     int64_t got = 0;
     const int64_t want = m->data_size;
+    // In-place landings report progress as bytes arrive (GPU engines stage and
+    // forward each chunk while the rest of the stream is still coming).
+    ProgressFn prog = m->in_place ? progress() : ProgressFn();
     // Buffered bytes first, then the socket.
     int64_t take = std::min<int64_t>(want, int64_t(buf.size()));
     if (take > 0) {
@@ -422,6 +425,7 @@ class TcpTransport : public Transport {
       if (pipe_conn) write_all(pipe_conn->fd, buf.data(), size_t(take));
       buf.erase(0, size_t(take));
       got = take;
+      if (prog) prog(*m, got);
     }
     while (got < want) {
       ssize_t r = ::recv(fd, dst + got, size_t(std::min<int64_t>(want - got, 8 << 20)), 0);
@@ -436,6 +440,7 @@ class TcpTransport : public Transport {
       }
       if (pipe_conn) write_all(pipe_conn->fd, dst + got, size_t(r));
       got += r;
+      if (prog) prog(*m, got);
     }
     bytes_received += want;
     m->dur_ms = double(log::now_us() - t0) / 1e3;

@@ -32,6 +32,9 @@ struct LayerPayload {
 // Receiver-side landing: given a Layer header, return where its bytes go
 // (host memory, at least data_size bytes), or nullptr to allocate a buffer.
 using LandingFn = std::function<uint8_t*(const Message& hdr)>;
+// Receiver-side progress of an in-place landing: `got` bytes of the range have
+// arrived (called from the reader thread as they come in; cut-through).
+using ProgressFn = std::function<void(const Message& hdr, int64_t got)>;
 
 class Transport {
  public:
@@ -62,9 +65,21 @@ class Transport {
     std::lock_guard<std::mutex> lk(reg_mu_);
     return registry_;
   }
-  void set_landing(LandingFn fn) {
+  // Receiver hooks of the node that currently runs on this transport (one
+  // node per session, the transport outlives it): `owner` tags them so a
+  // finished node clears only its own.
+  void set_hooks(const void* owner, LandingFn landing, ProgressFn progress) {
     std::lock_guard<std::mutex> lk(reg_mu_);
-    landing_ = std::move(fn);
+    hook_owner_ = owner;
+    landing_ = std::move(landing);
+    progress_ = std::move(progress);
+  }
+  void clear_hooks(const void* owner) {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    if (hook_owner_ != owner) return;
+    hook_owner_ = nullptr;
+    landing_ = nullptr;
+    progress_ = nullptr;
   }
 
   // Counters for observability.
@@ -83,10 +98,16 @@ class Transport {
     std::lock_guard<std::mutex> lk(reg_mu_);
     return landing_;
   }
+  ProgressFn progress() const {
+    std::lock_guard<std::mutex> lk(reg_mu_);
+    return progress_;
+  }
 
   mutable std::mutex reg_mu_;
   AddrRegistry registry_;
+  const void* hook_owner_ = nullptr;
   LandingFn landing_;
+  ProgressFn progress_;
   BlockingQueue<MessagePtr> inbox_;
 };
 

@@ -59,7 +59,11 @@ def n(request):
                                         (1, ["--pack", "fp8", "--layer-mib", "96"]),
                                         (1, ["--nccl-ctas", "4:16", "--reserve-cus", "64"]),
                                         (1, ["--nccl-register"])])
-def test_bench_modes(n, mode, extra):
+def test_bench_modes(n, mode, extra, request):
+    if n == 8 and _ngpus() < 2 and extra and extra != ["--pull-window", "2"]:
+        # one-GPU box: the 8-rank rehearsal covers modes 1/2/3 (every variant
+        # runs at 3 ranks; scripts/gpu.sh shared8 runs all of them at 8)
+        pytest.skip("variant covered at 3 ranks")
     r = _torchrun(n, ["bench.py", "--gpus", str(n), "--steps", "2", "--warmup", "1", "--layers", "16",
                       "--layer-mib", "64", "--chunk-mib", "16", "--mode", str(mode)] + extra)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -82,6 +86,8 @@ def test_cli_torchrun_rccl(n, tmp_path):
 
 
 def test_cli_rank_death_elastic_recovery(n, tmp_path):
+    if n == 8 and _ngpus() < 2:
+        pytest.skip("one-GPU box: rank death is rehearsed at 3 ranks")
     """A rank process dies mid-session (--inject kill-rank, os._exit): the
     survivors' RCCL groups with it fail or stall, the leader's probe finds it
     gone, the survivors abort the communicator and re-form one without it

@@ -124,3 +124,52 @@ def test_slow_link_costs_at_most_a_seventh_with_the_link_aware_plan():
     planned = predict_scaling.predict(8, slow_link=((0, 1), 0.5), plan_links=True, **kw)["ms_per_step"]
     assert slow > 1.5 * base, (base, slow)
     assert planned <= base * (1 + 1 / 7), (base, planned, slow)
+
+
+def test_client_stream_cut_through_to_peers():
+    """C17 pipe at chunk grain on the GPU data plane: node 1's external client
+    streams layer 9 at 20 MB/s; nodes 0 and 2 need it from node 1 over 20 MB/s
+    links. Node 1 stages and forwards each chunk as soon as it has landed in
+    host memory (transport.go:144-196 tees the TCP stream the same way), so the
+    session ends ~one stream time after the start - not stream + forward."""
+    from distributed_llm_dissemination_amd.parallel.runtime import layer_seed
+    from distributed_llm_dissemination_amd.utils.config import ClientConf
+
+    size, rate = 8 * MiB, 20_000_000
+    cfg = make_workload(3, 1, size, tier="host", seeding="leader", chunk_bytes=MiB)
+    cfg.clients.append(ClientConf(id=1, addr="", layers={9: rate}))
+    cfg.assignment = {r: [9] for r in range(3)}
+    key = f"tsim{os.getpid()}_{next(_keys)}"
+    t = _core.SimTiming()
+    t.link_bps = rate
+    _core.sim_set_timing(key, t)
+    data = _core.fill_random_host(size, layer_seed(0, 9))
+    ct = _core.tcp_transport("127.0.0.1:0", {}, True)
+    client = _core.ClientNode(1, ct, {9: _core.LayerSrc.inmem(data, rate)})
+    client.start()
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key) for i in range(3)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for i, r in enumerate(rts):
+        r.transport.set_registry({**reg, _core.CLIENT_ID: ct.address()} if i == 1 else reg)
+    ct.set_registry({1: reg[1]})
+    try:
+        for r in rts:
+            r.prepare(1)
+        res = [None] * 3
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(3)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        assert all(x.ok for x in res), [x.error for x in res]
+        for r in rts:
+            assert r.layer_bytes(9) == data
+        stream = (size - 256 * 1024) / rate  # the client's token bucket starts with a 256 KiB burst
+        assert dt < stream + 0.5 * size / rate, (dt, stream)  # store-and-forward would need stream + size/rate
+    finally:
+        for r in rts:
+            r.close()
+        client.stop()
+        ct.close()
