@@ -184,6 +184,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("data_size", &LayerSrc::data_size)
       .def_readwrite("offset", &LayerSrc::offset)
       .def_readwrite("meta", &LayerSrc::meta)
+      .def_readwrite("ranges", &LayerSrc::ranges)
       .def_property_readonly("has_host", [](const LayerSrc& s) { return bool(s.host); })
       .def_property_readonly("dev_ptr", [](const LayerSrc& s) { return reinterpret_cast<uintptr_t>(s.dev); })
       .def("host_bytes", [](const LayerSrc& s) { return host_bytes(s.host, 0, s.host ? s.host->size : 0); });
@@ -300,6 +301,7 @@ PYBIND11_MODULE(_core, m) {
       .def("manifest", &PlannedEngine::manifest)
       .def("set_source_packed", &PlannedEngine::set_source_packed)
       .def("set_seeded", &PlannedEngine::set_seeded)
+      .def("resident_chunks", &PlannedEngine::resident_chunks)
       .def("reset_session", [](PlannedEngine& e) {
         py::gil_scoped_release nogil;
         e.reset_session();

@@ -67,7 +67,11 @@ struct LayerSrc {
   int64_t data_size = 0;             // full layer size
   int64_t offset = 0;
   LayerMeta meta;
+  // Non-empty: only these [start, end) bytes of the layer are held (a copy
+  // resumed at chunk granularity from --persist-dir); not an owner of the rest.
+  std::vector<std::pair<int64_t, int64_t>> ranges;
 };
 using LayersSrc = std::map<LayerID, LayerSrc>;
+using PartialLayers = std::map<LayerID, std::vector<std::pair<int64_t, int64_t>>>;
 
 }  // namespace dissem

@@ -185,6 +185,20 @@ Json encode_payload(const Message& m) {
         }
         p["Manifest"] = man;
       }
+      if (!m.partial_layers.empty()) {
+        Json part = Json::object();
+        for (auto& kv : m.partial_layers) {
+          Json rs = Json::array();
+          for (auto& r : kv.second) {
+            Json e = Json::array();
+            e.push_back(Json(r.first));
+            e.push_back(Json(r.second));
+            rs.push_back(e);
+          }
+          part[std::to_string(kv.first)] = rs;
+        }
+        p["Partial"] = part;
+      }
       break;
     case MsgType::XferBatch: {
       src_id();
@@ -315,6 +329,12 @@ MessagePtr decode_envelope(const Json& env) {
           cm.chunk_bytes = e.at(0).as_i64();
           for (auto& x : e.at(1).as_array()) cm.crc.push_back(uint32_t(x.as_u64()));
           m->manifest[LayerID(strtoull(kv.first.c_str(), nullptr, 10))] = cm;
+        }
+      }
+      if (auto* part = p.find("Partial"); part && part->is_object()) {
+        for (auto& kv : part->as_object()) {
+          auto& rs = m->partial_layers[LayerID(strtoull(kv.first.c_str(), nullptr, 10))];
+          for (auto& e : kv.second.as_array()) rs.push_back({e.as_array().at(0).as_i64(), e.as_array().at(1).as_i64()});
         }
       }
       break;

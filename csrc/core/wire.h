@@ -91,6 +91,7 @@ struct Message {
   uint64_t batch = 0;
   std::vector<XferJob> jobs;
   std::map<LayerID, CrcManifest> manifest;
+  PartialLayers partial_layers;  // Announce extension: layers held only in these byte ranges
   // Simple
   std::string src_addr, payload_str;
 

@@ -166,6 +166,16 @@ void PlannedEngine::set_source_packed(LayerID id, bool packed) {
   layers_[id].src_packed = packed;
 }
 
+std::vector<int64_t> PlannedEngine::resident_chunks(LayerID id) {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  std::vector<int64_t> out;
+  auto it = layers_.find(id);
+  if (it == layers_.end()) return out;
+  for (size_t c = 0; c < it->second.st.size(); ++c)
+    if (it->second.st[c] == 2) out.push_back(int64_t(c));
+  return out;
+}
+
 std::map<LayerID, CrcManifest> PlannedEngine::manifest() {
   std::lock_guard<std::mutex> lk(req_mu_);
   std::map<LayerID, CrcManifest> out;

@@ -136,6 +136,8 @@ class PlannedEngine : public DataEngine {
   // The layer's host/disk source is already in the slot format (e.g. a layer
   // persisted by an earlier run): stage it byte for byte, without packing.
   void set_source_packed(LayerID layer, bool packed);
+  // Grid chunks of a layer verified resident in HBM (call while no session runs).
+  std::vector<int64_t> resident_chunks(LayerID layer);
   void reset_session();  // wait idle, forget landed chunks, poison non-seeded slots
   PlannedStats stats();
   std::string error();

@@ -29,7 +29,10 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
       is_leader_(is_leader),
       rng_(cfg_.seed) {
   if (cfg_.id != cfg_.leader) add_node(cfg_.leader);  // node.go:58-60
-  if (is_leader_) status_[cfg_.id] = store_.inventory();  // node.go:252-257
+  if (is_leader_) {
+    status_[cfg_.id] = store_.inventory();  // node.go:252-257
+    partial_[cfg_.id] = store_.partial();
+  }
   e_->bind(this);
   if (is_leader_ && e_->planned()) manifests_ = e_->manifest();
   // TCP payload bytes land directly in this node's host slot of the layer
@@ -150,7 +153,12 @@ void Node::announce() {
   Message m;
   m.type = MsgType::Announce;
   m.layers = store_.inventory();
-  if (e_->planned()) m.manifest = e_->manifest();
+  m.partial_layers = store_.partial();
+  if (e_->planned()) {
+    // Manifests of whole copies only: a resumed partial copy knows just its own chunks.
+    for (auto& kv : e_->manifest())
+      if (m.layers.count(kv.first)) m.manifest[kv.first] = kv.second;
+  }
   NodeID hop = next_hop(cfg_.leader);
   trace::mark("dissem.announce");
   if (!send_msg(hop, m)) throw std::runtime_error("announce failed");
@@ -421,6 +429,7 @@ void Node::on_announce(const MessagePtr& m) {
   if (!status_.count(m->src)) {
     std::lock_guard<std::mutex> lk(sig_mu_);
     status_[m->src] = m->layers;
+    partial_[m->src] = m->partial_layers;
     add_node(m->src);
   }
   for (auto& kv : m->manifest) {
@@ -1007,6 +1016,33 @@ void Node::schedule_mode1() {
           retransmit(layer, dest, dest);
           continue;
         }
+        // Chunk-granular resume: a dest that announced part of this layer (its
+        // persisted chunks) loads those ranges locally and receives only the gaps.
+        std::vector<std::pair<int64_t, int64_t>> gaps{{0, layer_size(layer)}};
+        if (e_->planned()) {
+          auto pit = partial_.find(dest);
+          auto lit = pit == partial_.end() ? PartialLayers::const_iterator() : pit->second.find(layer);
+          if (pit != partial_.end() && lit != pit->second.end() && !lit->second.empty()) {
+            gaps.clear();
+            int64_t pos = 0;
+            for (auto r : lit->second) {
+              r.second = std::min(r.second, layer_size(layer));
+              if (r.first >= r.second) continue;
+              if (r.first > pos) gaps.push_back({pos, r.first});
+              {
+                std::lock_guard<std::mutex> lk(sig_mu_);
+                stats_.jobs_dispatched++;
+              }
+              add_job(dest, dest, layer, r.first, r.second - r.first);
+              pos = std::max(pos, r.second);
+            }
+            if (pos < layer_size(layer)) gaps.push_back({pos, layer_size(layer)});
+            if (gaps.empty()) continue;
+          }
+        }
+        int64_t need = 0;
+        for (auto& g : gaps) need += g.second - g.first;
+        const bool ranged = gaps.size() != 1 || need != layer_size(layer);
         std::vector<NodeID> cand(oit->second.begin(), oit->second.end());
         NodeID owner;
         if (links) {
@@ -1016,14 +1052,13 @@ void Node::schedule_mode1() {
           owner = cand[0];
           std::pair<double, int64_t> best{1e300, INT64_MAX};
           for (NodeID c : cand) {
-            std::pair<double, int64_t> k{double(link_bytes_[{c, dest}] + layer_size(layer)) / cap(c, dest),
-                                         owner_bytes_[c]};
+            std::pair<double, int64_t> k{double(link_bytes_[{c, dest}] + need) / cap(c, dest), owner_bytes_[c]};
             if (k < best) {
               best = k;
               owner = c;
             }
           }
-          link_bytes_[{owner, dest}] += layer_size(layer);
+          link_bytes_[{owner, dest}] += need;
         } else if (cfg_.owner_policy == "balanced") {
           int64_t best = INT64_MAX;
           std::vector<NodeID> ties;
@@ -1040,9 +1075,17 @@ void Node::schedule_mode1() {
         } else {
           owner = cand[size_t(rng_() % cand.size())];  // uniform (quirk Q5)
         }
-        owner_bytes_[owner] += layer_size(layer);
+        owner_bytes_[owner] += need;
         if (links && e_->planned()) {
-          plan[{dest, layer}].push_back(PlanPart{owner, 0, layer_size(layer), 0});
+          for (auto& g : gaps) plan[{dest, layer}].push_back(PlanPart{owner, g.first, g.second - g.first, 0});
+        } else if (ranged) {
+          for (auto& g : gaps) {
+            {
+              std::lock_guard<std::mutex> lk(sig_mu_);
+              stats_.jobs_dispatched++;
+            }
+            add_job(owner, dest, layer, g.first, g.second - g.first);
+          }
         } else {
           retransmit(layer, owner, dest);
         }

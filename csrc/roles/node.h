@@ -224,6 +224,7 @@ class Node {
   uint64_t session_range_ = 0;  // roctx range: timer start -> assignment satisfied
   NodeStats stats_;
   std::set<LayerID> acked_;
+  std::map<NodeID, PartialLayers> partial_;  // leader: announced partial copies (chunk-granular resume)
   std::mutex stream_mu_;  // reader threads of the transport
   std::map<LayerID, int64_t> stream_prefix_;  // cut-through: host bytes of a client stream handed to the engine
 };

@@ -68,11 +68,20 @@ LayerIDs LayerStore::inventory() {
     // A provisioned-but-empty device slot is not an inventory entry.
     if (!s.has_target && !s.src.host && s.src.path.empty() && s.src.meta.location != Location::Client)
       continue;
+    if (!s.has_target && !s.src.ranges.empty()) continue;  // partial copy: announced separately
     LayerMeta m = s.src.meta;
     m.size = s.total;
     if (s.has_target) m.location = target_;
     out[kv.first] = m;
   }
+  return out;
+}
+
+PartialLayers LayerStore::partial() {
+  std::lock_guard<std::mutex> lk(mu);
+  PartialLayers out;
+  for (auto& kv : slots_)
+    if (!kv.second.has_target && !kv.second.src.ranges.empty()) out[kv.first] = kv.second.src.ranges;
   return out;
 }
 

@@ -49,6 +49,8 @@ class LayerStore {
   Location target() const { return target_; }
   // Inventory for Announce: {layer: {Location, LimitRate, SourceType, DataSize}}.
   LayerIDs inventory();
+  // Layers held only in part (resumed chunk ranges), for Announce's Partial.
+  PartialLayers partial();
   bool get(LayerID id, LayerSrc* out);
   bool has_target(LayerID id);
   void put(LayerID id, const LayerSrc& src);

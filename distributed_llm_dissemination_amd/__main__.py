@@ -262,10 +262,16 @@ def main(argv=None) -> int:
     if not res.ok:
         print(json.dumps({"level": "error", "node": my_id, "error": res.error, "message": f"{role} failed"}),
               file=sys.stderr)
-    elif args.persist_dir and cfg.assignment.get(my_id):
-        done = rt.persist()
-        print(json.dumps({"level": "info", "node": my_id, "layers": done, "dir": args.persist_dir,
-                          "message": "layers persisted"}), file=sys.stderr)
+    if args.persist_dir and cfg.assignment.get(my_id) and (res.ok or rt.engine is not None):
+        # After a failed session the planned engines keep what did land, chunk
+        # by chunk: the next run with the same --persist-dir resumes from there.
+        try:
+            done = rt.persist(partial=not res.ok)
+            print(json.dumps({"level": "info", "node": my_id, "layers": done, "dir": args.persist_dir,
+                              "partial": not res.ok, "message": "layers persisted"}), file=sys.stderr)
+        except Exception as e:  # noqa: BLE001 - a failed session must still exit cleanly
+            print(json.dumps({"level": "error", "node": my_id, "error": str(e)[:300],
+                              "message": "persist failed"}), file=sys.stderr)
     if barrier:
         # A rank may have died during the session (elastic recovery): do not
         # wait for it forever.

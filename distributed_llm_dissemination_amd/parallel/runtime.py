@@ -281,8 +281,15 @@ class Runtime:
             if l in layers:
                 continue
             # A layer this node received in an earlier run: announce it as a disk-tier
-            # copy, so the leader promotes it locally instead of moving it again.
-            layers[l] = _core.LayerSrc.disk(path, self.slot_sizes[l], 0, _core.SourceType.Disk)
+            # copy, so the leader promotes it locally instead of moving it again. A
+            # layer persisted in part (chunk-granular resume) is announced as the
+            # byte ranges of its chunks; the leader plans only the rest.
+            src = _core.LayerSrc.disk(path, self.slot_sizes[l], 0, _core.SourceType.Disk)
+            ranges = self._chunk_ranges(entry, self.slot_sizes[l])
+            if ranges is not None:
+                src.ranges = ranges
+                self.resumed_partial.append(l)
+            layers[l] = src
             if gpu:
                 self.engine.set_manifest(l, _core.CrcManifest(self.grid, entry["crc"]))
                 self.engine.set_source_packed(l, True)
@@ -317,9 +324,25 @@ class Runtime:
     def _persist_root(self) -> str:
         return os.path.join(self.persist_dir, str(self.node_id))
 
+    def _chunk_ranges(self, entry, stored: int):
+        """Merged [start, end) byte ranges of a partial entry's chunks (None: whole layer)."""
+        chunks = entry.get("chunks")
+        n = (stored + self.grid - 1) // self.grid
+        if chunks is None or len(set(chunks)) >= n:
+            return None
+        out = []
+        for c in sorted(set(chunks)):
+            a, b = c * self.grid, min((c + 1) * self.grid, stored)
+            if out and out[-1][1] == a:
+                out[-1] = (out[-1][0], b)
+            else:
+                out.append((a, b))
+        return out
+
     def _resumable(self) -> Dict[int, tuple]:
         """Persisted layers whose file and manifest entry match this run's layout."""
         self.resumed: List[int] = []
+        self.resumed_partial: List[int] = []
         if not self.persist_dir:
             return {}
         root = self._persist_root()
@@ -334,16 +357,21 @@ class Runtime:
             path = os.path.join(root, f"{l}.layer")
             if (l not in self.sizes or e.get("size") != self.sizes[l] or e.get("stored") != self.slot_sizes[l]
                     or e.get("pack") != self.pack or e.get("grid") != self.grid or not os.path.exists(path)
-                    or os.path.getsize(path) != e["stored"]):
+                    or os.path.getsize(path) != e["stored"] or (e.get("chunks") is not None and not e["chunks"])):
                 continue
             out[l] = (path, e)
         return out
 
-    def persist(self, layers: Optional[List[int]] = None) -> List[int]:
+    def persist(self, layers: Optional[List[int]] = None, partial: bool = False) -> List[int]:
         """Write this node's target-tier layers (default: its assignment) to
         <persist_dir>/<node>/<layer>.layer plus a manifest (size, slot size,
         packing, chunk grid, CRC32C per chunk). SURVEY §5.4; a later run with
-        the same --persist-dir announces them as disk-tier layers."""
+        the same --persist-dir announces them as disk-tier layers.
+
+        ``partial`` (planned engines, e.g. after a failed session): also keep
+        layers that landed only in part - each verified-resident chunk is
+        written at its offset of a sparse layer file and listed under
+        "chunks", so the next run receives only the missing chunks."""
         if not self.persist_dir:
             raise ValueError("no persist_dir configured")
         root = self._persist_root()
@@ -360,24 +388,43 @@ class Runtime:
             stored = self.slot_sizes[l]
             path = os.path.join(root, f"{l}.layer")
             tmp = path + ".tmp"
+            entry = {"size": self.sizes[l], "stored": stored, "pack": self.pack, "grid": self.grid}
             if self.engine is not None:
                 ptr = self.engine.device_ptr(l)
-                crc = self._dev_crc(ptr, stored)
+                nchunks = (stored + self.grid - 1) // self.grid
+                have = list(self.engine.resident_chunks(l)) if partial else list(range(nchunks))
+                if not have:
+                    continue
+                whole = len(have) == nchunks
+                crc_all = self._dev_crc(ptr, stored)
+                crc = [crc_all[c] if c in set(have) else 0 for c in range(nchunks)]
                 step = max(self.grid, 64 * MiB // self.grid * self.grid)
                 buf = (_core.HostBuffer.pinned(step) if self.engine_kind == "rccl" else _core.HostBuffer.malloc(step))
                 with open(tmp, "wb") as f:
-                    for off in range(0, stored, step):
-                        n = min(step, stored - off)
-                        self._dev_to_host(buf.ptr, ptr + off, n)
-                        f.write(buf.view()[:n])
+                    f.truncate(stored)  # sparse: chunks that did not land stay holes
+                    if whole:
+                        for off in range(0, stored, step):
+                            n = min(step, stored - off)
+                            self._dev_to_host(buf.ptr, ptr + off, n)
+                            f.write(buf.view()[:n])
+                    else:
+                        for c in have:
+                            off, n = c * self.grid, min(self.grid, stored - c * self.grid)
+                            self._dev_to_host(buf.ptr, ptr + off, n)
+                            f.seek(off)
+                            f.write(buf.view()[:n])
+                if not whole:
+                    entry["chunks"] = sorted(have)
             else:
                 data = self._last_node.layer(l).host_bytes()
+                if not data:
+                    continue
                 crc = [_core.crc32c(data[o : o + self.grid]) for o in range(0, len(data), self.grid)]
                 with open(tmp, "wb") as f:
                     f.write(data)
+            entry["crc"] = crc
             os.replace(tmp, path)
-            man["layers"][str(l)] = {"size": self.sizes[l], "stored": stored, "pack": self.pack,
-                                     "grid": self.grid, "crc": crc}
+            man["layers"][str(l)] = entry
             done.append(l)
         with open(mpath + ".tmp", "w") as f:
             json.dump(man, f)

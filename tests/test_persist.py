@@ -109,3 +109,64 @@ def test_resume_ignores_mismatched_layout_and_detects_corruption(tmp_path):
     finally:
         for r in rts:
             r.close()
+
+
+@pytest.mark.parametrize("owner_policy", ["random", "links"])
+def test_chunk_granular_resume_moves_only_missing_chunks(tmp_path, owner_policy):
+    """A rank that persisted only part of a layer (its resident chunks after a
+    failed session, Runtime.persist(partial=True)) announces those byte ranges;
+    the leader has it load them from its disk copy and sends only the missing
+    chunks (resumable at chunk granularity)."""
+    size = 4 * MiB
+    cfg = make_workload(3, 3, size, tier="host", seeding="random", chunk_bytes=MiB)
+    rts, key = _cluster(cfg, tmp_path)
+    try:
+        assert all(x.ok for x in _session(rts))
+        full = {l: rts[2].layer_bytes(l) for l in range(3)}
+        held = [l for l in range(3) if l in cfg.node(2).initial_layers.get(2, {})]
+        missing = [l for l in range(3) if l not in held]
+        target = missing[0]
+        # Keep 2 of node 2's 4 chunks of one received layer: write them as a partial persisted copy.
+        rts[2].persist(layers=[target])
+    finally:
+        for r in rts:
+            r.close()
+    import json
+
+    root = os.path.join(str(tmp_path), "2")
+    man = json.load(open(os.path.join(root, "manifest.json")))
+    e = man["layers"][str(target)]
+    e["chunks"] = [0, 2]
+    e["crc"] = [c if i in (0, 2) else 0 for i, c in enumerate(e["crc"])]
+    json.dump(man, open(os.path.join(root, "manifest.json"), "w"))
+    # the chunks that "did not land" are holes in the layer file
+    with open(os.path.join(root, f"{target}.layer"), "r+b") as f:
+        for c in (1, 3):
+            f.seek(c * MiB)
+            f.write(bytes(MiB))
+    # Node 0 and 1 start without persisted state.
+    for n in ("0", "1"):
+        import shutil
+
+        shutil.rmtree(os.path.join(str(tmp_path), n), ignore_errors=True)
+    rts, key = _cluster(cfg, tmp_path)
+    try:
+        assert rts[2].resumed_partial == [target]
+        for r in rts:
+            r.prepare(1, owner_policy=owner_policy)
+        res = [None] * 3
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        for r in rts:
+            for l in range(3):
+                assert r.layer_bytes(l) == full[l], (l,)
+        # Node 2 received the two missing chunks of `target` and every byte of the others.
+        got = rts[2].link_bytes()["recv"]
+        assert sum(got.values()) == (len(missing) - 1) * size + 2 * MiB
+    finally:
+        for r in rts:
+            r.close()
