@@ -58,6 +58,9 @@ def parse_args(argv=None):
     p.add_argument("--pack", default="none", choices=["none", "fp8"],
                    help="fp8: layers are bf16 sources packed to block-scaled e4m3fn while staging "
                         "(HBM + wire format; BASELINE config #5)")
+    p.add_argument("--store", default="packed", choices=["packed", "bf16"],
+                   help="with --pack fp8: bf16 = every resident chunk is also dequantized to bf16 in HBM by the "
+                        "fused verify+unpack kernel (the receive path of an inference deployment)")
     p.add_argument("--reserve-cus", type=int, default=-1,
                    help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
@@ -146,6 +149,7 @@ def main(argv=None) -> int:
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
+                 store=args.store,
                  engine_opts=engine_opts(args))
     if args.pack != "none":
         # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
@@ -241,6 +245,7 @@ def main(argv=None) -> int:
             out["config"]["model"] = f"{args.layers}x{args.layer_mib}MiB bf16 layers (Llama-3.1-405B-sized shards), fp8 in HBM"
             out["config"]["bf16_source_bytes_per_step"] = src_bytes
             out["config"]["bf16_equivalent_GBps"] = round(src_bytes * args.steps / total / 1e9, 3)
+            out["config"]["store"] = args.store
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
         if world > 1:

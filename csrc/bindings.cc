@@ -265,6 +265,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas)
       .def_readwrite("nccl_register", &PlannedConfig::nccl_register)
       .def_readwrite("lanes", &PlannedConfig::lanes)
+      .def_readwrite("unpack_store", &PlannedConfig::unpack_store)
       .def_readwrite("link_rate", &PlannedConfig::link_rate);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
@@ -297,6 +298,7 @@ PYBIND11_MODULE(_core, m) {
       .def("slot_size", &PlannedEngine::slot_size)
       .def_property_readonly("chunk_grid", &PlannedEngine::chunk_bytes)
       .def("device_ptr", [](PlannedEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.device_ptr(l)); })
+      .def("unpacked_ptr", [](PlannedEngine& e, LayerID l) { return reinterpret_cast<uint64_t>(e.unpacked_ptr(l)); })
       .def("set_manifest", &PlannedEngine::set_manifest)
       .def("manifest", &PlannedEngine::manifest)
       .def("set_source_packed", &PlannedEngine::set_source_packed)

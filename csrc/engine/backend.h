@@ -87,6 +87,11 @@ class Backend {
     }
     return last ? last : crc(nullptr, 0, 0, after);
   }
+  // verify queue: after `after`, the fused check + dequantization of one packed
+  // chunk (core/fp8.h layout of `src_len` bf16 source bytes on a `src_chunk`
+  // grid): CRC32C of the packed bytes into `slot`, bf16 values to `out`.
+  virtual Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out,
+                           uint32_t slot, Ev after) = 0;
   virtual int query(Ev e) = 0;  // 1 done, 0 pending, -1 failed
   virtual void release(Ev e) = 0;
   virtual uint32_t crc_result(uint32_t slot) = 0;

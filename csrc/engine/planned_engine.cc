@@ -63,6 +63,7 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
   } else if (cfg_.pack != 0) {
     throw std::runtime_error("unknown pack format " + std::to_string(cfg_.pack));
   }
+  if (cfg_.unpack_store && cfg_.pack != 1) throw std::runtime_error("unpack_store needs pack = fp8");
   inject_rng_.seed(cfg_.inject_seed * 0x9E3779B97F4A7C15ull + uint64_t(cfg_.rank));
   lanes_ = std::max(1, backend_->lanes());
   ops_.resize(size_t(lanes_));
@@ -90,8 +91,10 @@ void PlannedEngine::shutdown() {
   for (auto* b : bounce_all_) backend_->free_host(b);
   bounce_all_.clear();
   bounce_free_.clear();
-  for (auto& kv : layers_)
+  for (auto& kv : layers_) {
     if (kv.second.dev) backend_->free(kv.second.dev);
+    if (kv.second.out) backend_->free(kv.second.out);
+  }
   layers_.clear();
   backend_->destroy(failed_.load());
 }
@@ -140,6 +143,12 @@ uint8_t* PlannedEngine::provision(LayerID id, int64_t size) {
   if (L.size != size) throw std::runtime_error("layer " + std::to_string(id) + " re-provisioned with another size");
   if (!L.dev) L.dev = backend_->alloc(size);
   return L.dev;
+}
+
+uint8_t* PlannedEngine::unpacked_ptr(LayerID id) {
+  std::lock_guard<std::mutex> lk(req_mu_);
+  auto it = layers_.find(id);
+  return it == layers_.end() ? nullptr : it->second.out;
 }
 
 uint8_t* PlannedEngine::device_ptr(LayerID id) {
@@ -350,6 +359,14 @@ bool PlannedEngine::stage_paced(Layer& L, LayerID id, int64_t c) {
   return false;
 }
 
+Ev PlannedEngine::unpack_chunk(Layer& L, int64_t c, uint32_t slot, Ev after) {
+  const int64_t src_total = fp8::source_size(L.size, cfg_.chunk_bytes, cfg_.pack_block);
+  if (!L.out) L.out = backend_->alloc(src_total);
+  const int64_t slen = std::min(cfg_.chunk_bytes, src_total - c * cfg_.chunk_bytes);
+  return backend_->verify_unpack(L.dev + c * grid_, slen, cfg_.chunk_bytes, cfg_.pack_block,
+                                 L.out + c * cfg_.chunk_bytes, slot, after);
+}
+
 void PlannedEngine::landed(const Piece& p) {
   if (!node_) return;
   auto m = std::make_shared<Message>();
@@ -515,7 +532,17 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
   p.src_node = self_node_;
   Verify v;
-  if (cfg_.verify && int64_t(L.manifest.crc.size()) > c) {
+  if (cfg_.unpack_store) {
+    // fused: check the packed chunk and write its bf16 image (one pass)
+    const bool check = cfg_.verify && int64_t(L.manifest.crc.size()) > c;
+    if (check) {
+      p.has_crc = true;
+      p.crc = L.manifest.crc[size_t(c)];
+    }
+    uint32_t slot = crc_slot();
+    v.ev = unpack_chunk(L, c, slot, e);
+    v.slots.push_back(check ? slot : ~0u);
+  } else if (cfg_.verify && int64_t(L.manifest.crc.size()) > c) {
     p.has_crc = true;
     p.crc = L.manifest.crc[size_t(c)];
     uint32_t slot = crc_slot();
@@ -681,7 +708,8 @@ bool PlannedEngine::issue_lane(int lane) {
   auto& q = ops_[size_t(lane)];
   auto& infl = inflight_[size_t(lane)];
   const auto now = std::chrono::steady_clock::now();
-  while (!q.empty() && int(infl.size()) < cfg_.max_inflight_groups && !failed_) {
+  const int cap = std::max(4, cfg_.max_inflight_groups / lanes_);
+  while (!q.empty() && int(infl.size()) < cap && !failed_) {
     std::vector<Piece> group;
     std::map<int, int> nsend, nrecv;
     std::set<std::pair<LayerID, int64_t>> recv_chunks;
@@ -797,15 +825,25 @@ bool PlannedEngine::issue_lane(int lane) {
         set_chunk_ev(L, p.chunk, 0);  // pending on the comm queue itself: later sends are ordered behind it
       }
       uint32_t slot = ~0u;
-      if (cfg_.verify && p.has_crc && p.full) {
+      if (cfg_.unpack_store && p.full && !p.bcast) {
+        // fused check + dequantization of the landed packed chunk, per chunk
+        const uint32_t s = crc_slot();
+        if (last) backend_->release(last);
+        last = unpack_chunk(L, p.chunk, s, landed_ev);
+        if (cfg_.verify && p.has_crc) slot = s;
+      } else if (cfg_.verify && p.has_crc && p.full) {
         slot = crc_slot();
         checks.push_back(Backend::CrcReq{L.dev + p.off, p.len, slot});
       }
       v.pieces.push_back(p);
       v.slots.push_back(slot);
     }
-    // Every chunk this group landed is checked by one batched launch.
-    if (!v.pieces.empty()) last = backend_->crc_batch(checks, landed_ev);
+    // Every chunk this group landed is checked by one batched launch (behind
+    // any fused unpacks, which share the verify queue).
+    if (!v.pieces.empty() && (!checks.empty() || !last)) {
+      if (last) backend_->release(last);
+      last = backend_->crc_batch(checks, landed_ev);
+    }
     if (landed_ev != g) backend_->release(landed_ev);
     if (!v.pieces.empty()) {
       v.ev = last;

@@ -52,7 +52,11 @@ struct PlannedConfig {
   int64_t chunk_bytes = 64ll << 20;
   bool verify = true;
   bool poison = true;              // zero non-seeded slots between sessions
-  int max_inflight_groups = 64;   // per lane
+  // P2P groups in flight per rank, split evenly over the lanes (at least 4
+  // per lane): enough queued link time to hide the issue thread, few enough
+  // that RCCL's proxy never runs out of op slots behind a dead peer (which
+  // would block ncclGroupEnd on the host).
+  int max_inflight_groups = 64;
   // Independent comm lanes (communicator + stream each; backend.h lane_of).
   // 0 = auto: one lane per directed link, so every xGMI link of a GPU sends or
   // receives on its own. One-distance lanes are also what keeps irregular
@@ -69,6 +73,12 @@ struct PlannedConfig {
   // chunk grid. chunk_bytes stays the SOURCE (bf16) chunk.
   int pack = 0;                    // 0 none, 1 fp8 e4m3fn block-scaled
   int pack_block = 128;            // elements per f32 scale
+  // pack = fp8 only: every chunk that becomes resident (received or staged) is
+  // also dequantized to bf16 into a second HBM slot of the layer by the fused
+  // verify+unpack kernel - the CRC check and the dequantization in one pass
+  // over the packed bytes (--store bf16). Every rank then holds the same bf16
+  // image (the source rank too: it unpacks its own packed chunks).
+  bool unpack_store = false;
   // Fault handling: a chunk that fails its CRC is NACKed to the
   // leader, which re-sends it; after max_retries failures of one chunk the
   // engine fails. inject_corrupt overwrites received chunks with this
@@ -131,6 +141,7 @@ class PlannedEngine : public DataEngine {
   // ---- setup (call while no session runs)
   uint8_t* provision(LayerID layer, int64_t size);
   uint8_t* device_ptr(LayerID layer);
+  uint8_t* unpacked_ptr(LayerID layer);  // bf16 slot (unpack_store), nullptr if none yet
   void set_manifest(LayerID layer, const CrcManifest& m);
   void set_seeded(LayerID layer, bool device_resident);
   // The layer's host/disk source is already in the slot format (e.g. a layer
@@ -182,6 +193,7 @@ class PlannedEngine : public DataEngine {
   struct Layer {
     int64_t size = 0;
     uint8_t* dev = nullptr;
+    uint8_t* out = nullptr;          // unpack_store: bf16 slot (source size)
     bool seeded = false;
     CrcManifest manifest;
     const uint8_t* host = nullptr;   // host-tier source (set at first staging)
@@ -277,6 +289,8 @@ class PlannedEngine : public DataEngine {
   void landed(const Piece& p);
   void nack(const Piece& p, Layer& L, uint32_t got);
   uint32_t crc_slot();
+  // unpack_store: the fused check of chunk c (packed at L.dev) into its bf16 slot, after `after`.
+  Ev unpack_chunk(Layer& L, int64_t c, uint32_t slot, Ev after);
   void fail(const std::string& what);
   int64_t src_len(const Layer& L, int64_t c) const;  // source bytes of chunk c
   int64_t src_grid(const Layer& L) const { return cfg_.pack == 1 && !L.src_packed ? cfg_.chunk_bytes : grid_; }

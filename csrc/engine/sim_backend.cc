@@ -375,6 +375,26 @@ class SimBackend : public Backend {
     return id;
   }
 
+  Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out, uint32_t slot,
+                   Ev after) override {
+    auto [id, ev] = make_event();
+    auto dep = lookup(after);
+    const bool copy = fab_->timing.copy_bytes;
+    verify_.push([=] {
+      if (dep && !wait_event(dep, kTimeout)) {
+        ev->state = -1;
+        return;
+      }
+      (void)src_chunk;
+      const int64_t n = src_len / 2;
+      const int64_t plen = fp8::packed_len(src_len, block);
+      results_[slot] = crc32c(packed, size_t(plen));
+      if (copy) fp8::unpack_host(packed, reinterpret_cast<const float*>(packed + n), n, reinterpret_cast<uint16_t*>(out), block);
+      ev->state = 1;
+    });
+    return id;
+  }
+
   int query(Ev e) override {
     auto ev = lookup(e);
     if (!ev) return -1;

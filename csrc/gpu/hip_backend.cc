@@ -271,6 +271,15 @@ class HipBackend : public Backend {
     return record(verify_);
   }
 
+  Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out, uint32_t slot,
+                   Ev after) override {
+    if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
+    if (src_len > cfg_.max_crc_bytes) throw std::runtime_error("verify_unpack chunk larger than the verify workspace");
+    HIP_OK(kern::fp8_verify_unpack(packed, src_len, src_chunk, block, reinterpret_cast<uint16_t*>(out), crc_dev_ + slot,
+                                   ws_, verify_));
+    return record(verify_);
+  }
+
   int query(Ev e) override {
     hipError_t r = hipEventQuery(ev(e));
     if (r == hipSuccess) return 1;
@@ -313,10 +322,11 @@ class HipBackend : public Backend {
     // comm streams drain. (ncclCommShrink would keep the bootstrap, but the RCCL
     // PyTorch loads into the process predates it; abort + re-init of the
     // survivors works with any RCCL.)
-    for (auto& c : nccl_) {
-      if (c) (void)ncclCommAbort(c);
-      c = nullptr;
+    for (size_t l = nccl_.size(); l-- > 0;) {  // split lanes before the parent
+      if (nccl_[l]) (void)ncclCommAbort(nccl_[l]);
+      nccl_[l] = nullptr;
     }
+    log::warn(cfg_.rank).i("lanes", int64_t(nccl_.size())).msg("rccl communicators aborted; draining queues");
     std::vector<std::pair<uint8_t*, int64_t>> regd;  // re-register with the new communicators
     for (auto& kv : regs_) regd.push_back({kv.first, kv.second.first});
     regs_.clear();
@@ -340,7 +350,7 @@ class HipBackend : public Backend {
       auto t0 = std::chrono::steady_clock::now();
       hipError_t q;
       while ((q = hipEventQuery(e)) == hipErrorNotReady) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20)) {
           (void)hipEventDestroy(e);
           throw std::runtime_error("queues did not drain after ncclCommShrink");
         }

@@ -68,6 +68,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--pack", default="none", choices=["none", "fp8"],
                    help="fp8: bf16 layers are packed to block-scaled e4m3fn on staging (wire + HBM format)")
     p.add_argument("--pack-block", type=int, default=128, help="elements per fp8 scale")
+    p.add_argument("--store", default="packed", choices=["packed", "bf16"],
+                   help="with --pack fp8: bf16 = also keep each layer dequantized to bf16 in HBM (fused "
+                        "verify+unpack kernel on every landed chunk)")
     p.add_argument("--verify", default="crc32c", choices=["none", "crc32c"])
     p.add_argument("--streams-per-peer", type=int, default=1,
                    help="P2P ops per peer and direction in one RCCL group")
@@ -209,7 +212,7 @@ def main(argv=None) -> int:
     rt = Runtime(cfg, my_id, engine=args.engine, storage_path=args.s,
                  chunk_bytes=args.chunk_bytes or (args.chunk_mib << 20),
                  verify=not args.no_verify and args.verify != "none", registry=registry, barrier=barrier,
-                 nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block,
+                 nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block, store=args.store,
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
                  host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
                  persist_dir=args.persist_dir, engine_opts=engine_opts(args))

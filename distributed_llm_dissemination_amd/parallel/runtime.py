@@ -92,6 +92,7 @@ class Runtime:
         sim_key: str = "sim",
         pack: str = "none",
         pack_block: int = 128,
+        store: str = "packed",
         inject_corrupt: float = 0.0,
         inject_seed: int = 1,
         max_retries: int = 4,
@@ -112,7 +113,12 @@ class Runtime:
             raise ValueError(f"unknown pack format {pack!r}")
         if pack != "none" and engine not in ("rccl", "sim"):
             raise ValueError("--pack needs the planned (rccl/sim) data engine")
+        if store not in ("packed", "bf16"):
+            raise ValueError(f"unknown store format {store!r}")
+        if store == "bf16" and pack != "fp8":
+            raise ValueError("--store bf16 dequantizes fp8-packed layers: it needs --pack fp8")
         self.pack = pack
+        self.store = store
         self.pack_block = pack_block
         self.host_link_rate = dict(host_link_rate or {})
         self.persist_dir = persist_dir
@@ -145,6 +151,7 @@ class Runtime:
             pcfg.poison = poison
             pcfg.pack = 1 if pack == "fp8" else 0
             pcfg.pack_block = pack_block
+            pcfg.unpack_store = store == "bf16"
             pcfg.inject_corrupt = inject_corrupt
             pcfg.inject_seed = inject_seed
             pcfg.max_retries = max_retries
@@ -311,6 +318,9 @@ class Runtime:
         (126 x 3 GiB bf16 = 378 GiB does not fit 288 GB; fp8 packing or a partitioned
         assignment does)."""
         need = sum(self.slot_sizes[l] for l in layers)
+        if self.store == "bf16":
+            # every layer this rank holds also gets its dequantized bf16 slot
+            need += sum(self.sizes[l] for l in layers)
         free, total = _core.mem_info()
         if need + self.HBM_HEADROOM > free:
             raise ValueError(
@@ -628,6 +638,16 @@ class Runtime:
         if self.pack != "fp8":
             return self.layer_bytes(layer)
         size = self.sizes[layer]
+        if self.store == "bf16":
+            # already dequantized on the data path (fused verify+unpack per resident chunk)
+            out = self.engine.unpacked_ptr(layer)
+            if not out:
+                raise RuntimeError(f"layer {layer} has no bf16 image (not resident here)")
+            if self.engine_kind == "sim":
+                return _core.sim_read(out, size)
+            buf = _core.HostBuffer.malloc(size)
+            _core.memcpy(buf.ptr, out, size)
+            return buf.bytes()
         ptr = self.engine.device_ptr(layer)
         if self.engine_kind == "sim":
             packed = _core.sim_read(ptr, self.slot_sizes[layer])

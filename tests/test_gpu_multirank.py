@@ -22,6 +22,17 @@ def _ngpus():
     return torch.cuda.device_count()
 
 
+def _keep_logs(outs):
+    """Copy each rank's output where a GPU-box run can read it (DISSEM_TEST_LOGDIR)."""
+    d = os.environ.get("DISSEM_TEST_LOGDIR")
+    if not d:
+        return
+    os.makedirs(d, exist_ok=True)
+    for r, (out, err) in enumerate(outs):
+        with open(os.path.join(d, f"rank{r}.log"), "w") as f:
+            f.write((out or "") + "\n----- stderr -----\n" + (err or ""))
+
+
 def _port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -86,14 +97,14 @@ def test_cli_torchrun_rccl(n, tmp_path):
 
 
 def test_cli_rank_death_elastic_recovery(n, tmp_path):
-    if n == 8 and _ngpus() < 2:
-        pytest.skip("one-GPU box: rank death is rehearsed at 3 ranks")
     """A rank process dies mid-session (--inject kill-rank, os._exit): the
     survivors' RCCL groups with it fail or stall, the leader's probe finds it
     gone, the survivors abort the communicator and re-form one without it
     (fresh unique id from the leader), and the leader re-plans the unacked
     layers from live holders. Plain processes, not torchrun: its agent would
     tear every worker down when one exits."""
+    if n == 8 and _ngpus() < 2:
+        pytest.skip("one-GPU box: rank death is rehearsed at 3 ranks")
     from distributed_llm_dissemination_amd.models.catalog import make_workload
 
     cfg = make_workload(n, 24, 64 << 20, tier="host", seeding="uniform", copies=2, seed=7, chunk_bytes=8 << 20)
@@ -114,11 +125,14 @@ def test_cli_rank_death_elastic_recovery(n, tmp_path):
     outs = []
     for p in procs:
         try:
-            outs.append(p.communicate(timeout=200))
+            outs.append(p.communicate(timeout=150))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
+            outs = [q.communicate() for q in procs]
+            _keep_logs(outs)
             raise
+    _keep_logs(outs)
     rcs = [p.returncode for p in procs]
     assert rcs[victim] == 86, outs[victim][1][-3000:]
     for r in range(n):

@@ -31,7 +31,7 @@ def expected_image(rt, layer, size):
     return data
 
 
-def run_cluster(cfg, mode, sessions=1, chunk=MiB, rt_kw=None, **policy):
+def run_cluster(cfg, mode, sessions=1, chunk=MiB, rt_kw=None, inspect=None, **policy):
     key = f"sim{next(_keys)}"
     n = len(cfg.nodes)
     rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=chunk, sim_key=key,
@@ -60,6 +60,8 @@ def run_cluster(cfg, mode, sessions=1, chunk=MiB, rt_kw=None, **policy):
                 for l in cfg.assignment.get(i, []):
                     assert r.layer_bytes(l) == expected_image(r, l, sizes[l]), (i, l)
             out.append(res)
+        if inspect is not None:
+            inspect(rts)
         return out, key
     finally:
         for r in rts:
@@ -187,6 +189,25 @@ def test_fp8_packed_replication(mode, tier):
     assert packed == 3 * (MiB // 2 + MiB // 64) + 2048 + 64
     need = sum(1 for r in range(n) for l in range(L) if r not in _owners(cfg, l))
     assert _core.sim_fabric_bytes(key) == need * packed  # every remote copy moved packed
+    assert res[0].engine_stats["verify_failures"] == 0
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_fp8_store_bf16_fused_unpack_on_landing(mode):
+    """--store bf16: every chunk that becomes resident - received or staged -
+    goes through the fused verify+unpack (CRC of the packed chunk and its bf16
+    image in one pass), so every rank ends with the same dequantized layer."""
+    n, L, size = 4, 6, 3 * MiB + 4096
+    cfg = make_workload(n, L, size, tier="host", seeding="random", chunk_bytes=MiB)
+
+    def check(rts):
+        for l in range(L):
+            packed = _core.fp8_pack_layer_host(_core.fill_random_host(size, layer_seed(0, l)), MiB, 128)
+            want = _core.fp8_unpack_layer_host(packed, size, MiB, 128)
+            for r in rts:
+                assert r.unpacked_layer_bytes(l) == want, (r.node_id, l)
+
+    (res,), _ = run_cluster(cfg, mode, rt_kw={"pack": "fp8", "store": "bf16"}, inspect=check, pull_window=n - 1)
     assert res[0].engine_stats["verify_failures"] == 0
 
 
