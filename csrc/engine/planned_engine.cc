@@ -74,6 +74,22 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
   self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
   th_ = std::thread([this] { run(); });
+  monitor_ = std::thread([this] { monitor_loop(); });
+}
+
+void PlannedEngine::monitor_loop() {
+  int64_t reported = 0;
+  while (!stop_req_) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    const char* what = call_what_.load();
+    const int64_t since = call_since_us_.load();
+    if (!what || since == reported) continue;
+    const double age = double(CallMark::now_us() - since) / 1e6;
+    if (age < 3.0) continue;
+    reported = since;
+    log::warn(int64_t(self_node_)).s("call", what).i("lane", call_lane_.load()).f("seconds", age)
+        .msg("issue thread blocked inside a backend call");
+  }
 }
 
 PlannedEngine::~PlannedEngine() { shutdown(); }
@@ -83,6 +99,7 @@ void PlannedEngine::shutdown() {
   stop_req_ = true;
   req_cv_.notify_all();
   if (th_.joinable()) th_.join();
+  if (monitor_.joinable()) monitor_.join();
   disk_cv_.notify_all();
   for (auto& t : readers_) t.join();
   readers_.clear();
@@ -790,7 +807,11 @@ bool PlannedEngine::issue_lane(int lane) {
       }
       xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len, p.bcast});
     }
-    Ev g = backend_->group(xops, waits, lane);
+    Ev g;
+    {
+      CallMark cm(this, "group", lane);
+      g = backend_->group(xops, waits, lane);
+    }
     Inflight inf{g, now, {}};
     for (auto& p : group)
       if (std::find(inf.peers.begin(), inf.peers.end(), p.peer) == inf.peers.end()) inf.peers.push_back(p.peer);
@@ -819,7 +840,10 @@ bool PlannedEngine::issue_lane(int lane) {
       Layer& L = layers_[p.layer];
       L.st[size_t(p.chunk)] = 1;
       if (lanes_ > 1 && !p.bcast) {
-        if (!mark) mark = backend_->mark(lane);
+        if (!mark) {
+          CallMark cm(this, "mark", lane);
+          mark = backend_->mark(lane);
+        }
         set_chunk_ev(L, p.chunk, mark);
       } else {
         set_chunk_ev(L, p.chunk, 0);  // pending on the comm queue itself: later sends are ordered behind it
@@ -921,7 +945,11 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
   const int old_rank = cfg_.rank;
   int64_t aborted = 0;
   for (auto& q : ops_) aborted += int64_t(q.size());
-  const int new_rank = backend_->shrink(dead, generation, comm_id);
+  int new_rank;
+  {
+    CallMark cm(this, "shrink", -1);
+    new_rank = backend_->shrink(dead, generation, comm_id);
+  }
   for (auto& lane : inflight_) {
     for (auto& g : lane) backend_->release(g.ev);
     lane.clear();

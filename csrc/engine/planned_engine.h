@@ -341,6 +341,27 @@ class PlannedEngine : public DataEngine {
   std::atomic<bool> stopped_{false};
   std::atomic<bool> stop_req_{false};
   std::thread th_;
+  // Host-side watchdog: the issue thread marks every backend call that can
+  // block inside RCCL/HIP; a monitor thread logs one that has not returned for
+  // a few seconds (a hang there would also silence poll()'s group watchdog).
+  struct CallMark {
+    PlannedEngine* e;
+    CallMark(PlannedEngine* eng, const char* what, int lane) : e(eng) {
+      e->call_lane_ = lane;
+      e->call_since_us_ = now_us();
+      e->call_what_ = what;
+    }
+    ~CallMark() { e->call_what_ = nullptr; }
+    static int64_t now_us() {
+      return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+          .count();
+    }
+  };
+  std::atomic<const char*> call_what_{nullptr};
+  std::atomic<int64_t> call_since_us_{0};
+  std::atomic<int> call_lane_{0};
+  std::thread monitor_;
+  void monitor_loop();
 };
 
 constexpr uint32_t kCrcSlots = 1u << 16;

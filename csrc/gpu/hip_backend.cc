@@ -322,10 +322,7 @@ class HipBackend : public Backend {
     // comm streams drain. (ncclCommShrink would keep the bootstrap, but the RCCL
     // PyTorch loads into the process predates it; abort + re-init of the
     // survivors works with any RCCL.)
-    for (size_t l = nccl_.size(); l-- > 0;) {  // split lanes before the parent
-      if (nccl_[l]) (void)ncclCommAbort(nccl_[l]);
-      nccl_[l] = nullptr;
-    }
+    abort_all();
     log::warn(cfg_.rank).i("lanes", int64_t(nccl_.size())).msg("rccl communicators aborted; draining queues");
     std::vector<std::pair<uint8_t*, int64_t>> regd;  // re-register with the new communicators
     for (auto& kv : regs_) regd.push_back({kv.first, kv.second.first});
@@ -365,6 +362,22 @@ class HipBackend : public Backend {
     return new_rank;
   }
 
+  // Abort every lane's communicator at once, one thread each. ncclCommAbort
+  // raises the comm's abort flag and then waits for its work to drain; a lane
+  // kernel of another, not yet aborted communicator that waits for a dead peer
+  // would never drain, so aborting the lanes one after another can hang. In
+  // parallel every flag is up within microseconds and every kernel exits.
+  void abort_all() {
+    std::vector<std::thread> ths;
+    for (auto& c : nccl_) {
+      if (!c) continue;
+      ncclComm_t comm = c;
+      c = nullptr;
+      ths.emplace_back([comm] { (void)ncclCommAbort(comm); });
+    }
+    for (auto& t : ths) t.join();
+  }
+
   void sync_all() override {
     (void)hipSetDevice(cfg_.device);
     for (hipStream_t s : comm_) (void)hipStreamSynchronize(s);
@@ -377,11 +390,13 @@ class HipBackend : public Backend {
     destroyed_ = true;
     (void)hipSetDevice(cfg_.device);
     if (!abort) sync_all();
-    for (size_t l = nccl_.size(); l-- > 0;) {  // split lanes before the parent
-      if (!nccl_[l]) continue;
-      if (abort) ncclCommAbort(nccl_[l]);
-      else ncclCommDestroy(nccl_[l]);
-      nccl_[l] = nullptr;
+    if (abort) {
+      abort_all();
+    } else {
+      for (size_t l = nccl_.size(); l-- > 0;) {  // split lanes before the parent
+        if (nccl_[l]) ncclCommDestroy(nccl_[l]);
+        nccl_[l] = nullptr;
+      }
     }
     for (auto e : pool_) (void)hipEventDestroy(e);
     pool_.clear();

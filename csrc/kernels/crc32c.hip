@@ -426,10 +426,12 @@ hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_byte
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  const bool mfma = impl == CrcImpl::kMfma || (impl == CrcImpl::kAuto && crc32c_mfma_default() &&
-                                               crc32c_mfma_applies(bytes, chunk_bytes));
+  const bool mfma = impl == CrcImpl::kMfma || impl == CrcImpl::kMfma1 || impl == CrcImpl::kMfma4 ||
+                    (impl == CrcImpl::kAuto && crc32c_mfma_default() && crc32c_mfma_applies(bytes, chunk_bytes));
   if (mfma) {
-    if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks); e != hipSuccess) return e;
+    const int chains = impl == CrcImpl::kMfma1 ? 1 : impl == CrcImpl::kMfma4 ? 4 : 2;
+    if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks, chains); e != hipSuccess)
+      return e;
   } else {
     crc32c_segments_kernel<<<seg_grid(p.total_segs), dim3(kSegThreads), 0, s>>>(
         static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,

@@ -77,6 +77,10 @@ __device__ __forceinline__ uint32_t shift2k(const uint32_t* L, uint32_t x) {
 // consts layout: [A fragments: 16 steps x 64 lanes x 4 ints][shift-2KiB nibble tables: 8 x 16]
 constexpr int kAFragInts = 16 * 64 * 4;
 
+// NACC independent accumulator chains per batch: K-step s accumulates into
+// chain s % NACC, so consecutive MFMAs do not wait on each other's result;
+// the chains' int32 sums are added before taking bit 0 (parity is additive).
+template <int NACC>
 __global__ void __launch_bounds__(kThreads) crc32c_mfma_segments_kernel(
     const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc, int64_t total_segs,
     const int* __restrict__ consts, const uint32_t* __restrict__ lshift, const uint32_t* __restrict__ lshift_last,
@@ -118,7 +122,9 @@ __global__ void __launch_bounds__(kThreads) crc32c_mfma_segments_kernel(
       u32x4 qn[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) qn[i] = __builtin_nontemporal_load(nblk + i);
-      v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      v16i accs[NACC];
+#pragma unroll
+      for (int j = 0; j < NACC; ++j) accs[j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const uint32_t w = q[s >> 2][s & 3] >> (4 * h);
@@ -127,8 +133,11 @@ __global__ void __launch_bounds__(kThreads) crc32c_mfma_segments_kernel(
         bv[1] = int((w >> 1) & 0x01010101u);
         bv[2] = int((w >> 2) & 0x01010101u);
         bv[3] = int((w >> 3) & 0x01010101u);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bv, acc, 0, 0, 0);
+        accs[s % NACC] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bv, accs[s % NACC], 0, 0, 0);
       }
+      v16i acc = accs[0];
+#pragma unroll
+      for (int j = 1; j < NACC; ++j) acc += accs[j];
       uint32_t part = 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) part |= uint32_t(acc[r] & 1) << ((r & 3) + 8 * (r >> 2) + 4 * h);
@@ -237,7 +246,7 @@ bool crc32c_mfma_applies(int64_t bytes, int64_t chunk_bytes) {
 }
 
 hipError_t crc32c_mfma_segments(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* seg_out,
-                                hipStream_t s, int max_blocks) {
+                                hipStream_t s, int max_blocks, int chains) {
   if (!crc32c_mfma_applies(bytes, chunk_bytes) || (reinterpret_cast<uintptr_t>(src) & 15))
     return hipErrorInvalidValue;
   int* consts = mfma_consts();
@@ -250,8 +259,20 @@ hipError_t crc32c_mfma_segments(const void* src, int64_t bytes, int64_t chunk_by
   const int64_t waves = kThreads / 64;
   const int64_t cap = max_blocks > 0 ? max_blocks : 4 * 256;
   const unsigned grid = unsigned(std::min<int64_t>((total + waves - 1) / waves, cap));
-  crc32c_mfma_segments_kernel<<<dim3(grid), dim3(kThreads), 0, s>>>(
-      static_cast<const uint8_t*>(src), bytes, chunk_bytes, spc, total, consts, sh, sh + spc * 32, seg_out);
+  const auto* sp = static_cast<const uint8_t*>(src);
+  switch (chains) {
+    case 1:
+      crc32c_mfma_segments_kernel<1><<<dim3(grid), dim3(kThreads), 0, s>>>(sp, bytes, chunk_bytes, spc, total, consts, sh,
+                                                                           sh + spc * 32, seg_out);
+      break;
+    case 4:
+      crc32c_mfma_segments_kernel<4><<<dim3(grid), dim3(kThreads), 0, s>>>(sp, bytes, chunk_bytes, spc, total, consts, sh,
+                                                                           sh + spc * 32, seg_out);
+      break;
+    default:
+      crc32c_mfma_segments_kernel<2><<<dim3(grid), dim3(kThreads), 0, s>>>(sp, bytes, chunk_bytes, spc, total, consts, sh,
+                                                                           sh + spc * 32, seg_out);
+  }
   return hipGetLastError();
 }
 

@@ -45,15 +45,16 @@ size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
 // matrix product on the matrix cores (crc32c_mfma.hip; bytes and chunk_bytes
 // whole 16 KiB segments); kAuto = kMfma where it applies and
 // crc32c_mfma_default() (env DISSEM_CRC_IMPL=mfma), else kNibble.
-// max_blocks caps the MFMA grid (0 = default).
-enum class CrcImpl { kAuto = 0, kNibble = 1, kMfma = 2 };
+// max_blocks caps the MFMA grid (0 = default). kMfma1 / kMfma4: the MFMA
+// kernel with 1 / 4 independent accumulator chains (kMfma: 2), for A/B runs.
+enum class CrcImpl { kAuto = 0, kNibble = 1, kMfma = 2, kMfma1 = 3, kMfma4 = 4 };
 hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                               hipStream_t s, CrcImpl impl, int max_blocks);
 bool crc32c_mfma_applies(int64_t bytes, int64_t chunk_bytes);
 bool crc32c_mfma_default();
 // seg_out: crc32c_workspace_bytes(bytes, chunk_bytes) layout (chunk-end-shifted segment CRCs).
 hipError_t crc32c_mfma_segments(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* seg_out,
-                                hipStream_t s, int max_blocks);
+                                hipStream_t s, int max_blocks, int chains = 2);
 hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """A/B of the two CRC32C segment kernels on one MI355X.
 
-impl 1 = LDS nibble tables (crc32c.hip), impl 2 = GF(2) matrix product on the
-matrix cores (crc32c_mfma.hip), over a grid-cap sweep for the MFMA kernel.
+impl 1 = LDS nibble tables (crc32c.hip), impls 3/2/4 = GF(2) matrix product on
+the matrix cores (crc32c_mfma.hip) with 1/2/4 independent accumulator chains,
+over a grid-cap sweep for the MFMA kernel.
 Shapes: 1 GiB in 64 MiB chunks (bulk throughput) and one 64 MiB chunk (the
 per-landing verify of the data engine). Prints one JSON object.
 """
@@ -37,7 +38,8 @@ def main():
     host = buf.cpu().numpy().tobytes()
     want = [_core.crc32c(host[i:i + chunk]) for i in range(0, n, chunk)]
     out = {}
-    variants = [("nibble", 1, 0)] + [(f"mfma_cap{c}", 2, c) for c in (256, 512, 768, 1024, 2048, 4096)]
+    variants = [("nibble", 1, 0)] + [(f"mfma{ch}_cap{c}", impl, c) for ch, impl in (("1", 3), ("2", 2), ("4", 4))
+                                     for c in (512, 1024, 2048, 4096)]
     for name, impl, cap in variants:
         def bulk():
             _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)

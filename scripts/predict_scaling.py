@@ -36,12 +36,17 @@ _n = [0]
 
 def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
-            slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False) -> dict:
+            slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
+            slowdown: float = 1.0) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
     plan_links: the leader's plan knows every link's capacity (config Links),
-    so mode 1 with owner_policy "links" can relay around the slow one."""
+    so mode 1 with owner_policy "links" can relay around the slow one.
+    slowdown: run every rate this many times slower and divide the measured time
+    by it (keeps the simulator's own per-op thread overhead small next to the
+    modeled transfer times)."""
+    pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
     t = _core.SimTiming()
@@ -84,13 +89,15 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             times.append(time.perf_counter() - t0)
             if not all(x.ok for x in res):
                 raise RuntimeError([x.error for x in res if not x.ok])
+        lanes_used = rts[0].engine.stats().lanes
     finally:
         for r in rts:
             r.close()
-    sec = min(times)
+    sec = min(times) / slowdown
     total = delivered_bytes(cfg) * scale
-    return {"n": n, "link_GBps": link_gbps, "pcie_GBps": pcie_gbps, "mode": mode, "lanes": lanes or max(1, n - 1),
-            "ms_per_step": round(sec * 1e3, 1), "value_GBps": round(total / sec / 1e9, 1), "scale": scale}
+    return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode,
+            "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
+            "value_GBps": round(total / sec / 1e9, 1), "scale": scale}
 
 
 def main() -> int:
@@ -98,14 +105,16 @@ def main() -> int:
     ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--link-gbps", type=float, nargs="+", default=[50.0])
     ap.add_argument("--pcie-gbps", type=float, default=57.5)
-    ap.add_argument("--scale", type=int, default=256)
+    ap.add_argument("--scale", type=int, default=1024)
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--mode", type=int, default=1)
+    ap.add_argument("--slowdown", type=float, default=4.0)
     args = ap.parse_args()
     _core.set_log_level(3)
     for lg in args.link_gbps:
         for n in args.ns:
-            r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode)
+            r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,
+                        slowdown=args.slowdown)
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
             bound = 85.899e9 / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)

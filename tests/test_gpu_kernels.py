@@ -59,7 +59,8 @@ def test_crc32c_mfma_matches_host(gpu, n, chunk):
     torch.cuda.synchronize()
     host = t.cpu().numpy().tobytes()
     want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
-    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=2) == want
+    for impl in (2, 3, 4):  # 2, 1 and 4 independent accumulator chains
+        assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=impl) == want, impl
     assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=1) == want
     # a single flipped bit anywhere changes exactly its chunk's CRC
     for pos in (0, n // 2 + 5, n - 1):

@@ -103,8 +103,8 @@ def test_predicted_scaling_follows_the_link_bound():
     85.9 GB / (N * min(PCIe, link)) - the schedule keeps every GPU's PCIe
     copy and its N-1 links busy together (sim thread overhead included)."""
     for n in (1, 2, 4):
-        r = predict_scaling.predict(n, scale=1024, link_gbps=50.0 / 4, pcie_gbps=57.5 / 4, steps=1)
-        bound = 85.899e9 / n / (min(57.5, 50.0 if n > 1 else 1e9) / 4 * 1e9)
+        r = predict_scaling.predict(n, scale=1024, link_gbps=50.0, pcie_gbps=57.5, steps=1, slowdown=4)
+        bound = 85.899e9 / n / (min(57.5, 50.0 if n > 1 else 1e9) * 1e9)
         assert r["ms_per_step"] / 1e3 <= bound * 1.35, (n, r, bound)
         assert r["ms_per_step"] / 1e3 >= bound * 0.95, (n, r, bound)
 
@@ -117,7 +117,7 @@ def test_slow_link_costs_at_most_a_seventh_with_the_link_aware_plan():
     carries onto relays - ranks that receive the same layer directly - until
     the slowest link no longer sets the pace: <= 1/7 extra time, where a plan
     that ignores the link takes ~2x."""
-    kw = dict(layers=32, scale=1024, link_gbps=50.0 / 4, pcie_gbps=57.5 / 4, mode=1, steps=1,
+    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=1, slowdown=4,
               policy={"owner_policy": "links"})
     base = predict_scaling.predict(8, **kw)["ms_per_step"]
     slow = predict_scaling.predict(8, slow_link=((0, 1), 0.5), **kw)["ms_per_step"]
