@@ -286,12 +286,15 @@ class SimBackend : public Backend {
     int rank = rank_;
     auto fab = fab_;
     comm_.at(size_t(lane))->push([=] {
-      for (auto& d : deps)
+      for (size_t i = 0; i < deps.size(); ++i) {
+        auto& d = deps[i];
         if (!d || !wait_event(d, kTimeout)) {
-          set_error("group dependency failed");
+          set_error(std::string("group dependency failed: event ") + std::to_string(waits[i]) +
+                    (d ? (d->state.load() < 0 ? " failed" : " timed out") : " was already released"));
           ev->state = -1;
           return;
         }
+      }
       const auto t0 = Clock::now();
       std::vector<std::unique_ptr<Posted>> posted;
       // Optional RCCL round model: ops grouped by ring distance, each round
