@@ -67,6 +67,12 @@ def parse_args(argv=None):
     p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
     p.add_argument("--lanes", type=int, default=0,
                    help="comm lanes (RCCL communicator + stream each); 0 = world-1 (one ring distance per lane)")
+    p.add_argument("--inject", action="append", default=[], metavar="SPEC",
+                   help="fault injection (utils/faults.py), e.g. slow-link=0:1:20G (rank 0 -> 1 capped at 20 GB/s)")
+    p.add_argument("--source-pool", type=int, default=0,
+                   help="host tier: layers share this many distinct pinned source buffers (layer l holds "
+                        "pool buffer l %% P: random bytes, identical across layers of one residue) - fits "
+                        "126 x 3 GiB bf16 sources in host memory; 0 = one buffer per layer")
     p.add_argument("--preset", default="", choices=["", "llama70b", "llama405b-fp8"],
                    help="llama70b = 80 x 1 GiB (default); llama405b-fp8 = 126 x 3 GiB with --pack fp8")
     args = p.parse_args(argv)
@@ -117,6 +123,9 @@ def main(argv=None) -> int:
     from distributed_llm_dissemination_amd.models.catalog import delivered_bytes, make_workload
     from distributed_llm_dissemination_amd.__main__ import engine_opts
     from distributed_llm_dissemination_amd.parallel.runtime import Runtime
+    from distributed_llm_dissemination_amd.utils.faults import parse_inject
+
+    faults = parse_inject(args.inject)
 
     _core.set_log_level(2)
 
@@ -150,7 +159,8 @@ def main(argv=None) -> int:
                  verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
                  store=args.store,
-                 engine_opts=engine_opts(args))
+                 engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(rank)},
+                 inject_corrupt=faults.drop_chunk, source_pool=args.source_pool)
     if args.pack != "none":
         # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
         src_bytes = total_bytes

@@ -215,7 +215,8 @@ def main(argv=None) -> int:
                  nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block, store=args.store,
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
                  host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
-                 persist_dir=args.persist_dir, engine_opts=engine_opts(args))
+                 persist_dir=args.persist_dir,
+                 engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(my_id)})
     if barrier is not None:
         # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
         import torch.distributed as dist

@@ -35,9 +35,11 @@ from ..utils.config import (
 MiB = 1 << 20
 
 
-def layer_seed(base: int, layer: int) -> int:
-    """Deterministic per-layer payload seed: every holder of a layer has identical bytes."""
-    h = hashlib.blake2b(f"{base}:{layer}".encode(), digest_size=8).digest()
+def layer_seed(base: int, layer: int, pool: int = 0) -> int:
+    """Deterministic per-layer payload seed: every holder of a layer has identical bytes
+    (with a source pool of P buffers, layer l carries pool buffer l % P)."""
+    key = layer % pool if pool > 0 else layer
+    h = hashlib.blake2b(f"{base}:{key}".encode(), digest_size=8).digest()
     return int.from_bytes(h, "little")
 
 
@@ -101,6 +103,7 @@ class Runtime:
         group_peers: int = 1,
         persist_dir: str = "",
         engine_opts: Optional[Dict[str, object]] = None,
+        source_pool: int = 0,
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -122,6 +125,11 @@ class Runtime:
         self.pack_block = pack_block
         self.host_link_rate = dict(host_link_rate or {})
         self.persist_dir = persist_dir
+        # Host-tier sources share `source_pool` distinct buffers (layer l -> l % P):
+        # large presets (126 x 3 GiB bf16) fit host memory; every layer still
+        # carries random bytes and its own CRC manifest.
+        self.source_pool = int(source_pool)
+        self._pool: Dict[int, object] = {}
         self.verify = verify
         self.payload_seed = payload_seed
         self._barrier = barrier or (lambda: None)
@@ -252,7 +260,7 @@ class Runtime:
         for st, per in sorted(self.me.initial_layers.items()):
             rate = self.me.sources.get(st, 0)
             for l, size in sorted(per.items()):
-                seed = layer_seed(self.payload_seed, l)
+                seed = layer_seed(self.payload_seed, l, self.source_pool)
                 if st == SOURCE_CLIENT:  # metadata only: the node's external client holds the bytes
                     layers[l] = _core.LayerSrc.client(size, rate)
                 elif st == SOURCE_DISK or (self.storage_path and st != SOURCE_DEVICE):
@@ -267,8 +275,17 @@ class Runtime:
                     self.engine.set_seeded(l, True)
                     layers[l] = _core.layer_src_device(ptr, self.slot_sizes[l])
                 elif gpu:
-                    buf = _core.HostBuffer.pinned(size) if self.engine_kind == "rccl" else _core.HostBuffer.malloc(size)
-                    self._gen_layer(l, size, seed, host_buf=buf)
+                    key = (l % self.source_pool, size) if self.source_pool > 0 else None
+                    if key is not None and key in self._pool:
+                        # shared pool buffer: already holds this residue's bytes
+                        buf = self._pool[key]
+                        self._gen_layer(l, size, seed)
+                    else:
+                        buf = (_core.HostBuffer.pinned(size) if self.engine_kind == "rccl"
+                               else _core.HostBuffer.malloc(size))
+                        self._gen_layer(l, size, seed, host_buf=buf)
+                        if key is not None:
+                            self._pool[key] = buf
                     src = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
                     if self.slot_sizes[l] != size:  # packed: bf16 source, fp8 slot
                         src.data_size = self.slot_sizes[l]

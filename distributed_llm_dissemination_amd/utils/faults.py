@@ -7,10 +7,14 @@
                          catches it, the receiver NACKs, the leader re-sends
     kill-rank=R@T        node R exits abruptly T seconds after it starts
                          sending layer bytes (host engines: the leader's job deadline
-                         re-dispatches its jobs; planned engines: the group
-                         watchdog fails the session and aborts the communicator)
+                         re-dispatches its jobs; planned engines: the survivors'
+                         group watchdog reports it, the leader probes and the
+                         survivors abort and re-form the communicators without it,
+                         then the leader re-plans - elastic recovery)
     slow-link=S:D:RATE   sender S paces layer bytes to D at RATE B/s (host
-                         engine; K/M/G suffixes are powers of 1000)
+                         engine: per-connection token bucket; planned engines:
+                         the issue thread's per-link bucket; K/M/G suffixes are
+                         powers of 1000)
 
 Several specs may be given (``--inject drop-chunk=0.01 --inject kill-rank=3@2``).
 """

@@ -69,7 +69,10 @@ def n(request):
                                         (0, ["--seeding", "leader", "--bcast", "collective"]),
                                         (1, ["--pack", "fp8", "--layer-mib", "96"]),
                                         (1, ["--nccl-ctas", "4:16", "--reserve-cus", "64"]),
-                                        (1, ["--nccl-register"])])
+                                        (1, ["--nccl-register"]),
+                                        (1, ["--pack", "fp8", "--store", "bf16", "--layer-mib", "96"]),
+                                        (1, ["--inject", "slow-link=0:1:2G"]),
+                                        (1, ["--seeding", "uniform", "--source-pool", "3"])])
 def test_bench_modes(n, mode, extra, request):
     if n == 8 and _ngpus() < 2 and extra and extra != ["--pull-window", "2"]:
         # one-GPU box: the 8-rank rehearsal covers modes 1/2/3 (every variant

@@ -25,7 +25,7 @@ _keys = itertools.count()
 
 def expected_image(rt, layer, size):
     """The layer's bytes in the target tier: the source, or its fp8-packed form."""
-    data = _core.fill_random_host(size, layer_seed(0, layer))
+    data = _core.fill_random_host(size, layer_seed(0, layer, rt.source_pool))
     if rt.pack == "fp8":
         return _core.fp8_pack_layer_host(data, rt.chunk_bytes, rt.pack_block)
     return data
@@ -349,3 +349,20 @@ def test_mode1_balanced_seeding_forms_full_all_to_all_rounds(n, lanes):
     for r in res:
         assert r.engine_stats["groups"] == per_rank_rounds * nl
         assert r.engine_stats["pieces"] == per_rank_rounds * 2 * (n - 1)
+
+
+def test_source_pool_shares_host_buffers():
+    """--source-pool P: host-tier layers share P distinct pinned source buffers
+    (layer l carries buffer l % P), so 126 x 3 GiB bf16 sources fit host memory;
+    every layer is still delivered and CRC-verified from its own manifest."""
+    n, L, size = 3, 7, 2 * MiB
+    cfg = make_workload(n, L, size, tier="host", seeding="random", chunk_bytes=MiB)
+
+    def check(rts):
+        for r in rts:
+            assert len(r._pool) <= 2
+            for l in range(L):
+                assert r.layer_bytes(l) == _core.fill_random_host(size, layer_seed(0, l, 2)), (r.node_id, l)
+
+    (res,), _ = run_cluster(cfg, 1, rt_kw={"source_pool": 2}, inspect=check)
+    assert res[0].engine_stats["verify_failures"] == 0
