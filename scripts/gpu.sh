@@ -14,6 +14,8 @@
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
 #   profile    kernel trace of the headline bench and the fp8 subset
 #   disk       NVMe tier bench + diskspeed
+#   fp8        BASELINE #5 at N = 1: full 126 x 3 GiB fp8 preset; --store bf16 subset
+#   crcpmc     SQ issue/wait counters + fetch of the CRC kernels (nibble vs MFMA)
 #   contention probe-kernel launch delay under a CRC burst (CU reservation)
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -22,13 +24,6 @@ RECIPE=${1:-check}
 OUT=gpurun_out/${2:-$RECIPE}
 mkdir -p "$OUT"
 PYTEST="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-
-shared_rank() {  # shared_rank <world> <rank> <port> <outfile> <bench args...>: one bench rank on device 0
-  local world=$1 rank=$2 port=$3 out=$4
-  shift 4
-  DISSEM_SHARED_GPU=1 RANK=$rank LOCAL_RANK=0 WORLD_SIZE=$world MASTER_ADDR=127.0.0.1 MASTER_PORT=$port \
-    timeout -k 10 300 python3 bench.py --gpus "$world" "$@" > "$out" 2> "${out%.json}.log"
-}
 
 case "$RECIPE" in
   check)
@@ -86,6 +81,22 @@ case "$RECIPE" in
     timeout -k 10 900 python bench.py --tier disk --layers 16 --storage /tmp/dl_disk --steps 2 --warmup 1 \
       > $OUT/bench_disk.json 2> $OUT/bench_disk.log &&
     timeout -k 10 120 bin/diskspeed -path /tmp/dl_disk/layers/0/0.layer > $OUT/diskspeed.log 2>&1
+    ;;
+  fp8)
+    # BASELINE config #5 at N = 1: the full 126 x 3 GiB preset (bf16 sources from a 2-buffer
+    # pinned pool), and the --store bf16 receive path on a 20 x 3 GiB subset
+    timeout -k 10 900 python bench.py --preset llama405b-fp8 --source-pool 2 --steps 2 --warmup 1 \
+      > $OUT/bench_405b_fp8.json 2> $OUT/bench_405b_fp8.log &&
+    timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --source-pool 2 \
+      --steps 2 --warmup 1 > $OUT/bench_fp8_store_bf16.json 2> $OUT/bench_fp8_store_bf16.log
+    ;;
+  crcpmc)
+    # issue/wait breakdown of the CRC kernels (one counter pass, 8 SQ counters)
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+      SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --output-format csv \
+      -d $OUT/sq -o sq -- python3 scripts/crc_impl_bench.py --quick > $OUT/sq.log 2>&1 &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv \
+      -d $OUT/fetch -o fetch -- python3 scripts/crc_impl_bench.py --quick > $OUT/fetch.log 2>&1
     ;;
   contention)
     timeout -k 10 120 bin/contention -trials 40 -reserve 32 > $OUT/contention.jsonl 2>&1 &&
