@@ -52,6 +52,45 @@ hipError_t fill_random(void* dst, int64_t bytes, uint64_t seed, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Read roofline probe: every byte read once (16 B per lane, `depth` loads in
+// flight per lane, grid-stride), XOR-folded to one dword per wave so the loads
+// cannot be elided. The bound a read-only verify kernel could reach with the
+// same access pattern.
+template <int DEPTH>
+__global__ void __launch_bounds__(256) read_xor_kernel(const uint4* __restrict__ src, int64_t nvec,
+                                                       uint32_t* __restrict__ out) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  uint32_t acc = 0;
+  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+  for (; i + (DEPTH - 1) * stride < nvec; i += DEPTH * stride) {
+    u32x4 v[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) v[d] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i + d * stride));
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) acc ^= v[d][0] ^ v[d][1] ^ v[d][2] ^ v[d][3];
+  }
+  for (; i < nvec; i += stride) {
+    const uint4 v = src[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc ^= uint32_t(__shfl_xor(int(acc), o, 64));
+  if ((threadIdx.x & 63) == 0) out[(int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6] = acc;
+}
+
+hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, int depth, hipStream_t s) {
+  if (bytes <= 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) || bytes % 16 || blocks <= 0) return hipErrorInvalidValue;
+  const auto* p = static_cast<const uint4*>(src);
+  switch (depth) {
+    case 1: read_xor_kernel<1><<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(p, bytes / 16, out); break;
+    case 2: read_xor_kernel<2><<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(p, bytes / 16, out); break;
+    case 8: read_xor_kernel<8><<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(p, bytes / 16, out); break;
+    default: read_xor_kernel<4><<<dim3(unsigned(blocks)), dim3(256), 0, s>>>(p, bytes / 16, out); break;
+  }
+  return hipGetLastError();
+}
+
 void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset) {
   // Bytes [offset, offset+bytes) of the stream (offset: any byte position).
   auto* p = static_cast<uint8_t*>(dst);

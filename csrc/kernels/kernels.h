@@ -23,6 +23,9 @@ namespace kern {
 // 16 B per lane stores; byte-identical to kern::fill_random_host.
 hipError_t fill_random(void* dst, int64_t bytes, uint64_t seed, hipStream_t s);
 void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset = 0);
+// Read-bandwidth probe: XOR of [src, src+bytes) into blocks*4 dwords at out
+// (bytes % 16 == 0); `depth` 16-B loads in flight per lane (1, 2, 4, 8).
+hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, int depth, hipStream_t s);
 
 // ---- crc32c.hip: CRC32C of every `chunk_bytes` chunk of [src, src+bytes).
 // out[c] (device or host-mapped memory) receives the standard CRC32C of chunk c.

@@ -59,6 +59,12 @@ def main():
         torch.cuda.synchronize()
         got = [int(x) & 0xFFFFFFFF for x in res.cpu().tolist()]
         out[f"{name}_match"] = got == want
+    # Read roofline of this box for the same buffer: a read-only XOR stream.
+    outx = torch.empty(4096 * 4, dtype=torch.int32, device="cuda")
+    for blocks in (1024, 2048, 4096):
+        for depth in (4, 8):
+            t = timed(lambda: _core.read_xor_async(buf.data_ptr(), n, outx.data_ptr(), blocks, depth, 0), 20)
+            out[f"read_xor_b{blocks}_d{depth}_GBps"] = round(n / t / 1e9, 1)
     print(json.dumps(out))
 
 

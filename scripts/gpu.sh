@@ -90,6 +90,13 @@ case "$RECIPE" in
     timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --source-pool 2 \
       --steps 2 --warmup 1 > $OUT/bench_fp8_store_bf16.json 2> $OUT/bench_fp8_store_bf16.log
     ;;
+  storeprof)
+    # kernel trace of the --store bf16 receive path (fused verify+unpack per staged chunk)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o st -- \
+      python3 bench.py --pack fp8 --store bf16 --layers 8 --layer-mib 3072 --source-pool 2 --steps 1 --warmup 1 \
+      > $OUT/bench.log 2>&1 &&
+    timeout -k 10 300 python scripts/crc_impl_bench.py --quick > $OUT/crc_quick.json 2> $OUT/crc_quick.log
+    ;;
   crcpmc)
     # issue/wait breakdown of the CRC kernels (one counter pass, 8 SQ counters)
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
