@@ -237,6 +237,20 @@ crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t c
   segment_crcs<16>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
 }
 
+// Occupancy variant: 1024 threads, 8 waves per SIMD (two 80 KiB workgroups
+// still fill the 160 KiB LDS), 8 words in flight per lane within 64 VGPRs -
+// twice the waves to hide the segment loads behind other waves' lookups.
+constexpr int kSegThreads8 = 1024;
+__global__ void __launch_bounds__(kSegThreads8) __attribute__((amdgpu_waves_per_eu(8)))
+crc32c_segments_kernel8(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
+                        int64_t total_segs, const uint32_t* __restrict__ consts, const uint32_t* __restrict__ shift,
+                        const uint32_t* __restrict__ shift_last, uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t lds[kNibLds];
+  load_nib_lds(lds, consts);
+  NoVisit v;
+  segment_crcs<8>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
+}
+
 template <int BLOCK>
 __global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
 verify_unpack_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t pchunk, int64_t spc,
@@ -432,6 +446,12 @@ hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_byte
     const int chains = impl == CrcImpl::kMfma1 ? 1 : impl == CrcImpl::kMfma4 ? 4 : 2;
     if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks, chains); e != hipSuccess)
       return e;
+  } else if (impl == CrcImpl::kNibble8) {
+    const int64_t waves = kSegThreads8 / 64;
+    const dim3 grid(unsigned(std::min<int64_t>((p.total_segs + waves - 1) / waves, 2 * 256)));
+    crc32c_segments_kernel8<<<grid, dim3(kSegThreads8), 0, s>>>(
+        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
+        p.fold + p.spc * 64, seg);
   } else {
     crc32c_segments_kernel<<<seg_grid(p.total_segs), dim3(kSegThreads), 0, s>>>(
         static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,

@@ -50,7 +50,8 @@ size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
 // crc32c_mfma_default() (env DISSEM_CRC_IMPL=mfma), else kNibble.
 // max_blocks caps the MFMA grid (0 = default). kMfma1 / kMfma4: the MFMA
 // kernel with 1 / 4 independent accumulator chains (kMfma: 2), for A/B runs.
-enum class CrcImpl { kAuto = 0, kNibble = 1, kMfma = 2, kMfma1 = 3, kMfma4 = 4 };
+// kNibble8: the nibble kernel at 8 waves per SIMD (1024-thread workgroups).
+enum class CrcImpl { kAuto = 0, kNibble = 1, kMfma = 2, kMfma1 = 3, kMfma4 = 4, kNibble8 = 5 };
 hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                               hipStream_t s, CrcImpl impl, int max_blocks);
 bool crc32c_mfma_applies(int64_t bytes, int64_t chunk_bytes);

@@ -39,10 +39,10 @@ def main():
     host = buf.cpu().numpy().tobytes()
     want = [_core.crc32c(host[i:i + chunk]) for i in range(0, n, chunk)]
     out = {}
-    variants = [("nibble", 1, 0)] + [(f"mfma{ch}_cap{c}", impl, c) for ch, impl in (("1", 3), ("2", 2), ("4", 4))
-                                     for c in (512, 1024, 2048, 4096)]
+    variants = [("nibble", 1, 0), ("nibble8", 5, 0)] + [
+        (f"mfma{ch}_cap{c}", impl, c) for ch, impl in (("1", 3), ("2", 2), ("4", 4)) for c in (512, 1024, 2048, 4096)]
     if quick:
-        variants = [("nibble", 1, 0), ("mfma2_cap1024", 2, 1024)]
+        variants = [("nibble", 1, 0), ("nibble8", 5, 0), ("mfma2_cap1024", 2, 1024)]
     for name, impl, cap in variants:
         def bulk():
             _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)

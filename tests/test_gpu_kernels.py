@@ -62,6 +62,7 @@ def test_crc32c_mfma_matches_host(gpu, n, chunk):
     for impl in (2, 3, 4):  # 2, 1 and 4 independent accumulator chains
         assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=impl) == want, impl
     assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=1) == want
+    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=5) == want  # nibble kernel, 8 waves/SIMD
     # a single flipped bit anywhere changes exactly its chunk's CRC
     for pos in (0, n // 2 + 5, n - 1):
         t[pos] ^= 0x10
