@@ -110,6 +110,9 @@ class Backend {
   }
   virtual void sync_all() = 0;
   virtual void destroy(bool abort) = 0;
+  // Fault injection: this rank "crashes" - nothing it posted may still move
+  // bytes (a dead process's outstanding ops vanish with it).
+  virtual void crash() {}
   virtual double comm_init_ms() const { return 0; }
 };
 

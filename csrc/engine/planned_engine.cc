@@ -899,6 +899,7 @@ void PlannedEngine::die() {
   // control endpoint disappears (the leader's liveness probe sees it dead).
   log::warn(int64_t(self_node_)).i("groups", groups_issued_).msg("fault injection: rank dies");
   dead_ = true;
+  backend_->crash();
   if (node_) node_->transport()->close();
 }
 

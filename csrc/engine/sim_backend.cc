@@ -22,6 +22,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <tuple>
 
@@ -57,6 +58,7 @@ struct Fabric {
   // (lane, src, dst) -> sends, recvs
   std::map<std::tuple<int, int, int>, std::pair<std::deque<Posted*>, std::deque<Posted*>>> ch;
   SimFabricStats stats;
+  std::set<int> crashed;  // fault injection: ranks whose posts no longer move bytes
   SimTiming timing;
   std::map<std::pair<int, int>, Clock::time_point> link_free;  // timing model: directed link busy until
 
@@ -67,7 +69,7 @@ struct Fabric {
 
   void post(int lane, int src, int dst, bool send, Posted* op) {
     std::lock_guard<std::mutex> lk(mu);
-    if (aborted) {  // like an aborted communicator: nothing moves any more
+    if (aborted || crashed.count(send ? src : dst)) {  // aborted communicator / crashed poster: nothing moves
       op->done = op->bad = true;
       cv.notify_all();
       return;
@@ -108,6 +110,22 @@ struct Fabric {
           for (auto& o : ops) mine = mine || o.get() == *it;
           it = mine ? q->erase(it) : std::next(it);
         }
+  }
+  // A crashed rank: withdraw every op it has posted and not yet matched (they
+  // fail), so no peer copies into or out of its memory any more.
+  void crash_rank(int rank) {
+    std::lock_guard<std::mutex> lk(mu);
+    crashed.insert(rank);  // ops its queues still post later fail at once
+    for (auto& kv : ch) {
+      const int src = std::get<1>(kv.first), dst = std::get<2>(kv.first);
+      auto drop = [](std::deque<Posted*>& q) {
+        for (auto* p : q) p->done = p->bad = true;
+        q.clear();
+      };
+      if (src == rank) drop(kv.second.first);   // its sends
+      if (dst == rank) drop(kv.second.second);  // its recvs
+    }
+    cv.notify_all();
   }
   // Returns false on timeout (deadlock) or a size mismatch.
   bool wait_all(const std::vector<std::unique_ptr<Posted>>& ops, double timeout_s) {
@@ -431,6 +449,8 @@ class SimBackend : public Backend {
     fab_ = fabric(key_ + "/shrink" + std::to_string(generation), fab_.get());
     return rank_;
   }
+
+  void crash() override { fab_->crash_rank(rank_); }
 
   void sync_all() override {
     for (auto& q : comm_) q->drain();

@@ -3,6 +3,7 @@
 // paths: TCP + in-proc transports, every role/mode on the host engine, and the
 // planned (GPU-schedule) engine on the simulated RCCL fabric with 4 ranks.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -125,7 +126,7 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
       pc.suspect_s = 0.2;
       if (i == die) pc.inject_die_after_groups = 2;
     }
-    auto e = std::make_shared<PlannedEngine>(pc, make_sim_backend(key, i, n));
+    auto e = std::make_shared<PlannedEngine>(pc, make_sim_backend(key, i, n, resolve_lanes(pc)));  // directed lanes
     LayersSrc mine;
     for (int l = 0; l < L; ++l) {
       e->provision(LayerID(l), size);
@@ -139,6 +140,8 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
         e->set_manifest(LayerID(l), m);
       }
     }
+    if (getenv("SELFTEST_PTRS"))
+      for (int l = 0; l < L; ++l) fprintf(stderr, "rank %d layer %d slot %p\n", i, l, (void*)e->device_ptr(LayerID(l)));
     engines.push_back(e);
     NodeConfig c;
     c.id = NodeID(i);
@@ -165,16 +168,21 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
   for (auto& t : ts) t->close();
 }
 
-int main() {
+int main(int argc, char** argv) {
   log::set_level(log::Error);
+  // optional: run one case only (0-3 ring modes, 4-6 planned modes 1-3, 7 corruption, 8-9 rank death)
+  const int only = argc > 1 ? atoi(argv[1]) : -1;
+  auto on = [&](int k) { return only < 0 || only == k; };
   for (int mode = 0; mode <= 3; ++mode) {
+    if (!on(mode)) continue;
     ring(false, mode);
     ring(true, mode);
   }
-  for (int mode = 1; mode <= 3; ++mode) planned_sim(mode);
-  planned_sim(1, 0.3);  // NACK / re-send path under injected corruption
-  planned_sim(1, 0, 3);  // a rank dies: suspect -> probe -> shrink -> re-plan
-  planned_sim(2, 0, 2);
+  for (int mode = 1; mode <= 3; ++mode)
+    if (on(3 + mode)) planned_sim(mode);
+  if (on(7)) planned_sim(1, 0.3);  // NACK / re-send path under injected corruption
+  if (on(8)) planned_sim(1, 0, 3);  // a rank dies: suspect -> probe -> shrink -> re-plan
+  if (on(9)) planned_sim(2, 0, 2);
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;
