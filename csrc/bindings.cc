@@ -290,7 +290,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("lane_busy_ms", &PlannedStats::lane_busy_ms)
       .def_readonly("lanes", &PlannedStats::lanes)
       .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)
-      .def_readonly("paced", &PlannedStats::paced);
+      .def_readonly("paced", &PlannedStats::paced)
+      .def_readonly("order_violations", &PlannedStats::order_violations);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
         return reinterpret_cast<uint64_t>(e.provision(l, n));

@@ -14,7 +14,12 @@
 // (no comm dependency) or, when it forwards a chunk this rank receives on
 // another lane, for a mark recorded after that recv's group; a group that
 // receives a chunk with a queued forward is closed right after that recv, so
-// the mark covers keys <= the recv's key < the forward's key. Those finished
+// the mark covers keys <= the recv's key < the forward's key. When both ends
+// hold a layer, a rank can be asked to send a chunk (key k1) and to receive
+// it (key k2 > k1) in one batch on two lanes; the recv is then not posted
+// before that send, which stages from the local copy, so the send never
+// waits on the recv (the recv's host-side wait is on the posting of a
+// smaller key, which needs only smaller keys). Those finished
 // too, so k* completes - a contradiction. Hence no deadlock for any
 // interleaving of batches (mode 2's dynamic dispatch included) and any number
 // of lanes. tests/test_planned_sim.py checks this on the simulated fabric for
@@ -147,6 +152,7 @@ PlannedEngine::Layer& PlannedEngine::layer(LayerID id, int64_t size_hint) {
   if (int64_t(L.st.size()) != n) {
     L.st.assign(size_t(n), L.seeded ? 2 : 0);
     L.ev.assign(size_t(n), 0);
+    L.rkey.assign(size_t(n), Key{});
     L.want.assign(size_t(n), 0);
     L.fails.assign(size_t(n), 0);
   }
@@ -545,6 +551,7 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   Ev e = cfg_.pack == 1 && !L.src_packed ? backend_->stage_pack(L.dev + off, src, slen, cfg_.pack_block)
                                          : backend_->stage(L.dev + off, src, len);
   L.st[size_t(c)] = 1;
+  L.rkey[size_t(c)] = Key{};
   set_chunk_ev(L, c, e);
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
   p.src_node = self_node_;
@@ -631,10 +638,18 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   return -1;
 }
 
+bool PlannedEngine::has_local_source(const Layer& L, LayerID id) {
+  if (L.host || !L.path.empty()) return true;
+  LayerSrc src;
+  return node_ && node_->store().get(id, &src) &&
+         (src.host || !src.path.empty() || src.meta.location == Location::Client);
+}
+
 void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
   std::sort(jobs.begin(), jobs.end(), [](const XferJob& a, const XferJob& b) { return a.seq < b.seq; });
   std::vector<Piece> pieces;
   const int64_t cb = grid_;
+  const uint64_t batch = ++batches_;
   for (auto& j : jobs) {
     Kind kind;
     int peer;
@@ -676,6 +691,7 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       p.src_node = j.src;
       p.bcast = bcast;
       p.rate = j.rate;
+      p.batch = batch;
       // Collectives run on lane 0 (every rank's copy of the lane-0 communicator).
       p.lane = bcast || kind == Kind::Local ? 0 : lane_for(peer, kind == Kind::Send);
       const int64_t ci = c - first_chunk;
@@ -698,7 +714,7 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       if (ensure_chunk(L, p.layer, p.chunk, true) < 0) fail("no source to load layer " + std::to_string(p.layer));
       continue;
     }
-    if (p.kind == Kind::Send && !p.bcast) fwd_pending_[{p.layer, p.chunk}]++;
+    if (p.kind == Kind::Send && !p.bcast) fwd_pending_[{p.layer, p.chunk}].insert(key_of(p));
     ops_[size_t(p.lane)].push_back(p);
   }
 }
@@ -767,6 +783,16 @@ bool PlannedEngine::issue_lane(int lane) {
         continue;
       }
       if (nrecv[p.peer] >= cfg_.group_peers) break;
+      if (!p.bcast) {
+        // Crossing jobs (both ends hold the layer, e.g. mode-2 steals): this
+        // rank also sends the chunk, with a smaller key, on another lane. Post
+        // that send first - it stages from the local source - so it never
+        // waits on this recv's mark (a larger key; see the argument above).
+        auto f = fwd_pending_.find({p.layer, p.chunk});
+        if (f != fwd_pending_.end() && !f->second.empty() && *f->second.begin() < key_of(p) &&
+            has_local_source(layer(p.layer), p.layer))
+          break;
+      }
       nrecv[p.peer]++;
       recv_chunks.insert({p.layer, p.chunk});
       group.push_back(p);
@@ -775,7 +801,7 @@ bool PlannedEngine::issue_lane(int lane) {
       // here so the mark never waits on pieces with larger keys.
       if (lanes_ > 1) {
         auto f = fwd_pending_.find({p.layer, p.chunk});
-        if (f != fwd_pending_.end() && f->second > 0) {
+        if (f != fwd_pending_.end() && !f->second.empty()) {
           ++take;
           break;
         }
@@ -793,13 +819,23 @@ bool PlannedEngine::issue_lane(int lane) {
       Layer& L = layers_[p.layer];
       if (!L.dev) L.dev = backend_->alloc(L.size);
       if (p.kind == Kind::Send) {
+        if (L.st[size_t(p.chunk)] == 1 && L.rkey[size_t(p.chunk)] > key_of(p)) {
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          if (stats_.order_violations++ == 0)
+            log::error(int64_t(self_node_)).u("layer", p.layer).i("chunk", p.chunk)
+                .msg("send waits on a recv with a larger key (deadlock-prone order)");
+        }
         if (L.st[size_t(p.chunk)] == 1 && L.ev[size_t(p.chunk)]) {
           Ev e = L.ev[size_t(p.chunk)];
           if (std::find(waits.begin(), waits.end(), e) == waits.end()) waits.push_back(e);
         }
         if (!p.bcast) {
           auto f = fwd_pending_.find({p.layer, p.chunk});
-          if (f != fwd_pending_.end() && --f->second <= 0) fwd_pending_.erase(f);
+          if (f != fwd_pending_.end()) {
+            auto k = f->second.find(key_of(p));
+            if (k != f->second.end()) f->second.erase(k);
+            if (f->second.empty()) fwd_pending_.erase(f);
+          }
         }
         sent += p.len;
       } else {
@@ -839,6 +875,7 @@ bool PlannedEngine::issue_lane(int lane) {
       if (p.kind != Kind::Recv) continue;
       Layer& L = layers_[p.layer];
       L.st[size_t(p.chunk)] = 1;
+      L.rkey[size_t(p.chunk)] = key_of(p);
       if (lanes_ > 1 && !p.bcast) {
         if (!mark) {
           CallMark cm(this, "mark", lane);

@@ -36,8 +36,10 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <set>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "engine/backend.h"
@@ -128,6 +130,7 @@ struct PlannedStats {
   int lanes = 1;
   double comm_init_ms = 0;
   int64_t paced = 0;  // issue attempts a token bucket deferred
+  int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
   std::vector<int64_t> group_us_hist = std::vector<int64_t>(32, 0);  // P2P group issue -> complete
   std::vector<int64_t> land_us_hist = std::vector<int64_t>(32, 0);   // chunk issue -> landed + verified
@@ -189,7 +192,10 @@ class PlannedEngine : public DataEngine {
     bool bcast = false;  // collective from rank `peer` (root: Send with peer == own rank; others: Recv)
     int lane = 0;
     int64_t rate = 0;    // job pacing (B/s, 0 = unlimited)
+    uint64_t batch = 0;  // add_batch ordinal (most significant part of the key)
   };
+  using Key = std::tuple<uint64_t, int64_t, uint64_t>;
+  static Key key_of(const Piece& p) { return Key{p.batch, p.pidx, p.seq}; }
   struct Layer {
     int64_t size = 0;
     uint8_t* dev = nullptr;
@@ -209,6 +215,7 @@ class PlannedEngine : public DataEngine {
     // later receiver detects it and NACKs too)
     std::vector<uint8_t> st;
     std::vector<Ev> ev;              // staging event of a pending chunk (0: pending on the comm queue)
+    std::vector<Key> rkey;           // key of the recv a pending chunk waits on (Key{}: staged)
     std::vector<uint8_t> want;       // inject Landed when resident (assigned here)
     std::vector<uint8_t> fails;      // CRC failures per chunk
   };
@@ -281,6 +288,7 @@ class PlannedEngine : public DataEngine {
   Layer& layer(LayerID id, int64_t size_hint = 0);
   // 1: resident or in flight on a device queue, 0: still reading from disk, -1: no source
   int ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed);
+  bool has_local_source(const Layer& L, LayerID id);  // staging can supply the layer's chunks
   void stage_chunk(Layer& L, LayerID id, int64_t c);
   void stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* src, uint8_t* bounce);
   void submit_disk(Layer& L, LayerID id, int64_t c);
@@ -317,7 +325,10 @@ class PlannedEngine : public DataEngine {
   std::deque<Verify> verifies_;
   std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
   std::deque<std::pair<LayerID, int64_t>> local_wait_;  // local promotions deferred by tier pacing
-  std::map<std::pair<LayerID, int64_t>, int> fwd_pending_;  // queued sends per chunk (relay cuts)
+  // keys of the queued (not yet posted) sends of each chunk: relay cuts, and
+  // recvs of a chunk held back behind this rank's earlier-key send of it
+  std::map<std::pair<LayerID, int64_t>, std::multiset<Key>> fwd_pending_;
+  uint64_t batches_ = 0;
   std::map<Ev, int> evref_;
   std::map<uint64_t, Pace> pace_;
   bool recovering_ = false;  // issue thread: waiting for the leader's Shrink

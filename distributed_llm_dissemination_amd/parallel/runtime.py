@@ -604,7 +604,7 @@ class Runtime:
             k: getattr(es, k)
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
-                      "suspects", "shrinks", "aborted_pieces", "paced", "group_us_hist", "land_us_hist")
+                      "suspects", "shrinks", "aborted_pieces", "paced", "order_violations", "group_us_hist", "land_us_hist")
         }
 
     def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0) -> Dict[tuple, int]:
