@@ -401,6 +401,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("network_bw", &NodeConfig::network_bw)
       .def_readwrite("link_bw", &NodeConfig::link_bw)
       .def_readwrite("stage_bw", &NodeConfig::stage_bw)
+      .def_readwrite("hbm_bw", &NodeConfig::hbm_bw)
       .def_readwrite("integer_seconds", &NodeConfig::integer_seconds)
       .def_readwrite("align", &NodeConfig::align)
       .def_readwrite("storage_path", &NodeConfig::storage_path)

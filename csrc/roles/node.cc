@@ -1434,6 +1434,11 @@ void Node::schedule_mode3() {
     p.egress_bps[kv.first] = kv.second;
     p.ingress_bps[kv.first] = kv.second;
   }
+  for (auto& kv : cfg_.hbm_bw) {
+    if (kv.second <= 0) continue;
+    auto it = p.ingress_bps.find(kv.first);
+    if (it == p.ingress_bps.end() || it->second <= 0 || it->second > kv.second) p.ingress_bps[kv.first] = kv.second;
+  }
   p.link_bps = cfg_.link_bw;
   p.stage_bps = cfg_.stage_bw;
   p.align = cfg_.align;

@@ -38,6 +38,7 @@ struct NodeConfig {
   std::map<NodeID, int64_t> network_bw;  // mode 3: NetworkBW per node (B/s, 0 = unlimited)
   std::map<std::pair<NodeID, NodeID>, int64_t> link_bw;  // mode 1 links / mode 3 topology: per directed link
   std::map<NodeID, int64_t> stage_bw;  // mode 3: per node host->HBM staging (PCIe) budget for non-HBM tiers
+  std::map<NodeID, int64_t> hbm_bw;    // mode 3: per node HBM ingress (write) budget; min'd with NetworkBW
   bool integer_seconds = false;     // mode 3: reference T search over integer seconds
   int64_t align = 1;                // mode 3: byte alignment of ranges
   std::string storage_path;         // receiver persist dir ("" = none)

@@ -325,6 +325,10 @@ class Runtime:
     # measured, profiles/r1_h2d/).
     XGMI_PLAN_GBPS = 50.0
     PCIE_PLAN_GBPS = 55.0
+    # HBM ingress (write) budget of a GPU for the mode-3 graph: measured HBM copy
+    # rate (profiles/r1_fp8/kernel_bench.json: 5.3 TB/s) - never binding next to
+    # 7 xGMI links, but the graph states it (SURVEY C13')
+    HBM_PLAN_GBPS = 5000.0
 
     # Headroom kept free of layer slots: CRC workspaces, fp8 staging scratch,
     # RCCL's own buffers, PyTorch's context.
@@ -497,6 +501,7 @@ class Runtime:
         xgmi_link_gbps: Optional[float] = None,
         stage_gbps: Optional[float] = None,
         link_bw: Optional[Dict[tuple, int]] = None,
+        hbm_gbps: Optional[float] = None,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed).
 
@@ -505,7 +510,8 @@ class Runtime:
         count; default XGMI_PLAN_GBPS) and every GPU's host->HBM staging at
         ``stage_gbps`` (default PCIE_PLAN_GBPS). ``link_bw`` overrides both the
         config's Links and the probe (e.g. per-link rates measured in an earlier
-        session)."""
+        session). ``hbm_gbps`` is every GPU's HBM ingress budget in the mode-3
+        graph (default HBM_PLAN_GBPS on rccl, unlimited elsewhere)."""
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()
@@ -533,6 +539,10 @@ class Runtime:
             nc.link_bw = dict(link_bw)
         if stage_gbps > 0:
             nc.stage_bw = {n.id: int(stage_gbps * 1e9) for n in self.cfg.nodes}
+        if hbm_gbps is None:
+            hbm_gbps = self.HBM_PLAN_GBPS if gpu else 0.0
+        if hbm_gbps > 0:
+            nc.hbm_bw = {n.id: int(hbm_gbps * 1e9) for n in self.cfg.nodes}
         nc.integer_seconds = integer_seconds
         nc.job_timeout_s = job_timeout_s
         nc.job_min_rate = job_min_rate

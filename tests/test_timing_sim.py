@@ -97,6 +97,17 @@ def test_mode3_jobs_finish_at_the_planned_T():
     assert res[0].engine_stats["paced"] > 0
 
 
+def test_mode3_hbm_ingress_budget_binds_the_plan():
+    """The mode-3 graph's per-GPU HBM ingress cap (prepare(hbm_gbps=...),
+    SURVEY C13'): with every dest's ingress at 20 MB/s and no other limit,
+    T is the busiest dest's bytes / 20 MB/s, and the paced jobs finish there."""
+    cfg = make_workload(3, 3, 2 * MiB, tier="host", seeding="leader", chunk_bytes=MiB // 4)
+    dt, res = run_timed(cfg, 3, chunk=MiB // 4, hbm_gbps=0.02)
+    T = res[0].flow_T
+    assert T == pytest.approx(3 * 2 * MiB / 20e6, rel=0.02)
+    assert abs(dt - T) <= 0.15 * T + 0.05, (dt, T)
+
+
 def test_predicted_scaling_follows_the_link_bound():
     """The headline schedule on the timing model (scripts/predict_scaling.py)
     at 1/1024 size: T(N) stays within 35 % of the closed form
