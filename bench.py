@@ -136,6 +136,10 @@ def main(argv=None) -> int:
         print("error: no GPU visible", file=sys.stderr)
         return 2
     torch.cuda.set_device(local_rank)
+    # pinned host layers on the GPU's NUMA node (allocated below, on this thread)
+    from distributed_llm_dissemination_amd.utils.numa import bind_to_gpu
+
+    numa = bind_to_gpu(local_rank)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         barrier = dist.barrier
@@ -258,6 +262,7 @@ def main(argv=None) -> int:
             out["config"]["store"] = args.store
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
+        out["config"]["numa_rank0"] = numa  # {} when the GPU's node is unknown or outside this cpuset
         if world > 1:
             es = rt.engine.stats()
             out["config"]["comm_lanes"] = es.lanes

@@ -197,6 +197,9 @@ def main(argv=None) -> int:
             local_rank = int(os.environ.get("LOCAL_RANK", "0"))
             device = rank_device(int(os.environ.get("RANK", "0")), local_rank, me.device)
             torch.cuda.set_device(device)
+            from .utils.numa import bind_to_gpu
+
+            bind_to_gpu(device)  # host layers on the GPU's NUMA node
         if world > 1:
             # Bootstrap only (gloo over TCP): barriers, the ncclUniqueId, addresses.
             dist.init_process_group("gloo")
