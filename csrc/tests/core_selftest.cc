@@ -98,8 +98,9 @@ static void ring(bool tcp, int mode) {
 
 // Planned engine on the simulated fabric: 4 ranks, full replication.
 // die >= 0: that rank stops dead after two groups (elastic recovery path;
-// every layer then has two holders).
-static void planned_sim(int mode, double corrupt = 0, int die = -1) {
+// every layer then has two holders). crossing: two holders per layer and
+// mode-2 chunk jobs, so steals hand out crossing sends of the same chunk.
+static void planned_sim(int mode, double corrupt = 0, int die = -1, bool crossing = false) {
   const int n = 4, L = 6;
   const int64_t chunk = 1 << 16, size = 3 * chunk + 100;
   static int uniq = 0;
@@ -130,7 +131,7 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
     LayersSrc mine;
     for (int l = 0; l < L; ++l) {
       e->provision(LayerID(l), size);
-      if (l % n == i || (die >= 0 && (l + 1) % n == i)) {
+      if (l % n == i || ((die >= 0 || crossing) && (l + 1) % n == i)) {
         mine[LayerID(l)] = inmem(data[size_t(l)]);
         CrcManifest m;
         m.chunk_bytes = chunk;
@@ -148,6 +149,10 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
     c.leader = 0;
     c.mode = mode;
     c.pull_window = 3;
+    if (crossing) {
+      c.pull_job_bytes = chunk;
+      c.range_acks = true;
+    }
     nodes.push_back(std::make_unique<Node>(c, ts[size_t(i)], e, mine, i == 0 ? asg : Assignment{}, i == 0));
   }
   for (auto& nd : nodes) nd->start();
@@ -161,6 +166,7 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
     for (int l = 0; l < L; ++l)
       EXPECT(memcmp(engines[size_t(i)]->device_ptr(LayerID(l)), data[size_t(l)]->ptr, size_t(size)) == 0);
     EXPECT(engines[size_t(i)]->error().empty());
+    EXPECT(engines[size_t(i)]->stats().order_violations == 0);
   }
   for (auto& nd : nodes) nd->stop();
   nodes.clear();
@@ -170,7 +176,8 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1) {
 
 int main(int argc, char** argv) {
   log::set_level(log::Error);
-  // optional: run one case only (0-3 ring modes, 4-6 planned modes 1-3, 7 corruption, 8-9 rank death)
+  // optional: run one case only (0-3 ring modes, 4-6 planned modes 1-3, 7 corruption, 8-9 rank death,
+  // 10 crossing mode-2 chunk jobs)
   const int only = argc > 1 ? atoi(argv[1]) : -1;
   auto on = [&](int k) { return only < 0 || only == k; };
   for (int mode = 0; mode <= 3; ++mode) {
@@ -183,6 +190,7 @@ int main(int argc, char** argv) {
   if (on(7)) planned_sim(1, 0.3);  // NACK / re-send path under injected corruption
   if (on(8)) planned_sim(1, 0, 3);  // a rank dies: suspect -> probe -> shrink -> re-plan
   if (on(9)) planned_sim(2, 0, 2);
+  if (on(10)) planned_sim(2, 0, -1, true);
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;
