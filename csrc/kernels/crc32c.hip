@@ -251,6 +251,79 @@ crc32c_segments_kernel8(const uint8_t* __restrict__ src, int64_t bytes, int64_t 
   segment_crcs<8>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
 }
 
+// Rolling-prefetch variant: a wave that owns several full segments issues the
+// load of word i of its NEXT segment right after consuming word i of the
+// current one, so the next segment's 16 KiB is in flight while this one's
+// lookups run (same 64 data VGPRs as the plain kernel). The segment index
+// math is wave-uniform (scalar). Partial segments take the plain path.
+__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_segments_roll_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
+                            int64_t total_segs, const uint32_t* __restrict__ consts,
+                            const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
+                            uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t lds[kNibLds];
+  load_nib_lds(lds, consts);
+  using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const uint32_t* L = lds + (lane & 31);
+  const int64_t wave =
+      __builtin_amdgcn_readfirstlane(int(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)));
+  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
+  struct Geo {
+    int64_t chunk_start, chunk_len, seg_start, seg_len, k;
+  };
+  auto geo = [&](int64_t g) {
+    Geo o;
+    const int64_t c = g / spc;
+    o.k = g - c * spc;
+    o.chunk_start = c * chunk_bytes;
+    o.chunk_len = min(chunk_bytes, bytes - o.chunk_start);
+    o.seg_start = o.k * kSegBytes;
+    o.seg_len = min(int64_t(kSegBytes), o.chunk_len - o.seg_start);
+    return o;
+  };
+  u32x4 w[kWordsPerLane];
+  bool loaded = false;
+  NoVisit v;
+  int64_t g = wave;
+  if (g >= total_segs) return;
+  Geo cur = geo(g);
+  for (; g < total_segs; g += nwaves) {
+    const u32x4* cw = reinterpret_cast<const u32x4*>(src + cur.chunk_start + cur.seg_start);
+    const int64_t gn = g + nwaves;
+    Geo nxt{};
+    bool nfull = false;
+    if (gn < total_segs) {
+      nxt = geo(gn);
+      nfull = nxt.seg_len == kSegBytes;
+    }
+    const uint32_t* row = (cur.chunk_len == chunk_bytes ? shift : shift_last) + cur.k * 64;
+    uint32_t s;
+    if (cur.seg_len == kSegBytes) {
+      if (!loaded) {
+#pragma unroll
+        for (int i = 0; i < kWordsPerLane; ++i) w[i] = __builtin_nontemporal_load(cw + lane + 64 * i);
+      }
+      // no next full segment: the prefetch re-reads this one (harmless, in bounds)
+      const u32x4* nw = nfull ? reinterpret_cast<const u32x4*>(src + nxt.chunk_start + nxt.seg_start) : cw;
+      s = 0;
+#pragma unroll
+      for (int i = 0; i < kWordsPerLane; ++i) {
+        const u32x4 x = w[i];
+        w[i] = __builtin_nontemporal_load(nw + lane + 64 * i);
+        s = nib_step(L, s, make_uint4(x[0], x[1], x[2], x[3]));
+      }
+      loaded = nfull;
+      s = wave_xor(multmodp(row[lane], s));
+    } else {
+      s = one_segment<4>(src + cur.chunk_start + cur.seg_start, cur.seg_start, cur.seg_len, row, consts, L, lane, v);
+      loaded = false;
+    }
+    if (lane == 0) seg_out[g] = s;
+    cur = nxt;
+  }
+}
+
 template <int BLOCK>
 __global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
 verify_unpack_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t pchunk, int64_t spc,
@@ -446,6 +519,18 @@ hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_byte
     const int chains = impl == CrcImpl::kMfma1 ? 1 : impl == CrcImpl::kMfma4 ? 4 : 2;
     if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks, chains); e != hipSuccess)
       return e;
+  } else if (impl == CrcImpl::kNibbleRoll ||
+             (impl == CrcImpl::kAuto && p.total_segs >= 2 * int64_t(2 * 256) * (kSegThreads / 64))) {
+    // (auto: bulk launches where every wave of the full grid owns >= 2 segments:
+    // 3.0 vs 2.67 TB/s on 1 GiB; a single 64 MiB chunk stays on the plain kernel,
+    // 31 vs 33 us - profiles/r2_crc_ab/crc_roll.json)
+    // max_blocks sets segments per wave (grid-stride); default: the plain grid
+    const int64_t waves = kSegThreads / 64;
+    const int64_t cap = max_blocks > 0 ? max_blocks : 2 * 256;
+    const dim3 grid(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + waves - 1) / waves, cap))));
+    crc32c_segments_roll_kernel<<<grid, dim3(kSegThreads), 0, s>>>(
+        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
+        p.fold + p.spc * 64, seg);
   } else if (impl == CrcImpl::kNibble8) {
     const int64_t waves = kSegThreads8 / 64;
     const dim3 grid(unsigned(std::min<int64_t>((p.total_segs + waves - 1) / waves, 2 * 256)));

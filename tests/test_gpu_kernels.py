@@ -88,6 +88,32 @@ def test_crc32c_mfma_capped_grid_matches_host(gpu, max_blocks):
     assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
 
 
+@pytest.mark.parametrize(
+    "n,chunk",
+    [
+        ((3 << 20) + 5, 1 << 20),  # byte tail
+        (5 << 20, (1 << 20) + 4096),  # partial segment at every chunk end
+        (96 << 20, 64 << 20),  # short last chunk of whole segments
+    ],
+)
+@pytest.mark.parametrize("max_blocks", [0, 3, 64])
+def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks):
+    """impl 6: the nibble kernel that prefetches each wave's next segment while
+    computing the current one; capped grids put many segments (full and
+    partial, across chunk boundaries) on every wave."""
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 5 + n)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
+    nch = len(want)
+    out = torch.zeros(nch, dtype=torch.int32, device="cuda")
+    ws = torch.empty(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, 6, max_blocks)
+    torch.cuda.synchronize()
+    assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
+
+
 def test_crc32c_mfma_refuses_partial_segments(gpu):
     assert not gpu.crc32c_mfma_applies((1 << 20) + 16, 1 << 20)
     t = _dev_bytes((1 << 20) + 16)
