@@ -933,6 +933,7 @@ void Node::schedule_mode0() {
   for (auto& kv : assignment_)
     for (auto& l : kv.second)
       if (!at(status_[kv.first], l.first, e_->target())) need[l.first].push_back(kv.first);
+  int64_t rot = 0;  // relay: which dests take a layer's leftover chunks rotates, so every link carries 1/k
   for (auto& kv : need) {
     LayerSrc src;
     if (!store_.get(kv.first, &src)) {
@@ -968,13 +969,18 @@ void Node::schedule_mode0() {
         const int64_t k = int64_t(remote.size());
         int64_t off = 0;
         for (int64_t i = 0; i < k; ++i) {
-          int64_t cnt = nchunks / k + (i < nchunks % k ? 1 : 0);
+          // nchunks % k dests get one chunk more; a fixed choice would give the
+          // same dests (and their relay links) 3/16 of every 16-chunk layer
+          // instead of 1/7 at k = 7
+          const int64_t r = ((i - rot) % k + k) % k;
+          int64_t cnt = nchunks / k + (r < nchunks % k ? 1 : 0);
           int64_t len = std::min(total - off, cnt * cb);
           add_job(cfg_.id, remote[size_t(i)], kv.first, off, len, 0);
           for (int64_t j = 0; j < k; ++j)
             if (j != i) add_job(remote[size_t(i)], remote[size_t(j)], kv.first, off, len, 1);
           off += len;
         }
+        rot += nchunks % k;
       } else {
         for (NodeID d : remote) add_job(cfg_.id, d, kv.first, 0, -1);
       }

@@ -37,7 +37,7 @@ _n = [0]
 def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
-            slowdown: float = 1.0) -> dict:
+            slowdown: float = 1.0, tier: str = "host") -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -58,7 +58,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
         t.link = {(s, d): link_gbps * 1e9 / scale * frac}
     _core.sim_set_timing(key, t)
     lb, cb = layer_bytes // scale, chunk // scale
-    cfg = make_workload(n, layers, lb, tier="host", seeding=seeding, chunk_bytes=cb)
+    cfg = make_workload(n, layers, lb, tier=tier, seeding=seeding, chunk_bytes=cb)
     if plan_links:
         bw = int(link_gbps * 1e9)
         cfg.links = {s: {d: bw for d in range(n) if d != s} for s in range(n)}
@@ -95,7 +95,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             r.close()
     sec = min(times) / slowdown
     total = delivered_bytes(cfg) * scale
-    return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode,
+    return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
+            "seeding": seeding, **({"policy": policy} if policy else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
             "value_GBps": round(total / sec / 1e9, 1), "scale": scale}
 
@@ -109,8 +110,20 @@ def main() -> int:
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--mode", type=int, default=1)
     ap.add_argument("--slowdown", type=float, default=4.0)
+    ap.add_argument("--mode0", action="store_true",
+                    help="BASELINE config #2 instead: mode 0 from the leader (relay vs ncclBroadcast, host vs HBM source)")
     args = ap.parse_args()
     _core.set_log_level(3)
+    if args.mode0:
+        for lg in args.link_gbps:
+            for n in args.ns:
+                for tier in ("device", "host"):
+                    for relay, coll in ((True, False), (False, True)):
+                        r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes,
+                                    mode=0, slowdown=args.slowdown, seeding="leader", tier=tier,
+                                    policy={"relay": relay, "collective": coll})
+                        print(json.dumps(r), flush=True)
+        return 0
     for lg in args.link_gbps:
         for n in args.ns:
             r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,

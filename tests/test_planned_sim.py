@@ -87,6 +87,18 @@ def test_mode0_broadcast_relay(n, relay):
     assert moved == (n - 1) * 4 * 4 * MiB  # relay moves the same bytes, spread over all links
 
 
+def test_mode0_relay_rotates_leftover_chunks():
+    """Relay broadcast at 8 ranks: a 16-chunk layer splits 3+3+2+2+2+2+2 over 7
+    dests; which dests take the extra chunk rotates from layer to layer, so over
+    14 layers every dest's slice - and each of its 6 relay links - carries the
+    same 32 chunks (a fixed choice: 42 on two dests, 28 on the rest)."""
+    n, L = 8, 14
+    cfg = make_workload(n, L, 16 * MiB, tier="host", seeding="leader", chunk_bytes=MiB)
+    got = {}
+    run_cluster(cfg, 0, relay=True, inspect=lambda rts: got.update(rts[0].link_stats()["sent"]))
+    assert sorted(got.values()) == [32 * MiB] * (n - 1), got
+
+
 @pytest.mark.parametrize("n", [2, 3, 8])
 @pytest.mark.parametrize("tier", ["host", "device"])
 def test_mode0_collective_broadcast(n, tier):
