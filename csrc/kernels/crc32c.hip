@@ -103,11 +103,16 @@ __device__ inline void load_nib_lds(uint32_t* lds, const uint32_t* __restrict__ 
 // segment is always its chunk's last, so its lanes only align to it). The
 // result is valid in lane 0. Visit sees every 16-B word with its byte offset
 // in the chunk (seg_start + offset in the segment).
-template <int DEPTH, class Visit>
-__device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg, int64_t seg_start, int64_t seg_len,
-                                       const uint32_t* __restrict__ shift_row,
-                                       const uint32_t* __restrict__ consts, const uint32_t* L, int lane,
-                                       Visit& visit) {
+struct NibStep {  // bank-private nibble tables (load_nib_lds layout)
+  const uint32_t* L;
+  __device__ __forceinline__ uint32_t operator()(uint32_t s, uint4 w) const { return nib_step(L, s, w); }
+};
+
+template <int DEPTH, class Visit, class Step>
+__device__ __forceinline__ uint32_t one_segment_s(const uint8_t* __restrict__ seg, int64_t seg_start, int64_t seg_len,
+                                         const uint32_t* __restrict__ shift_row,
+                                         const uint32_t* __restrict__ consts, const Step& step, int lane,
+                                         Visit& visit) {
   const int64_t nw = seg_len >> 4;
   const uint4* words = reinterpret_cast<const uint4*>(seg);
   uint32_t s = 0;
@@ -123,7 +128,7 @@ __device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg,
 #pragma unroll
       for (int i = 0; i < DEPTH; ++i) {
         const uint4 w = make_uint4(wv[i][0], wv[i][1], wv[i][2], wv[i][3]);
-        s = nib_step(L, s, w);
+        s = step(s, w);
         visit(w, seg_start + 16 * (lane + 64 * (b + i)));
       }
     }
@@ -132,7 +137,7 @@ __device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg,
     int64_t last = -1;
     for (int64_t j = lane; j < nw; j += 64) {
       const uint4 w = words[j];
-      s = nib_step(L, s, w);
+      s = step(s, w);
       visit(w, seg_start + 16 * j);
       last = j;
     }
@@ -145,6 +150,70 @@ __device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg,
     for (int64_t b = 0; b < (seg_len & 15); ++b) s = consts[kOffT0 + ((s ^ tail[b]) & 255)] ^ (s >> 8);
   }
   return s;
+}
+
+template <int DEPTH, class Visit>
+__device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg, int64_t seg_start, int64_t seg_len,
+                                       const uint32_t* __restrict__ shift_row,
+                                       const uint32_t* __restrict__ consts, const uint32_t* L, int lane,
+                                       Visit& visit) {
+  return one_segment_s<DEPTH>(seg, seg_start, seg_len, shift_row, consts, NibStep{L}, lane, visit);
+}
+
+// ---- byte-addressed table layout (v2): fewer VALU per lookup ----
+// A lookup address is (nibble << stride) | lane_offset + table offset. In the
+// layout above every nibble is first shifted down and then scaled (2 VALU
+// before the ds_read). Here a byte of the value is moved to bits 8-15 once (one
+// shift per byte, none for byte 1) and both of its nibbles are masked in place:
+// the low nibble (bits 8-11) indexes tables with 256-B entry stride (two tables
+// interleaved per 4 KiB), the high nibble (bits 12-15) tables with 4-KiB stride
+// (up to 32 interleaved, 128 B apart). Each entry still holds 32 replicas, one
+// per bank, and lane l reads replica l & 31: conflict-free as before. Per
+// 32-bit value: 3 shifts + 8 and-or + 8 xor instead of 16 + 8.
+// Tables: 20 low-nibble (class A) and 20 high-nibble (class B) tables, index
+// idx = byte position (data bytes 0-15, state bytes 16-19).
+constexpr uint32_t kNib2B = 40960;                 // class A: 10 pairs x 4 KiB
+constexpr uint32_t kNib2Bytes = kNib2B + 65536;    // class B: 16 rows x 4 KiB
+constexpr int kSeg2Threads = 1024;                 // one 104 KiB workgroup per CU, 4 waves per SIMD
+
+__device__ __forceinline__ uint32_t lds_word(const uint8_t* lds, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t*>(lds + byte_addr);
+}
+
+template <int IDX>  // v: the value with this byte at bits 8-15
+__device__ __forceinline__ uint32_t byte_lookup2(const uint8_t* lds, uint32_t v, uint32_t lo) {
+  constexpr uint32_t offA = (IDX >> 1) * 4096u + (IDX & 1) * 128u;
+  constexpr uint32_t offB = kNib2B + IDX * 128u;
+  return lds_word(lds, ((v & 0xF00u) | lo) + offA) ^ lds_word(lds, ((v & 0xF000u) | lo) + offB);
+}
+
+template <int K0>  // the 4 bytes of x are byte positions K0..K0+3
+__device__ __forceinline__ uint32_t bytes4_lookup2(const uint8_t* lds, uint32_t x, uint32_t lo) {
+  return byte_lookup2<K0>(lds, x << 8, lo) ^ byte_lookup2<K0 + 1>(lds, x, lo) ^
+         byte_lookup2<K0 + 2>(lds, x >> 8, lo) ^ byte_lookup2<K0 + 3>(lds, x >> 16, lo);
+}
+
+struct NibStep2 {
+  const uint8_t* lds;
+  uint32_t lo;  // (lane & 31) * 4: this lane's replica
+  __device__ __forceinline__ uint32_t operator()(uint32_t s, uint4 w) const {
+    return bytes4_lookup2<16>(lds, s, lo) ^ bytes4_lookup2<0>(lds, w.x, lo) ^ bytes4_lookup2<4>(lds, w.y, lo) ^
+           bytes4_lookup2<8>(lds, w.z, lo) ^ bytes4_lookup2<12>(lds, w.w, lo);
+  }
+};
+
+__device__ inline void load_nib2_lds(uint8_t* lds, const uint32_t* __restrict__ consts) {
+  // same 40 x 16 table values as load_nib_lds (t = 2 * byte + hi), 32 replicas as 8 x 16 B
+  const uint32_t* nib = consts + kOffNib;
+  for (int i = threadIdx.x; i < kNibTables * 16 * 8; i += blockDim.x) {
+    const int e = i >> 3, q = i & 7;
+    const int t = e >> 4, v = e & 15, idx = t >> 1;
+    const uint32_t val = nib[e];
+    const uint32_t addr = (t & 1) ? kNib2B + uint32_t(v) * 4096u + uint32_t(idx) * 128u
+                                  : uint32_t(idx >> 1) * 4096u + uint32_t(v) * 256u + uint32_t(idx & 1) * 128u;
+    reinterpret_cast<uint4*>(lds + addr)[q] = make_uint4(val, val, val, val);
+  }
+  __syncthreads();
 }
 
 // Segment walk of the plain and the fused kernels: `bytes` cut into chunks of
@@ -256,16 +325,13 @@ crc32c_segments_kernel8(const uint8_t* __restrict__ src, int64_t bytes, int64_t 
 // current one, so the next segment's 16 KiB is in flight while this one's
 // lookups run (same 64 data VGPRs as the plain kernel). The segment index
 // math is wave-uniform (scalar). Partial segments take the plain path.
-__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_segments_roll_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
-                            int64_t total_segs, const uint32_t* __restrict__ consts,
-                            const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
-                            uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t lds[kNibLds];
-  load_nib_lds(lds, consts);
+template <class Step>
+__device__ __forceinline__ void roll_walk(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
+                                          int64_t spc, int64_t total_segs, const uint32_t* __restrict__ consts,
+                                          const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
+                                          uint32_t* __restrict__ seg_out, const Step& step) {
   using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
-  const uint32_t* L = lds + (lane & 31);
   const int64_t wave =
       __builtin_amdgcn_readfirstlane(int(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)));
   const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
@@ -311,17 +377,42 @@ crc32c_segments_roll_kernel(const uint8_t* __restrict__ src, int64_t bytes, int6
       for (int i = 0; i < kWordsPerLane; ++i) {
         const u32x4 x = w[i];
         w[i] = __builtin_nontemporal_load(nw + lane + 64 * i);
-        s = nib_step(L, s, make_uint4(x[0], x[1], x[2], x[3]));
+        s = step(s, make_uint4(x[0], x[1], x[2], x[3]));
       }
       loaded = nfull;
       s = wave_xor(multmodp(row[lane], s));
     } else {
-      s = one_segment<4>(src + cur.chunk_start + cur.seg_start, cur.seg_start, cur.seg_len, row, consts, L, lane, v);
+      s = one_segment_s<4>(src + cur.chunk_start + cur.seg_start, cur.seg_start, cur.seg_len, row, consts, step, lane,
+                           v);
       loaded = false;
     }
     if (lane == 0) seg_out[g] = s;
     cur = nxt;
   }
+}
+
+__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_segments_roll_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
+                            int64_t total_segs, const uint32_t* __restrict__ consts,
+                            const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
+                            uint32_t* __restrict__ seg_out) {
+  __shared__ uint32_t lds[kNibLds];
+  load_nib_lds(lds, consts);
+  roll_walk(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out,
+            NibStep{lds + (threadIdx.x & 31)});
+}
+
+// Byte-addressed tables (v2 layout above) + rolling prefetch.
+__global__ void __launch_bounds__(kSeg2Threads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_segments_roll2_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
+                             int64_t total_segs, const uint32_t* __restrict__ consts,
+                             const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
+                             uint32_t* __restrict__ seg_out) {
+  __shared__ uint4 lds[kNib2Bytes / 16];
+  uint8_t* base = reinterpret_cast<uint8_t*>(lds);
+  load_nib2_lds(base, consts);
+  roll_walk(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out,
+            NibStep2{base, (threadIdx.x & 31u) * 4u});
 }
 
 template <int BLOCK>
@@ -519,16 +610,24 @@ hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_byte
     const int chains = impl == CrcImpl::kMfma1 ? 1 : impl == CrcImpl::kMfma4 ? 4 : 2;
     if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks, chains); e != hipSuccess)
       return e;
-  } else if (impl == CrcImpl::kNibbleRoll ||
-             (impl == CrcImpl::kAuto && p.total_segs >= 2 * int64_t(2 * 256) * (kSegThreads / 64))) {
-    // (auto: bulk launches where every wave of the full grid owns >= 2 segments:
-    // 3.0 vs 2.67 TB/s on 1 GiB; a single 64 MiB chunk stays on the plain kernel,
-    // 31 vs 33 us - profiles/r2_crc_ab/crc_roll.json)
+  } else if (impl == CrcImpl::kNibbleRoll) {
     // max_blocks sets segments per wave (grid-stride); default: the plain grid
     const int64_t waves = kSegThreads / 64;
     const int64_t cap = max_blocks > 0 ? max_blocks : 2 * 256;
     const dim3 grid(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + waves - 1) / waves, cap))));
     crc32c_segments_roll_kernel<<<grid, dim3(kSegThreads), 0, s>>>(
+        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
+        p.fold + p.spc * 64, seg);
+  } else if (impl == CrcImpl::kNibbleRoll2 ||
+             (impl == CrcImpl::kAuto && p.total_segs >= 2 * int64_t(256) * (kSeg2Threads / 64))) {
+    // (auto: bulk launches where every wave of the full grid owns >= 2 segments:
+    // 3.32 TB/s on 1 GiB vs 2.99 rolling on nibble tables and 2.69 plain; a
+    // single 64 MiB chunk has one segment per wave, nothing to overlap, and stays
+    // on the plain kernel: 31 vs 38 us - profiles/r2_crc_ab/crc_roll2.json)
+    const int64_t waves = kSeg2Threads / 64;
+    const int64_t cap = max_blocks > 0 ? max_blocks : 256;
+    const dim3 grid(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + waves - 1) / waves, cap))));
+    crc32c_segments_roll2_kernel<<<grid, dim3(kSeg2Threads), 0, s>>>(
         static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
         p.fold + p.spc * 64, seg);
   } else if (impl == CrcImpl::kNibble8) {

@@ -52,9 +52,12 @@ size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
 // kernel with 1 / 4 independent accumulator chains (kMfma: 2), for A/B runs.
 // kNibble8: the nibble kernel at 8 waves per SIMD (1024-thread workgroups).
 // kNibbleRoll: the nibble kernel with a rolling prefetch of each wave's next
-// segment (max_blocks caps the grid, i.e. sets segments per wave); kAuto picks
-// it for bulk launches (>= 2 segments per wave of the full grid).
-enum class CrcImpl { kAuto = 0, kNibble = 1, kMfma = 2, kMfma1 = 3, kMfma4 = 4, kNibble8 = 5, kNibbleRoll = 6 };
+// segment (max_blocks caps the grid, i.e. sets segments per wave).
+// kNibbleRoll2: the rolling kernel on byte-addressed tables (fewer VALU per
+// lookup); kAuto picks it for bulk launches (>= 2 segments per wave).
+enum class CrcImpl {
+  kAuto = 0, kNibble = 1, kMfma = 2, kMfma1 = 3, kMfma4 = 4, kNibble8 = 5, kNibbleRoll = 6, kNibbleRoll2 = 7
+};
 hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                               hipStream_t s, CrcImpl impl, int max_blocks);
 bool crc32c_mfma_applies(int64_t bytes, int64_t chunk_bytes);

@@ -3,7 +3,7 @@
 
 impl 1 = LDS nibble tables (crc32c.hip), 5 = the same at 8 waves/SIMD, 6 = the
 same with a rolling prefetch of each wave's next segment (capped grids: more
-segments per wave), impls 3/2/4 = GF(2) matrix product on
+segments per wave), 7 = rolling on byte-addressed tables, impls 3/2/4 = GF(2) matrix product on
 the matrix cores (crc32c_mfma.hip) with 1/2/4 independent accumulator chains,
 over a grid-cap sweep for the MFMA kernel.
 Shapes: 1 GiB in 64 MiB chunks (bulk throughput) and one 64 MiB chunk (the
@@ -42,10 +42,10 @@ def main():
     want = [_core.crc32c(host[i:i + chunk]) for i in range(0, n, chunk)]
     out = {}
     variants = [("nibble", 1, 0), ("nibble8", 5, 0), ("roll", 6, 0), ("roll_cap256", 6, 256),
-                ("roll_cap128", 6, 128)] + [
+                ("roll_cap128", 6, 128), ("roll2", 7, 0), ("roll2_cap128", 7, 128)] + [
         (f"mfma{ch}_cap{c}", impl, c) for ch, impl in (("1", 3), ("2", 2), ("4", 4)) for c in (512, 1024, 2048, 4096)]
     if quick:
-        variants = [("nibble", 1, 0), ("nibble8", 5, 0), ("roll", 6, 0), ("roll_cap256", 6, 256),
+        variants = [("nibble", 1, 0), ("nibble8", 5, 0), ("roll", 6, 0), ("roll2", 7, 0), ("roll2_cap128", 7, 128),
                     ("mfma2_cap1024", 2, 1024)]
     for name, impl, cap in variants:
         def bulk():

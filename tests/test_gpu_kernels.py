@@ -30,6 +30,7 @@ def test_fill_random_matches_host(gpu, n):
         (64 << 20, 64 << 20),
         ((64 << 20) + (5 << 10) + 3, 64 << 20),  # short last chunk: its own segment shifts and init term
         (100 << 10, 100 << 10),  # a partial 16 KiB segment inside one chunk
+        ((160 << 20) + 48, 64 << 20),  # bulk: auto picks the rolling byte-table kernel
     ],
 )
 def test_crc32c_chunks_match_host(gpu, n, chunk):
@@ -97,10 +98,12 @@ def test_crc32c_mfma_capped_grid_matches_host(gpu, max_blocks):
     ],
 )
 @pytest.mark.parametrize("max_blocks", [0, 3, 64])
-def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks):
+@pytest.mark.parametrize("impl", [6, 7])
+def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks, impl):
     """impl 6: the nibble kernel that prefetches each wave's next segment while
-    computing the current one; capped grids put many segments (full and
-    partial, across chunk boundaries) on every wave."""
+    computing the current one (7: the same on byte-addressed tables); capped
+    grids put many segments (full and partial, across chunk boundaries) on
+    every wave."""
     t = _dev_bytes(n)
     gpu.fill_random(t.data_ptr(), n, 5 + n)
     torch.cuda.synchronize()
@@ -109,7 +112,7 @@ def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks):
     nch = len(want)
     out = torch.zeros(nch, dtype=torch.int32, device="cuda")
     ws = torch.empty(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
-    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, 6, max_blocks)
+    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, impl, max_blocks)
     torch.cuda.synchronize()
     assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
 
