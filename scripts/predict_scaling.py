@@ -74,7 +74,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     try:
         for _ in range(steps):
             for r in rts:
-                r.prepare(mode, pull_window=max(1, n - 1), **(policy or {}))
+                r.prepare(mode, **{"pull_window": max(1, n - 1), **(policy or {})})
             res = [None] * n
 
             def go(i):
