@@ -41,8 +41,10 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
-    plan_links: the leader's plan knows every link's capacity (config Links),
-    so mode 1 with owner_policy "links" can relay around the slow one.
+    plan_links: the leader's plan knows every link's capacity (config Links)
+    and every GPU's staging rate, at the simulated (scaled) rates: mode 1 with
+    owner_policy "links" can relay around a slow link, and mode 3 plans - and
+    paces its jobs at size/T - with the rates the fabric will deliver.
     slowdown: run every rate this many times slower and divide the measured time
     by it (keeps the simulator's own per-op thread overhead small next to the
     modeled transfer times)."""
@@ -60,7 +62,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     lb, cb = layer_bytes // scale, chunk // scale
     cfg = make_workload(n, layers, lb, tier=tier, seeding=seeding, chunk_bytes=cb)
     if plan_links:
-        bw = int(link_gbps * 1e9)
+        # the plan's rates are the simulated ones (scaled): mode 3 paces jobs at size/T
+        bw = int(link_gbps * 1e9 / scale)
         cfg.links = {s: {d: bw for d in range(n) if d != s} for s in range(n)}
         if slow_link is not None:
             (s, d), frac = slow_link
@@ -71,10 +74,12 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     for r in rts:
         r.transport.set_registry(reg)
     times = []
+    flow_T = 0.0
     try:
         for _ in range(steps):
             for r in rts:
-                r.prepare(mode, **{"pull_window": max(1, n - 1), **(policy or {})})
+                extra = {"stage_gbps": pcie_gbps / scale} if plan_links else {}
+                r.prepare(mode, **{"pull_window": max(1, n - 1), **extra, **(policy or {})})
             res = [None] * n
 
             def go(i):
@@ -89,6 +94,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             times.append(time.perf_counter() - t0)
             if not all(x.ok for x in res):
                 raise RuntimeError([x.error for x in res if not x.ok])
+            flow_T = res[0].flow_T
         lanes_used = rts[0].engine.stats().lanes
     finally:
         for r in rts:
@@ -98,7 +104,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
             "seeding": seeding, **({"policy": policy} if policy else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
-            "value_GBps": round(total / sec / 1e9, 1), "scale": scale}
+            "value_GBps": round(total / sec / 1e9, 1), "scale": scale,
+            **({"planned_T_ms": round(flow_T * 1e3 / slowdown, 1)} if flow_T > 0 else {})}
 
 
 def main() -> int:

@@ -128,7 +128,7 @@ def test_slow_link_costs_at_most_a_seventh_with_the_link_aware_plan():
     carries onto relays - ranks that receive the same layer directly - until
     the slowest link no longer sets the pace: <= 1/7 extra time, where a plan
     that ignores the link takes ~2x."""
-    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=1, slowdown=4,
+    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=2, slowdown=4,
               policy={"owner_policy": "links"})
     base = predict_scaling.predict(8, **kw)["ms_per_step"]
     slow = predict_scaling.predict(8, slow_link=((0, 1), 0.5), **kw)["ms_per_step"]
