@@ -248,7 +248,7 @@ class PlannedEngine : public DataEngine {
     std::chrono::steady_clock::time_point t0;
     std::vector<int> peers;  // partner ranks
   };
-  struct Pace {  // token bucket, one chunk of burst (TokenBucket semantics, non-blocking)
+  struct Pace {  // token bucket, non-blocking (burst: one chunk; mode-3 jobs two, see pace_ready)
     double rate = 0, tokens = 0, burst = 0;
     std::chrono::steady_clock::time_point last{};
   };
