@@ -173,8 +173,10 @@ class HipBackend : public Backend {
   }
   void free_host(uint8_t* p) override { (void)hipHostFree(p); }
   void zero_sync(uint8_t* p, int64_t n) override {
-    HIP_OK(hipMemsetAsync(p, 0, size_t(n), comm_[0]));
-    HIP_OK(hipStreamSynchronize(comm_[0]));
+    // On the copy queue, never a comm lane: a lane may still hold an RCCL
+    // kernel waiting for a dead peer after a failed session.
+    HIP_OK(hipMemsetAsync(p, 0, size_t(n), copy_));
+    HIP_OK(hipStreamSynchronize(copy_));
   }
 
   Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {

@@ -10,7 +10,7 @@
 #   check      GPU tests, smoke(), 1-GPU headline bench
 #   multirank  multi-rank RCCL rehearsal on one GPU (ranks share device 0)
 #   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
-#   queues     per-rank rocprofv3 kernel traces of a shared-GPU 3-rank bench (HW queue ids)
+#   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
 #   profile    kernel trace of the headline bench and the fp8 subset
 #   disk       NVMe tier bench + diskspeed
@@ -48,11 +48,13 @@ case "$RECIPE" in
     ;;
   queues)
     # Plain per-rank processes (no torchrun): rocprofv3 wraps the python program itself.
+    # QRANKS ranks (default 3; 8 = the driver's lane count, 14 lanes per rank).
+    NR=${QRANKS:-3}
     pids=()
-    for r in 0 1 2; do
-      DISSEM_SHARED_GPU=1 RANK=$r LOCAL_RANK=0 WORLD_SIZE=3 MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
+    for r in $(seq 0 $((NR - 1))); do
+      DISSEM_SHARED_GPU=1 RANK=$r LOCAL_RANK=0 WORLD_SIZE=$NR MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
         timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/rank$r -o q -- \
-        python3 bench.py --gpus 3 --steps 1 --warmup 1 --layers 8 --layer-mib 64 --chunk-mib 16 \
+        python3 bench.py --gpus $NR --steps 1 --warmup 1 --layers $((NR * 2)) --layer-mib 64 --chunk-mib 16 \
         > $OUT/rank$r.json 2> $OUT/rank$r.log &
       pids+=($!)
     done
