@@ -8,7 +8,8 @@
 // of its own. The copy and verify streams are CU-masked whenever RCCL runs
 // (reserve_cus > 0, the default with peers) and extra comm lanes are created
 // with a mask of every CU, so no RCCL kernel waiting for a peer can hold back
-// a copy, a check or another lane (queue ids: profiles/r2_queues/).
+// a copy, a check or another lane (queue ids: profiles/r2_queues/ at 3 ranks,
+// profiles/r2_queues8/ at 8 ranks with 14 lanes each).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
