@@ -210,3 +210,36 @@ def test_multi_destination_layer_and_alignment(core):
 def test_infeasible_when_nobody_holds_layer(core):
     plan = core.solve_flow({0: {}}, [(5, 1, 100)])
     assert not plan.feasible
+
+
+def test_topology_link_bw_from_probe(monkeypatch):
+    """The planners' per-directed-link capacities from the GPU topology probe
+    (SURVEY C4/C13'): xGMI at the plan rate divided by the hop count, other
+    links (PCIe peer path) at the PCIe rate; nodes map to devices by config
+    Device, else by rank."""
+    from types import SimpleNamespace
+
+    from distributed_llm_dissemination_amd import _core
+    from distributed_llm_dissemination_amd.parallel.runtime import Runtime
+
+    topo = []
+    for i in range(4):
+        for j in range(4):
+            if i == j:
+                continue
+            kind, hops = "xgmi", 1
+            if {i, j} == {0, 3}:
+                hops = 2
+            if {i, j} == {1, 2}:
+                kind = "pcie"
+            topo.append((i, j, kind, hops, True))
+    monkeypatch.setattr(_core, "gpu_topology", lambda: topo, raising=False)
+    nodes = [SimpleNamespace(id=10 + r, device=None) for r in range(4)]
+    nodes[1].device, nodes[2].device = 2, 1  # config Device overrides the rank order
+    fake = SimpleNamespace(cfg=SimpleNamespace(nodes=nodes), node_ids=[10, 11, 12, 13])
+    bw = Runtime.topology_link_bw(fake, 50.0, pcie_gbps=20.0)
+    assert bw[(10, 11)] == 50e9 and bw[(11, 10)] == 50e9
+    assert bw[(11, 12)] == 20e9 and bw[(12, 11)] == 20e9  # devices 2 <-> 1: PCIe peer path
+    assert bw[(10, 13)] == 25e9  # devices 0 -> 3: two xGMI hops
+    assert bw[(13, 12)] == 50e9
+    assert len(bw) == 12
