@@ -37,7 +37,7 @@ _n = [0]
 def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
-            slowdown: float = 1.0, tier: str = "host") -> dict:
+            slowdown: float = 1.0, tier: str = "host", pack: str = "none") -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -69,7 +69,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             (s, d), frac = slow_link
             cfg.links[s][d] = int(bw * frac)
     rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
-                   poison=False, engine_opts={"lanes": lanes}) for i in range(n)]
+                   poison=False, engine_opts={"lanes": lanes}, pack=pack) for i in range(n)]
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
         r.transport.set_registry(reg)
@@ -102,6 +102,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     sec = min(times) / slowdown
     total = delivered_bytes(cfg) * scale
     return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
+            **({"pack": pack, "layers": layers, "layer_MiB": layer_bytes >> 20} if pack != "none" else {}),
             "seeding": seeding, **({"policy": policy} if policy else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
             "value_GBps": round(total / sec / 1e9, 1), "scale": scale,
