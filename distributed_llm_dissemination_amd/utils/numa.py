@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import platform
 from typing import Dict, Optional, Set
 
 _SYS_SET_MEMPOLICY = 238  # x86_64
@@ -69,6 +70,8 @@ def node_cpus(node: int, sysfs: str = "/sys") -> Set[int]:
 
 
 def _prefer_node(node: int) -> bool:
+    if platform.machine() != "x86_64":  # the syscall number below is x86_64's
+        return False
     try:
         libc = ctypes.CDLL(None, use_errno=True)
         mask = ctypes.c_ulong(1 << node)
