@@ -10,6 +10,8 @@ rates scaled by the same factor, so every chunk takes its full-size time and a
 session takes its full-size wall time in a fraction of the memory.
 
     python scripts/predict_scaling.py --link-gbps 50 64 --ns 1 2 4 8
+    python scripts/predict_scaling.py --ns 8 --mode0                 # BASELINE config #2
+    python scripts/predict_scaling.py --ns 8 --pack fp8 --layers 126 --layer-mib 3072 --slowdown 8   # config #5
 
 Prints one JSON line per (link rate, N): predicted ms per step and the
 aggregate GB/s value bench.py would report (N x 80 GiB / T).
@@ -118,6 +120,10 @@ def main() -> int:
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--mode", type=int, default=1)
     ap.add_argument("--slowdown", type=float, default=4.0)
+    ap.add_argument("--layers", type=int, default=80)
+    ap.add_argument("--layer-mib", type=int, default=1024)
+    ap.add_argument("--pack", choices=["none", "fp8"], default="none",
+                    help="fp8: BASELINE config #5 (bf16 over PCIe, packed fp8 over the links)")
     ap.add_argument("--mode0", action="store_true",
                     help="BASELINE config #2 instead: mode 0 from the leader (relay vs ncclBroadcast, host vs HBM source)")
     args = ap.parse_args()
@@ -135,11 +141,13 @@ def main() -> int:
     for lg in args.link_gbps:
         for n in args.ns:
             r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,
-                        slowdown=args.slowdown)
+                        slowdown=args.slowdown, layers=args.layers, layer_bytes=args.layer_mib << 20, pack=args.pack)
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
-            bound = 85.899e9 / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)
-            r["closed_form_ms"] = round(bound * 1e3, 1)
+            if args.pack == "none":
+                total = args.layers * (args.layer_mib << 20)
+                bound = total / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)
+                r["closed_form_ms"] = round(bound * 1e3, 1)
             print(json.dumps(r), flush=True)
     return 0
 
