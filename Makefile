@@ -56,7 +56,7 @@ $(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h) Makefile
 
 tools: bin/diskspeed bin/h2dbench bin/contention
 
-bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(BUILD)/kernels/crc32c_mfma.hip.o $(BUILD)/kernels/fill.hip.o $(BUILD)/core/crc32c.o
+bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(BUILD)/kernels/fill.hip.o $(BUILD)/core/crc32c.o
 	@mkdir -p bin
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
 

@@ -176,7 +176,7 @@ void register_gpu_bindings(PyObject* module) {
   m.def("fill_random", [](uint64_t ptr, int64_t n, uint64_t seed, uint64_t stream) {
     check(kern::fill_random(reinterpret_cast<void*>(ptr), n, seed, as_stream(stream)), "fill_random");
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("seed"), py::arg("stream") = 0);
-  // impl: 0 auto, 1 LDS nibble tables, 2 MFMA (kern::CrcImpl).
+  // impl: 0 auto, 1 plain nibble-table kernel, 2 rolling byte-table kernel (kern::CrcImpl).
   m.def("crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t stream, int impl) {
     py::gil_scoped_release nogil;
     return crc_chunks_sync(ptr, n, chunk, stream, impl);
@@ -188,7 +188,6 @@ void register_gpu_bindings(PyObject* module) {
           "crc32c_chunks");
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("out"), py::arg("workspace"),
      py::arg("stream") = 0, py::arg("impl") = 0, py::arg("max_blocks") = 0);
-  m.def("crc32c_mfma_applies", &kern::crc32c_mfma_applies);
   m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
   // Batched CRC of independent device buffers [(ptr, nbytes), ...] (synchronous).
   m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream) {

@@ -306,25 +306,11 @@ crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t c
   segment_crcs<16>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
 }
 
-// Occupancy variant: 1024 threads, 8 waves per SIMD (two 80 KiB workgroups
-// still fill the 160 KiB LDS), 8 words in flight per lane within 64 VGPRs -
-// twice the waves to hide the segment loads behind other waves' lookups.
-constexpr int kSegThreads8 = 1024;
-__global__ void __launch_bounds__(kSegThreads8) __attribute__((amdgpu_waves_per_eu(8)))
-crc32c_segments_kernel8(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
-                        int64_t total_segs, const uint32_t* __restrict__ consts, const uint32_t* __restrict__ shift,
-                        const uint32_t* __restrict__ shift_last, uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t lds[kNibLds];
-  load_nib_lds(lds, consts);
-  NoVisit v;
-  segment_crcs<8>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
-}
-
-// Rolling-prefetch variant: a wave that owns several full segments issues the
-// load of word i of its NEXT segment right after consuming word i of the
-// current one, so the next segment's 16 KiB is in flight while this one's
-// lookups run (same 64 data VGPRs as the plain kernel). The segment index
-// math is wave-uniform (scalar). Partial segments take the plain path.
+// Rolling prefetch: a wave that owns several full segments issues the load of
+// word i of its NEXT segment right after consuming word i of the current one,
+// so the next segment's 16 KiB is in flight while this one's lookups run (the
+// same 64 data VGPRs as the plain kernel). The segment index math is
+// wave-uniform (scalar). Partial segments take the plain path.
 template <class Step>
 __device__ __forceinline__ void roll_walk(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
                                           int64_t spc, int64_t total_segs, const uint32_t* __restrict__ consts,
@@ -389,17 +375,6 @@ __device__ __forceinline__ void roll_walk(const uint8_t* __restrict__ src, int64
     if (lane == 0) seg_out[g] = s;
     cur = nxt;
   }
-}
-
-__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_segments_roll_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
-                            int64_t total_segs, const uint32_t* __restrict__ consts,
-                            const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
-                            uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t lds[kNibLds];
-  load_nib_lds(lds, consts);
-  roll_walk(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out,
-            NibStep{lds + (threadIdx.x & 31)});
 }
 
 // Byte-addressed tables (v2 layout above) + rolling prefetch.
@@ -604,36 +579,16 @@ hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_byte
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  const bool mfma = impl == CrcImpl::kMfma || impl == CrcImpl::kMfma1 || impl == CrcImpl::kMfma4 ||
-                    (impl == CrcImpl::kAuto && crc32c_mfma_default() && crc32c_mfma_applies(bytes, chunk_bytes));
-  if (mfma) {
-    const int chains = impl == CrcImpl::kMfma1 ? 1 : impl == CrcImpl::kMfma4 ? 4 : 2;
-    if (hipError_t e = crc32c_mfma_segments(src, bytes, chunk_bytes, seg, s, max_blocks, chains); e != hipSuccess)
-      return e;
-  } else if (impl == CrcImpl::kNibbleRoll) {
-    // max_blocks sets segments per wave (grid-stride); default: the plain grid
-    const int64_t waves = kSegThreads / 64;
-    const int64_t cap = max_blocks > 0 ? max_blocks : 2 * 256;
-    const dim3 grid(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + waves - 1) / waves, cap))));
-    crc32c_segments_roll_kernel<<<grid, dim3(kSegThreads), 0, s>>>(
-        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
-        p.fold + p.spc * 64, seg);
-  } else if (impl == CrcImpl::kNibbleRoll2 ||
-             (impl == CrcImpl::kAuto && p.total_segs >= 2 * int64_t(256) * (kSeg2Threads / 64))) {
-    // (auto: bulk launches where every wave of the full grid owns >= 2 segments:
-    // 3.32 TB/s on 1 GiB vs 2.99 rolling on nibble tables and 2.69 plain; a
-    // single 64 MiB chunk has one segment per wave, nothing to overlap, and stays
-    // on the plain kernel: 31 vs 38 us - profiles/r2_crc_ab/crc_roll2.json)
+  if (impl == CrcImpl::kRolling ||
+      (impl == CrcImpl::kAuto && p.total_segs >= 2 * int64_t(256) * (kSeg2Threads / 64))) {
+    // bulk launches where every wave of the full grid owns >= 2 segments:
+    // 3.32 TB/s on 1 GiB vs 2.69 for the plain kernel; a single 64 MiB chunk
+    // has one segment per wave - nothing to overlap - and stays on the plain
+    // kernel: 31 vs 38 us (profiles/r2_crc_ab/crc_roll2.json)
     const int64_t waves = kSeg2Threads / 64;
     const int64_t cap = max_blocks > 0 ? max_blocks : 256;
     const dim3 grid(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + waves - 1) / waves, cap))));
     crc32c_segments_roll2_kernel<<<grid, dim3(kSeg2Threads), 0, s>>>(
-        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
-        p.fold + p.spc * 64, seg);
-  } else if (impl == CrcImpl::kNibble8) {
-    const int64_t waves = kSegThreads8 / 64;
-    const dim3 grid(unsigned(std::min<int64_t>((p.total_segs + waves - 1) / waves, 2 * 256)));
-    crc32c_segments_kernel8<<<grid, dim3(kSegThreads8), 0, s>>>(
         static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
         p.fold + p.spc * 64, seg);
   } else {

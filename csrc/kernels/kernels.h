@@ -44,27 +44,16 @@ struct CrcItem {
   uint32_t* out;
 };
 size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
-// Segment kernel choice: kNibble = LDS nibble tables (any shape); kMfma = GF(2)
-// matrix product on the matrix cores (crc32c_mfma.hip; bytes and chunk_bytes
-// whole 16 KiB segments); kAuto = kMfma where it applies and
-// crc32c_mfma_default() (env DISSEM_CRC_IMPL=mfma), else kNibble.
-// max_blocks caps the MFMA grid (0 = default). kMfma1 / kMfma4: the MFMA
-// kernel with 1 / 4 independent accumulator chains (kMfma: 2), for A/B runs.
-// kNibble8: the nibble kernel at 8 waves per SIMD (1024-thread workgroups).
-// kNibbleRoll: the nibble kernel with a rolling prefetch of each wave's next
-// segment (max_blocks caps the grid, i.e. sets segments per wave).
-// kNibbleRoll2: the rolling kernel on byte-addressed tables (fewer VALU per
-// lookup); kAuto picks it for bulk launches (>= 2 segments per wave).
-enum class CrcImpl {
-  kAuto = 0, kNibble = 1, kMfma = 2, kMfma1 = 3, kMfma4 = 4, kNibble8 = 5, kNibbleRoll = 6, kNibbleRoll2 = 7
-};
+// Segment kernel choice: kNibble = bank-private nibble tables, one 16 KiB
+// segment per wave (the per-landing check of one 64 MiB chunk: 31 us);
+// kRolling = byte-addressed tables with a rolling prefetch of each wave's next
+// segment (bulk launches: 3.3 TB/s); kAuto = kRolling when every wave of the
+// full grid owns >= 2 segments, else kNibble. max_blocks caps the grid of
+// kRolling (0 = one workgroup per CU). The A/B that chose these (MFMA GF(2)
+// products, 8 waves per SIMD, rolling on nibble tables) is in profiles/r2_crc_ab.
+enum class CrcImpl { kAuto = 0, kNibble = 1, kRolling = 2 };
 hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                               hipStream_t s, CrcImpl impl, int max_blocks);
-bool crc32c_mfma_applies(int64_t bytes, int64_t chunk_bytes);
-bool crc32c_mfma_default();
-// seg_out: crc32c_workspace_bytes(bytes, chunk_bytes) layout (chunk-end-shifted segment CRCs).
-hipError_t crc32c_mfma_segments(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* seg_out,
-                                hipStream_t s, int max_blocks, int chains = 2);
 hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
-"""A/B of the two CRC32C segment kernels on one MI355X.
+"""A/B of the CRC32C segment kernels on one MI355X.
 
-impl 1 = LDS nibble tables (crc32c.hip), 5 = the same at 8 waves/SIMD, 6 = the
-same with a rolling prefetch of each wave's next segment (capped grids: more
-segments per wave), 7 = rolling on byte-addressed tables, impls 3/2/4 = GF(2) matrix product on
-the matrix cores (crc32c_mfma.hip) with 1/2/4 independent accumulator chains,
-over a grid-cap sweep for the MFMA kernel.
+impl 1 = bank-private nibble tables, one 16 KiB segment per wave (the
+per-landing check), 2 = byte-addressed tables with a rolling prefetch of each
+wave's next segment (bulk; capped grids: more segments per wave), 0 = auto.
+(The MFMA GF(2)-product kernel, an 8-waves-per-SIMD variant and rolling on
+nibble tables lost this A/B and were removed: profiles/r2_crc_ab.)
 Shapes: 1 GiB in 64 MiB chunks (bulk throughput) and one 64 MiB chunk (the
 per-landing verify of the data engine). Prints one JSON object.
 """
@@ -41,12 +41,9 @@ def main():
     host = buf.cpu().numpy().tobytes()
     want = [_core.crc32c(host[i:i + chunk]) for i in range(0, n, chunk)]
     out = {}
-    variants = [("nibble", 1, 0), ("nibble8", 5, 0), ("roll", 6, 0), ("roll_cap256", 6, 256),
-                ("roll_cap128", 6, 128), ("roll2", 7, 0), ("roll2_cap128", 7, 128)] + [
-        (f"mfma{ch}_cap{c}", impl, c) for ch, impl in (("1", 3), ("2", 2), ("4", 4)) for c in (512, 1024, 2048, 4096)]
+    variants = [("nibble", 1, 0), ("roll2", 2, 0), ("roll2_cap128", 2, 128), ("roll2_cap512", 2, 512), ("auto", 0, 0)]
     if quick:
-        variants = [("nibble", 1, 0), ("nibble8", 5, 0), ("roll", 6, 0), ("roll2", 7, 0), ("roll2_cap128", 7, 128),
-                    ("mfma2_cap1024", 2, 1024)]
+        variants = [("nibble", 1, 0), ("roll2", 2, 0)]
     for name, impl, cap in variants:
         def bulk():
             _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)

@@ -45,65 +45,17 @@ def test_crc32c_chunks_match_host(gpu, n, chunk):
 @pytest.mark.parametrize(
     "n,chunk",
     [
-        (16 << 10, 16 << 10),  # one segment
-        (64 << 20, 64 << 20),  # the data engine's landed chunk
-        ((3 << 20) + (48 << 10), 1 << 20),  # short last chunk of whole segments
-        (7 << 20, 48 << 10),  # 3-segment chunks
-        (33 << 20, 4 << 20),
-    ],
-)
-def test_crc32c_mfma_matches_host(gpu, n, chunk):
-    """The matrix-core CRC (impl=2) against the host CRC32C and the LDS-table kernel."""
-    assert gpu.crc32c_mfma_applies(n, chunk)
-    t = _dev_bytes(n)
-    gpu.fill_random(t.data_ptr(), n, 11 + n)
-    torch.cuda.synchronize()
-    host = t.cpu().numpy().tobytes()
-    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
-    for impl in (2, 3, 4):  # 2, 1 and 4 independent accumulator chains
-        assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=impl) == want, impl
-    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=1) == want
-    assert gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=5) == want  # nibble kernel, 8 waves/SIMD
-    # a single flipped bit anywhere changes exactly its chunk's CRC
-    for pos in (0, n // 2 + 5, n - 1):
-        t[pos] ^= 0x10
-        got = gpu.crc32c_chunks(t.data_ptr(), n, chunk, impl=2)
-        t[pos] ^= 0x10
-        assert [i for i, (a, b) in enumerate(zip(got, want)) if a != b] == [pos // chunk]
-
-
-@pytest.mark.parametrize("max_blocks", [4, 64, 1024])
-def test_crc32c_mfma_capped_grid_matches_host(gpu, max_blocks):
-    """MFMA kernel, capped launch: every wave loops over many segments (grid-stride):
-    its per-iteration chain/accumulator reset must hold."""
-    n, chunk = 96 << 20, 64 << 20  # 6144 segments of 16 KiB: >= 24 per wave at 4 blocks
-    t = _dev_bytes(n)
-    gpu.fill_random(t.data_ptr(), n, 77)
-    torch.cuda.synchronize()
-    host = t.cpu().numpy().tobytes()
-    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
-    out = torch.zeros(2, dtype=torch.int32, device="cuda")
-    ws = torch.empty(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
-    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, 2, max_blocks)
-    torch.cuda.synchronize()
-    assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
-
-
-@pytest.mark.parametrize(
-    "n,chunk",
-    [
         ((3 << 20) + 5, 1 << 20),  # byte tail
         (5 << 20, (1 << 20) + 4096),  # partial segment at every chunk end
         (96 << 20, 64 << 20),  # short last chunk of whole segments
     ],
 )
 @pytest.mark.parametrize("max_blocks", [0, 3, 64])
-@pytest.mark.parametrize("impl", [6, 7])
+@pytest.mark.parametrize("impl", [1, 2])
 def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks, impl):
-    """impl 6: the nibble kernel that prefetches each wave's next segment while
-    computing the current one (7: the same on byte-addressed tables); capped
-    grids put many segments (full and partial, across chunk boundaries) on
-    every wave."""
+    """impl 2: the byte-table kernel that prefetches each wave's next segment
+    while computing the current one (impl 1: the plain kernel); capped grids put
+    many segments (full and partial, across chunk boundaries) on every wave."""
     t = _dev_bytes(n)
     gpu.fill_random(t.data_ptr(), n, 5 + n)
     torch.cuda.synchronize()
@@ -115,13 +67,6 @@ def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks, impl):
     gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, impl, max_blocks)
     torch.cuda.synchronize()
     assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
-
-
-def test_crc32c_mfma_refuses_partial_segments(gpu):
-    assert not gpu.crc32c_mfma_applies((1 << 20) + 16, 1 << 20)
-    t = _dev_bytes((1 << 20) + 16)
-    with pytest.raises(RuntimeError):
-        gpu.crc32c_chunks(t.data_ptr(), t.numel(), 1 << 20, impl=2)
 
 
 def test_crc32c_batch_matches_host(gpu):
