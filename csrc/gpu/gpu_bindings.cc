@@ -36,7 +36,7 @@ struct Scratch {
 std::mutex g_scratch_mu;
 std::map<int, Scratch> g_scratch;
 
-std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk, uint64_t stream, int impl = 0) {
+std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk, uint64_t stream) {
   int dev = 0;
   check(hipGetDevice(&dev), "hipGetDevice");
   std::lock_guard<std::mutex> lk(g_scratch_mu);
@@ -55,8 +55,7 @@ std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk
   }
   uint32_t* dout = nullptr;
   check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dout), s.out, 0), "hipHostGetDevicePointer");
-  check(kern::crc32c_chunks_impl(reinterpret_cast<const void*>(ptr), bytes, chunk, dout, s.ws, as_stream(stream),
-                                 kern::CrcImpl(impl), 0),
+  check(kern::crc32c_chunks(reinterpret_cast<const void*>(ptr), bytes, chunk, dout, s.ws, as_stream(stream)),
         "crc32c_chunks");
   check(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize");
   return std::vector<uint32_t>(s.out, s.out + n);
@@ -74,6 +73,11 @@ void register_gpu_bindings(PyObject* module) {
   }, py::arg("data"), py::arg("crc") = 0);
   m.def("crc32c_shift", &crc32c_shift);
   m.def("crc32c_multmodp", &crc32c_multmodp);
+  m.def("read_seg_async", [](uint64_t src, int64_t n, uint64_t out, int blocks, int layout, bool roll,
+                             uint64_t stream) {
+    check(kern::read_seg(reinterpret_cast<const void*>(src), n, reinterpret_cast<uint32_t*>(out), blocks, layout, roll,
+                         as_stream(stream)), "read_seg");
+  });
   m.def("read_xor_async", [](uint64_t src, int64_t n, uint64_t out, int blocks, int depth, uint64_t stream) {
     check(kern::read_xor(reinterpret_cast<const void*>(src), n, reinterpret_cast<uint32_t*>(out), blocks, depth,
                          as_stream(stream)), "read_xor");
@@ -176,18 +180,19 @@ void register_gpu_bindings(PyObject* module) {
   m.def("fill_random", [](uint64_t ptr, int64_t n, uint64_t seed, uint64_t stream) {
     check(kern::fill_random(reinterpret_cast<void*>(ptr), n, seed, as_stream(stream)), "fill_random");
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("seed"), py::arg("stream") = 0);
-  // impl: 0 auto, 1 plain nibble-table kernel, 2 rolling byte-table kernel (kern::CrcImpl).
-  m.def("crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t stream, int impl) {
+  m.def("crc32c_chunks", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t stream) {
     py::gil_scoped_release nogil;
-    return crc_chunks_sync(ptr, n, chunk, stream, impl);
-  }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("stream") = 0, py::arg("impl") = 0);
+    return crc_chunks_sync(ptr, n, chunk, stream);
+  }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("stream") = 0);
+  // max_blocks caps the segment kernel's grid (0: one workgroup per CU)
   m.def("crc32c_chunks_async", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t out_dev, uint64_t ws,
-                                  uint64_t stream, int impl, int max_blocks) {
-    check(kern::crc32c_chunks_impl(reinterpret_cast<const void*>(ptr), n, chunk, reinterpret_cast<uint32_t*>(out_dev),
-                                   reinterpret_cast<void*>(ws), as_stream(stream), kern::CrcImpl(impl), max_blocks),
+                                  uint64_t stream, int max_blocks) {
+    check(kern::crc32c_chunks_capped(reinterpret_cast<const void*>(ptr), n, chunk,
+                                     reinterpret_cast<uint32_t*>(out_dev), reinterpret_cast<void*>(ws),
+                                     as_stream(stream), max_blocks),
           "crc32c_chunks");
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("out"), py::arg("workspace"),
-     py::arg("stream") = 0, py::arg("impl") = 0, py::arg("max_blocks") = 0);
+     py::arg("stream") = 0, py::arg("max_blocks") = 0);
   m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
   // Batched CRC of independent device buffers [(ptr, nbytes), ...] (synchronous).
   m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream) {

@@ -5,11 +5,11 @@
 //   raw(A || B) = shift(raw(A), |B|) xor raw(B),  shift(r, L) = r * x^(8L) mod P.
 // Decomposition:
 //  * a chunk is cut into 16 KiB segments; one wave owns a segment;
-//  * lane l of the wave reads 16-B words l, l+64, l+128, ... (each wave
-//    instruction reads 1 KiB contiguous: fully coalesced) and keeps the raw CRC
-//    of its strided sub-message: s = shift_1KiB(s) xor crc16(word). Both maps
-//    are GF(2)-linear, so one step is the XOR of 40 nibble-table lookups (32 for
-//    the word's nibbles, 8 for the register's);
+//  * a segment is 4 blocks of 4 KiB, and lane l owns the contiguous 64-B piece
+//    l of every block. Within a piece the classic slice-by-4 recurrence runs
+//    (s ^= word; s = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3]): one table lookup per
+//    byte. Between its pieces a lane's register crosses the 4032 bytes of the
+//    other lanes as zeros: a fixed GF(2)-linear map, 8 nibble lookups;
 //  * each lane's CRC is shifted to the END OF ITS CHUNK with one GF(2)
 //    multiply by a host-computed constant (per segment and lane: the lane's
 //    distance to its segment end plus the segment's distance to the chunk
@@ -20,12 +20,30 @@
 // The result is the exact CRC32C of each chunk for any chunk length that is a
 // multiple of 16 (the buffer's final chunk may have any length).
 //
+// Loads stay coalesced: each 16-B load instruction of a wave reads one whole
+// KiB (lane m + 16 r: word r of piece 16 j + m of KiB j), and a 4x4 register
+// transpose across the wave's 4 rows (v_permlane16_swap / v_permlane32_swap,
+// 16 VALU per 64 B of lane data) hands lane l its piece l. Loading the pieces
+// directly (every lane 16 B of its own piece per instruction: 64 separate
+// 64-B spans) reads at 3.5-4.0 TB/s against 6.8 for whole KiBs in the same
+// 16-KiB-per-wave shape (kern::read_seg probe, profiles/r2_crc_ab).
+//
 // LDS layout (MI355X_MICROARCH.md, LDS): a ds_read_b32 is served in two groups
-// of 32 lanes over 32 banks; with data-dependent indices a plain 256-entry table
-// averages ~3 LDS cycles per group (bank conflicts measured at 2x the useful
-// cycles in round 1, profiles/r1_counters). Each nibble table entry is stored
-// 32 times, replica r in bank r, and lane l reads replica l & 31: conflict-free
-// by construction (profiles/r1_crc_ab: SQ_LDS_BANK_CONFLICT = 0).
+// of 32 lanes over 32 banks, and data-dependent indices into a plain table
+// conflict (2x the useful LDS cycles in round 1, profiles/r1_counters). Every
+// table entry is stored 32 times, replica r in bank r, and lane l reads replica
+// l & 31: conflict-free by construction. The 4 byte tables take 128 KiB (two
+// per 64 KiB: entry b at row b * 256 B, odd table at +128 B), so the address
+// of byte k of s is (b << 8) | (half * 128 + replica * 4) | (pair << 16): ONE
+// v_perm_b32 of s with a per-lane constant, then the ds_read_b32. With the
+// 16 KiB of shift tables that is 144 KiB: one 1024-thread workgroup per CU.
+//
+// History (profiles/r2_crc_ab): nibble tables on strided 16-B words (40
+// lookups per 16 B; 2.7 TB/s on 1 GiB, 31 us per 64 MiB chunk), the same on
+// byte-addressed nibble tables with a rolling prefetch (3.3 TB/s), an MFMA
+// GF(2) product (2.3 TB/s), slice-by-4 on directly loaded pieces (3.1 TB/s)
+// and with 4 independent recurrences per lane (2.3-2.5 TB/s) all lost to this
+// kernel: 5.26 TB/s on 1 GiB, 23.4 us per single 64 MiB chunk.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,18 +60,20 @@ namespace kern {
 
 namespace {
 
-// 16 KiB per wave: 16 strided words per lane. One 64 MiB landing chunk spreads
-// over 4096 waves (16 per CU).
 constexpr int kSegBytes = 16 * 1024;
-constexpr int kWordsPerLane = kSegBytes / 16 / 64;
-constexpr int kNibTables = 40;  // 32 for a 16-B word, 8 for the register shifted by 1 KiB
-// Global constants: [T0: 256][lanepow: 64][nibble tables: 40 x 16].
-constexpr int kOffT0 = 0;
-constexpr int kOffLanePow = 256;
-constexpr int kOffNib = 256 + 64;
-constexpr int kConstWords = kOffNib + kNibTables * 16;
-// 40 tables x 16 entries x 32 replicas x 4 B = 80 KiB: two workgroups per CU.
-constexpr int kNibLds = kNibTables * 16 * 32;
+constexpr int kPieceBytes = 64;                         // a lane's contiguous piece of a block
+constexpr int kBlockBytes = 64 * kPieceBytes;           // 4 KiB
+constexpr int kBlocksPerSeg = kSegBytes / kBlockBytes;  // 4
+constexpr int kGapBytes = kBlockBytes - kPieceBytes;    // between a lane's pieces
+constexpr uint32_t kShLds = 131072;                     // shift tables after the byte tables
+constexpr uint32_t kLdsBytes = kShLds + 8 * 16 * 128;   // 144 KiB
+constexpr int kThreads = 1024;                          // one workgroup per CU, 4 waves per SIMD
+constexpr int kWaves = kThreads / 64;
+// Global constants: [T: 4 x 256 (T[k][v]: byte v then k zero bytes)]
+// [gap: 8 x 16 nibble tables of the kGapBytes shift][pow16: 1024 (x^(8*16 m))].
+constexpr int kT = 0, kGap = 1024, kPow = kGap + 128, kConstWords = kPow + 1024;
+
+using u32x4_t = unsigned int __attribute__((ext_vector_type(4)));
 
 __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   uint32_t p = 0;
@@ -74,179 +94,215 @@ __device__ inline uint32_t wave_xor(uint32_t v) {
   return v;
 }
 
-// XOR of the 8 nibble tables t0..t0+7, indexed by the 8 nibbles of x.
-// L = lds + (lane & 31): entry (t, v) of this lane's bank-private replica.
-__device__ __forceinline__ uint32_t nib8(const uint32_t* L, int t0, uint32_t x) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int n = 0; n < 8; ++n) r ^= L[(t0 + n) * 512 + ((x >> (4 * n)) & 15) * 32];
-  return r;
-}
-
-// One strided step of a lane: s = shift_1KiB(s) xor crc16raw(w).
-__device__ __forceinline__ uint32_t nib_step(const uint32_t* L, uint32_t s, uint4 w) {
-  return nib8(L, 32, s) ^ nib8(L, 0, w.x) ^ nib8(L, 8, w.y) ^ nib8(L, 16, w.z) ^ nib8(L, 24, w.w);
-}
-
-__device__ inline void load_nib_lds(uint32_t* lds, const uint32_t* __restrict__ consts) {
-  // 32 identical replicas per entry, written 4 at a time (16-B stores).
-  const uint32_t* nib = consts + kOffNib;
-  for (int i = threadIdx.x; i < kNibLds / 4; i += blockDim.x) {
-    const uint32_t v = nib[i >> 3];
-    reinterpret_cast<uint4*>(lds)[i] = make_uint4(v, v, v, v);
-  }
-  __syncthreads();
-}
-
-// One 16 KiB segment on one wave: the raw CRC of [seg, seg + seg_len), shifted
-// to its chunk end (full segments: lane l multiplies by shift_row[l]; a partial
-// segment is always its chunk's last, so its lanes only align to it). The
-// result is valid in lane 0. Visit sees every 16-B word with its byte offset
-// in the chunk (seg_start + offset in the segment).
-struct NibStep {  // bank-private nibble tables (load_nib_lds layout)
-  const uint32_t* L;
-  __device__ __forceinline__ uint32_t operator()(uint32_t s, uint4 w) const { return nib_step(L, s, w); }
-};
-
-template <int DEPTH, class Visit, class Step>
-__device__ __forceinline__ uint32_t one_segment_s(const uint8_t* __restrict__ seg, int64_t seg_start, int64_t seg_len,
-                                         const uint32_t* __restrict__ shift_row,
-                                         const uint32_t* __restrict__ consts, const Step& step, int lane,
-                                         Visit& visit) {
-  const int64_t nw = seg_len >> 4;
-  const uint4* words = reinterpret_cast<const uint4*>(seg);
-  uint32_t s = 0;
-  if (nw == kSegBytes / 16) {
-    // Full segment: 16 strided words per lane, DEPTH loads in flight per batch.
-    using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int b = 0; b < kWordsPerLane; b += DEPTH) {
-      u32x4 wv[DEPTH];
-#pragma unroll
-      for (int i = 0; i < DEPTH; ++i)
-        wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(words + lane + 64 * (b + i)));
-#pragma unroll
-      for (int i = 0; i < DEPTH; ++i) {
-        const uint4 w = make_uint4(wv[i][0], wv[i][1], wv[i][2], wv[i][3]);
-        s = step(s, w);
-        visit(w, seg_start + 16 * (lane + 64 * (b + i)));
-      }
-    }
-    s = multmodp(shift_row[lane], s);
-  } else {
-    int64_t last = -1;
-    for (int64_t j = lane; j < nw; j += 64) {
-      const uint4 w = words[j];
-      s = step(s, w);
-      visit(w, seg_start + 16 * j);
-      last = j;
-    }
-    if (last >= 0) s = multmodp(consts[kOffLanePow + nw - 1 - last], s);
-  }
-  s = wave_xor(s);
-  if (lane == 0) {
-    // Byte tail (only a buffer's final segment can have one).
-    const uint8_t* tail = seg + (nw << 4);
-    for (int64_t b = 0; b < (seg_len & 15); ++b) s = consts[kOffT0 + ((s ^ tail[b]) & 255)] ^ (s >> 8);
-  }
-  return s;
-}
-
-template <int DEPTH, class Visit>
-__device__ __forceinline__ uint32_t one_segment(const uint8_t* __restrict__ seg, int64_t seg_start, int64_t seg_len,
-                                       const uint32_t* __restrict__ shift_row,
-                                       const uint32_t* __restrict__ consts, const uint32_t* L, int lane,
-                                       Visit& visit) {
-  return one_segment_s<DEPTH>(seg, seg_start, seg_len, shift_row, consts, NibStep{L}, lane, visit);
-}
-
-// ---- byte-addressed table layout (v2): fewer VALU per lookup ----
-// A lookup address is (nibble << stride) | lane_offset + table offset. In the
-// layout above every nibble is first shifted down and then scaled (2 VALU
-// before the ds_read). Here a byte of the value is moved to bits 8-15 once (one
-// shift per byte, none for byte 1) and both of its nibbles are masked in place:
-// the low nibble (bits 8-11) indexes tables with 256-B entry stride (two tables
-// interleaved per 4 KiB), the high nibble (bits 12-15) tables with 4-KiB stride
-// (up to 32 interleaved, 128 B apart). Each entry still holds 32 replicas, one
-// per bank, and lane l reads replica l & 31: conflict-free as before. Per
-// 32-bit value: 3 shifts + 8 and-or + 8 xor instead of 16 + 8.
-// Tables: 20 low-nibble (class A) and 20 high-nibble (class B) tables, index
-// idx = byte position (data bytes 0-15, state bytes 16-19).
-constexpr uint32_t kNib2B = 40960;                 // class A: 10 pairs x 4 KiB
-constexpr uint32_t kNib2Bytes = kNib2B + 65536;    // class B: 16 rows x 4 KiB
-constexpr int kSeg2Threads = 1024;                 // one 104 KiB workgroup per CU, 4 waves per SIMD
-
 __device__ __forceinline__ uint32_t lds_word(const uint8_t* lds, uint32_t byte_addr) {
   return *reinterpret_cast<const uint32_t*>(lds + byte_addr);
 }
 
-template <int IDX>  // v: the value with this byte at bits 8-15
-__device__ __forceinline__ uint32_t byte_lookup2(const uint8_t* lds, uint32_t v, uint32_t lo) {
-  constexpr uint32_t offA = (IDX >> 1) * 4096u + (IDX & 1) * 128u;
-  constexpr uint32_t offB = kNib2B + IDX * 128u;
-  return lds_word(lds, ((v & 0xF00u) | lo) + offA) ^ lds_word(lds, ((v & 0xF000u) | lo) + offB);
-}
-
-template <int K0>  // the 4 bytes of x are byte positions K0..K0+3
-__device__ __forceinline__ uint32_t bytes4_lookup2(const uint8_t* lds, uint32_t x, uint32_t lo) {
-  return byte_lookup2<K0>(lds, x << 8, lo) ^ byte_lookup2<K0 + 1>(lds, x, lo) ^
-         byte_lookup2<K0 + 2>(lds, x >> 8, lo) ^ byte_lookup2<K0 + 3>(lds, x >> 16, lo);
-}
-
-struct NibStep2 {
-  const uint8_t* lds;
-  uint32_t lo;  // (lane & 31) * 4: this lane's replica
-  __device__ __forceinline__ uint32_t operator()(uint32_t s, uint4 w) const {
-    return bytes4_lookup2<16>(lds, s, lo) ^ bytes4_lookup2<0>(lds, w.x, lo) ^ bytes4_lookup2<4>(lds, w.y, lo) ^
-           bytes4_lookup2<8>(lds, w.z, lo) ^ bytes4_lookup2<12>(lds, w.w, lo);
+__device__ inline void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc) {
+  for (int i = threadIdx.x; i < 4 * 256 * 8; i += blockDim.x) {  // 32 replicas = 8 x 16 B
+    const int e = i >> 3, q = i & 7, t = e >> 8, b = e & 255;
+    const uint32_t v = sc[kT + e];
+    const uint32_t addr = uint32_t(t >> 1) * 65536u + uint32_t(b) * 256u + uint32_t(t & 1) * 128u;
+    reinterpret_cast<uint4*>(lds + addr)[q] = make_uint4(v, v, v, v);
   }
-};
-
-__device__ inline void load_nib2_lds(uint8_t* lds, const uint32_t* __restrict__ consts) {
-  // same 40 x 16 table values as load_nib_lds (t = 2 * byte + hi), 32 replicas as 8 x 16 B
-  const uint32_t* nib = consts + kOffNib;
-  for (int i = threadIdx.x; i < kNibTables * 16 * 8; i += blockDim.x) {
+  for (int i = threadIdx.x; i < 8 * 16 * 8; i += blockDim.x) {
     const int e = i >> 3, q = i & 7;
-    const int t = e >> 4, v = e & 15, idx = t >> 1;
-    const uint32_t val = nib[e];
-    const uint32_t addr = (t & 1) ? kNib2B + uint32_t(v) * 4096u + uint32_t(idx) * 128u
-                                  : uint32_t(idx >> 1) * 4096u + uint32_t(v) * 256u + uint32_t(idx & 1) * 128u;
-    reinterpret_cast<uint4*>(lds + addr)[q] = make_uint4(val, val, val, val);
+    const uint32_t v = sc[kGap + e];
+    reinterpret_cast<uint4*>(lds + kShLds + uint32_t(e) * 128u)[q] = make_uint4(v, v, v, v);
   }
   __syncthreads();
 }
 
-// Segment walk of the plain and the fused kernels: `bytes` cut into chunks of
-// `chunk_bytes`, each wave owns 16 KiB segments (grid-stride). seg_out[g] gets
-// the segment's raw CRC shifted to the end of its chunk (shift: lane
-// constants of full chunks, shift_last: of a shorter final chunk).
-template <int DEPTH, class Visit>
-__device__ __forceinline__ void segment_crcs(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
-                                    int64_t spc, int64_t total_segs, const uint32_t* __restrict__ consts,
-                                    const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
-                                    uint32_t* __restrict__ seg_out, const uint32_t* lds, Visit& visit) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t* L = lds + (lane & 31);
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
-  for (int64_t g = wave; g < total_segs; g += nwaves) {
-    const int64_t c = g / spc, k = g % spc;
-    const int64_t chunk_start = c * chunk_bytes;
-    const int64_t chunk_len = min(chunk_bytes, bytes - chunk_start);
-    const int64_t seg_start = k * kSegBytes;
-    const int64_t seg_len = min(int64_t(kSegBytes), chunk_len - seg_start);
-    visit.begin(c, chunk_start, chunk_len);
-    const uint32_t* row = (chunk_len == chunk_bytes ? shift : shift_last) + k * 64;
-    const uint32_t s = one_segment<DEPTH>(src + chunk_start + seg_start, seg_start, seg_len, row, consts, L, lane,
-                                          visit);
-    if (lane == 0) seg_out[g] = s;
+struct Slice4 {
+  const uint8_t* lds;
+  uint32_t c3, c2, c1, c0;  // per table t: (pair << 16) | (half * 128 + replica * 4)
+  uint32_t g;               // kShLds + replica * 4
+  __device__ explicit Slice4(const uint8_t* l) : lds(l) {
+    const uint32_t r = (threadIdx.x & 31u) * 4u;
+    c0 = r;
+    c1 = 128u + r;
+    c2 = 0x10000u + r;
+    c3 = 0x10080u + r;
+    g = kShLds + r;
+  }
+  // byte k of s at bits 8-15, the constant's bytes 0 and 2 around it (v_perm_b32:
+  // selectors 0-3 pick bytes of the second operand, 4-7 of the first, 12 a zero)
+  template <uint32_t K>
+  __device__ __forceinline__ uint32_t lk(uint32_t s, uint32_t c) const {
+    return lds_word(lds, __builtin_amdgcn_perm(s, c, 0x0C020000u | ((4u + K) << 8)));
+  }
+  __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t w) const {
+    s ^= w;  // byte k of the word is followed by 3 - k bytes: table 3 - k
+    return (lk<0>(s, c3) ^ lk<1>(s, c2)) ^ (lk<2>(s, c1) ^ lk<3>(s, c0));
+  }
+  __device__ __forceinline__ uint32_t word16(uint32_t s, u32x4_t w) const {
+    return step(step(step(step(s, w[0]), w[1]), w[2]), w[3]);
+  }
+  __device__ __forceinline__ uint32_t gap(uint32_t s) const {  // shift over kGapBytes zeros
+    uint32_t r[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) r[n] = lds_word(lds, g + uint32_t(n) * 2048u + ((s >> (4 * n)) & 15u) * 128u);
+    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
+  }
+};
+
+// In-register 4x4 transpose across the 4 rows (16 lanes each) of a wave and 4
+// registers: afterwards register q of lane m + 16 r holds what register r of
+// lane m + 16 q held. permlane16_swap exchanges the odd rows of its first
+// operand with the even rows of its second (swaps row bit 0 with register bit
+// 0), permlane32_swap the upper half of the first with the lower half of the
+// second (row bit 1 with register bit 1).
+__device__ __forceinline__ void row_transpose(u32x4_t& r0, u32x4_t& r1, u32x4_t& r2, u32x4_t& r3) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const auto a = __builtin_amdgcn_permlane16_swap(r0[d], r1[d], false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(r2[d], r3[d], false, false);
+    const auto c = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+    const auto e = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+    r0[d] = c[0];
+    r2[d] = c[1];
+    r1[d] = e[0];
+    r3[d] = e[1];
   }
 }
 
-struct NoVisit {
-  __device__ void begin(int64_t, int64_t, int64_t) {}
-  __device__ void operator()(const uint4&, int64_t) {}
+// One segment as the walker sees it (all fields wave-uniform).
+struct Seg {
+  const uint8_t* p;     // first byte
+  int64_t len;          // bytes (16 KiB except a chunk's last)
+  const uint32_t* row;  // 64 lane shift constants of this full segment
+  int64_t chunk, chunk_start, chunk_len, seg_start;
 };
+
+struct NoVisit {
+  __device__ void begin(const Seg&) {}
+  __device__ void operator()(const u32x4_t&, int64_t) {}
+};
+
+// A segment shorter than 16 KiB (only ever its chunk's last): each lane takes
+// the strided 16-B words j = lane (mod 64), CRCs each from a zero register and
+// shifts it to the segment end with a pow16 constant; lane 0 adds the byte tail.
+template <class Visit>
+__device__ uint32_t slice_partial(const Seg& sg, const uint32_t* __restrict__ sc, const Slice4& st, int lane,
+                                  Visit& visit) {
+  const int64_t nw = sg.len >> 4;
+  const u32x4_t* words = reinterpret_cast<const u32x4_t*>(sg.p);
+  uint32_t acc = 0;
+  for (int64_t j = lane; j < nw; j += 64) {
+    const u32x4_t w = words[j];
+    visit(w, sg.seg_start + 16 * j);
+    acc ^= multmodp(sc[kPow + (nw - 1 - j)], st.word16(0, w));
+  }
+  acc = wave_xor(acc);
+  if (lane == 0) {
+    const uint8_t* tail = sg.p + (nw << 4);
+    for (int64_t b = 0; b < (sg.len & 15); ++b) acc = sc[kT + ((acc ^ tail[b]) & 255)] ^ (acc >> 8);
+  }
+  return acc;
+}
+
+// Every wave walks segments g = wave, wave + nwaves, ... (geo(g) -> Seg) and
+// writes seg_out[g]: the segment's raw CRC shifted to its chunk end. A wave
+// that owns several segments loads block b of the next one as soon as block b
+// of the current one is consumed (pinned with sched_barrier: left alone, the
+// compiler sinks those loads behind the math), so 16 KiB stay in flight per
+// wave. Visit sees every 16-B word (as loaded, before the transpose) with its
+// byte offset in the chunk.
+template <class Geo, class Visit>
+__device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, const uint32_t* __restrict__ sc,
+                                           const Slice4& st, Visit& visit, uint32_t* __restrict__ seg_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = __builtin_amdgcn_readfirstlane(int(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+  const int64_t nwaves = int64_t(gridDim.x) * kWaves;
+  // load i = 4 * block + j: KiB j of the block, lane m + 16 r reads word r of piece 16 j + m
+  const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
+  auto at = [&](const uint8_t* seg, int i) {
+    return reinterpret_cast<const u32x4_t*>(seg + (i >> 2) * kBlockBytes + (i & 3) * 1024 + lo);
+  };
+  u32x4_t w[4 * kBlocksPerSeg];
+  bool loaded = false;
+  int64_t g = wave;
+  if (g >= total_segs) return;
+  Seg cur = geo(g);
+  for (; g < total_segs; g += nwaves) {
+    const int64_t gn = g + nwaves;
+    Seg nxt{};
+    bool nfull = false;
+    if (gn < total_segs) {
+      nxt = geo(gn);
+      nfull = nxt.len == kSegBytes;
+    }
+    visit.begin(cur);
+    uint32_t s;
+    if (cur.len == kSegBytes) {
+      // the lane's shift constant first: behind the prefetches, its wait would
+      // also wait for the whole next segment
+      const uint32_t rowc = cur.row[lane];
+      if (!loaded) {
+#pragma unroll
+        for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
+          w[i] = __builtin_nontemporal_load(at(cur.p, i));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      s = 0;
+#pragma unroll
+      for (int b = 0; b < kBlocksPerSeg; ++b) {
+        if (b) s = st.gap(s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) visit(w[4 * b + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo);
+        row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s = st.word16(s, w[4 * b + q]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (nfull) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[4 * b + j] = __builtin_nontemporal_load(at(nxt.p, 4 * b + j));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      loaded = nfull;
+      s = wave_xor(multmodp(rowc, s));
+    } else {
+      s = slice_partial(cur, sc, st, lane, visit);
+      loaded = false;
+    }
+    if (lane == 0) seg_out[g] = s;
+    cur = nxt;
+  }
+}
+
+// `bytes` cut into chunks of `chunk_bytes`; shift / shift_last: lane constants
+// of full chunks / of a shorter final chunk.
+struct ChunkGeo {
+  const uint8_t* src;
+  int64_t bytes, chunk_bytes, spc;
+  const uint32_t* shift;
+  const uint32_t* shift_last;
+  __device__ Seg operator()(int64_t g) const {
+    const int64_t c = g / spc, k = g - c * spc;
+    Seg s;
+    s.chunk = c;
+    s.chunk_start = c * chunk_bytes;
+    s.chunk_len = min(chunk_bytes, bytes - s.chunk_start);
+    s.seg_start = k * kSegBytes;
+    s.p = src + s.chunk_start + s.seg_start;
+    s.len = min(int64_t(kSegBytes), s.chunk_len - s.seg_start);
+    s.row = (s.chunk_len == chunk_bytes ? shift : shift_last) + k * 64;
+    return s;
+  }
+};
+
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_segments_kernel(const ChunkGeo geo, int64_t total_segs, const uint32_t* __restrict__ sc,
+                       uint32_t* __restrict__ seg_out) {
+  __shared__ uint4 lds_raw[kLdsBytes / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  load_lds(lds, sc);
+  const Slice4 st(lds);
+  NoVisit v;
+  slice_walk(geo, total_segs, sc, st, v, seg_out);
+}
 
 __device__ inline uint16_t f32_to_bf16_rne(float f) {
   uint32_t u = __float_as_uint(f);
@@ -256,13 +312,12 @@ __device__ inline uint16_t f32_to_bf16_rne(float f) {
 }
 
 // 16 e4m3fn values (one 16-B word) times their block scale -> 16 bf16 (two 16-B words).
-__device__ inline void unpack16(uint4 w, float s, uint4* __restrict__ dst) {
-  const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+__device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ dst) {
   uint32_t o[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(int(d[i]), false);
-    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(int(d[i]), true);
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), true);
     o[2 * i] = uint32_t(f32_to_bf16_rne(lo[0] * s)) | (uint32_t(f32_to_bf16_rne(lo[1] * s)) << 16);
     o[2 * i + 1] = uint32_t(f32_to_bf16_rne(hi[0] * s)) | (uint32_t(f32_to_bf16_rne(hi[1] * s)) << 16);
   }
@@ -272,8 +327,10 @@ __device__ inline void unpack16(uint4 w, float s, uint4* __restrict__ dst) {
 
 // Fused verify + unpack of fp8-packed chunks (core/fp8.h layout
 // [q: n bytes][scales: n/BLOCK f32] per chunk): while computing each segment's
-// CRC, words in the q region are dequantized and written as bf16. Every packed
-// byte is read once from HBM; the scales (1/32 of the traffic) come from L2.
+// CRC, words in the q region are dequantized and written as bf16 (on the
+// words as loaded: each wave store instruction writes 2 whole KiB). Every
+// packed byte is read once from HBM; the scales (1/32 of the traffic) come
+// from L2.
 template <int BLOCK>
 struct UnpackVisit {
   int64_t out_chunk_elems;
@@ -282,124 +339,27 @@ struct UnpackVisit {
   int64_t n_q = 0;
   const float* scales = nullptr;
   uint16_t* obase = nullptr;
-  __device__ void begin(int64_t c, int64_t chunk_start, int64_t chunk_len) {
-    n_q = chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
-    scales = reinterpret_cast<const float*>(src + chunk_start + n_q);
-    obase = out + c * out_chunk_elems;
+  __device__ void begin(const Seg& sg) {
+    n_q = sg.chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
+    scales = reinterpret_cast<const float*>(src + sg.chunk_start + n_q);
+    obase = out + sg.chunk * out_chunk_elems;
   }
-  __device__ void operator()(const uint4& w, int64_t e) {  // e: byte offset in chunk = element index in q
+  __device__ void operator()(const u32x4_t& w, int64_t e) {  // e: byte offset in chunk = element index in q
     if (e < n_q) unpack16(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
   }
 };
 
-// Launch shape: 512 threads (8 waves), two workgroups per CU (LDS-bound at
-// 80 KiB each); waves_per_eu(4) keeps VGPRs <= 128 so both fit.
-constexpr int kSegThreads = 512;
-
-__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
-                       int64_t total_segs, const uint32_t* __restrict__ consts, const uint32_t* __restrict__ shift,
-                       const uint32_t* __restrict__ shift_last, uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t lds[kNibLds];
-  load_nib_lds(lds, consts);
-  NoVisit v;
-  segment_crcs<16>(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
-}
-
-// Rolling prefetch: a wave that owns several full segments issues the load of
-// word i of its NEXT segment right after consuming word i of the current one,
-// so the next segment's 16 KiB is in flight while this one's lookups run (the
-// same 64 data VGPRs as the plain kernel). The segment index math is
-// wave-uniform (scalar). Partial segments take the plain path.
-template <class Step>
-__device__ __forceinline__ void roll_walk(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes,
-                                          int64_t spc, int64_t total_segs, const uint32_t* __restrict__ consts,
-                                          const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
-                                          uint32_t* __restrict__ seg_out, const Step& step) {
-  using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-  const int lane = threadIdx.x & 63;
-  const int64_t wave =
-      __builtin_amdgcn_readfirstlane(int(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)));
-  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
-  struct Geo {
-    int64_t chunk_start, chunk_len, seg_start, seg_len, k;
-  };
-  auto geo = [&](int64_t g) {
-    Geo o;
-    const int64_t c = g / spc;
-    o.k = g - c * spc;
-    o.chunk_start = c * chunk_bytes;
-    o.chunk_len = min(chunk_bytes, bytes - o.chunk_start);
-    o.seg_start = o.k * kSegBytes;
-    o.seg_len = min(int64_t(kSegBytes), o.chunk_len - o.seg_start);
-    return o;
-  };
-  u32x4 w[kWordsPerLane];
-  bool loaded = false;
-  NoVisit v;
-  int64_t g = wave;
-  if (g >= total_segs) return;
-  Geo cur = geo(g);
-  for (; g < total_segs; g += nwaves) {
-    const u32x4* cw = reinterpret_cast<const u32x4*>(src + cur.chunk_start + cur.seg_start);
-    const int64_t gn = g + nwaves;
-    Geo nxt{};
-    bool nfull = false;
-    if (gn < total_segs) {
-      nxt = geo(gn);
-      nfull = nxt.seg_len == kSegBytes;
-    }
-    const uint32_t* row = (cur.chunk_len == chunk_bytes ? shift : shift_last) + cur.k * 64;
-    uint32_t s;
-    if (cur.seg_len == kSegBytes) {
-      if (!loaded) {
-#pragma unroll
-        for (int i = 0; i < kWordsPerLane; ++i) w[i] = __builtin_nontemporal_load(cw + lane + 64 * i);
-      }
-      // no next full segment: the prefetch re-reads this one (harmless, in bounds)
-      const u32x4* nw = nfull ? reinterpret_cast<const u32x4*>(src + nxt.chunk_start + nxt.seg_start) : cw;
-      s = 0;
-#pragma unroll
-      for (int i = 0; i < kWordsPerLane; ++i) {
-        const u32x4 x = w[i];
-        w[i] = __builtin_nontemporal_load(nw + lane + 64 * i);
-        s = step(s, make_uint4(x[0], x[1], x[2], x[3]));
-      }
-      loaded = nfull;
-      s = wave_xor(multmodp(row[lane], s));
-    } else {
-      s = one_segment_s<4>(src + cur.chunk_start + cur.seg_start, cur.seg_start, cur.seg_len, row, consts, step, lane,
-                           v);
-      loaded = false;
-    }
-    if (lane == 0) seg_out[g] = s;
-    cur = nxt;
-  }
-}
-
-// Byte-addressed tables (v2 layout above) + rolling prefetch.
-__global__ void __launch_bounds__(kSeg2Threads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_segments_roll2_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t chunk_bytes, int64_t spc,
-                             int64_t total_segs, const uint32_t* __restrict__ consts,
-                             const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
-                             uint32_t* __restrict__ seg_out) {
-  __shared__ uint4 lds[kNib2Bytes / 16];
-  uint8_t* base = reinterpret_cast<uint8_t*>(lds);
-  load_nib2_lds(base, consts);
-  roll_walk(src, bytes, chunk_bytes, spc, total_segs, consts, shift, shift_last, seg_out,
-            NibStep2{base, (threadIdx.x & 31u) * 4u});
-}
-
 template <int BLOCK>
-__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
-verify_unpack_segments_kernel(const uint8_t* __restrict__ src, int64_t bytes, int64_t pchunk, int64_t spc,
-                              int64_t total_segs, int64_t out_chunk_elems, const uint32_t* __restrict__ consts,
-                              const uint32_t* __restrict__ shift, const uint32_t* __restrict__ shift_last,
-                              uint32_t* __restrict__ seg_out, uint16_t* __restrict__ out) {
-  __shared__ uint32_t lds[kNibLds];
-  load_nib_lds(lds, consts);
-  UnpackVisit<BLOCK> v{out_chunk_elems, out, src};
-  segment_crcs<4>(src, bytes, pchunk, spc, total_segs, consts, shift, shift_last, seg_out, lds, v);
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
+                              const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
+                              uint16_t* __restrict__ out) {
+  __shared__ uint4 lds_raw[kLdsBytes / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  load_lds(lds, sc);
+  const Slice4 st(lds);
+  UnpackVisit<BLOCK> v{out_chunk_elems, out, geo.src};
+  slice_walk(geo, total_segs, sc, st, v, seg_out);
 }
 
 // One 256-thread block per chunk: XOR of the chunk's (pre-shifted) segment
@@ -433,25 +393,28 @@ struct BatchArgs {
   uint32_t* out[kCrcBatchMax];
 };
 
-__global__ void __launch_bounds__(kSegThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_batch_segments_kernel(const BatchArgs a, const uint32_t* __restrict__ consts, uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t lds[kNibLds];
-  load_nib_lds(lds, consts);
-  const int lane = threadIdx.x & 63;
-  const uint32_t* L = lds + (lane & 31);
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x / 64);
-  NoVisit v;
-  for (int64_t g = wave; g < a.seg_base[a.n]; g += nwaves) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_batch_segments_kernel(const BatchArgs a, const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out) {
+  __shared__ uint4 lds_raw[kLdsBytes / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  load_lds(lds, sc);
+  const Slice4 st(lds);
+  auto geo = [&](int64_t g) {
     int j = 0;
     while (g >= a.seg_base[j + 1]) ++j;
     const int64_t k = g - a.seg_base[j];
-    const int64_t seg_start = k * kSegBytes;
-    const int64_t seg_len = min(int64_t(kSegBytes), a.bytes[j] - seg_start);
-    const uint32_t s = one_segment<16>(a.src[j] + seg_start, seg_start, seg_len, a.shift[j] + k * 64, consts, L,
-                                       lane, v);
-    if (lane == 0) seg_out[g] = s;
-  }
+    Seg s;
+    s.chunk = j;
+    s.chunk_start = 0;
+    s.chunk_len = a.bytes[j];
+    s.seg_start = k * kSegBytes;
+    s.p = a.src[j] + s.seg_start;
+    s.len = min(int64_t(kSegBytes), a.bytes[j] - s.seg_start);
+    s.row = a.shift[j] + k * 64;
+    return s;
+  };
+  NoVisit v;
+  slice_walk(geo, a.seg_base[a.n], sc, st, v, seg_out);
 }
 
 __global__ void __launch_bounds__(256) crc32c_batch_fold_kernel(const BatchArgs a,
@@ -476,13 +439,13 @@ struct DeviceConsts {
 DeviceConsts g_consts;
 
 // Per full segment k of a `len`-byte chunk and lane l: x^(8 * (bytes from the
-// end of lane l's last word to the chunk end)) = x^(8*16*(63 - l)) * x^(8 * (len - end of k)).
+// end of lane l's last piece to the chunk end)) = x^(8*64*(63 - l)) * x^(8 * (len - end of k)).
 void lane_shifts(int64_t len, int64_t spc, uint32_t* out) {
   const int64_t nfull = len / kSegBytes;
   std::fill(out, out + spc * 64, 0u);  // partial / absent segments: unused
   if (nfull == 0) return;
   uint32_t lanepow[64];
-  for (int m = 0; m < 64; ++m) lanepow[m] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
+  for (int m = 0; m < 64; ++m) lanepow[m] = crc32c_xpow8n(uint64_t(kPieceBytes) * uint64_t(m));
   const uint32_t xs = crc32c_xpow8n(kSegBytes);
   uint32_t seg = crc32c_xpow8n(uint64_t(len - nfull * kSegBytes));  // last full segment
   for (int64_t k = nfull - 1; k >= 0; --k) {
@@ -517,19 +480,13 @@ uint32_t* device_consts() {
   std::lock_guard<std::mutex> lk(g_consts.mu);
   auto it = g_consts.by_device.find(dev);
   if (it != g_consts.by_device.end()) return it->second;
-  std::vector<uint32_t> T(16 * 256), A(4 * 256), h(kConstWords);
+  std::vector<uint32_t> T(16 * 256), h(kConstWords);
   crc32c_slice16_tables(T.data());
-  crc32c_shift_tables(1024, A.data());
-  for (int i = 0; i < 256; ++i) h[size_t(kOffT0 + i)] = T[size_t(i)];
-  for (int m = 0; m < 64; ++m) h[size_t(kOffLanePow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
-  // Nibble tables: t = 2k + hi for data byte k (slice-by-16 table 15 - k),
-  // t = 32 + 2i + hi for byte i of the register (1 KiB shift map).
-  for (int t = 0; t < kNibTables; ++t)
-    for (uint32_t v = 0; v < 16; ++v) {
-      const uint32_t byte = v << (4 * (t & 1));
-      h[size_t(kOffNib + t * 16 + int(v))] =
-          t < 32 ? T[size_t((15 - t / 2) * 256) + byte] : A[size_t(((t - 32) / 2) * 256) + byte];
-    }
+  for (int i = 0; i < 4 * 256; ++i) h[size_t(kT + i)] = T[size_t(i)];
+  const uint32_t xg = crc32c_xpow8n(kGapBytes);
+  for (int n = 0; n < 8; ++n)
+    for (uint32_t v = 0; v < 16; ++v) h[size_t(kGap + n * 16 + int(v))] = crc32c_multmodp(xg, v << (4 * n));
+  for (int m = 0; m < 1024; ++m) h[size_t(kPow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
   uint32_t* d = nullptr;
   if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
   if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
@@ -537,10 +494,11 @@ uint32_t* device_consts() {
   return d;
 }
 
-// Two workgroups per CU, one 16 KiB segment per wave (grid-stride beyond that).
-dim3 seg_grid(int64_t total_segs) {
-  const int64_t waves = kSegThreads / 64;
-  return dim3(unsigned(std::min<int64_t>((total_segs + waves - 1) / waves, 2 * 256)));
+// One workgroup per CU (LDS-bound), 16 segments per workgroup at a time;
+// grid-stride beyond that.
+dim3 seg_grid(int64_t total_segs, int max_blocks) {
+  const int64_t cap = max_blocks > 0 ? max_blocks : 256;
+  return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>((total_segs + kWaves - 1) / kWaves, cap))));
 }
 
 struct Plan {
@@ -569,33 +527,19 @@ size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes) {
 
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                          hipStream_t s) {
-  return crc32c_chunks_impl(src, bytes, chunk_bytes, out, workspace, s, CrcImpl::kAuto, 0);
+  return crc32c_chunks_capped(src, bytes, chunk_bytes, out, workspace, s, 0);
 }
 
-hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
-                              hipStream_t s, CrcImpl impl, int max_blocks) {
+hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
+                                hipStream_t s, int max_blocks) {
   if (bytes <= 0) return hipSuccess;
   if (chunk_bytes <= 0 || chunk_bytes % 16 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  if (impl == CrcImpl::kRolling ||
-      (impl == CrcImpl::kAuto && p.total_segs >= 2 * int64_t(256) * (kSeg2Threads / 64))) {
-    // bulk launches where every wave of the full grid owns >= 2 segments:
-    // 3.32 TB/s on 1 GiB vs 2.69 for the plain kernel; a single 64 MiB chunk
-    // has one segment per wave - nothing to overlap - and stays on the plain
-    // kernel: 31 vs 38 us (profiles/r2_crc_ab/crc_roll2.json)
-    const int64_t waves = kSeg2Threads / 64;
-    const int64_t cap = max_blocks > 0 ? max_blocks : 256;
-    const dim3 grid(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + waves - 1) / waves, cap))));
-    crc32c_segments_roll2_kernel<<<grid, dim3(kSeg2Threads), 0, s>>>(
-        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
-        p.fold + p.spc * 64, seg);
-  } else {
-    crc32c_segments_kernel<<<seg_grid(p.total_segs), dim3(kSegThreads), 0, s>>>(
-        static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.total_segs, p.consts, p.fold,
-        p.fold + p.spc * 64, seg);
-  }
+  const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.fold, p.fold + p.spc * 64};
+  crc32c_segments_kernel<<<seg_grid(p.total_segs, max_blocks), dim3(kThreads), 0, s>>>(geo, p.total_segs, p.consts,
+                                                                                        seg);
   crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, chunk_bytes, p.spc,
                                                                      p.fold + 2 * p.spc * 64, out);
   return hipGetLastError();
@@ -631,7 +575,7 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
   }
   if (a.n == 0) return hipSuccess;
   auto* seg = static_cast<uint32_t*>(workspace);
-  crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n]), dim3(kSegThreads), 0, s>>>(a, consts, seg);
+  crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n], 0), dim3(kThreads), 0, s>>>(a, consts, seg);
   crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(256), 0, s>>>(a, seg);
   return hipGetLastError();
 }
@@ -648,16 +592,15 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   Plan p;
   if (hipError_t e = plan(bytes, pchunk, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  auto* src = static_cast<const uint8_t*>(packed);
+  const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.fold, p.fold + p.spc * 64};
   const int64_t oc = src_chunk / 2;
-  const dim3 grid = seg_grid(p.total_segs), tpb{kSegThreads};
-  const uint32_t *sp = p.fold, *sl = p.fold + p.spc * 64;
+  const dim3 grid = seg_grid(p.total_segs, 0), tpb{kThreads};
   switch (block) {
-    case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
-    case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
-    case 128: verify_unpack_segments_kernel<128><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
-    case 256: verify_unpack_segments_kernel<256><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
-    case 512: verify_unpack_segments_kernel<512><<<grid, tpb, 0, s>>>(src, bytes, pchunk, p.spc, p.total_segs, oc, p.consts, sp, sl, seg, out); break;
+    case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
+    case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
+    case 128: verify_unpack_segments_kernel<128><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
+    case 256: verify_unpack_segments_kernel<256><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
+    case 512: verify_unpack_segments_kernel<512><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
     default: return hipErrorInvalidValue;
   }
   crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, pchunk, p.spc,

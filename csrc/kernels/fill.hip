@@ -91,6 +91,67 @@ hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, i
   return hipGetLastError();
 }
 
+// Segment-read probe: the CRC kernels' access shape with no compute. One wave
+// reads one 16 KiB segment at a time (16 x 16-B loads per lane, all in flight),
+// grid-strided over segments, 1024-thread workgroups. layout 0: lane l takes
+// the 64-B piece l of each 4 KiB block (crc32c v3); 1: the 16-B words l + 64 i
+// (v1/v2). rolling: the next segment's word i is loaded as word i is consumed.
+template <int LAYOUT, bool ROLL>
+__global__ void __launch_bounds__(1024) read_seg_kernel(const uint8_t* __restrict__ src, int64_t nseg,
+                                                        uint32_t* __restrict__ out) {
+  using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = int64_t(blockIdx.x) * 16 + (threadIdx.x >> 6);
+  const int64_t nwaves = int64_t(gridDim.x) * 16;
+  auto at = [&](int64_t g, int i) {
+    const uint8_t* seg = src + g * 16384;
+    return reinterpret_cast<const u32x4*>(LAYOUT == 0 ? seg + (i >> 2) * 4096 + 64 * lane + 16 * (i & 3)
+                                                      : seg + 16 * (lane + 64 * i));
+  };
+  uint32_t acc = 0;
+  u32x4 w[16];
+  int64_t g = wave;
+  if (g < nseg) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = __builtin_nontemporal_load(at(g, i));
+  }
+  for (; g < nseg; g += nwaves) {
+    const int64_t gn = g + nwaves;
+    if (ROLL && gn < nseg) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const u32x4 x = w[i];
+        acc ^= x[0] ^ x[1] ^ x[2] ^ x[3];
+        w[i] = __builtin_nontemporal_load(at(gn, i));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc ^= w[i][0] ^ w[i][1] ^ w[i][2] ^ w[i][3];
+      if (gn < nseg) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_nontemporal_load(at(gn, i));
+      }
+    }
+  }
+  out[int64_t(blockIdx.x) * blockDim.x + threadIdx.x] = acc;
+}
+
+hipError_t read_seg(const void* src, int64_t bytes, uint32_t* out, int blocks, int layout, bool roll, hipStream_t s) {
+  if (bytes <= 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) || bytes % 16384 || blocks <= 0) return hipErrorInvalidValue;
+  const auto* p = static_cast<const uint8_t*>(src);
+  const int64_t nseg = bytes / 16384;
+  const dim3 g{unsigned(blocks)}, b{1024};
+  if (layout == 0) {
+    if (roll) read_seg_kernel<0, true><<<g, b, 0, s>>>(p, nseg, out);
+    else read_seg_kernel<0, false><<<g, b, 0, s>>>(p, nseg, out);
+  } else {
+    if (roll) read_seg_kernel<1, true><<<g, b, 0, s>>>(p, nseg, out);
+    else read_seg_kernel<1, false><<<g, b, 0, s>>>(p, nseg, out);
+  }
+  return hipGetLastError();
+}
+
 void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset) {
   // Bytes [offset, offset+bytes) of the stream (offset: any byte position).
   auto* p = static_cast<uint8_t*>(dst);

@@ -26,6 +26,11 @@ void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset = 
 // Read-bandwidth probe: XOR of [src, src+bytes) into blocks*4 dwords at out
 // (bytes % 16 == 0); `depth` 16-B loads in flight per lane (1, 2, 4, 8).
 hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, int depth, hipStream_t s);
+// Segment-read probe (the CRC kernels' load shape, no compute): 16 KiB per
+// wave, 1024-thread workgroups, `blocks` of them; layout 0 = 64-B lane pieces,
+// 1 = strided 16-B words; roll = prefetch the next segment while consuming.
+// out: blocks * 1024 dwords; bytes % 16384 == 0.
+hipError_t read_seg(const void* src, int64_t bytes, uint32_t* out, int blocks, int layout, bool roll, hipStream_t s);
 
 // ---- crc32c.hip: CRC32C of every `chunk_bytes` chunk of [src, src+bytes).
 // out[c] (device or host-mapped memory) receives the standard CRC32C of chunk c.
@@ -44,16 +49,12 @@ struct CrcItem {
   uint32_t* out;
 };
 size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
-// Segment kernel choice: kNibble = bank-private nibble tables, one 16 KiB
-// segment per wave (the per-landing check of one 64 MiB chunk: 31 us);
-// kRolling = byte-addressed tables with a rolling prefetch of each wave's next
-// segment (bulk launches: 3.3 TB/s); kAuto = kRolling when every wave of the
-// full grid owns >= 2 segments, else kNibble. max_blocks caps the grid of
-// kRolling (0 = one workgroup per CU). The A/B that chose these (MFMA GF(2)
-// products, 8 waves per SIMD, rolling on nibble tables) is in profiles/r2_crc_ab.
-enum class CrcImpl { kAuto = 0, kNibble = 1, kRolling = 2 };
-hipError_t crc32c_chunks_impl(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
-                              hipStream_t s, CrcImpl impl, int max_blocks);
+// crc32c_chunks with the segment kernel's grid capped at max_blocks workgroups
+// (0 = one per CU); capped grids put many segments on every wave (tests, A/B).
+// The segment kernel (slice-by-4 byte tables on lane-contiguous 64-B pieces of
+// coalesced loads) and the variants it replaced: crc32c.hip, profiles/r2_crc_ab.
+hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
+                                hipStream_t s, int max_blocks);
 hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements

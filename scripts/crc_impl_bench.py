@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
-"""A/B of the CRC32C segment kernels on one MI355X.
+"""Throughput of the CRC32C segment kernel on one MI355X, against read probes.
 
-impl 1 = bank-private nibble tables, one 16 KiB segment per wave (the
-per-landing check), 2 = byte-addressed tables with a rolling prefetch of each
-wave's next segment (bulk; capped grids: more segments per wave), 0 = auto.
-(The MFMA GF(2)-product kernel, an 8-waves-per-SIMD variant and rolling on
-nibble tables lost this A/B and were removed: profiles/r2_crc_ab.)
-Shapes: 1 GiB in 64 MiB chunks (bulk throughput) and one 64 MiB chunk (the
-per-landing verify of the data engine). Prints one JSON object.
+The kernel (csrc/kernels/crc32c.hip): slice-by-4 byte tables on lane-contiguous
+64-B pieces of coalesced loads, one 1024-thread workgroup per CU; capped grids
+(max_blocks) put more segments on every wave. The variants it replaced (nibble
+tables on strided words, rolling byte-addressed nibble tables, MFMA GF(2)
+products, directly loaded pieces, 4 recurrences per lane) and their numbers are
+in profiles/r2_crc_ab. Shapes: 1 GiB in 64 MiB chunks (bulk throughput) and one
+64 MiB chunk (the per-landing verify of the data engine). Prints one JSON object.
 """
 
 import json
@@ -32,7 +32,7 @@ def timed(fn, reps):
 
 
 def main():
-    quick = "--quick" in sys.argv  # one variant per kernel (counter passes)
+    quick = "--quick" in sys.argv  # default grid only (counter passes)
     n, chunk = 1 << 30, 64 << 20
     buf = torch.empty(n, dtype=torch.uint8, device="cuda")
     _core.fill_random(buf.data_ptr(), n, 3)
@@ -41,15 +41,15 @@ def main():
     host = buf.cpu().numpy().tobytes()
     want = [_core.crc32c(host[i:i + chunk]) for i in range(0, n, chunk)]
     out = {}
-    variants = [("nibble", 1, 0), ("roll2", 2, 0), ("roll2_cap128", 2, 128), ("roll2_cap512", 2, 512), ("auto", 0, 0)]
+    variants = [("slice", 0), ("slice_cap128", 128), ("slice_cap512", 512)]
     if quick:
-        variants = [("nibble", 1, 0), ("roll2", 2, 0)]
-    for name, impl, cap in variants:
+        variants = [("slice", 0)]
+    for name, cap in variants:
         def bulk():
-            _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)
+            _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0, cap)
 
         def one():
-            _core.crc32c_chunks_async(buf.data_ptr(), chunk, chunk, res.data_ptr(), ws.data_ptr(), 0, impl, cap)
+            _core.crc32c_chunks_async(buf.data_ptr(), chunk, chunk, res.data_ptr(), ws.data_ptr(), 0, cap)
 
         t = timed(bulk, 20)
         out[f"{name}_1GiB_GBps"] = round(n / t / 1e9, 1)
@@ -66,6 +66,14 @@ def main():
         for depth in (4, 8):
             t = timed(lambda: _core.read_xor_async(buf.data_ptr(), n, outx.data_ptr(), blocks, depth, 0), 20)
             out[f"read_xor_b{blocks}_d{depth}_GBps"] = round(n / t / 1e9, 1)
+    # The CRC kernels' load shape without the CRC math (16 KiB per wave, 1024-thread
+    # workgroups): layout 0 = 64-B lane pieces (slice), 1 = strided words (nibble, roll2).
+    outs = torch.empty(1024 * 1024, dtype=torch.int32, device="cuda")
+    for blocks in (256, 512):
+        for layout in (0, 1):
+            for roll in (False, True):
+                t = timed(lambda: _core.read_seg_async(buf.data_ptr(), n, outs.data_ptr(), blocks, layout, roll, 0), 20)
+                out[f"read_seg_b{blocks}_l{layout}_r{int(roll)}_GBps"] = round(n / t / 1e9, 1)
     print(json.dumps(out))
 
 

@@ -30,7 +30,7 @@ def test_fill_random_matches_host(gpu, n):
         (64 << 20, 64 << 20),
         ((64 << 20) + (5 << 10) + 3, 64 << 20),  # short last chunk: its own segment shifts and init term
         (100 << 10, 100 << 10),  # a partial 16 KiB segment inside one chunk
-        ((160 << 20) + 48, 64 << 20),  # bulk: auto picks the rolling byte-table kernel
+        ((160 << 20) + 48, 64 << 20),  # bulk: every wave owns several segments (rolling prefetch)
     ],
 )
 def test_crc32c_chunks_match_host(gpu, n, chunk):
@@ -51,11 +51,9 @@ def test_crc32c_chunks_match_host(gpu, n, chunk):
     ],
 )
 @pytest.mark.parametrize("max_blocks", [0, 3, 64])
-@pytest.mark.parametrize("impl", [1, 2])
-def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks, impl):
-    """impl 2: the byte-table kernel that prefetches each wave's next segment
-    while computing the current one (impl 1: the plain kernel); capped grids put
-    many segments (full and partial, across chunk boundaries) on every wave."""
+def test_crc32c_capped_grid_matches_host(gpu, n, chunk, max_blocks):
+    """Capped grids put many segments (full and partial, across chunk boundaries)
+    on every wave, so the rolling prefetch of each wave's next segment runs."""
     t = _dev_bytes(n)
     gpu.fill_random(t.data_ptr(), n, 5 + n)
     torch.cuda.synchronize()
@@ -64,7 +62,7 @@ def test_crc32c_rolling_prefetch_matches_host(gpu, n, chunk, max_blocks, impl):
     nch = len(want)
     out = torch.zeros(nch, dtype=torch.int32, device="cuda")
     ws = torch.empty(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
-    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, impl, max_blocks)
+    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, max_blocks)
     torch.cuda.synchronize()
     assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
 
