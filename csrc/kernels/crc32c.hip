@@ -43,7 +43,11 @@
 // byte-addressed nibble tables with a rolling prefetch (3.3 TB/s), an MFMA
 // GF(2) product (2.3 TB/s), slice-by-4 on directly loaded pieces (3.1 TB/s)
 // and with 4 independent recurrences per lane (2.3-2.5 TB/s) all lost to this
-// kernel: 5.26 TB/s on 1 GiB, 23.4 us per single 64 MiB chunk.
+// kernel: 5.06 TB/s on 1 GiB (212 us, kernel trace; the same load shape with
+// no math reads at 6.8 TB/s), 19.2 us + 4.8 us fold per single 64 MiB chunk.
+// Two recurrences per lane (blocks 0-1 and 2-3, joined by an 8 KiB shift
+// table in the last 16 KiB of LDS) measured 229 us: the chain latency is not
+// what bounds it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -201,6 +205,19 @@ __device__ uint32_t slice_partial(const Seg& sg, const uint32_t* __restrict__ sc
   return acc;
 }
 
+// The 16 loads of a segment's words go through a buffer resource whose size is
+// 16 KiB for a full segment and 0 otherwise: an out-of-range buffer load
+// returns zeros without touching memory, so every path issues the same loads
+// and the compiler's vmcnt waits stay exact (with the prefetch under an `if`,
+// it had to wait for ALL outstanding loads, the next segment's included).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const uint8_t* p, bool full) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, full ? kSegBytes : 0, 0x00020000);
+}
+// load i = 4 * block + j: KiB j of the block, lane m + 16 r reads word r of piece 16 j + m (nt)
+__device__ __forceinline__ u32x4_t seg_load(__amdgpu_buffer_rsrc_t r, int lo, int i) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (i >> 2) * kBlockBytes + (i & 3) * 1024 + lo, 0, 2);
+}
+
 // Every wave walks segments g = wave, wave + nwaves, ... (geo(g) -> Seg) and
 // writes seg_out[g]: the segment's raw CRC shifted to its chunk end. A wave
 // that owns several segments loads block b of the next one as soon as block b
@@ -214,37 +231,33 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
   const int lane = threadIdx.x & 63;
   const int64_t wave = __builtin_amdgcn_readfirstlane(int(blockIdx.x * kWaves + (threadIdx.x >> 6)));
   const int64_t nwaves = int64_t(gridDim.x) * kWaves;
-  // load i = 4 * block + j: KiB j of the block, lane m + 16 r reads word r of piece 16 j + m
   const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
-  auto at = [&](const uint8_t* seg, int i) {
-    return reinterpret_cast<const u32x4_t*>(seg + (i >> 2) * kBlockBytes + (i & 3) * 1024 + lo);
-  };
-  u32x4_t w[4 * kBlocksPerSeg];
-  bool loaded = false;
   int64_t g = wave;
   if (g >= total_segs) return;
   Seg cur = geo(g);
+  // invariant at the loop top: w holds cur's words if cur is a full segment
+  u32x4_t w[4 * kBlocksPerSeg];
+  {
+    const auto r = seg_rsrc(cur.p, cur.len == kSegBytes);
+#pragma unroll
+    for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {  // in order: every path issues w[0..15] oldest first
+      w[i] = seg_load(r, lo, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   for (; g < total_segs; g += nwaves) {
     const int64_t gn = g + nwaves;
-    Seg nxt{};
+    Seg nxt = cur;  // no next segment: loads against an empty resource
     bool nfull = false;
     if (gn < total_segs) {
       nxt = geo(gn);
       nfull = nxt.len == kSegBytes;
     }
+    const auto rn = seg_rsrc(nxt.p, nfull);
     visit.begin(cur);
     uint32_t s;
     if (cur.len == kSegBytes) {
-      // the lane's shift constant first: behind the prefetches, its wait would
-      // also wait for the whole next segment
       const uint32_t rowc = cur.row[lane];
-      if (!loaded) {
-#pragma unroll
-        for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
-          w[i] = __builtin_nontemporal_load(at(cur.p, i));
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
       s = 0;
 #pragma unroll
       for (int b = 0; b < kBlocksPerSeg; ++b) {
@@ -255,19 +268,22 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
 #pragma unroll
         for (int q = 0; q < 4; ++q) s = st.word16(s, w[4 * b + q]);
         __builtin_amdgcn_sched_barrier(0);
-        if (nfull) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) w[4 * b + j] = __builtin_nontemporal_load(at(nxt.p, 4 * b + j));
-        }
+        for (int j = 0; j < 4; ++j) w[4 * b + j] = seg_load(rn, lo, 4 * b + j);
         __builtin_amdgcn_sched_barrier(0);
       }
-      loaded = nfull;
       s = wave_xor(multmodp(rowc, s));
     } else {
       s = slice_partial(cur, sc, st, lane, visit);
-      loaded = false;
     }
     if (lane == 0) seg_out[g] = s;
+    if (cur.len != kSegBytes) {  // (rare) w did not take the next segment's words yet
+#pragma unroll
+      for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
+        w[i] = seg_load(rn, lo, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     cur = nxt;
   }
 }
@@ -494,8 +510,9 @@ uint32_t* device_consts() {
   return d;
 }
 
-// One workgroup per CU (LDS-bound), 16 segments per workgroup at a time;
-// grid-stride beyond that.
+// One workgroup per CU (LDS-bound), 16 segments per workgroup at a time,
+// grid-stride beyond that. Kernel trace on 1 GiB (profiles/r2_crc_slice):
+// 212 us with 256 workgroups, 243 with 512, 224 with 1024.
 dim3 seg_grid(int64_t total_segs, int max_blocks) {
   const int64_t cap = max_blocks > 0 ? max_blocks : 256;
   return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>((total_segs + kWaves - 1) / kWaves, cap))));

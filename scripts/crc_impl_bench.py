@@ -41,7 +41,7 @@ def main():
     host = buf.cpu().numpy().tobytes()
     want = [_core.crc32c(host[i:i + chunk]) for i in range(0, n, chunk)]
     out = {}
-    variants = [("slice", 0), ("slice_cap128", 128), ("slice_cap512", 512)]
+    variants = [("slice", 0), ("slice_cap128", 128), ("slice_cap512", 512), ("slice_cap1024", 1024)]
     if quick:
         variants = [("slice", 0)]
     for name, cap in variants:

@@ -15,7 +15,7 @@
 #   profile    kernel trace of the headline bench and the fp8 subset
 #   disk       NVMe tier bench + diskspeed
 #   fp8        BASELINE #5 at N = 1: full 126 x 3 GiB fp8 preset; --store bf16 subset
-#   crcpmc     SQ issue/wait counters + fetch of the CRC kernels (plain vs rolling byte tables)
+#   crcpmc     SQ issue/wait counters + fetch of the CRC segment kernel
 #   contention probe-kernel launch delay under a CRC burst (CU reservation)
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
