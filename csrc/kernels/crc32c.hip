@@ -320,11 +320,13 @@ crc32c_segments_kernel(const ChunkGeo geo, int64_t total_segs, const uint32_t* _
   slice_walk(geo, total_segs, sc, st, v, seg_out);
 }
 
-__device__ inline uint16_t f32_to_bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return uint16_t(u >> 16);
+// Two f32 -> packed bf16 (a in the low half), round-to-nearest-even, NaN kept
+// quiet: gfx950's v_cvt_pk_bf16_f32, one VALU per pair (the integer RNE
+// sequence it replaces took ~6 per value and made the fused kernel spill).
+__device__ inline uint32_t pk_bf16(float a, float b) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
 
 // 16 e4m3fn values (one 16-B word) times their block scale -> 16 bf16 (two 16-B words).
@@ -334,8 +336,8 @@ __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ d
   for (int i = 0; i < 4; ++i) {
     const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), false);
     const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), true);
-    o[2 * i] = uint32_t(f32_to_bf16_rne(lo[0] * s)) | (uint32_t(f32_to_bf16_rne(lo[1] * s)) << 16);
-    o[2 * i + 1] = uint32_t(f32_to_bf16_rne(hi[0] * s)) | (uint32_t(f32_to_bf16_rne(hi[1] * s)) << 16);
+    o[2 * i] = pk_bf16(lo[0] * s, lo[1] * s);
+    o[2 * i + 1] = pk_bf16(hi[0] * s, hi[1] * s);
   }
   dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
   dst[1] = make_uint4(o[4], o[5], o[6], o[7]);

@@ -23,11 +23,13 @@ namespace {
 
 __device__ inline float bf16_to_f32(uint16_t b) { return __uint_as_float(uint32_t(b) << 16); }
 
-__device__ inline uint16_t f32_to_bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return uint16_t(u >> 16);
+// Two f32 -> packed bf16 (a in the low half), round-to-nearest-even, NaN kept
+// quiet: gfx950's v_cvt_pk_bf16_f32, one VALU per pair (the integer RNE
+// sequence it replaces took ~6 per value and made the fused kernel spill).
+__device__ inline uint32_t pk_bf16(float a, float b) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
 
 __device__ inline bool finite(float x) { return (__float_as_uint(x) & 0x7F800000u) != 0x7F800000u; }
@@ -80,9 +82,7 @@ __global__ void __launch_bounds__(256) fp8_unpack_kernel(const uint2* __restrict
   const auto f1 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.x), true);
   const auto f2 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.y), false);
   const auto f3 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.y), true);
-  auto pk = [s](float a, float b) {
-    return uint32_t(f32_to_bf16_rne(a * s)) | (uint32_t(f32_to_bf16_rne(b * s)) << 16);
-  };
+  auto pk = [s](float a, float b) { return pk_bf16(a * s, b * s); };
   out[t] = make_uint4(pk(f0[0], f0[1]), pk(f1[0], f1[1]), pk(f2[0], f2[1]), pk(f3[0], f3[1]));
 }
 

@@ -67,7 +67,8 @@ def main():
             t = timed(lambda: _core.read_xor_async(buf.data_ptr(), n, outx.data_ptr(), blocks, depth, 0), 20)
             out[f"read_xor_b{blocks}_d{depth}_GBps"] = round(n / t / 1e9, 1)
     # The CRC kernels' load shape without the CRC math (16 KiB per wave, 1024-thread
-    # workgroups): layout 0 = 64-B lane pieces (slice), 1 = strided words (nibble, roll2).
+    # workgroups): layout 0 = each lane loads its own 64-B piece, 1 = every load instruction reads
+    # one whole KiB (the CRC kernel's loads, before its in-register transpose).
     outs = torch.empty(1024 * 1024, dtype=torch.int32, device="cuda")
     for blocks in (256, 512):
         for layout in (0, 1):
