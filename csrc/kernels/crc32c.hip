@@ -43,8 +43,11 @@
 // byte-addressed nibble tables with a rolling prefetch (3.3 TB/s), an MFMA
 // GF(2) product (2.3 TB/s), slice-by-4 on directly loaded pieces (3.1 TB/s)
 // and with 4 independent recurrences per lane (2.3-2.5 TB/s) all lost to this
-// kernel: 5.06 TB/s on 1 GiB (212 us, kernel trace; the same load shape with
-// no math reads at 6.8 TB/s), 19.2 us + 4.8 us fold per single 64 MiB chunk.
+// kernel: 5.76 TB/s on 1 GiB (186.5 us, kernel trace; the same load shape with
+// no math reads at 6.8 TB/s), 16.6 us + 4.5 us fold per single 64 MiB chunk.
+// Per 16 KiB segment a wave issues ~256 v_perm + ~130 v_bitop3 (3-input XORs)
+// for the lookups, 64 permlane swaps and ~160 VALU for the branch-free shift to
+// the chunk end (the divergent multiply loop cost 212 us per GiB).
 // Two recurrences per lane (blocks 0-1 and 2-3, joined by an 8 KiB shift
 // table in the last 16 KiB of LDS) measured 229 us: the chain latency is not
 // what bounds it.
@@ -92,10 +95,34 @@ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
+// a(x) * b(x) mod P with no branches: 32 unrolled steps, each a masked XOR and
+// a conditional reduction (the loop above diverges per lane and costs ~3x the
+// instructions; it stays for the rare partial segments).
+__device__ __forceinline__ uint32_t multmodp_unrolled(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; --i) {
+    p ^= b & (0u - ((a >> i) & 1u));
+    b = (b >> 1) ^ (kCrc32cPoly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
 __device__ inline uint32_t wave_xor(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
   return v;
+}
+
+// XOR of v over the wave, wave-uniform: DPP within each row of 16 lanes
+// (quad swaps, half-row and row mirrors), then the 4 row results by readlane.
+__device__ __forceinline__ uint32_t wave_xor_dpp(uint32_t v) {
+  v ^= uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v ^= uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v ^= uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v ^= uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return uint32_t(__builtin_amdgcn_readlane(int(v), 0)) ^ uint32_t(__builtin_amdgcn_readlane(int(v), 16)) ^
+         uint32_t(__builtin_amdgcn_readlane(int(v), 32)) ^ uint32_t(__builtin_amdgcn_readlane(int(v), 48));
 }
 
 __device__ __forceinline__ uint32_t lds_word(const uint8_t* lds, uint32_t byte_addr) {
@@ -135,18 +162,25 @@ struct Slice4 {
   __device__ __forceinline__ uint32_t lk(uint32_t s, uint32_t c) const {
     return lds_word(lds, __builtin_amdgcn_perm(s, c, 0x0C020000u | ((4u + K) << 8)));
   }
-  __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t w) const {
-    s ^= w;  // byte k of the word is followed by 3 - k bytes: table 3 - k
-    return (lk<0>(s, c3) ^ lk<1>(s, c2)) ^ (lk<2>(s, c1) ^ lk<3>(s, c0));
+  // One slice-by-4 step on a register that already holds (crc ^ word), with the
+  // NEXT word folded in: T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3] ^ next (byte k of
+  // the word is followed by 3 - k bytes: table 3 - k) - two 3-input XORs.
+  __device__ __forceinline__ uint32_t mix(uint32_t s, uint32_t next) const {
+    return x3(x3(lk<0>(s, c3), lk<1>(s, c2), lk<2>(s, c1)), lk<3>(s, c0), next);
   }
   __device__ __forceinline__ uint32_t word16(uint32_t s, u32x4_t w) const {
-    return step(step(step(step(s, w[0]), w[1]), w[2]), w[3]);
+    return mix(mix(mix(mix(s ^ w[0], w[1]), w[2]), w[3]), 0u);
   }
-  __device__ __forceinline__ uint32_t gap(uint32_t s) const {  // shift over kGapBytes zeros
+  // shift over kGapBytes zeros, with `next` folded in
+  __device__ __forceinline__ uint32_t gap(uint32_t s, uint32_t next) const {
     uint32_t r[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) r[n] = lds_word(lds, g + uint32_t(n) * 2048u + ((s >> (4 * n)) & 15u) * 128u);
-    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
+    return x3(x3(x3(r[0], r[1], r[2]), r[3], r[4]), x3(r[5], r[6], r[7]), next);
+  }
+  // a ^ b ^ c in one v_bitop3_b32
+  static __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
 };
 
@@ -258,21 +292,23 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
     uint32_t s;
     if (cur.len == kSegBytes) {
       const uint32_t rowc = cur.row[lane];
+      // s holds (register ^ next word) between steps: 16 mix steps per block,
+      // the block's first word folded into the gap shift before it
       s = 0;
 #pragma unroll
       for (int b = 0; b < kBlocksPerSeg; ++b) {
-        if (b) s = st.gap(s);
 #pragma unroll
         for (int j = 0; j < 4; ++j) visit(w[4 * b + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo);
         row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
+        s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s = st.word16(s, w[4 * b + q]);
+        for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[4 * b + j] = seg_load(rn, lo, 4 * b + j);
         __builtin_amdgcn_sched_barrier(0);
       }
-      s = wave_xor(multmodp(rowc, s));
+      s = wave_xor_dpp(multmodp_unrolled(rowc, s));
     } else {
       s = slice_partial(cur, sc, st, lane, visit);
     }
@@ -514,7 +550,7 @@ uint32_t* device_consts() {
 
 // One workgroup per CU (LDS-bound), 16 segments per workgroup at a time,
 // grid-stride beyond that. Kernel trace on 1 GiB (profiles/r2_crc_slice):
-// 212 us with 256 workgroups, 243 with 512, 224 with 1024.
+// 186.5 us with 256 workgroups, 185.0 with 512, 187.8 with 1024.
 dim3 seg_grid(int64_t total_segs, int max_blocks) {
   const int64_t cap = max_blocks > 0 ? max_blocks : 256;
   return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>((total_segs + kWaves - 1) / kWaves, cap))));
