@@ -60,6 +60,14 @@ class HipBackend : public Backend {
     if ((cfg_.world == 1 && !cfg_.self_comm) || cfg_.reserve_cus > 0)
       copy2_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     verify_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
+    // The CRC kernels run one workgroup per CU (144 KiB of LDS tables each): on
+    // the masked verify stream a 256-workgroup grid would leave the last
+    // reserve_cus workgroups for a second wave, so cap it at the stream's CUs.
+    {
+      int cus = 0;
+      HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+      crc_grid_ = cfg_.reserve_cus > 0 && cfg_.reserve_cus < cus ? cus - cfg_.reserve_cus : 0;
+    }
     HIP_OK(hipMalloc(&ws_, std::max(kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes),
                                      kern::crc32c_batch_workspace_bytes(cfg_.max_crc_bytes, kern::kCrcBatchMax))));
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
@@ -250,7 +258,7 @@ class HipBackend : public Backend {
     if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
     if (n > 0) {
       if (n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
-      HIP_OK(kern::crc32c_chunks(p, n, n, crc_dev_ + slot, ws_, verify_));
+      HIP_OK(kern::crc32c_chunks_capped(p, n, n, crc_dev_ + slot, ws_, verify_, crc_grid_));
     }
     return record(verify_);
   }
@@ -262,7 +270,7 @@ class HipBackend : public Backend {
     std::vector<kern::CrcItem> items;
     for (size_t i = 0; i <= reqs.size(); ++i) {
       if (i == reqs.size() || items.size() == size_t(kern::kCrcBatchMax)) {
-        if (!items.empty()) HIP_OK(kern::crc32c_batch(items.data(), int(items.size()), ws_, verify_));
+        if (!items.empty()) HIP_OK(kern::crc32c_batch(items.data(), int(items.size()), ws_, verify_, crc_grid_));
         items.clear();
         if (i == reqs.size()) break;
       }
@@ -278,7 +286,7 @@ class HipBackend : public Backend {
     if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
     if (src_len > cfg_.max_crc_bytes) throw std::runtime_error("verify_unpack chunk larger than the verify workspace");
     HIP_OK(kern::fp8_verify_unpack(packed, src_len, src_chunk, block, reinterpret_cast<uint16_t*>(out), crc_dev_ + slot,
-                                   ws_, verify_));
+                                   ws_, verify_, crc_grid_));
     return record(verify_);
   }
 
@@ -456,6 +464,7 @@ class HipBackend : public Backend {
   std::map<Ev, hipEvent_t> starts_;  // timed group end -> its start event
   std::vector<hipEvent_t> timed_pool_;
   void* ws_ = nullptr;
+  int crc_grid_ = 0;  // CRC segment-kernel grid cap: the verify stream's CUs (0 = all)
   void* scratch_[2] = {nullptr, nullptr};  // bf16 landing chunk for stage_pack, per copy queue
   int64_t scratch_bytes_[2] = {0, 0};
   uint32_t* crc_host_ = nullptr;

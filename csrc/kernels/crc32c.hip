@@ -605,7 +605,7 @@ size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n) {
   return size_t(int64_t(std::max(n, 1)) * spc * 4 + 16);
 }
 
-hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s) {
+hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int max_blocks) {
   if (n <= 0) return hipSuccess;
   if (n > kCrcBatchMax) return hipErrorInvalidValue;
   BatchArgs a{};
@@ -630,13 +630,13 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
   }
   if (a.n == 0) return hipSuccess;
   auto* seg = static_cast<uint32_t*>(workspace);
-  crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n], 0), dim3(kThreads), 0, s>>>(a, consts, seg);
+  crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n], max_blocks), dim3(kThreads), 0, s>>>(a, consts, seg);
   crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(256), 0, s>>>(a, seg);
   return hipGetLastError();
 }
 
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
-                             uint32_t* crc_out, void* workspace, hipStream_t s) {
+                             uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks) {
   if (src_bytes <= 0) return hipSuccess;
   if (src_chunk <= 0 || src_chunk % 4096 || src_bytes % (2 * block) || (reinterpret_cast<uintptr_t>(packed) & 15) ||
       (reinterpret_cast<uintptr_t>(out) & 15))
@@ -649,7 +649,7 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   auto* seg = static_cast<uint32_t*>(workspace);
   const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.fold, p.fold + p.spc * 64};
   const int64_t oc = src_chunk / 2;
-  const dim3 grid = seg_grid(p.total_segs, 0), tpb{kThreads};
+  const dim3 grid = seg_grid(p.total_segs, max_blocks), tpb{kThreads};
   switch (block) {
     case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
     case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;

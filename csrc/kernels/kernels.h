@@ -55,7 +55,10 @@ size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
 // coalesced loads) and the variants it replaced: crc32c.hip, profiles/r2_crc_ab.
 hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                                 hipStream_t s, int max_blocks);
-hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s);
+// max_blocks (here and in fp8_verify_unpack): cap on the segment kernel's grid,
+// one workgroup per CU (0 = all 256); a CU-masked stream passes its CU count so
+// no workgroup waits for a second wave.
+hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int max_blocks = 0);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements
 // (scale = amax/448; non-finite inputs: +-inf saturate, NaN stays NaN), and back.
@@ -69,7 +72,7 @@ hipError_t fp8_pack_chunks(const void* src, int64_t src_bytes, int64_t src_chunk
 // packed chunk c, out = the bf16 layer (src_bytes). One pass over the packed bytes.
 // `workspace`: crc32c_workspace_bytes(packed bytes, packed chunk) bytes.
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
-                             uint32_t* crc_out, void* workspace, hipStream_t s);
+                             uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks = 0);
 
 }  // namespace kern
 }  // namespace dissem

@@ -4,13 +4,14 @@
 //   bin/contention [-trials N] [-reserve R]
 //
 // In the planned engine a P2P group lands up to 7 chunks at once; their CRC
-// launches (each filling every CU's LDS: two 80 KiB workgroups per CU) run on
-// the verify stream while the next RCCL group kernel waits to launch on the
-// comm stream. The probe here stands in for that kernel: 28 workgroups x 256
-// threads, 16 KiB of LDS each, ~20 us of work. For each trial we enqueue 7 CRC
-// checks of 64 MiB chunks on the verify stream, then the probe, and time the
-// probe from its enqueue to its end (HIP events on its own idle stream).
-// Verify stream without a CU mask vs one created with R CUs left free.
+// (one batched launch; one 144 KiB-LDS workgroup per CU) runs on the verify
+// stream while the next RCCL group kernel waits to launch on the comm stream.
+// The probe here stands in for that kernel: 28 workgroups x 256 threads, 16 KiB
+// of LDS each, ~20 us of work. For each trial we enqueue the batched CRC of 7
+// 64 MiB chunks on the verify stream, then the probe, and time the probe from
+// its enqueue to its end (HIP events on its own idle stream), and the burst.
+// Verify stream without a CU mask vs one created with R CUs left free, with
+// the CRC grid at 256 workgroups or capped at the stream's 256 - R CUs.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -67,7 +68,9 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&buf, size_t(chunk * nchunks)));
   CHECK(dissem::kern::fill_random(buf, chunk * nchunks, 42, nullptr));
   void* ws = nullptr;
-  CHECK(hipMalloc(&ws, dissem::kern::crc32c_workspace_bytes(chunk, chunk)));
+  CHECK(hipMalloc(&ws, dissem::kern::crc32c_batch_workspace_bytes(chunk, int(nchunks))));
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   uint32_t *crc = nullptr, *probe_out = nullptr;
   CHECK(hipMalloc(&crc, 64 * sizeof(uint32_t)));
   CHECK(hipMalloc(&probe_out, 64 * sizeof(uint32_t)));
@@ -97,13 +100,18 @@ int main(int argc, char** argv) {
   };
   printf("{\"case\": \"probe_alone\", \"p50_us\": %.1f, \"max_us\": %.1f}\n", pct(alone, 0.5), pct(alone, 1.0));
 
-  for (int r : {0, reserve}) {
+  // The 7 chunks as the engine verifies a landed P2P group: one batched launch
+  // on the verify stream, unmasked, masked with the full 256-workgroup grid, and
+  // masked with the grid capped at the stream's CUs (what HipBackend does).
+  dissem::kern::CrcItem items[nchunks];
+  for (int64_t c = 0; c < nchunks; ++c) items[c] = dissem::kern::CrcItem{buf + c * chunk, chunk, crc + c};
+  const std::pair<int, int> cases[] = {{0, 0}, {reserve, 0}, {reserve, cus - reserve}};
+  for (auto [r, cap] : cases) {
     hipStream_t verify = make_stream(r);
     std::vector<float> lat, burst;
     for (int t = 0; t < trials + 2; ++t) {
       CHECK(hipEventRecord(v0, verify));
-      for (int64_t c = 0; c < nchunks; ++c)
-        CHECK(dissem::kern::crc32c_chunks(buf + c * chunk, chunk, chunk, crc + c, ws, verify));
+      CHECK(dissem::kern::crc32c_batch(items, int(nchunks), ws, verify, cap));
       CHECK(hipEventRecord(v1, verify));
       CHECK(hipEventRecord(e0, comm));
       probe_kernel<<<28, 256, 0, comm>>>(probe_out, ticks);
@@ -118,9 +126,9 @@ int main(int argc, char** argv) {
         burst.push_back(vms * 1e3f);
       }
     }
-    printf("{\"case\": \"probe_during_7_crc64MiB\", \"reserved_cus\": %d, \"probe_p50_us\": %.1f, "
-           "\"probe_p90_us\": %.1f, \"probe_max_us\": %.1f, \"crc_burst_p50_us\": %.1f}\n",
-           r, pct(lat, 0.5), pct(lat, 0.9), pct(lat, 1.0), pct(burst, 0.5));
+    printf("{\"case\": \"probe_during_7_crc64MiB\", \"reserved_cus\": %d, \"crc_grid_cap\": %d, "
+           "\"probe_p50_us\": %.1f, \"probe_p90_us\": %.1f, \"probe_max_us\": %.1f, \"crc_burst_p50_us\": %.1f}\n",
+           r, cap, pct(lat, 0.5), pct(lat, 0.9), pct(lat, 1.0), pct(burst, 0.5));
     CHECK(hipStreamDestroy(verify));
   }
   return 0;
