@@ -195,7 +195,8 @@ void register_gpu_bindings(PyObject* module) {
      py::arg("stream") = 0, py::arg("max_blocks") = 0);
   m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
   // Batched CRC of independent device buffers [(ptr, nbytes), ...] (synchronous).
-  m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream) {
+  // max_blocks: cap on the segment kernel's grid (0 = one workgroup per CU)
+  m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream, int max_blocks) {
     py::gil_scoped_release nogil;
     if (bufs.size() > size_t(kern::kCrcBatchMax)) throw std::invalid_argument("too many buffers for one batch");
     int64_t mx = 0;
@@ -209,14 +210,14 @@ void register_gpu_bindings(PyObject* module) {
     std::vector<kern::CrcItem> items;
     for (size_t i = 0; i < bufs.size(); ++i)
       items.push_back(kern::CrcItem{reinterpret_cast<const void*>(bufs[i].first), bufs[i].second, dev + i});
-    hipError_t e = kern::crc32c_batch(items.data(), int(items.size()), ws, as_stream(stream));
+    hipError_t e = kern::crc32c_batch(items.data(), int(items.size()), ws, as_stream(stream), max_blocks);
     if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
     std::vector<uint32_t> out(host, host + bufs.size());
     (void)hipFree(ws);
     (void)hipHostFree(host);
     check(e, "crc32c_batch");
     return out;
-  }, py::arg("buffers"), py::arg("stream") = 0);
+  }, py::arg("buffers"), py::arg("stream") = 0, py::arg("max_blocks") = 0);
   m.def("crc32c_batch_async", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t out_dev, uint64_t ws,
                                  uint64_t stream) {
     std::vector<kern::CrcItem> items;

@@ -82,6 +82,21 @@ def test_crc32c_batch_matches_host(gpu):
     assert got == [gpu.crc32c_chunks(t.data_ptr(), t.numel(), t.numel())[0] for t in bufs]
 
 
+@pytest.mark.parametrize("max_blocks", [1, 7, 224])
+def test_crc32c_batch_capped_grid_matches_host(gpu, max_blocks):
+    """The engine caps the batched verify at its CU-masked stream's CUs (224 with
+    32 reserved); small caps put many segments of several buffers on one wave."""
+    sizes = [64 << 20, 3 * (16 << 10) + 32, 16, (5 << 20) + 4096, 48 << 10]
+    bufs = []
+    for i, n in enumerate(sizes):
+        t = _dev_bytes(n)
+        gpu.fill_random(t.data_ptr(), n, 2000 + i)
+        bufs.append(t)
+    torch.cuda.synchronize()
+    got = gpu.crc32c_batch([(t.data_ptr(), t.numel()) for t in bufs], 0, max_blocks)
+    assert got == [gpu.crc32c(t.cpu().numpy().tobytes()) for t in bufs]
+
+
 def test_crc32c_detects_single_bit_flip(gpu):
     n = 4 << 20
     t = _dev_bytes(n)
