@@ -9,7 +9,7 @@
 //
 // Each thread moves 8 elements: a 16-B bf16 load and an 8-B fp8 store (pack),
 // or the reverse (unpack). A block of `block` elements is handled by
-// block/8 adjacent lanes that reduce the amax with cross-lane shuffles.
+// block/8 adjacent lanes that reduce the amax with DPP / permlane swaps.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,6 +34,32 @@ __device__ inline uint32_t pk_bf16(float a, float b) {
 
 __device__ inline bool finite(float x) { return (__float_as_uint(x) & 0x7F800000u) != 0x7F800000u; }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Max over each aligned group of LANES lanes (4..64), result in every lane of
+// the group, without LDS: DPP quad swaps and half-row / row mirrors inside a
+// row of 16, then v_permlane16_swap / v_permlane32_swap of a value with itself
+// across rows (replaces __shfl_xor's ds_bpermute + address math per step).
+template <int LANES>
+__device__ __forceinline__ float group_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));                      // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_f<0x4E>(v));                      // quad_perm [2,3,0,1]
+  if constexpr (LANES >= 8) v = fmaxf(v, dpp_f<0x141>(v));   // row_half_mirror
+  if constexpr (LANES >= 16) v = fmaxf(v, dpp_f<0x140>(v));  // row_mirror
+  if constexpr (LANES >= 32) {
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  }
+  if constexpr (LANES >= 64) {
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  }
+  return v;
+}
+
 template <int LANES>  // lanes per scale block (block / 8)
 __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__ in, int64_t nthreads,
                                                        uint2* __restrict__ out, float* __restrict__ scales) {
@@ -51,8 +77,7 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__
 #pragma unroll
   for (int i = 0; i < 8; ++i)
     if (finite(x[i])) amax = fmaxf(amax, fabsf(x[i]));
-#pragma unroll
-  for (int o = LANES / 2; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  amax = group_max<LANES>(amax);
   const float inv = amax > 0.f ? 448.0f / amax : 1.0f;
   float y[8];
 #pragma unroll
