@@ -235,7 +235,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bytes (bf16-sized layer shards)",
+            "dtype": "bf16",
             "data": "synthetic: random-byte layers (splitmix64), balanced random seeding in pinned host memory",
             "config": {
                 "model": f"{args.layers}x{args.layer_mib}MiB layers (Llama-3-70B-sized shards)",
@@ -255,10 +255,12 @@ def main(argv=None) -> int:
                            "rccl-p2p-xgmi" if world > 1 else "hip-h2d (no peers)") + (
                                f", {engine_note}" if engine_note else ""),
                 "pack": args.pack,
+                "payload": "bf16 layer shards as raw bytes, moved bit-exact (CRC32C per chunk)",
             },
         }
         if args.pack != "none":
-            out["dtype"] = "fp8 e4m3fn (block-scaled, packed from bf16 on the GPU)"
+            out["dtype"] = "fp8"
+            out["config"]["payload"] = "bf16 sources packed on the GPU to fp8 e4m3fn, one f32 scale per block"
             out["config"]["model"] = f"{args.layers}x{args.layer_mib}MiB bf16 layers (Llama-3.1-405B-sized shards), fp8 in HBM"
             out["config"]["bf16_source_bytes_per_step"] = src_bytes
             out["config"]["bf16_equivalent_GBps"] = round(src_bytes * args.steps / total / 1e9, 3)
