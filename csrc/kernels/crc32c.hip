@@ -588,7 +588,12 @@ hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, ui
 hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                                 hipStream_t s, int max_blocks) {
   if (bytes <= 0) return hipSuccess;
-  if (chunk_bytes <= 0 || chunk_bytes % 16 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
+  if (chunk_bytes <= 0 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
+  // One chunk (the engine's per-chunk checks) may have any length: only a
+  // chunk's last segment is partial, and it takes a byte tail. Several chunks
+  // need a 16-B multiple so that every chunk starts 16-B aligned.
+  if (bytes <= chunk_bytes) chunk_bytes = bytes;
+  else if (chunk_bytes % 16) return hipErrorInvalidValue;
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
@@ -616,7 +621,7 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
   for (int i = 0; i < n; ++i) {
     const CrcItem& it = items[i];
     if (it.bytes <= 0) continue;
-    if (it.bytes % 16 || (reinterpret_cast<uintptr_t>(it.src) & 15)) return hipErrorInvalidValue;
+    if (reinterpret_cast<uintptr_t>(it.src) & 15) return hipErrorInvalidValue;  // any length
     uint32_t* fold = fold_consts(it.bytes, it.bytes);
     if (!fold) return hipErrorOutOfMemory;
     const int64_t spc = (it.bytes + kSegBytes - 1) / kSegBytes;

@@ -35,13 +35,14 @@ hipError_t read_seg(const void* src, int64_t bytes, uint32_t* out, int blocks, i
 // ---- crc32c.hip: CRC32C of every `chunk_bytes` chunk of [src, src+bytes).
 // out[c] (device or host-mapped memory) receives the standard CRC32C of chunk c.
 // `workspace` must hold crc32c_workspace_bytes(bytes, chunk_bytes) bytes of
-// device memory. chunk_bytes must be a multiple of 16 and src 16-B aligned.
+// device memory. src 16-B aligned; chunk_bytes a multiple of 16 unless the span
+// is one chunk (bytes <= chunk_bytes: any length, e.g. a layer's last chunk).
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes);
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                          hipStream_t s);
 // Batched: the standard CRC32C of each of up to kCrcBatchMax independent
-// buffers (bytes % 16 == 0, 16-B aligned) in one launch pair - the chunks a
-// P2P group landed. `workspace`: crc32c_batch_workspace_bytes(max bytes, n).
+// buffers (any length, 16-B aligned) in one launch pair - the chunks a P2P
+// group landed. `workspace`: crc32c_batch_workspace_bytes(max bytes, n).
 constexpr int kCrcBatchMax = 16;
 struct CrcItem {
   const void* src;

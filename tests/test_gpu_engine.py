@@ -30,6 +30,23 @@ def test_host_tier_promotion_all_modes(gpu, mode):
         rt.close()
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_layer_size_not_a_multiple_of_16(gpu, mode):
+    """Layers of any byte size (the reference's experiment layers are 10,930,691,768 B):
+    the last chunk of every layer has a length that is not a multiple of 16."""
+    size = 3 * MiB + 13
+    cfg = make_workload(1, 3, size, tier="host", chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"})
+    try:
+        res = rt.run(mode, timeout=60)
+        assert res.ok, res.error
+        assert res.engine_stats["verify_failures"] == 0
+        for l in range(3):
+            assert rt.layer_bytes(l) == gpu.fill_random_host(size, layer_seed(0, l))
+    finally:
+        rt.close()
+
+
 def test_device_seeded_nothing_to_move(gpu):
     cfg = make_workload(1, 3, 2 * MiB, tier="device", chunk_bytes=MiB)
     rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"})

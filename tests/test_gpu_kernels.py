@@ -97,6 +97,21 @@ def test_crc32c_batch_capped_grid_matches_host(gpu, max_blocks):
     assert got == [gpu.crc32c(t.cpu().numpy().tobytes()) for t in bufs]
 
 
+@pytest.mark.parametrize("n", [5, 16 + 7, (16 << 10) + 9, 59055800, (64 << 20) - 8])
+def test_crc32c_single_chunk_any_length(gpu, n):
+    """A layer whose size is not a multiple of 16 ends in such a chunk (the
+    reference's experiment layers are 10,930,691,768 B: last 64 MiB-grid chunk
+    59,055,800 B); the per-chunk check and the batched check take it."""
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 300 + n)
+    torch.cuda.synchronize()
+    want = gpu.crc32c(t.cpu().numpy().tobytes())
+    assert gpu.crc32c_chunks(t.data_ptr(), n, n) == [want]
+    assert gpu.crc32c_chunks(t.data_ptr(), n, 64 << 20) == [want]
+    assert gpu.crc32c_batch([(t.data_ptr(), n), (t.data_ptr(), n - 1)]) == [
+        want, gpu.crc32c(t.cpu().numpy().tobytes()[: n - 1])]
+
+
 def test_crc32c_detects_single_bit_flip(gpu):
     n = 4 << 20
     t = _dev_bytes(n)
