@@ -137,6 +137,13 @@ class Runtime:
         self.rank = self.node_ids.index(node_id)
         self.world = len(self.node_ids)
         self.sizes = cfg.layer_sizes()
+        if pack == "fp8":
+            # fp8 packs whole bf16 scale blocks of every chunk (core/fp8.h layout)
+            unit = 2 * pack_block
+            bad = {l: s for l, s in self.sizes.items() if s % unit}
+            if bad or self.chunk_bytes % unit:
+                raise ValueError(f"--pack fp8 needs layer sizes and the chunk size to be multiples of {unit} B "
+                                 f"(2 bytes x {pack_block}-element scale blocks); layers {sorted(bad)[:8]} are not")
         self.epoch = 0
         self.keep: List[object] = []  # buffers that must outlive sessions
 

@@ -87,10 +87,14 @@ def test_bench_modes(n, mode, extra, request):
     assert st["verify_failures"] == 0 and st["unverified_pieces"] == 0
 
 
-def test_cli_torchrun_rccl(n, tmp_path):
+@pytest.mark.parametrize("size", [32 << 20, (32 << 20) + 13])
+def test_cli_torchrun_rccl(n, size, tmp_path):
+    """The CLI over RCCL; the second size is not a multiple of 16 (like the
+    reference's experiment layers): every layer ends in an odd-length chunk that
+    crosses RCCL and the batched CRC check."""
     from distributed_llm_dissemination_amd.models.catalog import make_workload
 
-    cfg = make_workload(n, 8, 32 << 20, tier="host", seeding="random", chunk_bytes=8 << 20)
+    cfg = make_workload(n, 8, size, tier="host", seeding="random", chunk_bytes=8 << 20)
     path = tmp_path / "cfg.json"
     path.write_text(json.dumps(cfg.to_json()))
     r = _torchrun(n, ["-m", "distributed_llm_dissemination_amd", "-f", str(path), "-m", "1", "--engine", "rccl",

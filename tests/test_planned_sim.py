@@ -78,6 +78,17 @@ def test_replicate_random_seeding(n, mode):
     assert leader.engine_stats["verify_failures"] == 0
 
 
+@pytest.mark.parametrize("mode,tier", [(0, "host"), (1, "host"), (2, "host"), (3, "host"), (1, "disk")])
+def test_layer_sizes_not_multiples_of_16(mode, tier, tmp_path):
+    """Layers of any byte size (the reference's experiment layers are
+    10,930,691,768 B): every layer's last chunk has an odd length, and the split
+    of chunks over owners, relays and mode-3 ranges still delivers every byte."""
+    cfg = make_workload(4, 6, 3 * MiB + 13, tier=tier, seeding="random" if mode else "leader", chunk_bytes=MiB)
+    (res,), key = run_cluster(cfg, mode, rt_kw={"storage_path": str(tmp_path)}, pull_window=3)
+    assert res[0].bytes_planned == delivered_bytes(cfg)
+    assert res[0].engine_stats["verify_failures"] == 0
+
+
 @pytest.mark.parametrize("n", [3, 8])
 @pytest.mark.parametrize("relay", [True, False])
 def test_mode0_broadcast_relay(n, relay):
@@ -239,6 +250,15 @@ def test_fp8_store_bf16_fused_unpack_on_landing(mode):
 
 def _owners(cfg, layer):
     return {nd.id for nd in cfg.nodes for per in nd.initial_layers.values() if layer in per}
+
+
+def test_fp8_rejects_layer_sizes_off_the_scale_block():
+    """fp8 packs whole bf16 scale blocks: a layer size that is not a multiple of
+    2 x block bytes is refused up front with a clear error (not a kernel error)."""
+    cfg = make_workload(1, 2, 2 * MiB + 13, tier="host", chunk_bytes=MiB)
+    with pytest.raises(ValueError, match="multiples of 256 B"):
+        Runtime(cfg, 0, engine="sim", registry={0: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=f"sim{next(_keys)}",
+                pack="fp8")
 
 
 def test_fp8_unpacked_layer_roundtrip_disk(tmp_path):
