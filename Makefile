@@ -65,6 +65,7 @@ bin/h2dbench: csrc/tools/h2dbench.hip
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
 
 bin/diskspeed: csrc/tools/diskspeed.cc
+	@mkdir -p bin
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Icsrc -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lpthread
 
 # ---- host-only sanitizer builds of the core
