@@ -216,9 +216,14 @@ def test_fp8_pack_chunks_matches_host_layout(gpu, size, chunk, block):
     _host_fp8_codes_close(out.cpu().numpy().tobytes(), want, n_q, pchunk)
 
 
-@pytest.mark.parametrize("size,chunk,block", [(3 * (1 << 20) + 4096, 1 << 20, 128), (2 << 20, 1 << 20, 64),
-                                              ((1 << 20) + 1024, 64 << 10, 512), (64 << 20, 64 << 20, 128)])
-def test_fp8_fused_verify_unpack(gpu, size, chunk, block):
+@pytest.mark.parametrize("size,chunk,block,max_blocks", [
+    (3 * (1 << 20) + 4096, 1 << 20, 128, 0), (2 << 20, 1 << 20, 64, 0), ((1 << 20) + 1024, 64 << 10, 512, 0),
+    (64 << 20, 64 << 20, 128, 0), (2 << 20, 1 << 20, 256, 0), (2 << 20, 1 << 20, 32, 0),
+    # capped grids: every wave walks many segments (scales prefetched one segment ahead,
+    # partial segments between full ones)
+    (48 << 20, 16 << 20, 128, 3), ((24 << 20) + 4096, 1 << 20, 256, 7), (16 << 20, (1 << 20) + 4096, 64, 1),
+    (8 << 20, 4 << 20, 32, 2), ((8 << 20) + 1024, 64 << 10, 512, 5)])
+def test_fp8_fused_verify_unpack(gpu, size, chunk, block, max_blocks):
     """One pass: CRC32C of every packed chunk + bf16 dequantization; compared with
     the CRC kernel, the host CRC and the standalone unpack kernel (same math)."""
     raw = _dev_bytes(size)
@@ -227,7 +232,7 @@ def test_fp8_fused_verify_unpack(gpu, size, chunk, block):
     packed = _dev_bytes(packed_n)
     gpu.fp8_pack_chunks(raw.data_ptr(), size, chunk, block, packed.data_ptr())
     out = _dev_bytes(size)
-    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr())
+    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr(), max_blocks=max_blocks)
     pchunk = chunk // 2 + chunk // 2 // block * 4
     assert crcs == gpu.crc32c_chunks(packed.data_ptr(), packed_n, pchunk)
     host = packed.cpu().numpy().tobytes()
