@@ -10,6 +10,7 @@
 #   check      GPU tests, smoke(), 1-GPU headline bench
 #   multirank  multi-rank RCCL rehearsal on one GPU (ranks share device 0)
 #   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
+#   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
 #   profile    kernel trace of the headline bench and the fp8 subset
@@ -45,6 +46,15 @@ case "$RECIPE" in
         --layer-mib 64 --chunk-mib 16 --mode "$mode" "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
     done
     [ $rc -eq 0 ]
+    ;;
+  shared24)
+    timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 240 python bench.py --gpus 2 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \
+      --chunk-mib 16 > $OUT/bench_n2.json 2> $OUT/bench_n2.log &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 240 python bench.py --gpus 4 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \
+      --chunk-mib 16 > $OUT/bench_n4.json 2> $OUT/bench_n4.log &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 240 python bench.py --gpus 2 --steps 2 --warmup 1 --layers 8 --layer-mib 1024 \
+      > $OUT/bench_n2_1GiB.json 2> $OUT/bench_n2_1GiB.log
     ;;
   queues)
     # Plain per-rank processes (no torchrun): rocprofv3 wraps the python program itself.
