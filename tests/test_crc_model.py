@@ -158,3 +158,31 @@ def test_slice_model_matches_crc32c():
     raw ^= _partial_raw(data[2 * SEG:])
     init_term = _core.crc32c_shift(0xFFFFFFFF, chunk) ^ 0xFFFFFFFF
     assert raw ^ init_term == _core.crc32c(data.tobytes())
+
+
+def test_fused_unpack_scale_handoff():
+    """The fused verify+unpack kernel loads a full segment's scales one segment
+    ahead (lane l, register r: scale l + 64 r of the segment) and hands word i of
+    lane m + 16 r its scale with ds_bpermute from lane `from`, register base >> 6
+    (UnpackVisit::word). Model it for every block size that takes this path: the
+    register index is the same for all 64 lanes of a word (one VGPR operand per
+    bpermute) and the fetched scale is the word's own, e / BLOCK."""
+    for block in (64, 128, 256, 512):
+        n_scales = SEG // block
+        regs = max(1, n_scales // 64)
+        assert regs <= 4  # BLOCK 32 (16 registers) keeps the per-word load
+        held = np.full((regs, 64), -1)  # scale index held by (register, lane)
+        for r in range(regs):
+            for lane in range(64):
+                held[r, lane] = lane + 64 * r
+        for i in range(16):  # load i = 4 * block4k + j
+            base = ((i >> 2) * BLOCK + (i & 3) * 1024) // block
+            reg = base >> 6
+            assert reg < regs
+            for lane in range(64):
+                lo = 64 * (lane & 15) + 16 * (lane >> 4)
+                frm = (base & 63) + lo // block
+                assert 0 <= frm < 64
+                e = (i >> 2) * BLOCK + (i & 3) * 1024 + lo  # byte offset of the word in the segment
+                assert held[reg, frm] == e // block, (block, i, lane)
+                assert (e + 15) // block == e // block  # one scale per 16-B word
