@@ -99,6 +99,10 @@ def relaunch_with_torchrun(args) -> int:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    # RCCL's cross-process buffer sharing on these hosts needs dmabuf IPC (the
+    # legacy IPC path fails in hipIpcGetMemHandle); set before any HIP init and
+    # inherited by the torchrun children.
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus is None:
         args.gpus = world

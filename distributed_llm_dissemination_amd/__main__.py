@@ -131,6 +131,7 @@ def engine_opts(args) -> dict:
 
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL across rank processes
     if args.example_config:
         from .utils.config import example_config
 
