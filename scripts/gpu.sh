@@ -18,6 +18,7 @@
 #   fp8        BASELINE #5 at N = 1: full 126 x 3 GiB fp8 preset; --store bf16 subset
 #   crcpmc     SQ issue/wait counters + fetch of the CRC segment kernel
 #   contention probe-kernel launch delay under a CRC burst (CU reservation)
+#   poolshare  fp8 8 x 3 GiB staging with 0 / 2 / 8 pooled source buffers (shared vs distinct sources)
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
@@ -95,17 +96,17 @@ case "$RECIPE" in
     timeout -k 10 120 bin/diskspeed -path /tmp/dl_disk/layers/0/0.layer > $OUT/diskspeed.log 2>&1
     ;;
   fp8)
-    # BASELINE config #5 at N = 1: the full 126 x 3 GiB preset (bf16 sources from a 2-buffer
+    # BASELINE config #5 at N = 1: the full 126 x 3 GiB preset (bf16 sources from an 8-buffer
     # pinned pool), and the --store bf16 receive path on a 20 x 3 GiB subset
-    timeout -k 10 900 python bench.py --preset llama405b-fp8 --source-pool 2 --steps 2 --warmup 1 \
+    timeout -k 10 900 python bench.py --preset llama405b-fp8 --source-pool 8 --steps 2 --warmup 1 \
       > $OUT/bench_405b_fp8.json 2> $OUT/bench_405b_fp8.log &&
-    timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --source-pool 2 \
+    timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --source-pool 8 \
       --steps 2 --warmup 1 > $OUT/bench_fp8_store_bf16.json 2> $OUT/bench_fp8_store_bf16.log
     ;;
   storeprof)
     # kernel trace of the --store bf16 receive path (fused verify+unpack per staged chunk)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o st -- \
-      python3 bench.py --pack fp8 --store bf16 --layers 8 --layer-mib 3072 --source-pool 2 --steps 1 --warmup 1 \
+      python3 bench.py --pack fp8 --store bf16 --layers 8 --layer-mib 3072 --source-pool 8 --steps 1 --warmup 1 \
       > $OUT/bench.log 2>&1 &&
     timeout -k 10 300 python scripts/crc_impl_bench.py --quick > $OUT/crc_quick.json 2> $OUT/crc_quick.log
     ;;
@@ -116,6 +117,16 @@ case "$RECIPE" in
       -d $OUT/sq -o sq -- python3 scripts/crc_impl_bench.py --quick > $OUT/sq.log 2>&1 &&
     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD --output-format csv \
       -d $OUT/fetch -o fetch -- python3 scripts/crc_impl_bench.py --quick > $OUT/fetch.log 2>&1
+    ;;
+  poolshare)
+    rc=0
+    for p in 0 2 8 2 0; do
+      timeout -k 10 150 python bench.py --pack fp8 --layers 8 --layer-mib 3072 --source-pool $p --steps 3 --warmup 1 \
+        > $OUT/pool$p.json 2>> $OUT/pool$p.log || { rc=$?; break; }
+      python3 -c "import json,sys; print('pool', sys.argv[1], json.load(open(sys.argv[2]))['ms_per_step'])" \
+        $p $OUT/pool$p.json >> $OUT/summary.txt
+    done
+    [ $rc -eq 0 ]
     ;;
   contention)
     timeout -k 10 120 bin/contention -trials 40 -reserve 32 > $OUT/contention.jsonl 2>&1 &&
