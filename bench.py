@@ -75,9 +75,8 @@ def parse_args(argv=None):
                    help="host tier: layers share this many distinct pinned source buffers (layer l holds "
                         "pool buffer l %% P: random bytes, identical across layers of one residue) - fits "
                         "126 x 3 GiB bf16 sources in host memory; 0 = one buffer per layer. Keep P at least the "
-                        "number of layers staging at once (8 is plenty): layers that stage concurrently from one "
-                        "shared buffer read the same host pages together and lose ~15%% of PCIe throughput "
-                        "(profiles/r2_pool_share)")
+                        "largest pool that fits: 8-20 layer runs lose 9-17%% of PCIe throughput when layers "
+                        "share buffers (profiles/r2_pool_share20; the 126-layer preset does not)")
     p.add_argument("--preset", default="", choices=["", "llama70b", "llama405b-fp8"],
                    help="llama70b = 80 x 1 GiB (default); llama405b-fp8 = 126 x 3 GiB with --pack fp8")
     args = p.parse_args(argv)

@@ -100,13 +100,13 @@ case "$RECIPE" in
     # pinned pool), and the --store bf16 receive path on a 20 x 3 GiB subset
     timeout -k 10 900 python bench.py --preset llama405b-fp8 --source-pool 8 --steps 2 --warmup 1 \
       > $OUT/bench_405b_fp8.json 2> $OUT/bench_405b_fp8.log &&
-    timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --source-pool 8 \
+    timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 \
       --steps 2 --warmup 1 > $OUT/bench_fp8_store_bf16.json 2> $OUT/bench_fp8_store_bf16.log
     ;;
   storeprof)
     # kernel trace of the --store bf16 receive path (fused verify+unpack per staged chunk)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o st -- \
-      python3 bench.py --pack fp8 --store bf16 --layers 8 --layer-mib 3072 --source-pool 8 --steps 1 --warmup 1 \
+      python3 bench.py --pack fp8 --store bf16 --layers 8 --layer-mib 3072 --steps 1 --warmup 1 \
       > $OUT/bench.log 2>&1 &&
     timeout -k 10 300 python scripts/crc_impl_bench.py --quick > $OUT/crc_quick.json 2> $OUT/crc_quick.log
     ;;
@@ -120,11 +120,13 @@ case "$RECIPE" in
     ;;
   poolshare)
     rc=0
-    for p in 0 2 8 2 0; do
-      timeout -k 10 150 python bench.py --pack fp8 --layers 8 --layer-mib 3072 --source-pool $p --steps 3 --warmup 1 \
-        > $OUT/pool$p.json 2>> $OUT/pool$p.log || { rc=$?; break; }
-      python3 -c "import json,sys; print('pool', sys.argv[1], json.load(open(sys.argv[2]))['ms_per_step'])" \
-        $p $OUT/pool$p.json >> $OUT/summary.txt
+    # POOL_LAYERS (default 8) layers; POOLS: the pool sizes to run in order (default 0 2 8 2 0)
+    L=${POOL_LAYERS:-8}
+    for p in ${POOLS:-0 2 8 2 0}; do
+      timeout -k 10 150 python bench.py --pack fp8 --layers $L --layer-mib 3072 --source-pool $p --steps 3 --warmup 1 \
+        > $OUT/L${L}_pool$p.json 2>> $OUT/L${L}_pool$p.log || { rc=$?; break; }
+      python3 -c "import json,sys; print('layers', sys.argv[3], 'pool', sys.argv[1], json.load(open(sys.argv[2]))['ms_per_step'])" \
+        $p $OUT/L${L}_pool$p.json $L >> $OUT/summary.txt
     done
     [ $rc -eq 0 ]
     ;;
