@@ -50,7 +50,8 @@ def parse_args(argv=None):
     p.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
                    help="mode 1 owner choice when a layer has several holders (--copies > 1); links also "
                         "relays around links the plan knows to be slow")
-    p.add_argument("--timeout", type=float, default=300.0)
+    p.add_argument("--timeout", type=float, default=120.0,
+                   help="seconds one session (step) may take before the rank gives up (also the P2P group timeout)")
     p.add_argument("--pull-window", type=int, default=0,
                    help="mode 2 jobs in flight per sender (0 = 2 x peers: the next layers stage over PCIe while "
                         "the current ones cross the links; sim sweep at N=8: 7 -> 264 ms, 14 -> 241, 21 -> 273)")
@@ -68,7 +69,16 @@ def parse_args(argv=None):
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
     p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
     p.add_argument("--lanes", type=int, default=0,
-                   help="comm lanes (RCCL communicator + stream each); 0 = world-1 (one ring distance per lane)")
+                   help="comm lanes (RCCL communicator + stream + dedicated HW queue each); 0 = one lane per "
+                        "directed link on up to 8 ranks (14 at N = 8), world-1 per-distance lanes beyond")
+    p.add_argument("--probe-mib", type=int, default=256,
+                   help="N > 1: untimed pre-flight probe of every directed link with this many MiB "
+                        "(all lanes at once, then each pair alone); 0 = skip")
+    p.add_argument("--probe-timeout", type=float, default=30.0,
+                   help="seconds the probe waits for a lane before naming it stalled and failing the attempt")
+    p.add_argument("--no-fallback", action="store_true",
+                   help="N > 1 under torchrun: run the worker in this process (no supervised fresh-process "
+                        "attempts with fallback data-plane settings)")
     p.add_argument("--inject", action="append", default=[], metavar="SPEC",
                    help="fault injection (utils/faults.py), e.g. slow-link=0:1:20G (rank 0 -> 1 capped at 20 GB/s)")
     p.add_argument("--source-pool", type=int, default=0,
@@ -99,11 +109,61 @@ def relaunch_with_torchrun(args) -> int:
     return subprocess.call(cmd)
 
 
+def load_supervise():
+    """utils/supervise.py on its own: a supervisor imports neither the package
+    (its __init__ loads the native runtime) nor anything that touches the GPU."""
+    import importlib.util
+
+    name = "dld_supervise"
+    if name not in sys.modules:
+        spec = importlib.util.spec_from_file_location(
+            name, os.path.join(HERE, "distributed_llm_dissemination_amd", "utils", "supervise.py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+    return sys.modules[name]
+
+
+def fallback_attempts(args, world):
+    """The supervised attempts at N > 1: as asked, then with one lane per ring
+    distance (world-1 communicators and HW queues instead of 14), then also
+    without RCCL's P2P/IPC transport (host shared memory between the GPUs)."""
+    Attempt = load_supervise().Attempt
+    atts = [Attempt("")]
+    if args.lanes == 0 and world > 2:
+        atts.append(Attempt(f"lanes={world - 1}", ["--lanes", str(world - 1)]))
+    atts.append(Attempt(f"lanes={world - 1}, NCCL_P2P_DISABLE=1", ["--lanes", str(world - 1)],
+                        {"NCCL_P2P_DISABLE": "1"}))
+    return atts
+
+
+def supervise(args, world, rank) -> int:
+    """torchrun rank process at N > 1: never touches the GPU; runs this rank's
+    worker in fresh child processes until an attempt succeeds (utils/supervise.py)."""
+    import tempfile
+
+    sup = load_supervise()
+
+    def log(msg):
+        print(f"[bench supervisor {rank}] {msg}", file=sys.stderr, flush=True)
+
+    json_path = os.path.join(tempfile.gettempdir(), f"dld_bench_{os.getpid()}.json") if rank == 0 else None
+    rc, hist = sup.run_attempts([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                            fallback_attempts(args, world), json_path=json_path, log=log)
+    if rank == 0:
+        if rc == 0 and not sup.emit_json(json_path):
+            log("the successful attempt left no result line")
+            rc = 1
+        if json_path and os.path.exists(json_path):
+            os.unlink(json_path)
+    return rc
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     # RCCL's cross-process buffer sharing on these hosts needs dmabuf IPC (the
-    # legacy IPC path fails in hipIpcGetMemHandle); set before any HIP init and
-    # inherited by the torchrun children.
+    # legacy IPC path fails in hipIpcGetMemHandle: tests/test_gpu_ipc.py,
+    # profiles/r3_ipc/); set before any HIP init and inherited by every child.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus is None:
@@ -114,19 +174,41 @@ def main(argv=None) -> int:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     rank = int(os.environ.get("RANK", "0"))
+    sys.path.insert(0, HERE)
+    sup = load_supervise()
+
+    if world > 1 and not os.environ.get(sup.ENV_PREFIX) and not args.no_fallback and sup.agent_store_available():
+        return supervise(args, world, rank)
+    chan = sup.WorkerChannel.from_env()
+    try:
+        return worker(args, world, rank, chan)
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 - report any failure to the supervisors, then exit non-zero
+        import traceback
+
+        traceback.print_exc()
+        if chan is not None:
+            chan.fail(f"{type(e).__name__}: {e}")
+            sys.stderr.flush()
+            os._exit(1)  # a stalled lane's kernels would hang the runtime's teardown
+        raise
+
+
+def worker(args, world, rank, chan) -> int:
     # stdout carries exactly one JSON line (rank 0): everything else any library
     # prints there (RCCL's version banner, gloo) goes to stderr.
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
-    sys.path.insert(0, HERE)
     from distributed_llm_dissemination_amd.utils.launch import rank_device, shared_gpu
 
+    beat = chan.heartbeat if chan is not None else (lambda phase: None)
+    beat("start")
     local_rank = rank_device(rank, int(os.environ.get("LOCAL_RANK", str(rank))))
     import torch
     import torch.distributed as dist
 
-    import distributed_llm_dissemination_amd as dl
     from distributed_llm_dissemination_amd import _core
     from distributed_llm_dissemination_amd.models.catalog import delivered_bytes, make_workload
     from distributed_llm_dissemination_amd.__main__ import engine_opts
@@ -140,6 +222,14 @@ def main(argv=None) -> int:
     def log(msg):
         print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
 
+    def failed(why):
+        log(why)
+        if chan is not None:
+            chan.fail(why)
+            sys.stderr.flush()
+            os._exit(1)
+        raise SystemExit(1)
+
     if not torch.cuda.is_available():
         print("error: no GPU visible", file=sys.stderr)
         return 2
@@ -149,10 +239,16 @@ def main(argv=None) -> int:
 
     numa = bind_to_gpu(local_rank)
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if chan is not None:
+            dist.init_process_group("gloo", store=chan.pg_store(), rank=rank, world_size=world)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         barrier = dist.barrier
     else:
         barrier = lambda: None  # noqa: E731
+    beat("setup")
+    if chan is not None and chan.attempt in faults.fail_attempts.get(rank, []):
+        failed(f"fault injection: fail-attempt={rank}@{chan.attempt}")
 
     layer_bytes = args.layer_mib << 20
     cfg = make_workload(world, args.layers, layer_bytes, seeding=args.seeding, tier=args.tier, copies=args.copies,
@@ -165,14 +261,16 @@ def main(argv=None) -> int:
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
     free, tot = _core.mem_info()
-    log(f"HBM free {free / 2**30:.1f} / {tot / 2**30:.1f} GiB; setting up {args.layers} x {args.layer_mib} MiB")
+    log(f"HBM free {free / 2**30:.1f} / {tot / 2**30:.1f} GiB; setting up {args.layers} x {args.layer_mib} MiB"
+        + (f" (attempt {chan.attempt}: {chan.label})" if chan is not None and chan.label else ""))
     t_setup = time.time()
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
-                 store=args.store,
+                 store=args.store, group_timeout_s=min(300.0, args.timeout),
                  engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(rank)},
                  inject_corrupt=faults.drop_chunk, source_pool=args.source_pool)
+    beat("comm ready")
     if args.pack != "none":
         # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
         src_bytes = total_bytes
@@ -183,12 +281,22 @@ def main(argv=None) -> int:
         rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
     log(f"setup done in {time.time() - t_setup:.1f}s")
 
+    probe = {}
+    if world > 1 and args.probe_mib > 0:
+        beat("probe")
+        try:
+            probe = rt.probe_links(args.probe_mib << 20, timeout_s=args.probe_timeout)
+        except RuntimeError as e:
+            failed(str(e))
+        log(f"link probe: {probe.get('probe_ms')} ms; concurrent GB/s {probe.get('concurrent')}")
+
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
     policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, 2 * (world - 1)),
                   owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective")
 
-    def step(timed: bool):
+    def step(timed: bool, i: int):
+        beat(f"{'step' if timed else 'warmup'} {i}")
         rt.prepare(args.mode, **policy)
         barrier()
         torch.cuda.synchronize()
@@ -200,20 +308,20 @@ def main(argv=None) -> int:
         dt = time.perf_counter() - t0
         _core.trace_pop()
         if not res.ok:
-            log(f"session failed: {res.error}")
-            raise SystemExit(1)
+            failed(f"session failed on rank {rank}: {res.error}")
         return dt, res
 
     for i in range(args.warmup):
-        dt, res = step(False)
+        dt, res = step(False, i)
         log(f"warmup {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s)")
     links0 = rt.link_stats()
     times = []
     last = None
     for i in range(args.steps):
-        dt, last = step(True)
+        dt, last = step(True, i)
         times.append(dt)
         log(f"step {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s) ttd={last.time_to_deliver_s * 1e3:.1f} ms")
+    beat("measured")
     total = sum(times)
     # Per directed link over the timed steps: bytes this rank sent to each peer,
     # and the device time of the P2P groups that involved the peer.
@@ -221,12 +329,18 @@ def main(argv=None) -> int:
     mine = {p: (links1["sent"].get(p, 0) - links0["sent"].get(p, 0),
                 links1["busy_ms"].get(p, 0.0) - links0["busy_ms"].get(p, 0.0)) for p in links1["sent"]}
     all_links = [mine]
+    all_probe = [probe]
+    init_ms = [rt.engine.stats().comm_init_ms]
     if world > 1:
         t = torch.tensor([total], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         total = float(t.item())
         all_links = [None] * world
         dist.all_gather_object(all_links, mine)
+        all_probe = [None] * world
+        dist.all_gather_object(all_probe, probe)
+        init_ms = [None] * world
+        dist.all_gather_object(init_ms, rt.engine.stats().comm_init_ms)
     ms_per_step = total / max(1, args.steps) * 1e3
     value = total_bytes * args.steps / total / 1e9
     if rank == 0:
@@ -274,10 +388,14 @@ def main(argv=None) -> int:
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
         out["config"]["numa_rank0"] = numa  # {} when the GPU's node is unknown or outside this cpuset
+        if chan is not None:
+            out["config"]["fallback"] = chan.label or None
+            out["config"]["failed_attempts"] = chan.history
         if world > 1:
             es = rt.engine.stats()
             out["config"]["comm_lanes"] = es.lanes
             out["config"]["comm_init_ms_rank0"] = round(es.comm_init_ms, 1)
+            out["config"]["comm_init_ms_max"] = round(max(init_ms), 1)
         if world > 1:
             # GB/s per directed link: averaged over the timed wall time, and while
             # its P2P groups were on the device (busy).
@@ -288,8 +406,26 @@ def main(argv=None) -> int:
                     busy[f"{src}->{p}"] = round(b / (ms / 1e3) / 1e9, 2) if ms > 0 else None
             out["config"]["per_link_GBps"] = wall
             out["config"]["per_link_busy_GBps"] = busy
-        json_out.write(json.dumps(out) + "\n")
-        json_out.flush()
+            if any(all_probe):
+                # untimed pre-flight probe: GB/s per directed link (sender's device time)
+                pr = {"MiB": args.probe_mib, "concurrent": {}, "solo": {}}
+                for src, p in enumerate(all_probe):
+                    for kind in ("concurrent", "solo"):
+                        for dst, gbps in sorted((p or {}).get(kind, {}).items()):
+                            pr[kind][f"{src}->{dst}"] = gbps
+                pr["probe_ms_max"] = max((p or {}).get("probe_ms", 0) for p in all_probe)
+                out["config"]["probe_lane_GBps"] = pr
+        line = json.dumps(out) + "\n"
+        json_file = os.environ.get("DLD_SUP_JSON")
+        if chan is not None and json_file:
+            with open(json_file + ".tmp", "w") as f:
+                f.write(line)
+            os.replace(json_file + ".tmp", json_file)
+            chan.ok()
+        else:
+            json_out.write(line)
+            json_out.flush()
+    beat("teardown")
     rt.close()
     if world > 1:
         dist.destroy_process_group()

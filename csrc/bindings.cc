@@ -314,6 +314,33 @@ PYBIND11_MODULE(_core, m) {
         e.quiesce();
       })
       .def("stats", &PlannedEngine::stats)
+      .def("probe", [](PlannedEngine& e, const std::vector<std::tuple<int, bool, int64_t>>& ops, double timeout_s) {
+        std::vector<ProbeOp> in;
+        for (auto& t : ops) {
+          ProbeOp o;
+          o.peer = std::get<0>(t);
+          o.send = std::get<1>(t);
+          o.bytes = std::get<2>(t);
+          in.push_back(o);
+        }
+        std::vector<ProbeOp> out;
+        {
+          py::gil_scoped_release nogil;
+          out = e.probe(in, timeout_s);
+        }
+        py::list res;
+        for (auto& o : out) {
+          py::dict d;
+          d["peer"] = o.peer;
+          d["send"] = o.send;
+          d["bytes"] = o.bytes;
+          d["done"] = o.done;
+          d["ms"] = o.ms;
+          d["lane"] = o.lane;
+          res.append(d);
+        }
+        return res;
+      }, py::arg("ops"), py::arg("timeout_s") = 30.0)
       .def("error", &PlannedEngine::error)
       .def_property_readonly("backend", [](PlannedEngine& e) { return e.backend()->name(); });
   // Simulated fabric (CPU): host "device" memory, RCCL P2P matching semantics between

@@ -308,6 +308,92 @@ void PlannedEngine::reset_session() {
   if (failed_) throw std::runtime_error("data engine failed: " + error());
 }
 
+std::vector<ProbeOp> PlannedEngine::probe(const std::vector<ProbeOp>& ops, double timeout_s) {
+  quiesce();
+  ProbeJob job;
+  job.ops = ops;
+  job.timeout_s = timeout_s;
+  {
+    std::lock_guard<std::mutex> lk(req_mu_);
+    Req r{Req::Probe, {}, 0, 0, 0};
+    r.probe = &job;
+    reqs_.push_back(std::move(r));
+    busy_ = true;
+  }
+  req_cv_.notify_all();
+  {
+    std::unique_lock<std::mutex> lk(req_mu_);
+    idle_cv_.wait(lk, [&] { return job.finished || failed_.load() || stopped_.load(); });
+    if (!job.finished) throw std::runtime_error("probe: data engine stopped: " + error());
+  }
+  return job.ops;
+}
+
+void PlannedEngine::run_probe(ProbeJob& job) {
+  trace::Scoped tr("dissem.probe");
+  int64_t maxb = 0;
+  std::map<int, std::vector<size_t>> by_lane;
+  for (size_t i = 0; i < job.ops.size(); ++i) {
+    ProbeOp& o = job.ops[i];
+    if (o.peer < 0 || o.peer >= cfg_.world || o.peer == cfg_.rank || o.bytes <= 0)
+      throw std::runtime_error("probe: bad op (peer " + std::to_string(o.peer) + ")");
+    o.lane = lane_for(o.peer, o.send);
+    by_lane[o.lane].push_back(i);
+    maxb = std::max(maxb, o.bytes);
+  }
+  // One send buffer read by every send; one landing buffer per recv.
+  std::vector<uint8_t*> bufs;
+  uint8_t* sbuf = backend_->alloc(maxb);
+  bufs.push_back(sbuf);
+  struct G {
+    Ev ev;
+    std::vector<size_t> ops;
+    bool done = false;
+  };
+  std::vector<G> groups;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (auto& kv : by_lane) {
+    std::vector<XOp> xops;
+    for (size_t i : kv.second) {
+      const ProbeOp& o = job.ops[i];
+      uint8_t* p = sbuf;
+      if (!o.send) {
+        p = backend_->alloc(o.bytes);
+        bufs.push_back(p);
+      }
+      xops.push_back(XOp{o.send, o.peer, p, o.bytes});
+    }
+    CallMark cm(this, "probe", kv.first);
+    groups.push_back(G{backend_->group(xops, {}, kv.first), kv.second});
+  }
+  size_t left = groups.size();
+  while (left > 0) {
+    const auto now = std::chrono::steady_clock::now();
+    for (auto& g : groups) {
+      if (g.done) continue;
+      const int r = backend_->query(g.ev);
+      if (r == 0) continue;
+      g.done = true;
+      --left;
+      double ms = r > 0 ? backend_->group_ms(g.ev) : -1;
+      if (r > 0 && ms < 0) ms = std::chrono::duration<double, std::milli>(now - t0).count();
+      for (size_t i : g.ops) {
+        job.ops[i].done = r > 0;
+        job.ops[i].ms = ms;
+      }
+      backend_->release(g.ev);
+    }
+    if (left == 0 || std::chrono::duration<double>(now - t0).count() > job.timeout_s) break;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  if (left == 0) {
+    for (uint8_t* b : bufs) backend_->free(b);
+  } else {
+    log::error(int64_t(self_node_)).i("stalled_groups", int64_t(left)).f("timeout_s", job.timeout_s)
+        .msg("link probe: lanes did not complete");
+  }
+}
+
 // ------------------------------------------------------------ issue thread
 
 uint32_t PlannedEngine::crc_slot() {
@@ -394,6 +480,39 @@ Ev PlannedEngine::unpack_chunk(Layer& L, int64_t c, uint32_t slot, Ev after) {
   const int64_t slen = std::min(cfg_.chunk_bytes, src_total - c * cfg_.chunk_bytes);
   return backend_->verify_unpack(L.dev + c * grid_, slen, cfg_.chunk_bytes, cfg_.pack_block,
                                  L.out + c * cfg_.chunk_bytes, slot, after);
+}
+
+void PlannedEngine::partial_landed(Layer& L, const Piece& p, std::vector<Verify>& out) {
+  PartChunk& pc = L.part[p.chunk];
+  pc.got.add(p.off, p.off + p.len);
+  if (p.has_ccrc) {
+    pc.has_crc = true;
+    pc.crc = p.ccrc;
+  }
+  const int64_t a = p.chunk * grid_, b = std::min(a + grid_, L.size);
+  if (!pc.got.contains(a, b)) return;
+  Piece f = p;
+  f.off = a;
+  f.len = b - a;
+  f.full = true;
+  f.has_crc = cfg_.verify && pc.has_crc;
+  f.crc = pc.crc;
+  L.part.erase(p.chunk);
+  Verify v;
+  uint32_t slot = ~0u;
+  if (cfg_.unpack_store) {
+    const uint32_t s = crc_slot();
+    v.ev = unpack_chunk(L, f.chunk, s, 0);
+    if (f.has_crc) slot = s;
+  } else if (f.has_crc) {
+    slot = crc_slot();
+    v.ev = backend_->crc(L.dev + a, b - a, slot, 0);
+  } else {
+    v.ev = backend_->crc(nullptr, 0, 0, 0);
+  }
+  v.pieces.push_back(f);
+  v.slots.push_back(slot);
+  out.push_back(std::move(v));
 }
 
 void PlannedEngine::landed(const Piece& p) {
@@ -622,6 +741,11 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   // becomes a source only once the node re-tags it Inmem (Node::on_layer).
   const bool client = have && src.meta.location == Location::Client;
   if (L.host || !L.path.empty() || (have && !client && (src.host || !src.path.empty()))) {
+    if (!source_covers(L, id, c)) {
+      // A hole of a resumed partial copy: a send of it waits for the chunk's
+      // recv; a promotion of it has no source here.
+      return want_landed ? -1 : 0;
+    }
     if (s == 0 && stage_paced(L, id, c)) {
       // The source tier's LimitRate holds this chunk back; promotions retry from
       // local_wait_, sends from their lane's next issue pass.
@@ -644,11 +768,28 @@ int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_lande
   return -1;
 }
 
-bool PlannedEngine::has_local_source(const Layer& L, LayerID id) {
+bool PlannedEngine::has_local_source(Layer& L, LayerID id, int64_t c) {
+  if (!source_covers(L, id, c)) return false;
   if (L.host || !L.path.empty()) return true;
   LayerSrc src;
   return node_ && node_->store().get(id, &src) &&
          (src.host || !src.path.empty() || src.meta.location == Location::Client);
+}
+
+bool PlannedEngine::source_covers(Layer& L, LayerID id, int64_t c) {
+  // A resumed partial copy (LayerSrc::ranges) holds only some chunks; the
+  // others are holes of its sparse file and must arrive over the wire first.
+  if (!L.ranges_known) {
+    LayerSrc src;
+    L.src_ranges.clear();
+    if (node_ && node_->store().get(id, &src)) L.src_ranges = src.ranges;
+    L.ranges_known = true;
+  }
+  if (L.src_ranges.empty()) return true;
+  const int64_t a = c * grid_, b = std::min(a + grid_, L.size);
+  for (auto& r : L.src_ranges)
+    if (r.first <= a && r.second >= b) return true;
+  return false;
 }
 
 void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
@@ -701,9 +842,11 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       // Collectives run on lane 0 (every rank's copy of the lane-0 communicator).
       p.lane = bcast || kind == Kind::Local ? 0 : lane_for(peer, kind == Kind::Send);
       const int64_t ci = c - first_chunk;
-      if (p.full && ci < int64_t(j.crc.size())) {
-        p.has_crc = true;
-        p.crc = j.crc[size_t(ci)];
+      if (ci < int64_t(j.crc.size())) {
+        // a partial piece carries its chunk's CRC for the check once every
+        // piece of the chunk has landed (partial_landed)
+        (p.full ? p.has_crc : p.has_ccrc) = true;
+        (p.full ? p.crc : p.ccrc) = j.crc[size_t(ci)];
       }
       pieces.push_back(p);
       pos = e;
@@ -796,7 +939,7 @@ bool PlannedEngine::issue_lane(int lane) {
         // waits on this recv's mark (a larger key; see the argument above).
         auto f = fwd_pending_.find({p.layer, p.chunk});
         if (f != fwd_pending_.end() && !f->second.empty() && *f->second.begin() < key_of(p) &&
-            has_local_source(layer(p.layer), p.layer))
+            has_local_source(layer(p.layer), p.layer, p.chunk))
           break;
       }
       nrecv[p.peer]++;
@@ -892,7 +1035,7 @@ bool PlannedEngine::issue_lane(int lane) {
         set_chunk_ev(L, p.chunk, 0);  // pending on the comm queue itself: later sends are ordered behind it
       }
       uint32_t slot = ~0u;
-      if (cfg_.unpack_store && p.full && !p.bcast) {
+      if (cfg_.unpack_store && p.full) {
         // fused check + dequantization of the landed packed chunk, per chunk
         const uint32_t s = crc_slot();
         if (last) backend_->release(last);
@@ -1015,6 +1158,7 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
       set_chunk_ev(L, int64_t(c), 0);
       L.fails[c] = 0;
     }
+    L.part.clear();
   }
   std::vector<NodeID> nodes;
   for (int r = 0; r < cfg_.world; ++r)
@@ -1093,6 +1237,7 @@ void PlannedEngine::poll() {
     }
     if (failed_ || recovering_) break;
   }
+  std::vector<Verify> followups;  // whole-chunk checks of chunks completed by partial pieces
   for (auto it = verifies_.begin(); it != verifies_.end();) {
     int r = backend_->query(it->ev);
     if (r == 0) {
@@ -1119,6 +1264,11 @@ void PlannedEngine::poll() {
         }
         std::lock_guard<std::mutex> lk(stats_mu_);
         stats_.bytes_verified += p.len;
+      } else if (p.kind == Kind::Recv && !p.full) {
+        // Part of a chunk (e.g. two relays split it): it is checked, and
+        // reported landed, as a whole once all of its bytes are here.
+        partial_landed(L, p, followups);
+        continue;
       } else if (p.kind == Kind::Recv) {
         std::lock_guard<std::mutex> lk(stats_mu_);
         stats_.unverified_pieces++;
@@ -1140,6 +1290,7 @@ void PlannedEngine::poll() {
     if (it->bounce) bounce_free_.push_back(it->bounce);
     it = verifies_.erase(it);
   }
+  for (auto& v : followups) verifies_.push_back(std::move(v));
   std::vector<std::pair<LayerID, int64_t>> again;
   again.swap(restage_);
   for (auto& lc : again) {
@@ -1186,6 +1337,8 @@ void PlannedEngine::take_requests(bool block) {
           L.host_prefix = -1;
           L.client_requested = false;
           L.stage_rate = -1;
+          L.ranges_known = false;
+          L.part.clear();
           if (cfg_.poison && !L.seeded && L.dev) backend_->zero_sync(L.dev, L.size);
         }
         pace_.clear();
@@ -1212,6 +1365,17 @@ void PlannedEngine::take_requests(bool block) {
           if (L.want[size_t(c)] && L.st[size_t(c)] == 0 && ensure_chunk(L, r.layer, c, true) < 0)
             fail("no source to load layer " + std::to_string(r.layer));
         }
+        break;
+      }
+      case Req::Probe: {
+        try {
+          run_probe(*r.probe);
+        } catch (const std::exception& e) {
+          fail(std::string("probe: ") + e.what());
+        }
+        std::lock_guard<std::mutex> lk(req_mu_);
+        r.probe->finished = true;
+        idle_cv_.notify_all();
         break;
       }
       case Req::Stop:

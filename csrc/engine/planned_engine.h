@@ -44,6 +44,7 @@
 
 #include "engine/backend.h"
 #include "engine/engine.h"
+#include "store/store.h"
 
 namespace dissem {
 
@@ -136,6 +137,16 @@ struct PlannedStats {
   std::vector<int64_t> land_us_hist = std::vector<int64_t>(32, 0);   // chunk issue -> landed + verified
 };
 
+// One op of an untimed link probe (PlannedEngine::probe).
+struct ProbeOp {
+  int peer = 0;          // partner rank
+  bool send = true;
+  int64_t bytes = 0;
+  bool done = false;     // completed within the probe's time limit
+  double ms = -1;        // device time of its group (lane reached it -> end); host time where unknown
+  int lane = 0;
+};
+
 class PlannedEngine : public DataEngine {
  public:
   PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> backend);
@@ -156,6 +167,11 @@ class PlannedEngine : public DataEngine {
   PlannedStats stats();
   std::string error();
   Backend* backend() { return backend_.get(); }
+  // Untimed pre-flight probe between sessions: every op is posted at once, each
+  // on its directed pair's lane (one group per lane), and timed; ops still
+  // pending after timeout_s are returned with done = false (their lanes are
+  // stalled: the buffers are then left allocated, a kernel may still use them).
+  std::vector<ProbeOp> probe(const std::vector<ProbeOp>& ops, double timeout_s);
 
   // ---- DataEngine
   std::string name() const override { return backend_->name(); }
@@ -188,6 +204,8 @@ class PlannedEngine : public DataEngine {
     bool full;      // covers the whole grid chunk
     bool has_crc = false;
     uint32_t crc = 0;
+    bool has_ccrc = false;  // partial piece: the CRC of its whole grid chunk
+    uint32_t ccrc = 0;
     NodeID src_node = 0;
     bool bcast = false;  // collective from rank `peer` (root: Send with peer == own rank; others: Recv)
     int lane = 0;
@@ -196,6 +214,11 @@ class PlannedEngine : public DataEngine {
   };
   using Key = std::tuple<uint64_t, int64_t, uint64_t>;
   static Key key_of(const Piece& p) { return Key{p.batch, p.pidx, p.seq}; }
+  struct PartChunk {
+    RangeSet got;
+    bool has_crc = false;
+    uint32_t crc = 0;
+  };
   struct Layer {
     int64_t size = 0;
     uint8_t* dev = nullptr;
@@ -210,6 +233,8 @@ class PlannedEngine : public DataEngine {
     int64_t stage_rate = -1;         // source tier LimitRate (-1: not looked up yet)
     int64_t host_prefix = -1;        // source bytes present at `host` (-1: all; a client stream still landing)
     int stage_tier = 0;
+    std::vector<std::pair<int64_t, int64_t>> src_ranges;  // partial source: the byte ranges it holds
+    bool ranges_known = false;       // src_ranges looked up this session
     // per chunk: 0 absent, 1 pending, 2 resident, 3 reading from disk,
     // 4 failed its CRC and awaits the leader's re-send (still forwardable: a
     // later receiver detects it and NACKs too)
@@ -218,6 +243,7 @@ class PlannedEngine : public DataEngine {
     std::vector<Key> rkey;           // key of the recv a pending chunk waits on (Key{}: staged)
     std::vector<uint8_t> want;       // inject Landed when resident (assigned here)
     std::vector<uint8_t> fails;      // CRC failures per chunk
+    std::map<int64_t, PartChunk> part;  // chunks landing as several partial pieces
   };
   struct Verify {  // landing (recv group or staging copy) awaiting its check
     Ev ev = 0;
@@ -233,8 +259,13 @@ class PlannedEngine : public DataEngine {
     uint8_t* bounce = nullptr;
     bool ok = true;
   };
+  struct ProbeJob {
+    std::vector<ProbeOp> ops;
+    double timeout_s = 0;
+    bool finished = false;
+  };
   struct Req {
-    enum Type { Batch, Load, Reset, Stop, Shrink, HostReady } type;
+    enum Type { Batch, Load, Reset, Stop, Shrink, HostReady, Probe } type;
     std::vector<XferJob> jobs;
     LayerID layer = 0;
     int64_t off = 0, len = 0;
@@ -242,7 +273,9 @@ class PlannedEngine : public DataEngine {
     uint64_t generation = 0;   // Shrink
     std::string comm_id;       // Shrink: the survivors' new communicator id
     const uint8_t* base = nullptr;  // HostReady: host copy; `off` = bytes present, `len` = total
+    ProbeJob* probe = nullptr;  // Probe
   };
+  void run_probe(ProbeJob& job);
   struct Inflight {  // a P2P group on a comm lane
     Ev ev;
     std::chrono::steady_clock::time_point t0;
@@ -288,13 +321,16 @@ class PlannedEngine : public DataEngine {
   Layer& layer(LayerID id, int64_t size_hint = 0);
   // 1: resident or in flight on a device queue, 0: still reading from disk, -1: no source
   int ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed);
-  bool has_local_source(const Layer& L, LayerID id);  // staging can supply the layer's chunks
+  bool has_local_source(Layer& L, LayerID id, int64_t c);  // staging can supply chunk c
+  bool source_covers(Layer& L, LayerID id, int64_t c);      // chunk c is not a hole of a partial source
   void stage_chunk(Layer& L, LayerID id, int64_t c);
   void stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* src, uint8_t* bounce);
   void submit_disk(Layer& L, LayerID id, int64_t c);
   void pump_disk();
   void reader_loop();
   void landed(const Piece& p);
+  // A partial recv piece landed: once the chunk's pieces cover it, queue its whole-chunk check to `out`.
+  void partial_landed(Layer& L, const Piece& p, std::vector<Verify>& out);
   void nack(const Piece& p, Layer& L, uint32_t got);
   uint32_t crc_slot();
   // unpack_store: the fused check of chunk c (packed at L.dev) into its bf16 slot, after `after`.

@@ -34,7 +34,18 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
     partial_[cfg_.id] = store_.partial();
   }
   e_->bind(this);
-  if (is_leader_ && e_->planned()) manifests_ = e_->manifest();
+  if (is_leader_ && e_->planned()) {
+    // Whole copies only, the filter announce() applies: a resumed partial copy's
+    // manifest holds CRC 0 for every chunk it lacks. Its real chunks are merged
+    // per chunk (merge_partial_manifest), like any other partial holder's.
+    const LayerIDs inv = store_.inventory();
+    const PartialLayers part = store_.partial();
+    for (auto& kv : e_->manifest()) {
+      if (inv.count(kv.first)) manifests_[kv.first] = kv.second;
+      auto pit = part.find(kv.first);
+      if (pit != part.end()) merge_partial_manifest(kv.first, kv.second, pit->second);
+    }
+  }
   // TCP payload bytes land directly in this node's host slot of the layer
   // (host engines: the target itself; GPU engines: the staging source of a
   // client-held layer, see on_layer).
@@ -155,9 +166,10 @@ void Node::announce() {
   m.layers = store_.inventory();
   m.partial_layers = store_.partial();
   if (e_->planned()) {
-    // Manifests of whole copies only: a resumed partial copy knows just its own chunks.
+    // Whole copies' manifests, and a resumed partial copy's too: the leader
+    // takes from the latter only the chunks inside its announced ranges.
     for (auto& kv : e_->manifest())
-      if (m.layers.count(kv.first)) m.manifest[kv.first] = kv.second;
+      if (m.layers.count(kv.first) || m.partial_layers.count(kv.first)) m.manifest[kv.first] = kv.second;
   }
   NodeID hop = next_hop(cfg_.leader);
   trace::mark("dissem.announce");
@@ -433,6 +445,11 @@ void Node::on_announce(const MessagePtr& m) {
     add_node(m->src);
   }
   for (auto& kv : m->manifest) {
+    auto pit = m->partial_layers.find(kv.first);
+    if (pit != m->partial_layers.end()) {  // a partial copy vouches for its own chunks only
+      merge_partial_manifest(kv.first, kv.second, pit->second);
+      continue;
+    }
     auto it = manifests_.find(kv.first);
     if (it == manifests_.end()) {
       manifests_[kv.first] = kv.second;
@@ -859,8 +876,36 @@ void Node::add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_
     int64_t first = j.offset / j.chunk_bytes;
     int64_t last = (j.offset + j.size + j.chunk_bytes - 1) / j.chunk_bytes;
     for (int64_t c = first; c < last && c < int64_t(it->second.crc.size()); ++c) j.crc.push_back(it->second.crc[size_t(c)]);
+  } else if (auto pc = partial_crc_.find(layer); pc != partial_crc_.end() && pc->second.first > 0) {
+    // No whole copy announced a manifest: the chunks partial holders vouched
+    // for. One unknown chunk leaves the job unverified (never a wrong CRC).
+    j.chunk_bytes = pc->second.first;
+    const int64_t first = j.offset / j.chunk_bytes, last = (j.offset + j.size + j.chunk_bytes - 1) / j.chunk_bytes;
+    for (int64_t c = first; c < last; ++c) {
+      auto ci = pc->second.second.find(c);
+      if (ci == pc->second.second.end()) {
+        j.crc.clear();
+        break;
+      }
+      j.crc.push_back(ci->second);
+    }
   }
   pending_jobs_.push_back({j, phase});
+}
+
+void Node::merge_partial_manifest(LayerID layer, const CrcManifest& m,
+                                  const std::vector<std::pair<int64_t, int64_t>>& ranges) {
+  if (m.chunk_bytes <= 0) return;
+  auto& pc = partial_crc_[layer];
+  if (pc.first && pc.first != m.chunk_bytes) return;  // another grid: keep the first
+  pc.first = m.chunk_bytes;
+  const int64_t total = layer_size(layer);
+  for (int64_t c = 0; c < int64_t(m.crc.size()); ++c) {
+    const int64_t a = c * m.chunk_bytes, b = total > 0 ? std::min(a + m.chunk_bytes, total) : a + m.chunk_bytes;
+    bool inside = false;
+    for (auto& r : ranges) inside = inside || (r.first <= a && r.second >= b);
+    if (inside) pc.second.emplace(c, m.crc[size_t(c)]);
+  }
 }
 
 void Node::flush_batch() {
@@ -1149,24 +1194,30 @@ void Node::relay_rebalance(RelayPlan& plan, const std::function<double(NodeID, N
       auto& parts = kv.second;
       for (size_t i = 0; i < parts.size() && !moved; ++i) {
         PlanPart& p = parts[i];
-        if (p.phase != 0 || p.src != s || p.size <= unit) continue;
+        if (p.phase != 0 || p.src != s) continue;
+        // The slice is the part's last grid chunk: cut on the chunk grid, so an
+        // odd layer end moves as one short whole chunk (never two partial
+        // pieces of one chunk from different senders).
+        const int64_t end = p.off + p.size, cut = (end - 1) / unit * unit;
+        if (cut <= p.off) continue;
+        const int64_t slice = end - cut;
         // the best relay: receives this layer directly (phase 0 only) in this plan
         NodeID best = 0;
         double tb = 1e300;
         for (auto& other : plan) {
           const NodeID x = other.first.first;
           if (other.first.second != layer || x == d || x == s || relayed_into.count(other.first)) continue;
-          const double tx = t(x, d, unit);
+          const double tx = t(x, d, slice);
           if (tx < tb) {
             tb = tx;
             best = x;
           }
         }
         if (tb >= tw) continue;  // no relay improves on this link
-        p.size -= unit;
-        parts.push_back(PlanPart{best, p.off + p.size, unit, 1});
-        bytes[{s, d}] -= unit;
-        bytes[{best, d}] += unit;
+        p.size -= slice;
+        parts.push_back(PlanPart{best, cut, slice, 1});
+        bytes[{s, d}] -= slice;
+        bytes[{best, d}] += slice;
         relayed_into.insert(kv.first);
         relays_from.insert({best, layer});
         moved = true;

@@ -199,7 +199,11 @@ class Node {
   };
   std::vector<PendingJob> pending_jobs_;
   uint64_t next_seq_ = 1, next_batch_ = 1;
-  std::map<LayerID, CrcManifest> manifests_;
+  std::map<LayerID, CrcManifest> manifests_;  // whole copies' manifests
+  // chunk CRCs vouched for by partial copies: layer -> (grid, chunk -> crc)
+  std::map<LayerID, std::pair<int64_t, std::map<int64_t, uint32_t>>> partial_crc_;
+  void merge_partial_manifest(LayerID layer, const CrcManifest& m,
+                              const std::vector<std::pair<int64_t, int64_t>>& ranges);
   // failure handling (leader, event-loop thread)
   struct Outstanding {
     NodeID sender;

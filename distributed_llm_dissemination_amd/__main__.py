@@ -81,8 +81,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--nccl-register", action="store_true",
                    help="rccl: register every HBM layer slot with the communicator (ncclCommRegister)")
     p.add_argument("--lanes", type=int, default=0,
-                   help="rccl: independent comm lanes (RCCL communicator + HIP stream each); 0 = world-1, "
-                        "one ring distance per lane, so a slow peer stalls only its own lane")
+                   help="rccl: independent comm lanes (RCCL communicator + HIP stream + dedicated HW queue "
+                        "each); 0 = one lane per directed link on up to 8 ranks (14 at 8 ranks), world-1 "
+                        "per-distance lanes beyond; a slow peer stalls only its own lane")
     p.add_argument("--suspect-timeout", type=float, default=10.0,
                    help="rccl: report a P2P group stalled this long to the leader, which probes the peers and "
                         "shrinks the communicator around dead ranks (elastic recovery; 0 = only on failure)")

@@ -641,6 +641,59 @@ class Runtime:
                 out[(a, b)] = int(gbps * 1e9)
         return out
 
+    def probe_links(self, nbytes: int = 256 * MiB, timeout_s: float = 30.0, solo: bool = True) -> Dict[str, object]:
+        """Untimed pre-flight probe of every directed link (planned engines, world > 1).
+
+        ``concurrent``: this rank sends ``nbytes`` to every peer and receives
+        ``nbytes`` from every peer at once, each transfer on its directed pair's
+        comm lane - the lane set a session drives. ``solo``: then every directed
+        pair once more on its own (barrier between pairs; ranks not in the pair
+        idle), which separates a slow link from a congested one. Every rank
+        calls this at the same time. Rates are this rank's sends (GB/s of device
+        time, keyed by peer node). A lane that does not complete within
+        ``timeout_s`` raises RuntimeError naming the lane and the pair."""
+        if self.engine is None or self.world < 2:
+            return {}
+        me = self.rank
+        peers = [r for r in range(self.world) if r != me]
+
+        def run(ops, what):
+            got = self.engine.probe(ops, timeout_s)
+            stalled = [o for o in got if not o["done"]]
+            if stalled:
+                desc = ", ".join(f"lane {o['lane']} ({'send to' if o['send'] else 'recv from'} node "
+                                 f"{self.node_ids[o['peer']]})" for o in stalled)
+                raise RuntimeError(f"link probe ({what}) stalled after {timeout_s:.0f} s on node {self.node_id}: {desc}")
+            return got
+
+        t0 = time.perf_counter()
+        self._barrier()
+        got = run([(p, True, nbytes) for p in peers] + [(p, False, nbytes) for p in peers], "concurrent")
+        self._barrier()
+        conc_ms = (time.perf_counter() - t0) * 1e3
+        out: Dict[str, object] = {
+            "bytes": nbytes,
+            "concurrent": {self.node_ids[o["peer"]]: round(nbytes / (o["ms"] / 1e3) / 1e9, 2) if o["ms"] > 0 else None
+                           for o in got if o["send"]},
+            "concurrent_wall_ms": round(conc_ms, 3),
+        }
+        if solo:
+            rates = {}
+            for a in range(self.world):
+                for b in range(self.world):
+                    if a == b:
+                        continue
+                    self._barrier()
+                    if me == a:
+                        o = run([(b, True, nbytes)], f"solo {self.node_ids[a]}->{self.node_ids[b]}")[0]
+                        rates[self.node_ids[b]] = round(nbytes / (o["ms"] / 1e3) / 1e9, 2) if o["ms"] > 0 else None
+                    elif me == b:
+                        run([(a, False, nbytes)], f"solo {self.node_ids[a]}->{self.node_ids[b]}")
+            self._barrier()
+            out["solo"] = rates
+        out["probe_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        return out
+
     def link_bytes(self) -> Dict[str, Dict[int, int]]:
         """Cumulative bytes this rank sent to / received from each peer rank (per-link counters)."""
         es = self.engine.stats()

@@ -15,6 +15,10 @@
                          engine: per-connection token bucket; planned engines:
                          the issue thread's per-link bucket; K/M/G suffixes are
                          powers of 1000)
+    fail-attempt=R@K     bench.py supervised runs (N > 1): rank R's worker fails
+                         right after its process group forms in attempt K, so
+                         the supervisors stop every worker and start the next,
+                         fallback attempt (utils/supervise.py)
 
 Several specs may be given (``--inject drop-chunk=0.01 --inject kill-rank=3@2``).
 """
@@ -43,6 +47,7 @@ class FaultPlan:
     drop_chunk: float = 0.0
     kill: Dict[int, float] = field(default_factory=dict)  # node id -> seconds after session start
     slow_links: Dict[Tuple[int, int], int] = field(default_factory=dict)  # (src, dst) -> B/s
+    fail_attempts: Dict[int, List[int]] = field(default_factory=dict)  # rank -> supervised attempts it fails
 
     def link_rates_from(self, node_id: int) -> Dict[int, int]:
         return {d: r for (s, d), r in self.slow_links.items() if s == node_id}
@@ -70,6 +75,11 @@ def parse_inject(specs: Optional[List[str]]) -> FaultPlan:
             if len(parts) != 3:
                 raise ValueError("slow-link wants S:D:RATE")
             plan.slow_links[(int(parts[0]), int(parts[1]))] = parse_rate(parts[2])
+        elif kind == "fail-attempt":
+            if "@" not in val:
+                raise ValueError("fail-attempt wants R@K (rank @ attempt index)")
+            r, k = val.split("@", 1)
+            plan.fail_attempts.setdefault(int(r), []).append(int(k))
         else:
             raise ValueError(f"unknown --inject kind {kind!r}")
     return plan

@@ -10,6 +10,7 @@
 #   check      GPU tests, smoke(), 1-GPU headline bench
 #   multirank  multi-rank RCCL rehearsal on one GPU (ranks share device 0)
 #   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
+#   insure     IPC variants, 14-lane rank death at 8 ranks, supervised bench --gpus 8 (+ forced fallback)
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
@@ -47,6 +48,20 @@ case "$RECIPE" in
         --layer-mib 64 --chunk-mib 16 --mode "$mode" "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
     done
     [ $rc -eq 0 ]
+    ;;
+  insure)
+    # Round-3 insurance for the first real 8-GPU run: cross-process IPC variants,
+    # the 14-lane rank-death recovery at 8 ranks, bench.py --gpus 8 through the
+    # supervisor with the link probe, and a forced first-attempt failure.
+    DISSEM_TEST_LOGDIR=$OUT/ipc timeout -k 10 200 $PYTEST tests/test_gpu_ipc.py > $OUT/pytest_ipc.log 2>&1 &&
+    DISSEM_FULL_REHEARSAL=1 DISSEM_TEST_LOGDIR=$OUT/death8 timeout -k 10 400 $PYTEST tests/test_gpu_multirank.py \
+      -k "rank_death and full" > $OUT/pytest_death8.log 2>&1 &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
+      --layer-mib 64 --chunk-mib 16 --probe-mib 64 > $OUT/bench8_probe.json 2> $OUT/bench8_probe.log &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 400 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
+      --layer-mib 64 --chunk-mib 16 --probe-mib 64 --inject fail-attempt=3@0 \
+      > $OUT/bench8_fallback.json 2> $OUT/bench8_fallback.log &&
+    timeout -k 10 300 python bench.py --steps 3 --warmup 1 > $OUT/bench1.json 2> $OUT/bench1.log
     ;;
   shared24)
     timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&

@@ -112,28 +112,34 @@ def test_resume_ignores_mismatched_layout_and_detects_corruption(tmp_path):
 
 
 @pytest.mark.parametrize("owner_policy", ["random", "links"])
-def test_chunk_granular_resume_moves_only_missing_chunks(tmp_path, owner_policy):
+@pytest.mark.parametrize("holder", [2, 0])
+def test_chunk_granular_resume_moves_only_missing_chunks(tmp_path, owner_policy, holder):
     """A rank that persisted only part of a layer (its resident chunks after a
     failed session, Runtime.persist(partial=True)) announces those byte ranges;
     the leader has it load them from its disk copy and sends only the missing
-    chunks (resumable at chunk granularity)."""
+    chunks (resumable at chunk granularity). holder 0 is the
+    leader itself: its partial copy's manifest (CRC 0 for the holes) must not
+    shadow the whole copies' manifests, and its holes must never be sent."""
+    import json
+    import shutil
+
     size = 4 * MiB
     cfg = make_workload(3, 3, size, tier="host", seeding="random", chunk_bytes=MiB)
+    assert cfg.leader().id == 0
     rts, key = _cluster(cfg, tmp_path)
     try:
         assert all(x.ok for x in _session(rts))
-        full = {l: rts[2].layer_bytes(l) for l in range(3)}
-        held = [l for l in range(3) if l in cfg.node(2).initial_layers.get(2, {})]
+        full = {l: rts[holder].layer_bytes(l) for l in range(3)}
+        held = [l for l in range(3) if l in cfg.node(holder).initial_layers.get(2, {})]
         missing = [l for l in range(3) if l not in held]
         target = missing[0]
-        # Keep 2 of node 2's 4 chunks of one received layer: write them as a partial persisted copy.
-        rts[2].persist(layers=[target])
+        # Keep 2 of the holder's 4 chunks of one received layer: write them as a partial persisted copy.
+        rts[holder].persist(layers=[target])
     finally:
         for r in rts:
             r.close()
-    import json
 
-    root = os.path.join(str(tmp_path), "2")
+    root = os.path.join(str(tmp_path), str(holder))
     man = json.load(open(os.path.join(root, "manifest.json")))
     e = man["layers"][str(target)]
     e["chunks"] = [0, 2]
@@ -144,14 +150,13 @@ def test_chunk_granular_resume_moves_only_missing_chunks(tmp_path, owner_policy)
         for c in (1, 3):
             f.seek(c * MiB)
             f.write(bytes(MiB))
-    # Node 0 and 1 start without persisted state.
-    for n in ("0", "1"):
-        import shutil
-
-        shutil.rmtree(os.path.join(str(tmp_path), n), ignore_errors=True)
+    # The other nodes start without persisted state.
+    for n in range(3):
+        if n != holder:
+            shutil.rmtree(os.path.join(str(tmp_path), str(n)), ignore_errors=True)
     rts, key = _cluster(cfg, tmp_path)
     try:
-        assert rts[2].resumed_partial == [target]
+        assert rts[holder].resumed_partial == [target]
         for r in rts:
             r.prepare(1, owner_policy=owner_policy)
         res = [None] * 3
@@ -164,8 +169,10 @@ def test_chunk_granular_resume_moves_only_missing_chunks(tmp_path, owner_policy)
         for r in rts:
             for l in range(3):
                 assert r.layer_bytes(l) == full[l], (l,)
-        # Node 2 received the two missing chunks of `target` and every byte of the others.
-        got = rts[2].link_bytes()["recv"]
+            st = r.engine.stats()
+            assert st.verify_failures == 0 and st.nacks == 0
+        # The holder received the two missing chunks of `target` and every byte of the others.
+        got = rts[holder].link_bytes()["recv"]
         assert sum(got.values()) == (len(missing) - 1) * size + 2 * MiB
     finally:
         for r in rts:

@@ -229,13 +229,14 @@ def test_fp8_packed_replication(mode, tier):
     assert res[0].engine_stats["verify_failures"] == 0
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
-def test_fp8_store_bf16_fused_unpack_on_landing(mode):
-    """--store bf16: every chunk that becomes resident - received or staged -
-    goes through the fused verify+unpack (CRC of the packed chunk and its bf16
-    image in one pass), so every rank ends with the same dequantized layer."""
+@pytest.mark.parametrize("mode,policy", [(1, {}), (2, {}), (3, {}), (0, {"relay": True}), (0, {"collective": True})])
+def test_fp8_store_bf16_fused_unpack_on_landing(mode, policy):
+    """--store bf16: every chunk that becomes resident - received, relayed,
+    broadcast (mode 0 ncclBroadcast) or staged - goes through the fused
+    verify+unpack (CRC of the packed chunk and its bf16 image in one pass), so
+    every rank ends with the same dequantized layer."""
     n, L, size = 4, 6, 3 * MiB + 4096
-    cfg = make_workload(n, L, size, tier="host", seeding="random", chunk_bytes=MiB)
+    cfg = make_workload(n, L, size, tier="host", seeding="leader" if mode == 0 else "random", chunk_bytes=MiB)
 
     def check(rts):
         for l in range(L):
@@ -244,8 +245,30 @@ def test_fp8_store_bf16_fused_unpack_on_landing(mode):
             for r in rts:
                 assert r.unpacked_layer_bytes(l) == want, (r.node_id, l)
 
-    (res,), _ = run_cluster(cfg, mode, rt_kw={"pack": "fp8", "store": "bf16"}, inspect=check, pull_window=n - 1)
-    assert res[0].engine_stats["verify_failures"] == 0
+    (res,), _ = run_cluster(cfg, mode, rt_kw={"pack": "fp8", "store": "bf16"}, inspect=check, pull_window=n - 1,
+                            **policy)
+    assert all(r.engine_stats["verify_failures"] == 0 and r.engine_stats["unverified_pieces"] == 0 for r in res)
+
+
+@pytest.mark.parametrize("store", ["packed", "bf16"])
+def test_relays_around_slow_link_cut_on_chunk_grid(store):
+    """Mode 1 "links" policy with a slow link in the plan and layers whose size
+    is not a grid multiple: the relay slices moved off the slow link end on
+    chunk boundaries (the odd tail chunk moves whole), so no chunk arrives as
+    two partial pieces from different senders - every received chunk is
+    CRC-checked (and with --store bf16 dequantized)."""
+    n, L = 4, 4
+    pack = store == "bf16"
+    size = 4 * MiB + (512 if pack else 13)
+    cfg = make_workload(n, L, size, tier="host", seeding="random", chunk_bytes=MiB)
+    fast, slow = int(50e9), int(5e9)
+    link_bw = {(a, b): fast for a in range(n) for b in range(n) if a != b}
+    link_bw[(0, 1)] = link_bw[(1, 0)] = slow
+    kw = {"pack": "fp8", "store": "bf16"} if pack else {}
+    (res,), _ = run_cluster(cfg, 1, rt_kw=kw, owner_policy="links", link_bw=link_bw)
+    for r in res:
+        assert r.engine_stats["verify_failures"] == 0
+        assert r.engine_stats["unverified_pieces"] == 0, r.engine_stats
 
 
 def _owners(cfg, layer):
