@@ -71,6 +71,9 @@ def parse_args(argv=None):
     p.add_argument("--lanes", type=int, default=0,
                    help="comm lanes (RCCL communicator + stream + dedicated HW queue each); 0 = one lane per "
                         "directed link on up to 8 ranks (14 at N = 8), world-1 per-distance lanes beyond")
+    p.add_argument("--comm-init", default="parallel", choices=["parallel", "split"],
+                   help="lane communicators: one unique id each, initialized together (parallel), or split from "
+                        "the world communicator one after another (split; round 2's path)")
     p.add_argument("--probe-mib", type=int, default=256,
                    help="N > 1: untimed pre-flight probe of every directed link with this many MiB "
                         "(all lanes at once, then each pair alone); 0 = skip")
@@ -125,15 +128,16 @@ def load_supervise():
 
 
 def fallback_attempts(args, world):
-    """The supervised attempts at N > 1: as asked, then with one lane per ring
-    distance (world-1 communicators and HW queues instead of 14), then also
-    without RCCL's P2P/IPC transport (host shared memory between the GPUs)."""
+    """The supervised attempts at N > 1: as asked; then round 2's data plane
+    (one lane per ring distance - world-1 communicators and HW queues instead
+    of 14 - split from the world communicator one by one); then that without
+    RCCL's P2P/IPC transport (host shared memory between the GPUs)."""
     Attempt = load_supervise().Attempt
     atts = [Attempt("")]
-    if args.lanes == 0 and world > 2:
-        atts.append(Attempt(f"lanes={world - 1}", ["--lanes", str(world - 1)]))
-    atts.append(Attempt(f"lanes={world - 1}, NCCL_P2P_DISABLE=1", ["--lanes", str(world - 1)],
-                        {"NCCL_P2P_DISABLE": "1"}))
+    if args.lanes == 0 and world > 2 or args.comm_init != "split":
+        atts.append(Attempt(f"lanes={world - 1}, split comm init", ["--lanes", str(world - 1), "--comm-init", "split"]))
+    atts.append(Attempt(f"lanes={world - 1}, split comm init, NCCL_P2P_DISABLE=1",
+                        ["--lanes", str(world - 1), "--comm-init", "split"], {"NCCL_P2P_DISABLE": "1"}))
     return atts
 
 
@@ -255,7 +259,9 @@ def worker(args, world, rank, chan) -> int:
                         seed=args.seed, assignment=args.assignment, chunk_bytes=args.chunk_mib << 20)
     total_bytes = delivered_bytes(cfg)
 
-    uid = _core.nccl_unique_id() if (world > 1 and rank == 0) else None
+    from distributed_llm_dissemination_amd.__main__ import nccl_ids
+
+    uid = nccl_ids(_core, world, args) if (world > 1 and rank == 0) else None
     if world > 1:
         box = [uid]
         dist.broadcast_object_list(box, src=0)
@@ -396,6 +402,8 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["comm_lanes"] = es.lanes
             out["config"]["comm_init_ms_rank0"] = round(es.comm_init_ms, 1)
             out["config"]["comm_init_ms_max"] = round(max(init_ms), 1)
+            out["config"]["comm_connect_ms_rank0"] = round(es.comm_connect_ms, 1)
+            out["config"]["comm_init"] = args.comm_init
         if world > 1:
             # GB/s per directed link: averaged over the timed wall time, and while
             # its P2P groups were on the device (busy).

@@ -266,7 +266,14 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("nccl_register", &PlannedConfig::nccl_register)
       .def_readwrite("lanes", &PlannedConfig::lanes)
       .def_readwrite("unpack_store", &PlannedConfig::unpack_store)
-      .def_readwrite("link_rate", &PlannedConfig::link_rate);
+      .def_readwrite("link_rate", &PlannedConfig::link_rate)
+      .def_readwrite("comm_init", &PlannedConfig::comm_init);
+  m.def("resolve_lanes", [](int world, int lanes) {
+    PlannedConfig c;
+    c.world = world;
+    c.lanes = lanes;
+    return resolve_lanes(c);
+  }, py::arg("world"), py::arg("lanes") = 0);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)
@@ -290,6 +297,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("lane_busy_ms", &PlannedStats::lane_busy_ms)
       .def_readonly("lanes", &PlannedStats::lanes)
       .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)
+      .def_readonly("comm_connect_ms", &PlannedStats::comm_connect_ms)
+      .def_readonly("comm_reform_ms", &PlannedStats::comm_reform_ms)
       .def_readonly("paced", &PlannedStats::paced)
       .def_readonly("order_violations", &PlannedStats::order_violations);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")

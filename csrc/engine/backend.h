@@ -113,7 +113,8 @@ class Backend {
   // Fault injection: this rank "crashes" - nothing it posted may still move
   // bytes (a dead process's outstanding ops vanish with it).
   virtual void crash() {}
-  virtual double comm_init_ms() const { return 0; }
+  virtual double comm_init_ms() const { return 0; }     // communicator set-up, connects included
+  virtual double comm_connect_ms() const { return 0; }  // the connect part
 };
 
 // Lanes. Every directed pair (src -> dst) has one lane, computed identically

@@ -76,6 +76,7 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
   stats_.lanes = lanes_;
   stats_.lane_busy_ms.assign(size_t(lanes_), 0.0);
   stats_.comm_init_ms = backend_->comm_init_ms();
+  stats_.comm_connect_ms = backend_->comm_connect_ms();
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
   self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
   th_ = std::thread([this] { run(); });
@@ -1173,6 +1174,7 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
     std::lock_guard<std::mutex> lk(stats_mu_);
     stats_.shrinks++;
     stats_.aborted_pieces += aborted;
+    stats_.comm_reform_ms = backend_->comm_init_ms();  // the survivors' communicators, set up like the first
   }
   log::warn(int64_t(self_node_)).i("dead", int64_t(dead.size())).i("old_rank", old_rank).i("new_rank", new_rank)
       .i("world", cfg_.world).i("aborted_pieces", aborted).msg("communicator shrunk: continuing without dead ranks");

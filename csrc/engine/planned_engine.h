@@ -106,6 +106,12 @@ struct PlannedConfig {
   int nccl_min_ctas = 0;
   int nccl_max_ctas = 0;
   bool nccl_register = false;  // register every HBM slot with the communicator (ncclCommRegister)
+  // How the lane communicators are created: "parallel" = one ncclCommInitRankConfig
+  // per lane from its own unique id, all inside one group (they initialize
+  // concurrently), then every lane connected in one group; "split" = the world
+  // communicator, then ncclCommSplit per lane one after another and a grouped
+  // connect per ring distance (round 2's path; the bench's last fallback).
+  std::string comm_init = "parallel";
 };
 
 // Comm lanes an engine of this config runs. 0 = auto: one lane per directed
@@ -129,7 +135,8 @@ struct PlannedStats {
   std::map<int, double> peer_busy_ms;
   std::vector<double> lane_busy_ms;
   int lanes = 1;
-  double comm_init_ms = 0;
+  double comm_init_ms = 0, comm_connect_ms = 0;
+  double comm_reform_ms = 0;  // last elastic re-form (abort + re-init after a shrink)
   int64_t paced = 0;  // issue attempts a token bucket deferred
   int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us

@@ -325,7 +325,7 @@ void register_gpu_bindings(PyObject* module) {
   }, py::arg("device"), py::arg("bytes"), py::arg("chunk"));
 
   // ---- RCCL engine = planned engine on the HIP backend
-  m.def("nccl_unique_id", [] { return py::bytes(nccl_unique_id()); });
+  m.def("nccl_unique_id", [](int count) { return py::bytes(nccl_unique_id(count)); }, py::arg("count") = 1);
   m.def("gpu_engine", [](const PlannedConfig& cfg, int device, py::bytes uid) {
     HipBackendConfig hc;
     hc.device = device;
@@ -338,6 +338,9 @@ void register_gpu_bindings(PyObject* module) {
     hc.nccl_max_ctas = cfg.nccl_max_ctas;
     hc.nccl_register = cfg.nccl_register;
     hc.lanes = resolve_lanes(cfg);
+    if (cfg.comm_init != "parallel" && cfg.comm_init != "split")
+      throw std::runtime_error("comm_init must be parallel or split, not " + cfg.comm_init);
+    hc.parallel_init = cfg.comm_init == "parallel";
     py::gil_scoped_release nogil;
     return std::make_shared<PlannedEngine>(cfg, make_hip_backend(hc));
   }, py::arg("cfg"), py::arg("device") = 0, py::arg("nccl_uid") = py::bytes(""));

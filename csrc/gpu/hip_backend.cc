@@ -74,37 +74,53 @@ class HipBackend : public Backend {
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&crc_dev_), crc_host_, 0));
     if (cfg_.world > 1 || cfg_.self_comm) {
-      ncclUniqueId id;
-      if (cfg_.world == 1 && cfg_.nccl_uid.empty()) {
-        NCCL_OK(ncclGetUniqueId(&id));
-      } else {
-        if (cfg_.nccl_uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("nccl_uid must be ncclUniqueId bytes");
-        memcpy(&id, cfg_.nccl_uid.data(), sizeof id);
-      }
-      init_comm(id);
+      std::string ids = cfg_.nccl_uid;
+      if (cfg_.world == 1 && ids.empty()) ids = nccl_unique_id(int(nccl_.size()));
+      init_comm(ids);
     }
   }
 
-  void init_comm(const ncclUniqueId& id_in) {
-    ncclUniqueId id = id_in;
-    auto t0 = log::now_us();
+  ncclConfig_t comm_config() const {
     ncclConfig_t nc = NCCL_CONFIG_INITIALIZER;
     if (cfg_.nccl_min_ctas > 0) nc.minCTAs = cfg_.nccl_min_ctas;
     if (cfg_.nccl_max_ctas > 0) nc.maxCTAs = cfg_.nccl_max_ctas;
-    NCCL_OK(ncclCommInitRankConfig(&nccl_[0], cfg_.world, id, cfg_.rank, &nc));
-    // Further lanes: independent communicators over the same ranks (own
-    // channels and connections; collective split, same order on every rank).
-    for (size_t l = 1; l < nccl_.size(); ++l) {
-      ncclConfig_t lc = NCCL_CONFIG_INITIALIZER;
-      if (cfg_.nccl_min_ctas > 0) lc.minCTAs = cfg_.nccl_min_ctas;
-      if (cfg_.nccl_max_ctas > 0) lc.maxCTAs = cfg_.nccl_max_ctas;
-      lc.splitShare = 0;
-      NCCL_OK(ncclCommSplit(nccl_[0], 0, cfg_.rank, &nccl_[l], &lc));
+    return nc;
+  }
+
+  // `ids`: one ncclUniqueId per lane (parallel init), or a single id (split).
+  void init_comm(const std::string& ids) {
+    const size_t n = nccl_.size(), idb = sizeof(ncclUniqueId);
+    if (ids.size() != idb && ids.size() != n * idb)
+      throw std::runtime_error("nccl_uid must hold 1 or " + std::to_string(n) + " ncclUniqueIds");
+    const bool parallel = cfg_.parallel_init && ids.size() == n * idb;
+    auto t0 = log::now_us();
+    std::vector<ncclConfig_t> ncs(n, comm_config());
+    if (parallel) {
+      // Every lane communicator from its own unique id, all in one group: RCCL
+      // runs the inits (bootstrap, topology, channel set-up) concurrently, so
+      // 14 lanes cost about one communicator's set-up instead of fourteen.
+      std::vector<ncclUniqueId> uid(n);
+      memcpy(uid.data(), ids.data(), n * idb);
+      NCCL_OK(ncclGroupStart());
+      for (size_t l = 0; l < n; ++l) NCCL_OK(ncclCommInitRankConfig(&nccl_[l], cfg_.world, uid[l], cfg_.rank, &ncs[l]));
+      NCCL_OK(ncclGroupEnd());
+    } else {
+      ncclUniqueId id;
+      memcpy(&id, ids.data(), idb);
+      NCCL_OK(ncclCommInitRankConfig(&nccl_[0], cfg_.world, id, cfg_.rank, &ncs[0]));
+      // Further lanes: independent communicators over the same ranks (own
+      // channels and connections; collective split, same order on every rank).
+      for (size_t l = 1; l < n; ++l) {
+        ncs[l].splitShare = 0;
+        NCCL_OK(ncclCommSplit(nccl_[0], 0, cfg_.rank, &nccl_[l], &ncs[l]));
+      }
     }
-    connect_all();
+    const auto t1 = log::now_us();
+    connect_all(parallel);
     init_ms_ = double(log::now_us() - t0) / 1e3;
-    log::info(cfg_.rank).i("world", cfg_.world).i("lanes", int64_t(nccl_.size())).f("init_ms", init_ms_)
-        .msg("rccl communicators ready");
+    connect_ms_ = double(log::now_us() - t1) / 1e3;
+    log::info(cfg_.rank).i("world", cfg_.world).i("lanes", int64_t(n)).s("init", parallel ? "parallel" : "split")
+        .f("init_ms", init_ms_).f("connect_ms", connect_ms_).msg("rccl communicators ready");
   }
 
   // RCCL connects a pair lazily inside the first ncclGroupEnd that uses it, and
@@ -114,20 +130,28 @@ class HipBackend : public Backend {
   // setup the other has not reached yet would hang. So every lane connects
   // every distance it serves (and lane 0 its broadcast ring) here, in one fixed
   // order on every rank.
-  void connect_all() {
+  //
+  // `one_group`: every distance in a single group across the lane
+  // communicators (the same fixed order on every rank, so the per-lane
+  // connection set-ups RCCL runs inside ncclGroupEnd cannot wait on each other
+  // in a cycle: the lowest lane some rank waits on has all of its ranks there);
+  // otherwise one group per distance (round 2).
+  void connect_all(bool one_group = false) {
     const int world = cfg_.world, lanes = int(nccl_.size());
     if (world < 2) return;
-    if (!probe_) HIP_OK(hipMalloc(&probe_, 8192));
+    if (!probe_) HIP_OK(hipMalloc(&probe_, 64 * 1024));
     uint8_t* sbuf = static_cast<uint8_t*>(probe_);
-    uint8_t* rbuf = sbuf + 4096;
+    if (one_group) NCCL_OK(ncclGroupStart());
     for (int d = 1; d < world; ++d) {
       const int to = (cfg_.rank + d) % world, from = (cfg_.rank - d + world) % world;
       const size_t ls = size_t(lane_of(cfg_.rank, to, world, lanes)), lr = size_t(lane_of(from, cfg_.rank, world, lanes));
-      NCCL_OK(ncclGroupStart());
+      uint8_t* rbuf = sbuf + 4096 * size_t(std::min(d, 15));  // distinct landing per recv of the group
+      if (!one_group) NCCL_OK(ncclGroupStart());
       NCCL_OK(ncclSend(sbuf, 64, ncclUint8, to, nccl_[ls], comm_[ls]));
       NCCL_OK(ncclRecv(rbuf, 64, ncclUint8, from, nccl_[lr], comm_[lr]));
-      NCCL_OK(ncclGroupEnd());
+      if (!one_group) NCCL_OK(ncclGroupEnd());
     }
+    if (one_group) NCCL_OK(ncclGroupEnd());
     NCCL_OK(ncclBroadcast(sbuf, sbuf, 64, ncclUint8, 0, nccl_[0], comm_[0]));
     for (hipStream_t s : comm_) HIP_OK(hipStreamSynchronize(s));
   }
@@ -135,6 +159,7 @@ class HipBackend : public Backend {
   std::string name() const override { return "rccl"; }
   int lanes() const override { return int(comm_.size()); }
   double comm_init_ms() const override { return init_ms_; }
+  double comm_connect_ms() const override { return connect_ms_; }
 
   void init_thread() override { HIP_OK(hipSetDevice(cfg_.device)); }
 
@@ -323,11 +348,12 @@ class HipBackend : public Backend {
     }
     return "";
   }
-  std::string new_comm_id() override { return nccl_unique_id(); }
+  // The survivors' communicators after a shrink: one id per lane (parallel init).
+  std::string new_comm_id() override { return nccl_unique_id(cfg_.parallel_init ? int(nccl_.size()) : 1); }
 
   int shrink(const std::vector<int>& dead, uint64_t, const std::string& comm_id) override {
     if (!nccl_[0]) throw std::runtime_error("shrink without a communicator");
-    if (comm_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("shrink: bad communicator id");
+    if (comm_id.empty() || comm_id.size() % sizeof(ncclUniqueId)) throw std::runtime_error("shrink: bad communicator id");
     // Abort first: P2P groups waiting on the dead rank are terminated, so the
     // comm streams drain. (ncclCommShrink would keep the bootstrap, but the RCCL
     // PyTorch loads into the process predates it; abort + re-init of the
@@ -365,9 +391,7 @@ class HipBackend : public Backend {
       }
       (void)hipEventDestroy(e);
     }
-    ncclUniqueId id;
-    memcpy(&id, comm_id.data(), sizeof id);
-    init_comm(id);
+    init_comm(comm_id);
     for (auto& pr : regd) register_slot(pr.first, pr.second);
     return new_rank;
   }
@@ -459,7 +483,7 @@ class HipBackend : public Backend {
   std::map<uint8_t*, std::pair<int64_t, std::vector<void*>>> regs_;  // registered slots: size, handle per lane
   bool flip_ = false;
   std::vector<ncclComm_t> nccl_;  // one per lane (lane 0: the world communicator, others split from it)
-  double init_ms_ = 0;
+  double init_ms_ = 0, connect_ms_ = 0;
   void* probe_ = nullptr;  // connect_all() scratch
   std::map<Ev, hipEvent_t> starts_;  // timed group end -> its start event
   std::vector<hipEvent_t> timed_pool_;
@@ -502,10 +526,14 @@ std::shared_ptr<HostBuffer> alloc_pinned(int64_t size) {
                           std::shared_ptr<void>(p, [](void* q) { (void)hipHostFree(q); }));
 }
 
-std::string nccl_unique_id() {
-  ncclUniqueId id;
-  NCCL_OK(ncclGetUniqueId(&id));
-  return std::string(reinterpret_cast<const char*>(&id), sizeof id);
+std::string nccl_unique_id(int count) {
+  std::string out;
+  for (int i = 0; i < std::max(1, count); ++i) {
+    ncclUniqueId id;
+    NCCL_OK(ncclGetUniqueId(&id));
+    out.append(reinterpret_cast<const char*>(&id), sizeof id);
+  }
+  return out;
 }
 
 }  // namespace dissem

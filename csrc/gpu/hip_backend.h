@@ -26,7 +26,7 @@ struct HipBackendConfig {
   int device = 0;
   int rank = 0;
   int world = 1;
-  std::string nccl_uid;  // ncclUniqueId bytes (world > 1)
+  std::string nccl_uid;  // ncclUniqueId bytes (world > 1): one id, or one per lane (parallel init)
   int64_t max_crc_bytes = 64ll << 20;  // largest chunk the verify workspace must hold
   // world == 1: still build a one-rank communicator, so P2P groups to self
   // exercise the RCCL path on a single-GPU box (rccl_selftest)
@@ -37,6 +37,7 @@ struct HipBackendConfig {
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
   int lanes = 1;                               // comm lanes (communicator + stream each)
   bool nccl_register = false;                  // ncclCommRegister every layer slot
+  bool parallel_init = true;                   // per-lane ids: init all lane communicators in one group
 };
 
 // A non-default stream whose kernels may use every CU but the last `reserve`
@@ -46,6 +47,6 @@ hipStream_t create_stream_reserving(int device, int reserve, bool dedicated = fa
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg);
 std::shared_ptr<HostBuffer> alloc_pinned(int64_t size);
-std::string nccl_unique_id();
+std::string nccl_unique_id(int count = 1);  // `count` ncclUniqueIds, concatenated
 
 }  // namespace dissem

@@ -84,6 +84,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="rccl: independent comm lanes (RCCL communicator + HIP stream + dedicated HW queue "
                         "each); 0 = one lane per directed link on up to 8 ranks (14 at 8 ranks), world-1 "
                         "per-distance lanes beyond; a slow peer stalls only its own lane")
+    p.add_argument("--comm-init", default="parallel", choices=["parallel", "split"],
+                   help="rccl: lane communicators from one unique id each, initialized together in one group "
+                        "(parallel), or split from the world communicator one by one (split)")
     p.add_argument("--suspect-timeout", type=float, default=10.0,
                    help="rccl: report a P2P group stalled this long to the leader, which probes the peers and "
                         "shrinks the communicator around dead ranks (elastic recovery; 0 = only on failure)")
@@ -123,11 +126,18 @@ def build_parser() -> argparse.ArgumentParser:
 def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
     opts = {"reserve_cus": args.reserve_cus, "suspect_s": getattr(args, "suspect_timeout", 10.0),
-            "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0))}
+            "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0)),
+            "comm_init": getattr(args, "comm_init", "parallel")}
     if args.nccl_ctas:
         lo, _, hi = args.nccl_ctas.partition(":")
         opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)
     return opts
+
+
+def nccl_ids(core, world: int, args) -> bytes:
+    """Rank 0's RCCL bootstrap ids: one per comm lane (parallel init) or one (split)."""
+    n = core.resolve_lanes(world, int(getattr(args, "lanes", 0))) if getattr(args, "comm_init", "parallel") == "parallel" else 1
+    return core.nccl_unique_id(n)
 
 
 def main(argv=None) -> int:
@@ -206,7 +216,7 @@ def main(argv=None) -> int:
             # Bootstrap only (gloo over TCP): barriers, the ncclUniqueId, addresses.
             dist.init_process_group("gloo")
             if args.engine == "rccl":
-                box = [_core.nccl_unique_id() if dist.get_rank() == 0 else None]
+                box = [nccl_ids(_core, world, args) if dist.get_rank() == 0 else None]
                 dist.broadcast_object_list(box, src=0)
                 uid = box[0]
             barrier = dist.barrier

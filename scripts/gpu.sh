@@ -11,6 +11,7 @@
 #   multirank  multi-rank RCCL rehearsal on one GPU (ranks share device 0)
 #   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
 #   insure     IPC variants, 14-lane rank death at 8 ranks, supervised bench --gpus 8 (+ forced fallback)
+#   init       parallel vs split lane-communicator set-up at 8 shared ranks; rank-death re-form
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
@@ -62,6 +63,17 @@ case "$RECIPE" in
       --layer-mib 64 --chunk-mib 16 --probe-mib 64 --inject fail-attempt=3@0 \
       > $OUT/bench8_fallback.json 2> $OUT/bench8_fallback.log &&
     timeout -k 10 300 python bench.py --steps 3 --warmup 1 > $OUT/bench1.json 2> $OUT/bench1.log
+    ;;
+  init)
+    # lane communicator set-up: parallel (one id per lane, one group) vs split, at 8 shared ranks;
+    # the 14-lane rank-death re-form with the parallel init
+    for ci in parallel split; do
+      DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 1 --warmup 1 --layers 16 \
+        --layer-mib 64 --chunk-mib 16 --probe-mib 16 --comm-init $ci --no-fallback \
+        > $OUT/bench8_$ci.json 2> $OUT/bench8_$ci.log || exit 1
+    done
+    DISSEM_FULL_REHEARSAL=1 DISSEM_TEST_LOGDIR=$OUT/death8 timeout -k 10 400 $PYTEST tests/test_gpu_multirank.py \
+      -k "rank_death" > $OUT/pytest_death.log 2>&1
     ;;
   shared24)
     timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
