@@ -79,6 +79,9 @@ def parse_args(argv=None):
                         "(all lanes at once, then each pair alone); 0 = skip")
     p.add_argument("--probe-timeout", type=float, default=30.0,
                    help="seconds the probe waits for a lane before naming it stalled and failing the attempt")
+    p.add_argument("--no-adapt-links", action="store_true",
+                   help="plan every session on the fixed link estimates instead of the per-link rates the ranks "
+                        "measured (probe + earlier sessions' busy throughput, EWMA)")
     p.add_argument("--no-fallback", action="store_true",
                    help="N > 1 under torchrun: run the worker in this process (no supervised fresh-process "
                         "attempts with fallback data-plane settings)")
@@ -295,11 +298,14 @@ def worker(args, world, rank, chan) -> int:
         except RuntimeError as e:
             failed(str(e))
         log(f"link probe: {probe.get('probe_ms')} ms; concurrent GB/s {probe.get('concurrent')}")
+        # the probe's concurrent rates seed the closed-loop link estimates (B/s)
+        rt.observe_links({p: g * 1e9 for p, g in probe.get("concurrent", {}).items() if g})
 
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
     policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, 2 * (world - 1)),
                   owner_policy=args.owner_policy,
-                  relay=args.bcast == "relay", collective=args.bcast == "collective")
+                  relay=args.bcast == "relay", collective=args.bcast == "collective",
+                  adapt_links=not args.no_adapt_links)
 
     def step(timed: bool, i: int):
         beat(f"{'step' if timed else 'warmup'} {i}")
@@ -330,10 +336,10 @@ def worker(args, world, rank, chan) -> int:
     beat("measured")
     total = sum(times)
     # Per directed link over the timed steps: bytes this rank sent to each peer,
-    # and the device time of the P2P groups that involved the peer.
+    # and the device time of the P2P groups that sent to it.
     links1 = rt.link_stats()
     mine = {p: (links1["sent"].get(p, 0) - links0["sent"].get(p, 0),
-                links1["busy_ms"].get(p, 0.0) - links0["busy_ms"].get(p, 0.0)) for p in links1["sent"]}
+                links1["send_busy_ms"].get(p, 0.0) - links0["send_busy_ms"].get(p, 0.0)) for p in links1["sent"]}
     all_links = [mine]
     all_probe = [probe]
     init_ms = [rt.engine.stats().comm_init_ms]
@@ -406,7 +412,7 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["comm_init"] = args.comm_init
         if world > 1:
             # GB/s per directed link: averaged over the timed wall time, and while
-            # its P2P groups were on the device (busy).
+            # its send groups were on the device (busy).
             wall, busy = {}, {}
             for src, per in enumerate(all_links):
                 for p, (b, ms) in sorted(per.items()):
@@ -414,6 +420,10 @@ def worker(args, world, rank, chan) -> int:
                     busy[f"{src}->{p}"] = round(b / (ms / 1e3) / 1e9, 2) if ms > 0 else None
             out["config"]["per_link_GBps"] = wall
             out["config"]["per_link_busy_GBps"] = busy
+            # the per directed link rates the leader's last plan used (measured, closed loop)
+            plan = rt.plan_link_bw()
+            out["config"]["adapt_links"] = not args.no_adapt_links
+            out["config"]["plan_link_GBps"] = {f"{a}->{b}": round(v / 1e9, 2) for (a, b), v in sorted(plan.items())}
             if any(all_probe):
                 # untimed pre-flight probe: GB/s per directed link (sender's device time)
                 pr = {"MiB": args.probe_mib, "concurrent": {}, "solo": {}}

@@ -58,6 +58,7 @@ PYBIND11_MODULE(_core, m) {
 
   // ---- logging
   m.def("set_log_level", &log::set_level);
+  m.def("log_level", [] { return int(log::level()); });
   m.def("set_log_file", &log::set_file);
   // ---- roctx (rocprofv3 --marker-trace)
   m.def("trace_available", &trace::available);
@@ -294,6 +295,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("shrinks", &PlannedStats::shrinks)
       .def_readonly("aborted_pieces", &PlannedStats::aborted_pieces)
       .def_readonly("peer_busy_ms", &PlannedStats::peer_busy_ms)
+      .def_readonly("peer_send_busy_ms", &PlannedStats::peer_send_busy_ms)
       .def_readonly("lane_busy_ms", &PlannedStats::lane_busy_ms)
       .def_readonly("lanes", &PlannedStats::lanes)
       .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)
@@ -447,7 +449,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("range_acks", &NodeConfig::range_acks)
       .def_readwrite("job_timeout_s", &NodeConfig::job_timeout_s)
       .def_readwrite("job_min_rate", &NodeConfig::job_min_rate)
-      .def_readwrite("max_redispatch", &NodeConfig::max_redispatch);
+      .def_readwrite("max_redispatch", &NodeConfig::max_redispatch)
+      .def_readwrite("link_report", &NodeConfig::link_report)
+      .def_readwrite("adapt_links", &NodeConfig::adapt_links);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)
@@ -469,6 +473,7 @@ PYBIND11_MODULE(_core, m) {
            py::arg("cfg"), py::arg("transport"), py::arg("engine"), py::arg("layers"),
            py::arg("assignment") = py::dict(), py::arg("is_leader") = false)
       .def("start", &Node::start)
+      .def("plan_link_bw", &Node::plan_link_bw)
       .def("stop", [](Node& n) {
         py::gil_scoped_release nogil;
         n.stop();

@@ -185,6 +185,11 @@ Json encode_payload(const Message& m) {
         }
         p["Manifest"] = man;
       }
+      if (!m.link_rates.empty()) {  // measured outbound link rates (B/s), closed-loop planning
+        Json lr = Json::object();
+        for (auto& kv : m.link_rates) lr[std::to_string(kv.first)] = Json(kv.second);
+        p["LinkRates"] = lr;
+      }
       if (!m.partial_layers.empty()) {
         Json part = Json::object();
         for (auto& kv : m.partial_layers) {
@@ -337,6 +342,8 @@ MessagePtr decode_envelope(const Json& env) {
           for (auto& e : kv.second.as_array()) rs.push_back({e.as_array().at(0).as_i64(), e.as_array().at(1).as_i64()});
         }
       }
+      if (auto* lr = p.find("LinkRates"); lr && lr->is_object())
+        for (auto& kv : lr->as_object()) m->link_rates[NodeID(strtoull(kv.first.c_str(), nullptr, 10))] = kv.second.as_i64();
       break;
     case MsgType::XferBatch:
       m->batch = p.get_u64("Batch");

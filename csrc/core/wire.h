@@ -92,6 +92,7 @@ struct Message {
   std::vector<XferJob> jobs;
   std::map<LayerID, CrcManifest> manifest;
   PartialLayers partial_layers;  // Announce extension: layers held only in these byte ranges
+  std::map<NodeID, int64_t> link_rates;  // Announce extension: sender's measured rate to each peer (B/s)
   // Simple
   std::string src_addr, payload_str;
 

@@ -998,9 +998,13 @@ bool PlannedEngine::issue_lane(int lane) {
       CallMark cm(this, "group", lane);
       g = backend_->group(xops, waits, lane);
     }
-    Inflight inf{g, now, {}};
-    for (auto& p : group)
+    Inflight inf{g, now, {}, {}};
+    for (auto& p : group) {
       if (std::find(inf.peers.begin(), inf.peers.end(), p.peer) == inf.peers.end()) inf.peers.push_back(p.peer);
+      if (p.kind == Kind::Send && !p.bcast &&
+          std::find(inf.send_peers.begin(), inf.send_peers.end(), p.peer) == inf.send_peers.end())
+        inf.send_peers.push_back(p.peer);
+    }
     infl.push_back(std::move(inf));
     // Fault injection: damage some received chunks behind the group, before their check.
     Ev landed_ev = g;
@@ -1232,6 +1236,7 @@ void PlannedEngine::poll() {
         if (ms >= 0) {
           stats_.lane_busy_ms[size_t(lane)] += ms;
           for (int p : head.peers) stats_.peer_busy_ms[p] += ms;
+          for (int p : head.send_peers) stats_.peer_send_busy_ms[p] += ms;
         }
       }
       backend_->release(head.ev);

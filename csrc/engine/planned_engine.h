@@ -133,6 +133,7 @@ struct PlannedStats {
   std::map<int, int64_t> peer_sent, peer_recv;  // bytes per peer rank (per-link counters)
   // device time of completed groups involving each peer / on each lane (ms)
   std::map<int, double> peer_busy_ms;
+  std::map<int, double> peer_send_busy_ms;  // groups that sent to the peer (the directed link's own time)
   std::vector<double> lane_busy_ms;
   int lanes = 1;
   double comm_init_ms = 0, comm_connect_ms = 0;
@@ -287,6 +288,7 @@ class PlannedEngine : public DataEngine {
     Ev ev;
     std::chrono::steady_clock::time_point t0;
     std::vector<int> peers;  // partner ranks
+    std::vector<int> send_peers;  // ranks it sends to (point-to-point)
   };
   struct Pace {  // token bucket, non-blocking (burst: one chunk; mode-3 jobs two, see pace_ready)
     double rate = 0, tokens = 0, burst = 0;

@@ -32,6 +32,7 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
   if (is_leader_) {
     status_[cfg_.id] = store_.inventory();  // node.go:252-257
     partial_[cfg_.id] = store_.partial();
+    for (auto& kv : cfg_.link_report) measured_links_[{cfg_.id, kv.first}] = kv.second;
   }
   e_->bind(this);
   if (is_leader_ && e_->planned()) {
@@ -140,6 +141,11 @@ NodeID Node::next_hop(NodeID goal) {
   return it->second.first;
 }
 
+std::map<std::pair<NodeID, NodeID>, int64_t> Node::plan_link_bw() {
+  std::lock_guard<std::mutex> lk(sig_mu_);
+  return cfg_.link_bw;
+}
+
 void Node::update_leader(NodeID leader) {
   std::lock_guard<std::mutex> lk(rt_mu_);
   if (!routing_.count(leader)) throw std::runtime_error("routing entry for the specified leader does not exist");
@@ -165,6 +171,7 @@ void Node::announce() {
   m.type = MsgType::Announce;
   m.layers = store_.inventory();
   m.partial_layers = store_.partial();
+  m.link_rates = cfg_.link_report;
   if (e_->planned()) {
     // Whole copies' manifests, and a resumed partial copy's too: the leader
     // takes from the latter only the chunks inside its announced ranges.
@@ -443,6 +450,7 @@ void Node::on_announce(const MessagePtr& m) {
     status_[m->src] = m->layers;
     partial_[m->src] = m->partial_layers;
     add_node(m->src);
+    for (auto& kv : m->link_rates) measured_links_[{m->src, kv.first}] = kv.second;
   }
   for (auto& kv : m->manifest) {
     auto pit = m->partial_layers.find(kv.first);
@@ -476,7 +484,15 @@ void Node::start_distribution() {
     sig_cv_.notify_all();
   }
   initial_status_ = status_;
-  log::info(int64_t(cfg_.id)).i("mode", cfg_.mode).i("bytes_planned", planned).msg("timer start");
+  if (cfg_.adapt_links && !measured_links_.empty()) {
+    // Closed loop: plan on the rates the senders measured (reported with their
+    // announces) instead of the estimates; links nobody measured keep theirs.
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    for (auto& kv : measured_links_)
+      if (kv.second > 0) cfg_.link_bw[kv.first] = kv.second;
+  }
+  log::info(int64_t(cfg_.id)).i("mode", cfg_.mode).i("bytes_planned", planned)
+      .i("measured_links", int64_t(measured_links_.size())).msg("timer start");
   session_range_ = trace::start("dissem.session");
   int64_t t0 = log::now_us();
   {
@@ -827,7 +843,7 @@ void Node::on_tick() {
       for (auto& jd : lj.second)
         if (jd.second.state == JobState::Pending && suspects_.count(jd.second.sender)) {
           load_[jd.second.sender] = std::max<int64_t>(0, load_[jd.second.sender] - 1);
-          NodeID s = min_loaded_sender(lj.first);
+          NodeID s = min_loaded_sender(lj.first, jd.first.first);
           if (s == kClientID) continue;
           jd.second.sender = s;
           load_[s]++;
@@ -1233,8 +1249,11 @@ void Node::relay_rebalance(RelayPlan& plan, const std::function<double(NodeID, N
 
 // ------------------------------------------------------------------- mode 2
 
-NodeID Node::min_loaded_sender(LayerID layer) {
+NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
   // node.go:948-978 (the code picks the FASTEST source; quirk Q16 keeps that).
+  // A sender's rate for this job is its tier's LimitRate capped by its link to
+  // the dest when the plan knows it (measured or configured): on equal links
+  // this is the reference's choice.
   NodeID best = 0;
   bool found = false;
   int64_t best_rate = 0;
@@ -1247,6 +1266,8 @@ NodeID Node::min_loaded_sender(LayerID layer) {
     auto it = st->second.find(layer);
     if (it == st->second.end()) continue;
     int64_t eff = it->second.limit_rate == 0 ? INT64_MAX : it->second.limit_rate;
+    if (auto lb = cfg_.link_bw.find({sender, dest}); lb != cfg_.link_bw.end() && lb->second > 0 && sender != dest)
+      eff = std::min(eff, lb->second);
     int64_t count = kv.second;
     if (!found || eff > best_rate || (eff == best_rate && (count < min_count || (count == min_count && sender < best)))) {
       best = sender;
@@ -1414,7 +1435,7 @@ void Node::schedule_mode2() {
     auto lj = jobs_.find(layer);
     if (lj == jobs_.end()) continue;
     for (auto& jd : lj->second) {
-      NodeID sender = min_loaded_sender(layer);
+      NodeID sender = min_loaded_sender(layer, jd.first.first);
       if (sender == kClientID) {
         log::error(int64_t(cfg_.id)).u("layer", layer).msg("no owner holds the layer");
         continue;

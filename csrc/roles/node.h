@@ -51,6 +51,14 @@ struct NodeConfig {
   double job_timeout_s = 0;
   double job_min_rate = 0;          // B/s allowance added to the deadline (0 = flat timeout)
   int max_redispatch = 8;           // per (dest, layer, range)
+  // Closed-loop link rates: this node's measured outbound rate to each peer
+  // (B/s; e.g. an EWMA of earlier sessions' per-link busy throughput or the
+  // pre-flight probe), sent with its announce. With adapt_links the leader
+  // plans on every node's reported rates instead of link_bw's estimates:
+  // mode-1 "links" owners and relays, mode-3 capacities and T, mode-2 sender
+  // choice (reference: node.go:774-793 measures job times, :1044-1053 uses them).
+  std::map<NodeID, int64_t> link_report;
+  bool adapt_links = true;
 };
 
 struct NodeStats {
@@ -91,6 +99,8 @@ class Node {
   void add_routing(NodeID goal, NodeID next_hop, unsigned hops);
   NodeID next_hop(NodeID goal);
   void update_leader(NodeID leader);
+  // Leader: the per directed link rates the last plan used (B/s).
+  std::map<std::pair<NodeID, NodeID>, int64_t> plan_link_bw();
 
   // Accessors for engines.
   NodeID id() const { return cfg_.id; }
@@ -155,7 +165,7 @@ class Node {
   // mode 2 (node.go:628-1073); a job is (layer, dest, byte range)
   using JobKey = std::pair<NodeID, int64_t>;  // (dest, offset) within jobs_[layer]
   bool assign_new_job(NodeID node);
-  NodeID min_loaded_sender(LayerID layer);
+  NodeID min_loaded_sender(LayerID layer, NodeID dest);
   bool rarest_own_job(NodeID node, LayerID* layer, JobKey* key);
   bool rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID* victim);
   void dispatch_range(LayerID layer, NodeID sender, NodeID dest, int64_t off, int64_t size);
@@ -199,6 +209,7 @@ class Node {
   };
   std::vector<PendingJob> pending_jobs_;
   uint64_t next_seq_ = 1, next_batch_ = 1;
+  std::map<std::pair<NodeID, NodeID>, int64_t> measured_links_;  // leader: reported link rates (B/s)
   std::map<LayerID, CrcManifest> manifests_;  // whole copies' manifests
   // chunk CRCs vouched for by partial copies: layer -> (grid, chunk -> crc)
   std::map<LayerID, std::pair<int64_t, std::map<int64_t, uint32_t>>> partial_crc_;

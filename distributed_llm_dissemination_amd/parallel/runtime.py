@@ -146,6 +146,10 @@ class Runtime:
                                  f"(2 bytes x {pack_block}-element scale blocks); layers {sorted(bad)[:8]} are not")
         self.epoch = 0
         self.keep: List[object] = []  # buffers that must outlive sessions
+        # Closed-loop link rates (planned engines): EWMA of this rank's measured
+        # send rate to each peer node (B/s), reported with its announce.
+        self.link_est: Dict[int, float] = {}
+        self._links0: Optional[Dict[str, Dict[int, float]]] = None
 
         reg = dict(registry) if registry is not None else cfg.registry()
         if transport == "inproc":
@@ -509,6 +513,7 @@ class Runtime:
         stage_gbps: Optional[float] = None,
         link_bw: Optional[Dict[tuple, int]] = None,
         hbm_gbps: Optional[float] = None,
+        adapt_links: bool = True,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed).
 
@@ -518,11 +523,17 @@ class Runtime:
         ``stage_gbps`` (default PCIE_PLAN_GBPS). ``link_bw`` overrides both the
         config's Links and the probe (e.g. per-link rates measured in an earlier
         session). ``hbm_gbps`` is every GPU's HBM ingress budget in the mode-3
-        graph (default HBM_PLAN_GBPS on rccl, unlimited elsewhere)."""
+        graph (default HBM_PLAN_GBPS on rccl, unlimited elsewhere).
+
+        ``adapt_links`` (closed loop): this rank announces its measured send
+        rate to each peer (``link_report``: EWMA over earlier sessions and the
+        pre-flight probe), and the leader plans on every rank's reports in place
+        of the estimates above."""
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()
             self._stats0 = self._engine_stats()
+            self._links0 = self.link_stats()
         nc = _core.NodeConfig()
         nc.id = self.node_id
         nc.leader = self.cfg.leader().id
@@ -550,6 +561,9 @@ class Runtime:
             hbm_gbps = self.HBM_PLAN_GBPS if gpu else 0.0
         if hbm_gbps > 0:
             nc.hbm_bw = {n.id: int(hbm_gbps * 1e9) for n in self.cfg.nodes}
+        nc.adapt_links = adapt_links
+        if adapt_links:
+            nc.link_report = self.link_report()
         nc.integer_seconds = integer_seconds
         nc.job_timeout_s = job_timeout_s
         nc.job_min_rate = job_min_rate
@@ -610,10 +624,55 @@ class Runtime:
                 delta = [a - b for a, b in zip(now[h], self._stats0[h])]
                 for q in (0.5, 0.99):
                     res.engine_stats[f"{h[:-8]}_p{int(q * 100)}_us"] = hist_quantile(delta, q)
+        if self.engine is not None and ok:
+            self._observe_session_links()
         if ok:
             node.stop()
         self._last_node = node  # on failure keep it alive for inspection
         return res
+
+    # ------------------------------------------------- closed-loop link rates
+    LINK_EWMA_ALPHA = 0.5   # weight of the newest measurement
+    LINK_SNAP = 0.15        # reports within this fraction of the median are reported as the median
+    LINK_MIN_CHUNKS = 4     # a link must have carried this many grid chunks in a session to be measured
+
+    def observe_links(self, rates: Dict[int, float]) -> None:
+        """Fold measured send rates (peer node -> B/s) into the per-link EWMA."""
+        a = self.LINK_EWMA_ALPHA
+        for p, r in rates.items():
+            if r is None or r <= 0 or p == self.node_id:
+                continue
+            old = self.link_est.get(p)
+            self.link_est[p] = float(r) if old is None else old + a * (float(r) - old)
+
+    def _observe_session_links(self) -> None:
+        """After a session: this rank's bytes to each peer over the device time of
+        the P2P groups that carried them (per directed link busy throughput)."""
+        if self._links0 is None:
+            return
+        now = self.link_stats()
+        rates = {}
+        for p, b in now["sent"].items():
+            db = b - self._links0["sent"].get(p, 0)
+            dms = now["send_busy_ms"].get(p, 0.0) - self._links0["send_busy_ms"].get(p, 0.0)
+            if db >= self.LINK_MIN_CHUNKS * self.grid and dms > 0:
+                rates[self.node_ids[p]] = db / (dms / 1e3)
+        self.observe_links(rates)
+
+    def link_report(self) -> Dict[int, int]:
+        """What this rank announces: its EWMA rates, with every rate within
+        LINK_SNAP of the median replaced by the median - a uniform fabric's noise
+        must not reshape the plan from one session to the next, a slow link must."""
+        if not self.link_est:
+            return {}
+        vals = sorted(self.link_est.values())
+        med = vals[len(vals) // 2]
+        return {p: int(med if abs(r - med) <= self.LINK_SNAP * med else r) for p, r in self.link_est.items()}
+
+    def plan_link_bw(self) -> Dict[tuple, int]:
+        """Leader: the per directed link rates (B/s) its last plan used."""
+        node = getattr(self, "_last_node", None) or getattr(self, "_node", None)
+        return dict(node.plan_link_bw()) if node is not None and self.is_leader else {}
 
     def _engine_stats(self) -> Dict[str, float]:
         es = self.engine.stats()
@@ -704,6 +763,7 @@ class Runtime:
         of the P2P groups that involved the peer; per-lane device time."""
         es = self.engine.stats()
         return {"sent": dict(es.peer_sent), "recv": dict(es.peer_recv), "busy_ms": dict(es.peer_busy_ms),
+                "send_busy_ms": dict(es.peer_send_busy_ms),
                 "lane_busy_ms": list(es.lane_busy_ms)}
 
     def layer_bytes(self, layer: int) -> bytes:

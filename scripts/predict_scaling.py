@@ -39,7 +39,8 @@ _n = [0]
 def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
-            slowdown: float = 1.0, tier: str = "host", pack: str = "none") -> dict:
+            slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
+            adapt_links: bool = True) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -47,9 +48,25 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     and every GPU's staging rate, at the simulated (scaled) rates: mode 1 with
     owner_policy "links" can relay around a slow link, and mode 3 plans - and
     paces its jobs at size/T - with the rates the fabric will deliver.
+    plan_link_gbps: with plan_links, the rate the plan assumes for the links
+    (default: the simulated one) - e.g. a constant estimate the real fabric beats.
+    adapt_links: every session after the first plans on the link rates the ranks
+    measured in the earlier ones (closed loop, Runtime.link_report).
     slowdown: run every rate this many times slower and divide the measured time
     by it (keeps the simulator's own per-op thread overhead small next to the
     modeled transfer times)."""
+    plan_link_gbps = (plan_link_gbps if plan_link_gbps is not None else link_gbps) / slowdown
+    level = _core.log_level()
+    _core.set_log_level(3)  # per-event JSON lines on stderr would be part of the timed sessions
+    try:
+        return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
+                        seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links)
+    finally:
+        _core.set_log_level(level)
+
+
+def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
+             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -65,7 +82,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     cfg = make_workload(n, layers, lb, tier=tier, seeding=seeding, chunk_bytes=cb)
     if plan_links:
         # the plan's rates are the simulated ones (scaled): mode 3 paces jobs at size/T
-        bw = int(link_gbps * 1e9 / scale)
+        bw = int(plan_link_gbps * 1e9 / scale)
         cfg.links = {s: {d: bw for d in range(n) if d != s} for s in range(n)}
         if slow_link is not None:
             (s, d), frac = slow_link
@@ -75,13 +92,14 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
         r.transport.set_registry(reg)
-    times = []
+    times, flow_Ts = [], []
     flow_T = 0.0
+    plan_links_used = {}
     try:
         for _ in range(steps):
             for r in rts:
                 extra = {"stage_gbps": pcie_gbps / scale} if plan_links else {}
-                r.prepare(mode, **{"pull_window": max(1, n - 1), **extra, **(policy or {})})
+                r.prepare(mode, **{"pull_window": max(1, n - 1), "adapt_links": adapt_links, **extra, **(policy or {})})
             res = [None] * n
 
             def go(i):
@@ -97,6 +115,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             if not all(x.ok for x in res):
                 raise RuntimeError([x.error for x in res if not x.ok])
             flow_T = res[0].flow_T
+            flow_Ts.append(flow_T)
+            plan_links_used = rts[0].plan_link_bw()
         lanes_used = rts[0].engine.stats().lanes
     finally:
         for r in rts:
@@ -107,6 +127,10 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             **({"pack": pack, "layers": layers, "layer_MiB": layer_bytes >> 20} if pack != "none" else {}),
             "seeding": seeding, **({"policy": policy} if policy else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
+            "times_ms": [round(x / slowdown * 1e3, 1) for x in times],
+            **({"flow_T_ms": [round(x / slowdown * 1e3, 1) for x in flow_Ts]} if any(flow_Ts) else {}),
+            **({"plan_link_GBps_last": {f"{a}->{b}": round(v * scale * slowdown / 1e9, 1)
+                                        for (a, b), v in sorted(plan_links_used.items())}} if plan_links_used else {}),
             "value_GBps": round(total / sec / 1e9, 1), "scale": scale,
             **({"planned_T_ms": round(flow_T * 1e3 / slowdown, 1)} if flow_T > 0 else {})}
 
