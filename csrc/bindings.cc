@@ -16,6 +16,7 @@
 #include "engine/planned_engine.h"
 #include "gpu/gpu_api.h"
 #include "roles/node.h"
+#include "sched/lp.h"
 #include "sched/maxflow.h"
 #include "store/store.h"
 #include "transport/transport.h"
@@ -268,7 +269,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("lanes", &PlannedConfig::lanes)
       .def_readwrite("unpack_store", &PlannedConfig::unpack_store)
       .def_readwrite("link_rate", &PlannedConfig::link_rate)
-      .def_readwrite("comm_init", &PlannedConfig::comm_init);
+      .def_readwrite("comm_init", &PlannedConfig::comm_init)
+      .def_readwrite("node_disk_rate", &PlannedConfig::node_disk_rate)
+      .def_readwrite("node_disk_key", &PlannedConfig::node_disk_key);
   m.def("resolve_lanes", [](int world, int lanes) {
     PlannedConfig c;
     c.world = world;
@@ -302,6 +305,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("comm_connect_ms", &PlannedStats::comm_connect_ms)
       .def_readonly("comm_reform_ms", &PlannedStats::comm_reform_ms)
       .def_readonly("paced", &PlannedStats::paced)
+      .def_readonly("disk_wait_ms", &PlannedStats::disk_wait_ms)
       .def_readonly("order_violations", &PlannedStats::order_violations);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
@@ -451,7 +455,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("job_min_rate", &NodeConfig::job_min_rate)
       .def_readwrite("max_redispatch", &NodeConfig::max_redispatch)
       .def_readwrite("link_report", &NodeConfig::link_report)
-      .def_readwrite("adapt_links", &NodeConfig::adapt_links);
+      .def_readwrite("adapt_links", &NodeConfig::adapt_links)
+      .def_readwrite("disk_group", &NodeConfig::disk_group)
+      .def_readwrite("disk_group_bw", &NodeConfig::disk_group_bw);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)
@@ -533,14 +539,22 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("max_flow", &FlowPlan::max_flow)
       .def_readonly("solves", &FlowPlan::solves)
       .def_readonly("feasible", &FlowPlan::feasible)
+      .def_readonly("solver", &FlowPlan::solver)
+      .def_readonly("lp_pivots", &FlowPlan::lp_pivots)
       .def_readonly("jobs", &FlowPlan::jobs);
   m.def("solve_flow", [](const std::map<NodeID, LayerIDs>& holdings,
                          const std::vector<std::tuple<LayerID, NodeID, int64_t>>& demands,
                          const std::map<NodeID, int64_t>& egress, const std::map<NodeID, int64_t>& ingress,
                          const std::map<std::pair<NodeID, NodeID>, int64_t>& links, int64_t align,
-                         bool integer_seconds, bool allow_self, const std::map<NodeID, int64_t>& stage) {
+                         bool integer_seconds, bool allow_self, const std::map<NodeID, int64_t>& stage,
+                         bool stage_once, const std::map<NodeID, int>& disk_group,
+                         const std::map<int, int64_t>& disk_group_bps, const std::string& solver) {
     FlowProblem p;
     p.stage_bps = stage;
+    p.stage_once = stage_once;
+    p.disk_group = disk_group;
+    p.disk_group_bps = disk_group_bps;
+    p.solver = solver;
     p.holdings = holdings;
     for (auto& d : demands) p.demands.push_back({std::get<0>(d), std::get<1>(d), std::get<2>(d)});
     p.egress_bps = egress;
@@ -555,7 +569,22 @@ PYBIND11_MODULE(_core, m) {
      py::arg("ingress") = std::map<NodeID, int64_t>{},
      py::arg("links") = std::map<std::pair<NodeID, NodeID>, int64_t>{}, py::arg("align") = 1,
      py::arg("integer_seconds") = false, py::arg("allow_self") = false,
-     py::arg("stage") = std::map<NodeID, int64_t>{});
+     py::arg("stage") = std::map<NodeID, int64_t>{}, py::arg("stage_once") = false,
+     py::arg("disk_group") = std::map<NodeID, int>{}, py::arg("disk_group_bps") = std::map<int, int64_t>{},
+     py::arg("solver") = "auto");
+
+  // Dense two-phase simplex (sched/lp.h); rows as lists of ((col, coef) pairs, rhs).
+  m.def("solve_lp", [](int n, const std::vector<double>& c,
+                       const std::vector<std::pair<std::vector<std::pair<int, double>>, double>>& eq,
+                       const std::vector<std::pair<std::vector<std::pair<int, double>>, double>>& le) {
+    LpProblem p;
+    p.n = n;
+    p.c = c;
+    for (auto& r : eq) p.eq.push_back(LpRow{r.first, r.second});
+    for (auto& r : le) p.le.push_back(LpRow{r.first, r.second});
+    LpResult r = solve_lp(p);
+    return py::make_tuple(r.ok, r.status, r.obj, r.x, r.pivots);
+  }, py::arg("n"), py::arg("c"), py::arg("eq"), py::arg("le"));
 
   py::class_<RangeSet>(m, "RangeSet")
       .def(py::init<>())

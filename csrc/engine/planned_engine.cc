@@ -111,6 +111,10 @@ void PlannedEngine::shutdown() {
   readers_.clear();
   idle_cv_.notify_all();
   backend_->sync_all();
+  if (pacer_) {
+    pacer_.reset();
+    NodePacer::unlink(cfg_.node_disk_key.empty() ? "default" : cfg_.node_disk_key);
+  }
   for (auto* b : bounce_all_) backend_->free_host(b);
   bounce_all_.clear();
   bounce_free_.clear();
@@ -584,6 +588,9 @@ void PlannedEngine::stage_chunk(Layer& L, LayerID id, int64_t c) {
 
 void PlannedEngine::submit_disk(Layer& L, LayerID id, int64_t c) {
   if (readers_.empty()) {
+    if (cfg_.node_disk_rate > 0 && !pacer_)
+      pacer_ = std::make_unique<NodePacer>(cfg_.node_disk_key.empty() ? "default" : cfg_.node_disk_key,
+                                           cfg_.node_disk_rate);
     for (int i = 0; i < std::max(1, cfg_.disk_ring); ++i) {
       uint8_t* b = backend_->alloc_host(cfg_.chunk_bytes);
       bounce_all_.push_back(b);
@@ -603,6 +610,17 @@ void PlannedEngine::submit_disk(Layer& L, LayerID id, int64_t c) {
 }
 
 void PlannedEngine::pump_disk() {
+  // Buffers whose H2D copy landed go back to the ring.
+  for (auto it = bounce_busy_.begin(); it != bounce_busy_.end();) {
+    const int r = backend_->query(it->first);
+    if (r == 0) {
+      ++it;
+      continue;
+    }
+    ev_drop(it->first);
+    bounce_free_.push_back(it->second);
+    it = bounce_busy_.erase(it);
+  }
   // Hand waiting reads to the readers while bounce buffers are free.
   while (!disk_wait_.empty() && !bounce_free_.empty()) {
     DiskRead d = std::move(disk_wait_.front());
@@ -651,6 +669,11 @@ void PlannedEngine::reader_loop() {
     }
     // O_DIRECT needs 4 KiB aligned lengths; the bounce buffer holds a whole chunk.
     const int64_t want = std::min<int64_t>(((d.len + 4095) / 4096) * 4096, cfg_.chunk_bytes);
+    if (pacer_) {  // the node's one NVMe: wait for this read's slot in the shared budget
+      const int64_t w = pacer_->acquire(want);
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      stats_.disk_wait_ms += double(w) / 1e6;
+    }
     int64_t got = 0;
     while (fd >= 0 && got < d.len) {
       ssize_t r = ::pread(fd, d.bounce + got, size_t(want - got), off_t(d.file_off + got));
@@ -703,8 +726,15 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
     v.slots.push_back(~0u);
   }
   v.pieces.push_back(p);
-  v.bounce = bounce;
   verifies_.push_back(std::move(v));
+  if (bounce) {
+    // The bounce buffer is free again once its H2D copy has landed - not after
+    // the chunk's CRC check: the verify queue is in order, and a check queued
+    // behind a recv that waits on a peer (whose send may wait on a disk read of
+    // its own) would hold every buffer of the ring - two ranks deadlock.
+    ev_hold(e);
+    bounce_busy_.push_back({e, bounce});
+  }
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.bytes_staged += slen;
 }
@@ -1103,6 +1133,32 @@ std::vector<int> PlannedEngine::inflight_peers() const {
   return peers;
 }
 
+std::string PlannedEngine::describe_stall() const {
+  // What each lane is waiting for (the stall report's detail): its in-flight
+  // groups, the piece at the head of its queue and that chunk's state.
+  std::string out;
+  char buf[256];
+  for (int l = 0; l < lanes_; ++l) {
+    const auto& q = ops_[size_t(l)];
+    if (q.empty() && inflight_[size_t(l)].empty()) continue;
+    snprintf(buf, sizeof buf, "lane %d: %zu in flight, %zu queued", l, inflight_[size_t(l)].size(), q.size());
+    out += buf;
+    if (!q.empty()) {
+      const Piece& p = q.front();
+      auto it = layers_.find(p.layer);
+      const int st = it != layers_.end() && p.chunk < int64_t(it->second.st.size()) ? it->second.st[size_t(p.chunk)] : -1;
+      snprintf(buf, sizeof buf, "; head %s peer %d layer %llu chunk %lld key (%llu,%lld,%llu) chunk state %d",
+               p.kind == Kind::Send ? "send" : "recv", p.peer, (unsigned long long)p.layer, (long long)p.chunk,
+               (unsigned long long)p.batch, (long long)p.pidx, (unsigned long long)p.seq, st);
+      out += buf;
+    }
+    out += " | ";
+  }
+  snprintf(buf, sizeof buf, "verifies %zu, disk: %zu waiting for a buffer, %d reading, %zu buffers free",
+           verifies_.size(), disk_wait_.size(), disk_inflight_, bounce_free_.size());
+  return out + buf;
+}
+
 void PlannedEngine::suspect(const std::vector<int>& peers, const std::string& why, bool broken) {
   if (broken && !recovering_) {
     recovering_ = true;  // the communicator is unusable until the Shrink
@@ -1112,7 +1168,7 @@ void PlannedEngine::suspect(const std::vector<int>& peers, const std::string& wh
   m.type = MsgType::Suspect;
   for (int r : peers)
     if (r != cfg_.rank) m.peers.push_back(cfg_.rank_nodes[size_t(r)]);
-  log::warn(int64_t(self_node_)).s("why", why).i("peers", int64_t(m.peers.size()))
+  log::warn(int64_t(self_node_)).s("why", why).i("peers", int64_t(m.peers.size())).s("state", describe_stall())
       .msg("data plane stalled: reporting suspect peers to the leader");
   trace::mark("dissem.suspect");
   {
@@ -1149,9 +1205,13 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
   for (auto& v : verifies_) {
     aborted += int64_t(v.pieces.size());
     backend_->release(v.ev);
-    if (v.bounce) bounce_free_.push_back(v.bounce);
   }
   verifies_.clear();
+  for (auto& b : bounce_busy_) {  // every queue drained in the backend's shrink: the copies are done
+    ev_drop(b.first);
+    bounce_free_.push_back(b.second);
+  }
+  bounce_busy_.clear();
   for (auto& q : ops_) q.clear();
   restage_.clear();
   local_wait_.clear();
@@ -1294,7 +1354,6 @@ void PlannedEngine::poll() {
       stats_.land_us_hist[log2_bucket(it->t0)] += int64_t(it->pieces.size());
     }
     backend_->release(it->ev);
-    if (it->bounce) bounce_free_.push_back(it->bounce);
     it = verifies_.erase(it);
   }
   for (auto& v : followups) verifies_.push_back(std::move(v));

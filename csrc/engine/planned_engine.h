@@ -44,6 +44,7 @@
 
 #include "engine/backend.h"
 #include "engine/engine.h"
+#include "engine/node_pacer.h"
 #include "store/store.h"
 
 namespace dissem {
@@ -71,6 +72,11 @@ struct PlannedConfig {
   int group_peers = 1;             // ops per peer and direction per group
   int disk_readers = 4;            // NVMe reader threads (O_DIRECT pread into pinned bounce buffers)
   int disk_ring = 8;               // pinned bounce buffers of chunk_bytes each
+  // One NVMe shared by every rank of the node: > 0 paces this rank's disk
+  // reads through a node-wide budget of this many B/s (engine/node_pacer.h),
+  // shared by every process that uses the same node_disk_key.
+  int64_t node_disk_rate = 0;
+  std::string node_disk_key;
   // fp8 wire/storage format (core/fp8.h): layers are staged from bf16 sources
   // and packed on the copy queue; HBM slots, transfers and CRCs use the packed
   // chunk grid. chunk_bytes stays the SOURCE (bf16) chunk.
@@ -139,6 +145,7 @@ struct PlannedStats {
   double comm_init_ms = 0, comm_connect_ms = 0;
   double comm_reform_ms = 0;  // last elastic re-form (abort + re-init after a shrink)
   int64_t paced = 0;  // issue attempts a token bucket deferred
+  double disk_wait_ms = 0;  // time disk reads waited for the node-wide read budget
   int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
   std::vector<int64_t> group_us_hist = std::vector<int64_t>(32, 0);  // P2P group issue -> complete
@@ -258,7 +265,6 @@ class PlannedEngine : public DataEngine {
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     std::vector<Piece> pieces;
     std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
-    uint8_t* bounce = nullptr;    // disk staging buffer to recycle once landed
   };
   struct DiskRead {  // chunk of a disk-tier layer: pread into a bounce buffer, then H2D
     LayerID layer;
@@ -306,7 +312,8 @@ class PlannedEngine : public DataEngine {
       if (!q.empty()) return false;
     for (auto& q : inflight_)
       if (!q.empty()) return false;
-    return verifies_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty();
+    return verifies_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty() &&
+           bounce_busy_.empty();
   }
   int lane_for(int peer, bool send) const {
     return send ? lane_of(cfg_.rank, peer, cfg_.world, lanes_) : lane_of(peer, cfg_.rank, cfg_.world, lanes_);
@@ -325,6 +332,7 @@ class PlannedEngine : public DataEngine {
   // broken: the communicator failed (stop issuing) rather than merely stalled.
   void suspect(const std::vector<int>& peers, const std::string& why, bool broken);
   std::vector<int> inflight_peers() const;
+  std::string describe_stall() const;
   void do_shrink(const std::vector<NodeID>& dead, uint64_t generation, const std::string& comm_id);
   void die();  // fault injection
   Layer& layer(LayerID id, int64_t size_hint = 0);
@@ -383,12 +391,14 @@ class PlannedEngine : public DataEngine {
 
   // disk tier: issue thread owns bounce_free_/disk_wait_; readers exchange via disk_mu_
   std::vector<uint8_t*> bounce_all_, bounce_free_;
+  std::deque<std::pair<Ev, uint8_t*>> bounce_busy_;  // H2D copy event -> its bounce buffer
   std::deque<DiskRead> disk_wait_;                 // waiting for a bounce buffer
   std::mutex disk_mu_;
   std::condition_variable disk_cv_;
   std::deque<DiskRead> disk_todo_, disk_done_;
   std::vector<std::thread> readers_;
   int disk_inflight_ = 0;
+  std::unique_ptr<NodePacer> pacer_;  // node-shared disk budget (node_disk_rate > 0)
 
   std::mutex stats_mu_;
   PlannedStats stats_;

@@ -1521,11 +1521,23 @@ void Node::schedule_mode3() {
   p.stage_bps = cfg_.stage_bw;
   p.align = cfg_.align;
   p.integer_seconds = cfg_.integer_seconds;
+  p.disk_group = cfg_.disk_group;
+  p.disk_group_bps = cfg_.disk_group_bw;
+  if (e_->planned()) {
+    // GPU data plane: a layer is loaded into HBM once and forwarded from there;
+    // a self-job's load feeds the dest's own sends of that layer too.
+    p.stage_once = true;
+    for (auto& sj : self_jobs) {
+      auto st = status_[sj.dest].find(sj.layer);
+      if (st != status_[sj.dest].end() && st->second.source_type != SourceType::Device)
+        p.self_loads[sj.dest][sj.layer] = sj.size;
+    }
+  }
   log::info(int64_t(cfg_.id)).msg("assigning a job...");
   int64_t t0 = log::now_us();
   FlowPlan plan = solve_flow(p);
   log::info(int64_t(cfg_.id)).f("computation time[ms]", double(log::now_us() - t0) / 1e3).i("solves", plan.solves)
-      .msg("Job assignment completed");
+      .s("solver", plan.solver).i("lp_pivots", plan.lp_pivots).msg("Job assignment completed");
   log::info(int64_t(cfg_.id)).f("required minimum time(s)", plan.T).b("feasible", plan.feasible)
       .msg("job assignment calculated");
   {

@@ -59,6 +59,11 @@ struct NodeConfig {
   // choice (reference: node.go:774-793 measures job times, :1044-1053 uses them).
   std::map<NodeID, int64_t> link_report;
   bool adapt_links = true;
+  // Nodes whose disk tiers read one shared device (all ranks of one MI355X
+  // node share its NVMe): node -> group, group -> read rate (B/s). Mode 3 plans
+  // the group as one budget (sched/maxflow.h).
+  std::map<NodeID, int> disk_group;
+  std::map<int, int64_t> disk_group_bw;
 };
 
 struct NodeStats {

@@ -2,12 +2,15 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <queue>
 #include <set>
 #include <tuple>
 
 #include "core/trace.h"
+#include "sched/lp.h"
 
 namespace dissem {
 
@@ -185,8 +188,12 @@ Built build(const FlowProblem& p, double T) {
     }
   for (auto& kv : vst) {
     const NodeID s = kv.first.first;
-    const int parent = kv.first.second == kDevice ? vs[s] : vstage[s];
-    d.add(parent, kv.second, cap_for(tier_rate[kv.first], T));
+    const bool dev = kv.first.second == kDevice;
+    const int parent = dev ? vs[s] : vstage[s];
+    int64_t r = tier_rate[kv.first];
+    if (p.stage_once && !dev && r > 0 && layer_bytes[s] > 0)  // read once, forwarded to every dest
+      r = int64_t(double(r) * std::max(1.0, cand_bytes[s] / layer_bytes[s]));
+    d.add(parent, kv.second, cap_for(r, T));
   }
   for (auto& kv : vlink) {
     const NodeID s = std::get<0>(kv.first), dst = std::get<2>(kv.first);
@@ -226,7 +233,321 @@ int64_t required_bytes(const FlowProblem& p) {
   return r;
 }
 
+// Layers with the same holders (and tiers) and the same demands (dest, bytes):
+// one LP class. Its demand per dest is the sum over its layers, and an LP
+// solution splits back onto the layers in equal shares - exact, as every
+// layer of a class has the same constraints.
+struct LpClass {
+  std::vector<std::pair<NodeID, int>> holders;   // (sender, tier)
+  std::vector<std::pair<NodeID, int64_t>> dests; // (dest, bytes per layer)
+  std::vector<std::pair<NodeID, int64_t>> self;  // holders that load it for themselves (bytes per layer)
+  std::vector<LayerID> layers;
+};
+
+std::vector<LpClass> lp_classes(const FlowProblem& p) {
+  std::map<LayerID, std::vector<std::pair<NodeID, int>>> holders;
+  for (auto& hs : p.holdings)
+    for (auto& lm : hs.second) holders[lm.first].push_back({hs.first, int(lm.second.source_type)});
+  std::map<LayerID, std::map<NodeID, int64_t>> dem;  // layer -> dest -> bytes
+  for (auto& dm : p.demands) {
+    int64_t& z = dem[dm.layer][dm.dest];
+    z = std::max(z, dm.size);
+  }
+  std::map<LayerID, std::map<NodeID, int64_t>> selfl;  // layer -> loading holder -> bytes
+  for (auto& kv : p.self_loads)
+    for (auto& ls : kv.second) selfl[ls.first][kv.first] = ls.second;
+  using Key = std::tuple<std::vector<std::pair<NodeID, int>>, std::vector<std::pair<NodeID, int64_t>>,
+                         std::vector<std::pair<NodeID, int64_t>>>;
+  std::map<Key, size_t> index;
+  std::vector<LpClass> out;
+  for (auto& kv : selfl) dem[kv.first];  // a layer only its holders load still draws on their budgets
+  for (auto& kv : dem) {
+    auto h = holders[kv.first];
+    std::sort(h.begin(), h.end());
+    std::vector<std::pair<NodeID, int64_t>> ds(kv.second.begin(), kv.second.end());
+    std::vector<std::pair<NodeID, int64_t>> sl;
+    if (auto it = selfl.find(kv.first); it != selfl.end()) sl.assign(it->second.begin(), it->second.end());
+    Key key{h, ds, sl};
+    auto it = index.find(key);
+    if (it == index.end()) {
+      it = index.emplace(key, out.size()).first;
+      out.push_back(LpClass{h, ds, sl, {}});
+    }
+    out[it->second].layers.push_back(kv.first);
+  }
+  return out;
+}
+
+// Byte counts per (sender, layer, dest) -> ranges: per demand, aligned sizes
+// (remainder to the biggest), offsets in sender order, so a sender that serves
+// one layer to several dests sends each of them the same region where it can.
+void extract_jobs(std::map<std::pair<LayerID, NodeID>, std::vector<FlowJob>>& per_demand, int64_t align,
+                  FlowPlan& plan) {
+  for (auto& kv : per_demand) {
+    auto& jobs = kv.second;
+    if (align > 1 && jobs.size() > 1) {
+      int64_t total = 0;
+      for (auto& j : jobs) total += j.size;
+      int64_t acc = 0;
+      size_t biggest = 0;
+      for (size_t i = 0; i < jobs.size(); ++i) {
+        jobs[i].size = (jobs[i].size / align) * align;
+        acc += jobs[i].size;
+        if (jobs[i].size > jobs[biggest].size) biggest = i;
+      }
+      jobs[biggest].size += total - acc;
+      jobs.erase(std::remove_if(jobs.begin(), jobs.end(), [](const FlowJob& j) { return j.size <= 0; }), jobs.end());
+    }
+    int64_t off = 0;  // ranges partition the layer, senders in id order
+    for (auto& j : jobs) {
+      j.offset = off;
+      off += j.size;
+      plan.jobs.push_back(j);
+    }
+  }
+}
+
+FlowPlan solve_flow_lp(const FlowProblem& p) {
+  trace::Scoped tr("dissem.plan_lp");
+  FlowPlan plan;
+  plan.solver = "lp";
+  plan.required = required_bytes(p);
+  const int kDevice = int(SourceType::Device), kDisk = int(SourceType::Disk);
+  const auto classes = lp_classes(p);
+  // Scale: bytes by the largest class, rates by the largest rate -> O(1) coefficients.
+  double B0 = 1, R0 = 1;
+  for (auto& c : classes)
+    for (auto& d : c.dests) B0 = std::max(B0, double(d.second) * double(c.layers.size()));
+  auto upd = [&](int64_t r) {
+    if (r > 0) R0 = std::max(R0, double(r));
+  };
+  for (auto& kv : p.egress_bps) upd(kv.second);
+  for (auto& kv : p.ingress_bps) upd(kv.second);
+  for (auto& kv : p.link_bps) upd(kv.second);
+  for (auto& kv : p.stage_bps) upd(kv.second);
+  for (auto& kv : p.disk_group_bps) upd(kv.second);
+  for (auto& hs : p.holdings)
+    for (auto& lm : hs.second) upd(lm.second.limit_rate);
+  LpProblem lp;
+  lp.n = 1;  // column 0 = T (scaled)
+  struct X {
+    size_t c;
+    NodeID s;
+    int t;
+    NodeID d;
+    int col;
+  };
+  std::vector<X> xs;
+  std::map<std::pair<size_t, NodeID>, int> ycol;  // (class, sender) -> y column
+  for (size_t ci = 0; ci < classes.size(); ++ci) {
+    const LpClass& c = classes[ci];
+    for (auto& dz : c.dests) {
+      const NodeID d = dz.first;
+      LpRow dem;
+      dem.b = double(dz.second) * double(c.layers.size()) / B0;
+      for (auto& h : c.holders) {
+        if (h.first == d && !p.allow_self) continue;
+        xs.push_back(X{ci, h.first, h.second, d, lp.n});
+        dem.a.push_back({lp.n++, 1.0});
+      }
+      if (dem.a.empty()) return plan;  // a demand nobody can serve
+      lp.eq.push_back(dem);
+    }
+    // y = bytes of the class a sender loads into HBM (staged once, forwarded to
+    // every dest): the staging budget always charges y; tier rates and disk
+    // groups charge it with stage_once, else every transfer re-reads.
+    for (auto& h : c.holders) {
+      auto st = p.stage_bps.find(h.first);
+      if (h.second != kDevice && (p.stage_once || (st != p.stage_bps.end() && st->second > 0)))
+        ycol[{ci, h.first}] = lp.n++;
+    }
+    // A holder that also loads the layer for itself loads all of it: y >= its bytes
+    // (as an equality with a surplus column: y - surplus = bytes).
+    for (auto& sl : c.self) {
+      auto y = ycol.find({ci, sl.first});
+      if (y == ycol.end()) continue;
+      LpRow r;
+      r.a = {{y->second, 1.0}, {lp.n++, -1.0}};
+      r.b = double(sl.second) * double(c.layers.size()) / B0;
+      lp.eq.push_back(r);
+    }
+  }
+  lp.c.assign(size_t(lp.n), 0.0);
+  lp.c[0] = 1.0;
+  // x - y <= 0: what a sender forwards of a class to any one dest it must have loaded
+  for (size_t i = 0; i < xs.size(); ++i) {
+    auto y = ycol.find({xs[i].c, xs[i].s});
+    if (y == ycol.end()) continue;
+    LpRow r;
+    r.a = {{xs[i].col, 1.0}, {y->second, -1.0}};
+    lp.le.push_back(r);
+  }
+  auto budget = [&](int64_t rate, const std::vector<std::pair<int, double>>& cols) {
+    if (rate <= 0 || cols.empty()) return;
+    LpRow r;
+    std::map<int, double> merged;
+    for (auto& e : cols) merged[e.first] += e.second;
+    for (auto& e : merged) r.a.push_back(e);
+    r.a.push_back({0, -double(rate) / R0});
+    lp.le.push_back(r);
+  };
+  auto rate_of = [](const std::map<NodeID, int64_t>& m, NodeID k) {
+    auto it = m.find(k);
+    return it == m.end() ? int64_t(0) : it->second;
+  };
+  std::map<NodeID, std::vector<std::pair<int, double>>> egress, ingress, stage;
+  std::map<std::pair<NodeID, NodeID>, std::vector<std::pair<int, double>>> link;
+  std::map<std::pair<NodeID, int>, std::vector<std::pair<int, double>>> tier;
+  std::map<int, std::vector<std::pair<int, double>>> group;
+  for (size_t i = 0; i < xs.size(); ++i) {
+    const X& x = xs[i];
+    const int col = x.col;
+    egress[x.s].push_back({col, 1.0});
+    ingress[x.d].push_back({col, 1.0});
+    if (x.s != x.d) link[{x.s, x.d}].push_back({col, 1.0});
+    const bool y = ycol.count({x.c, x.s}) > 0;
+    if (!y || !p.stage_once) {  // read per transfer
+      tier[{x.s, x.t}].push_back({col, 1.0});
+      auto g = p.disk_group.find(x.s);
+      if (x.t == kDisk && g != p.disk_group.end()) group[g->second].push_back({col, 1.0});
+    }
+    if (!y && x.t != kDevice) stage[x.s].push_back({col, 1.0});
+  }
+  for (auto& kv : ycol) {
+    const size_t ci = kv.first.first;
+    const NodeID s = kv.first.second;
+    int t = kDevice;
+    for (auto& h : classes[ci].holders)
+      if (h.first == s) t = h.second;
+    stage[s].push_back({kv.second, 1.0});
+    if (p.stage_once) {  // read once
+      tier[{s, t}].push_back({kv.second, 1.0});
+      auto g = p.disk_group.find(s);
+      if (t == kDisk && g != p.disk_group.end()) group[g->second].push_back({kv.second, 1.0});
+    }
+  }
+  for (auto& kv : egress) budget(rate_of(p.egress_bps, kv.first), kv.second);
+  for (auto& kv : ingress) budget(rate_of(p.ingress_bps, kv.first), kv.second);
+  for (auto& kv : stage) budget(rate_of(p.stage_bps, kv.first), kv.second);
+  for (auto& kv : link) {
+    auto it = p.link_bps.find(kv.first);
+    if (it != p.link_bps.end()) budget(it->second, kv.second);
+  }
+  // tier rate: the tier's configured rate (its layers share one device; 0 = unlimited wins)
+  std::map<std::pair<NodeID, int>, int64_t> tier_rate;
+  for (auto& hs : p.holdings)
+    for (auto& lm : hs.second) {
+      auto key = std::make_pair(hs.first, int(lm.second.source_type));
+      const int64_t r = lm.second.limit_rate;
+      auto it = tier_rate.find(key);
+      if (it == tier_rate.end()) tier_rate[key] = r;
+      else if (it->second > 0 && (r <= 0 || r > it->second)) it->second = r;
+    }
+  for (auto& kv : tier) budget(tier_rate[kv.first], kv.second);
+  for (auto& kv : group) {
+    auto it = p.disk_group_bps.find(kv.first);
+    if (it != p.disk_group_bps.end()) budget(it->second, kv.second);
+  }
+  LpResult r = solve_lp(lp);
+  if (getenv("DLD_LP_DUMP")) {
+    fprintf(stderr, "LP n=%d B0=%g R0=%g\n", lp.n, B0, R0);
+    for (auto& row : lp.eq) {
+      fprintf(stderr, "EQ");
+      for (auto& e : row.a) fprintf(stderr, " %d:%g", e.first, e.second);
+      fprintf(stderr, " = %g\n", row.b);
+    }
+    for (auto& row : lp.le) {
+      fprintf(stderr, "LE");
+      for (auto& e : row.a) fprintf(stderr, " %d:%g", e.first, e.second);
+      fprintf(stderr, " <= %g\n", row.b);
+    }
+    fprintf(stderr, "status %s obj %g\n", r.status.c_str(), r.obj);
+  }
+  plan.lp_pivots = r.pivots;
+  if (!r.ok) return plan;
+  double T = r.x[0] * B0 / R0;
+  if (p.integer_seconds) T = std::max(1.0, std::ceil(T - 1e-9));
+  plan.T = T;
+  plan.max_flow = plan.required;
+  plan.feasible = true;
+  plan.solves = 1;
+  // Class bytes back to layers (each layer of a class takes its share of every x).
+  std::map<std::pair<LayerID, NodeID>, std::vector<FlowJob>> per_demand;
+  for (size_t i = 0; i < xs.size(); ++i) {
+    const double bytes = r.x[size_t(xs[i].col)] * B0;
+    if (bytes <= 0.5) continue;
+    const LpClass& c = classes[xs[i].c];
+    for (LayerID l : c.layers)
+      per_demand[{l, xs[i].d}].push_back(FlowJob{xs[i].s, l, xs[i].d, int64_t(bytes / double(c.layers.size())), 0});
+  }
+  // Integer bytes: every demand's shares add up to its size exactly (remainder to the biggest share).
+  std::map<std::pair<LayerID, NodeID>, int64_t> dsize;
+  for (auto& dm : p.demands) dsize[{dm.layer, dm.dest}] = std::max(dsize[{dm.layer, dm.dest}], dm.size);
+  for (auto& kv : per_demand) {
+    auto& jobs = kv.second;
+    std::sort(jobs.begin(), jobs.end(), [](const FlowJob& a, const FlowJob& b) { return a.sender < b.sender; });
+    int64_t acc = 0;
+    size_t biggest = 0;
+    for (size_t i = 0; i < jobs.size(); ++i) {
+      acc += jobs[i].size;
+      if (jobs[i].size > jobs[biggest].size) biggest = i;
+    }
+    jobs[biggest].size += dsize[kv.first] - acc;
+  }
+  extract_jobs(per_demand, p.align, plan);
+  return plan;
+}
+
 }  // namespace
+
+bool needs_lp(const FlowProblem& p) {
+  if (p.solver == "lp") return true;
+  if (p.solver == "flow") return false;
+  const int kDevice = int(SourceType::Device), kDisk = int(SourceType::Disk);
+  std::map<LayerID, std::map<NodeID, int64_t>> dests;  // layer -> dest -> bytes
+  for (auto& dm : p.demands) {
+    int64_t& z = dests[dm.layer][dm.dest];
+    z = std::max(z, dm.size);
+  }
+  std::map<std::pair<NodeID, NodeID>, std::set<int>> sd_tiers;
+  std::map<NodeID, std::set<double>> fanouts;  // effective fan-out: bytes sent per byte loaded
+  std::map<NodeID, bool> tier_capped;  // a non-HBM tier with a finite rate
+  for (auto& hs : p.holdings)
+    for (auto& lm : hs.second) {
+      auto it = dests.find(lm.first);
+      if (it == dests.end()) continue;
+      const int t = int(lm.second.source_type);
+      int64_t sent = 0, loaded = 0;
+      for (auto& dz : it->second) {
+        if (dz.first == hs.first && !p.allow_self) continue;
+        sd_tiers[{hs.first, dz.first}].insert(t);
+        sent += dz.second;
+        loaded = std::max(loaded, dz.second);
+      }
+      if (loaded == 0) continue;
+      const double fan = std::round(double(sent) / double(loaded) * 1e9) / 1e9;
+      // a disk shared with other senders
+      if (t == kDisk && p.disk_group.count(hs.first) && p.disk_group_bps.count(p.disk_group.at(hs.first))) return true;
+      if (t != kDevice) {
+        fanouts[hs.first].insert(fan);
+        if (lm.second.limit_rate > 0) tier_capped[hs.first] = true;
+      }
+    }
+  if (!p.link_bps.empty())  // a directed link shared by several of a sender's tiers
+    for (auto& kv : sd_tiers)
+      if (kv.second.size() > 1) {
+        auto lk = p.link_bps.find(kv.first);
+        if (lk != p.link_bps.end() && lk->second > 0) return true;
+      }
+  // A load-once budget (staging; tier rates with stage_once) over layers with
+  // different fan-outs: the flow's fan-out scaling is exact only for one fan-out.
+  for (auto& kv : fanouts) {
+    if (kv.second.size() < 2) continue;
+    auto st = p.stage_bps.find(kv.first);
+    if ((st != p.stage_bps.end() && st->second > 0) || (p.stage_once && tier_capped[kv.first])) return true;
+  }
+  return false;
+}
 
 int64_t max_flow_at(const FlowProblem& p, double T) {
   Built b = build(p, T);
@@ -234,8 +555,10 @@ int64_t max_flow_at(const FlowProblem& p, double T) {
 }
 
 FlowPlan solve_flow(const FlowProblem& p) {
+  if (needs_lp(p)) return solve_flow_lp(p);
   trace::Scoped tr("dissem.maxflow");
   FlowPlan plan;
+  plan.solver = "flow";
   plan.required = required_bytes(p);
   if (plan.required == 0) {
     plan.feasible = true;
@@ -293,29 +616,7 @@ FlowPlan solve_flow(const FlowProblem& p) {
     per_demand[{std::get<1>(kv.first), std::get<2>(kv.first)}].push_back(
         FlowJob{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), f, 0});
   }
-  for (auto& kv : per_demand) {
-    auto& jobs = kv.second;
-    if (p.align > 1 && jobs.size() > 1) {
-      int64_t total = 0;
-      for (auto& j : jobs) total += j.size;
-      int64_t acc = 0;
-      size_t biggest = 0;
-      for (size_t i = 0; i < jobs.size(); ++i) {
-        jobs[i].size = (jobs[i].size / p.align) * p.align;
-        acc += jobs[i].size;
-        if (jobs[i].size > jobs[biggest].size) biggest = i;
-      }
-      jobs[biggest].size += total - acc;
-      jobs.erase(std::remove_if(jobs.begin(), jobs.end(), [](const FlowJob& j) { return j.size <= 0; }),
-                 jobs.end());
-    }
-    int64_t off = 0;  // ranges partition the layer, senders in id order
-    for (auto& j : jobs) {
-      j.offset = off;
-      off += j.size;
-      plan.jobs.push_back(j);
-    }
-  }
+  extract_jobs(per_demand, p.align, plan);
   return plan;
 }
 

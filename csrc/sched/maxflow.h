@@ -24,7 +24,19 @@
 //  * searches T continuously (seconds as double), or over integer seconds for
 //    reference parity;
 //  * rounds byte counts to a chunk alignment so ranges map onto whole chunks.
+//
+// Constraints a single-commodity flow cannot state exactly - one directed link
+// shared by layers from several of a sender's tiers, a staging (PCIe) budget
+// paid once per loaded byte while layers fan out to different numbers of
+// dests, one NVMe shared by every sender of a node (disk groups) - are solved
+// as a linear program instead (sched/lp.h): min T over byte counts x[sender,
+// class, dest] and loaded bytes y[sender, class] >= x, with every budget a
+// rate * T row. Layers with the same holders (and tiers) and the same dests
+// form one class, which keeps the LP small; its optimum equals the per-layer
+// LP's. solver = "auto" uses the flow where it is exact and the LP otherwise.
 #pragma once
+
+#include <string>
 
 #include <map>
 #include <vector>
@@ -57,6 +69,21 @@ struct FlowProblem {
   int64_t align = 1;
   bool integer_seconds = false;
   bool allow_self = false;  // may a dest source a demand from its own lower tier
+  // Planned (GPU) engines: a sender loads each byte of a non-HBM layer into
+  // HBM once and forwards it to any number of dests, so its tier rate, its
+  // staging budget and its disk group are charged per loaded byte, not per
+  // transfer (the reference re-reads a layer for every transfer).
+  bool stage_once = false;
+  // Senders that read their disk tier from one shared device (one NVMe per
+  // MI355X node): sender -> group, group -> read rate (B/s) shared by all.
+  std::map<NodeID, int> disk_group;
+  std::map<int, int64_t> disk_group_bps;
+  // Planned engines: dests that load a layer from their own lower tier (mode-3
+  // self-jobs, node.go:1205-1217) - layer -> bytes. The LP charges that load
+  // to the dest's tier, staging and disk group, shared with whatever the dest
+  // forwards of the same layer to others.
+  std::map<NodeID, std::map<LayerID, int64_t>> self_loads;
+  std::string solver = "auto";  // "flow", "lp" or "auto"
 };
 
 struct FlowPlan {
@@ -65,6 +92,8 @@ struct FlowPlan {
   int64_t max_flow = 0;
   int solves = 0;
   bool feasible = false;
+  std::string solver;      // "flow" or "lp"
+  int lp_pivots = 0;
   std::vector<FlowJob> jobs;
 };
 
@@ -72,5 +101,7 @@ FlowPlan solve_flow(const FlowProblem& p);
 
 // Max-flow only (exposed for tests): returns max flow for a fixed T.
 int64_t max_flow_at(const FlowProblem& p, double T);
+// Does `p` need the LP for an exact answer (see above)?
+bool needs_lp(const FlowProblem& p);
 
 }  // namespace dissem

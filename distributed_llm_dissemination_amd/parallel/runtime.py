@@ -104,6 +104,8 @@ class Runtime:
         persist_dir: str = "",
         engine_opts: Optional[Dict[str, object]] = None,
         source_pool: int = 0,
+        node_disk_gbps: float = 0.0,
+        node_key: str = "",
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -130,6 +132,10 @@ class Runtime:
         # carries random bytes and its own CRC manifest.
         self.source_pool = int(source_pool)
         self._pool: Dict[int, object] = {}
+        # One NVMe shared by every rank of this node (BASELINE config #4): the
+        # disk readers of all ranks draw from one budget (engine/node_pacer.h,
+        # keyed by node_key) and mode 3 plans the ranks' disk tiers as one group.
+        self.node_disk_gbps = float(node_disk_gbps)
         self.verify = verify
         self.payload_seed = payload_seed
         self._barrier = barrier or (lambda: None)
@@ -176,6 +182,9 @@ class Runtime:
             pcfg.max_retries = max_retries
             pcfg.group_timeout_s = group_timeout_s
             pcfg.group_peers = group_peers
+            if self.node_disk_gbps > 0:
+                pcfg.node_disk_rate = int(self.node_disk_gbps * 1e9)
+                pcfg.node_disk_key = node_key or sim_key
             # Extra PlannedConfig fields (reserve_cus, nccl_min_ctas, max_inflight_groups, ...).
             for k, v in (engine_opts or {}).items():
                 if not hasattr(pcfg, k):
@@ -561,6 +570,9 @@ class Runtime:
             hbm_gbps = self.HBM_PLAN_GBPS if gpu else 0.0
         if hbm_gbps > 0:
             nc.hbm_bw = {n.id: int(hbm_gbps * 1e9) for n in self.cfg.nodes}
+        if self.node_disk_gbps > 0:  # every rank of this node reads the same NVMe
+            nc.disk_group = {n.id: 0 for n in self.cfg.nodes}
+            nc.disk_group_bw = {0: int(self.node_disk_gbps * 1e9)}
         nc.adapt_links = adapt_links
         if adapt_links:
             nc.link_report = self.link_report()
@@ -680,7 +692,8 @@ class Runtime:
             k: getattr(es, k)
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
-                      "suspects", "shrinks", "aborted_pieces", "paced", "order_violations", "group_us_hist", "land_us_hist")
+                      "suspects", "shrinks", "aborted_pieces", "paced", "order_violations", "disk_wait_ms",
+                      "group_us_hist", "land_us_hist")
         }
 
     def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0) -> Dict[tuple, int]:

@@ -75,6 +75,15 @@ case "$RECIPE" in
     DISSEM_FULL_REHEARSAL=1 DISSEM_TEST_LOGDIR=$OUT/death8 timeout -k 10 400 $PYTEST tests/test_gpu_multirank.py \
       -k "rank_death" > $OUT/pytest_death.log 2>&1
     ;;
+  initdbg)
+    # RCCL's own init timing breakdown (NCCL_DEBUG=INFO, INIT) for both lane set-ups at 8 shared ranks
+    for ci in parallel split; do
+      NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 \
+        --steps 1 --warmup 0 --layers 8 --layer-mib 16 --chunk-mib 16 --probe-mib 0 --comm-init $ci --no-fallback \
+        > $OUT/bench8_$ci.json 2> $OUT/bench8_$ci.log || exit 1
+      grep -E "Init timings|Init COMPLETE|communicators ready" $OUT/bench8_$ci.log > $OUT/init_$ci.txt || true
+    done
+    ;;
   shared24)
     timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
     DISSEM_SHARED_GPU=1 timeout -k 10 240 python bench.py --gpus 2 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \

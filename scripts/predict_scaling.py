@@ -40,7 +40,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
-            adapt_links: bool = True) -> dict:
+            adapt_links: bool = True, disk_gbps: float = 13.3) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -52,6 +52,10 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     (default: the simulated one) - e.g. a constant estimate the real fabric beats.
     adapt_links: every session after the first plans on the link rates the ranks
     measured in the earlier ones (closed loop, Runtime.link_report).
+    tier="disk" (BASELINE config #4): layers are files read by each rank's disk
+    readers through ONE node-wide budget of disk_gbps (the node's single NVMe,
+    engine/node_pacer.h), then staged over that rank's PCIe; mode 3 plans the
+    ranks' disk tiers as one group.
     slowdown: run every rate this many times slower and divide the measured time
     by it (keeps the simulator's own per-op thread overhead small next to the
     modeled transfer times)."""
@@ -60,13 +64,29 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     _core.set_log_level(3)  # per-event JSON lines on stderr would be part of the timed sessions
     try:
         return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
-                        seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links)
+                        seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
+                        disk_gbps / slowdown)
     finally:
         _core.set_log_level(level)
 
 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
-             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links):
+             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps):
+    import shutil
+    import tempfile
+
+    storage = tempfile.mkdtemp(prefix="dld_predict_") if tier == "disk" else ""
+    try:
+        return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
+                           seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
+                           storage)
+    finally:
+        if storage:
+            shutil.rmtree(storage, ignore_errors=True)
+
+
+def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
+                policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -87,8 +107,9 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
         if slow_link is not None:
             (s, d), frac = slow_link
             cfg.links[s][d] = int(bw * frac)
+    disk = dict(storage_path=storage, node_disk_gbps=disk_gbps / scale, node_key=key) if tier == "disk" else {}
     rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
-                   poison=False, engine_opts={"lanes": lanes}, pack=pack) for i in range(n)]
+                   poison=False, engine_opts={"lanes": lanes}, pack=pack, **disk) for i in range(n)]
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
         r.transport.set_registry(reg)
@@ -124,6 +145,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
     sec = min(times) / slowdown
     total = delivered_bytes(cfg) * scale
     return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
+            **({"node_disk_GBps": disk_gbps * slowdown} if tier == "disk" else {}),
             **({"pack": pack, "layers": layers, "layer_MiB": layer_bytes >> 20} if pack != "none" else {}),
             "seeding": seeding, **({"policy": policy} if policy else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
@@ -146,6 +168,9 @@ def main() -> int:
     ap.add_argument("--slowdown", type=float, default=4.0)
     ap.add_argument("--layers", type=int, default=80)
     ap.add_argument("--layer-mib", type=int, default=1024)
+    ap.add_argument("--tier", choices=["host", "disk"], default="host",
+                    help="disk: BASELINE config #4 - layer files behind one node-wide NVMe budget (--disk-gbps)")
+    ap.add_argument("--disk-gbps", type=float, default=13.3, help="the node's NVMe read rate (profiles/r1_diskspeed.log)")
     ap.add_argument("--pack", choices=["none", "fp8"], default="none",
                     help="fp8: BASELINE config #5 (bf16 over PCIe, packed fp8 over the links)")
     ap.add_argument("--mode0", action="store_true",
@@ -165,12 +190,15 @@ def main() -> int:
     for lg in args.link_gbps:
         for n in args.ns:
             r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,
-                        slowdown=args.slowdown, layers=args.layers, layer_bytes=args.layer_mib << 20, pack=args.pack)
+                        slowdown=args.slowdown, layers=args.layers, layer_bytes=args.layer_mib << 20, pack=args.pack,
+                        tier=args.tier, disk_gbps=args.disk_gbps)
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
             if args.pack == "none":
                 total = args.layers * (args.layer_mib << 20)
                 bound = total / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)
+                if args.tier == "disk":  # every byte leaves the node's one NVMe once
+                    bound = max(bound, total / (args.disk_gbps * 1e9))
                 r["closed_form_ms"] = round(bound * 1e3, 1)
             print(json.dumps(r), flush=True)
     return 0

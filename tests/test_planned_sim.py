@@ -435,3 +435,15 @@ def test_source_pool_shares_host_buffers():
 
     (res,), _ = run_cluster(cfg, 1, rt_kw={"source_pool": 2}, inspect=check)
     assert res[0].engine_stats["verify_failures"] == 0
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_disk_tier_more_chunks_than_the_bounce_ring(tmp_path, n):
+    """Disk-tier layers of 12 chunks with an 8-buffer bounce ring (config #4
+    shape at N > 1). A bounce buffer returns to the ring when its H2D copy has
+    landed; held until the chunk's CRC check instead, the in-order verify queue
+    (checks behind recvs that wait on the peer, whose sends wait on disk reads
+    of its own) held every buffer on both ranks - a deadlock."""
+    cfg = make_workload(n, 2 * n, 12 * MiB, tier="disk", seeding="random", chunk_bytes=MiB)
+    (res,), _ = run_cluster(cfg, 1, rt_kw={"storage_path": str(tmp_path)})
+    assert all(r.engine_stats["verify_failures"] == 0 for r in res)

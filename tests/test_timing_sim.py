@@ -227,3 +227,43 @@ def test_closed_loop_replans_mode3_on_faster_links():
     t, T = min((t2, T2), (t3, T3))
     assert abs(t - T) <= 0.10 * T, r
     assert t < t1, r
+
+
+def test_node_shared_disk_budget_paces_every_rank(tmp_path):
+    """One NVMe per node (config #4 at N > 1): the ranks' disk readers draw from
+    one node-wide budget (engine/node_pacer.h, shared memory): 4 ranks loading
+    8 x 1 MiB at a 20 MB/s node rate take ~0.42 s in total, not 1/4 of it."""
+    cfg = make_workload(4, 8, MiB, tier="disk", seeding="random", chunk_bytes=MiB // 4)
+    key = f"disk{os.getpid()}_{next(_keys)}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB // 4, sim_key=key,
+                   storage_path=str(tmp_path), node_disk_gbps=0.02, node_key=key) for i in range(4)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for r in rts:
+            r.prepare(1)
+        res = [None] * 4
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(60))) for i in range(4)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        assert all(x.ok for x in res), [x.error for x in res]
+        want = 8 * MiB / 20e6
+        assert want * 0.85 <= dt <= want * 1.5 + 0.2, (dt, want)
+        assert sum(x.engine_stats["disk_wait_ms"] for x in res) > 0
+    finally:
+        for r in rts:
+            r.close()
+
+
+def test_predicted_disk_tier_is_bound_by_the_node_nvme():
+    """predict_scaling --tier disk: at N = 4 the headline workload from NVMe is
+    bound by the node's single device (80 GiB / 13.3 GB/s = 6.46 s), not by
+    N x per-GPU staging."""
+    r = predict_scaling.predict(4, scale=4096, steps=1, slowdown=4, tier="disk", layers=16)
+    bound = 16 * (1 << 30) / 13.3e9
+    assert bound * 0.9 <= r["ms_per_step"] / 1e3 <= bound * 1.4, (r, bound)
