@@ -457,7 +457,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("link_report", &NodeConfig::link_report)
       .def_readwrite("adapt_links", &NodeConfig::adapt_links)
       .def_readwrite("disk_group", &NodeConfig::disk_group)
-      .def_readwrite("disk_group_bw", &NodeConfig::disk_group_bw);
+      .def_readwrite("disk_group_bw", &NodeConfig::disk_group_bw)
+      .def_readwrite("host_share", &NodeConfig::host_share);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)

@@ -705,19 +705,31 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
   p.src_node = self_node_;
   Verify v;
+  // The chunk's expected CRC: this rank's manifest of the layer, or - for a
+  // layer it stages from a node-shared host copy it did not generate - the
+  // CRC the leader put in the job.
+  uint32_t want = 0;
+  bool known = false;
+  if (int64_t(L.manifest.crc.size()) > c) {
+    want = L.manifest.crc[size_t(c)];
+    known = true;
+  } else if (auto jc = L.job_crc.find(c); jc != L.job_crc.end()) {
+    want = jc->second;
+    known = true;
+  }
   if (cfg_.unpack_store) {
     // fused: check the packed chunk and write its bf16 image (one pass)
-    const bool check = cfg_.verify && int64_t(L.manifest.crc.size()) > c;
+    const bool check = cfg_.verify && known;
     if (check) {
       p.has_crc = true;
-      p.crc = L.manifest.crc[size_t(c)];
+      p.crc = want;
     }
     uint32_t slot = crc_slot();
     v.ev = unpack_chunk(L, c, slot, e);
     v.slots.push_back(check ? slot : ~0u);
-  } else if (cfg_.verify && int64_t(L.manifest.crc.size()) > c) {
+  } else if (cfg_.verify && known) {
     p.has_crc = true;
-    p.crc = L.manifest.crc[size_t(c)];
+    p.crc = want;
     uint32_t slot = crc_slot();
     v.ev = backend_->crc(L.dev + off, len, slot, e);
     v.slots.push_back(slot);
@@ -878,6 +890,7 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
         // piece of the chunk has landed (partial_landed)
         (p.full ? p.has_crc : p.has_ccrc) = true;
         (p.full ? p.crc : p.ccrc) = j.crc[size_t(ci)];
+        if (p.full && kind != Kind::Recv) L.job_crc[c] = p.crc;  // staging checks it without a manifest
       }
       pieces.push_back(p);
       pos = e;

@@ -259,6 +259,7 @@ class PlannedEngine : public DataEngine {
     std::vector<uint8_t> want;       // inject Landed when resident (assigned here)
     std::vector<uint8_t> fails;      // CRC failures per chunk
     std::map<int64_t, PartChunk> part;  // chunks landing as several partial pieces
+    std::map<int64_t, uint32_t> job_crc;  // CRCs from the leader's jobs (layers without a local manifest)
   };
   struct Verify {  // landing (recv group or staging copy) awaiting its check
     Ev ev = 0;

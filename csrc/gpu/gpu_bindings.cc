@@ -3,6 +3,12 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -152,6 +158,55 @@ void register_gpu_bindings(PyObject* module) {
         return alloc_pinned(n);
       })
       .def_static("malloc", [](int64_t n) { return HostBuffer::alloc(n, true); })
+      // Node-shared host memory (POSIX shm): one process creates `name`, the
+      // others of the node map it; `pin` registers the mapping with HIP in this
+      // process (page-locked, DMA-able by this rank's GPU over its own PCIe).
+      // The creator removes the name when its buffer is released (unlink early
+      // with shared_unlink once every process has mapped it).
+      .def_static("shared", [](const std::string& name, int64_t n, bool create, bool pin) {
+        py::gil_scoped_release nogil;
+        const std::string nm = name.empty() || name[0] != '/' ? "/" + name : name;
+        int fd = shm_open(nm.c_str(), O_RDWR | (create ? O_CREAT | O_EXCL : 0), 0600);
+        if (fd < 0) throw std::runtime_error("shm_open " + nm + ": " + strerror(errno));
+        if (create && ftruncate(fd, off_t(n)) != 0) {
+          const int e = errno;
+          close(fd);
+          shm_unlink(nm.c_str());
+          throw std::runtime_error("ftruncate " + nm + ": " + strerror(e));
+        }
+        struct stat stt;
+        if (fstat(fd, &stt) != 0 || stt.st_size < n) {
+          close(fd);
+          throw std::runtime_error("shared buffer " + nm + " is smaller than requested");
+        }
+        void* p = mmap(nullptr, size_t(n), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) throw std::runtime_error("mmap " + nm + ": " + strerror(errno));
+        if (pin) {
+          hipError_t e = hipHostRegister(p, size_t(n), hipHostRegisterDefault);
+          if (e != hipSuccess) {
+            munmap(p, size_t(n));
+            throw std::runtime_error("hipHostRegister " + nm + ": " + hipGetErrorString(e));
+          }
+        }
+        auto owner = std::shared_ptr<void>(p, [n, pin, create, nm](void* q) {
+          if (pin) (void)hipHostUnregister(q);
+          munmap(q, size_t(n));
+          if (create) shm_unlink(nm.c_str());
+        });
+        return HostBuffer::wrap(static_cast<uint8_t*>(p), n, owner);
+      }, py::arg("name"), py::arg("size"), py::arg("create"), py::arg("pin") = true)
+      .def_static("shared_exists", [](const std::string& name) {
+        const std::string nm = name.empty() || name[0] != '/' ? "/" + name : name;
+        int fd = shm_open(nm.c_str(), O_RDONLY, 0);
+        if (fd < 0) return false;
+        close(fd);
+        return true;
+      })
+      .def_static("shared_unlink", [](const std::string& name) {
+        const std::string nm = name.empty() || name[0] != '/' ? "/" + name : name;
+        return shm_unlink(nm.c_str()) == 0;
+      })
       .def_property_readonly("ptr", [](const HostBuffer& b) { return reinterpret_cast<uint64_t>(b.ptr); })
       .def_property_readonly("size", [](const HostBuffer& b) { return b.size; })
       .def("view", [](HostBuffer& b) {

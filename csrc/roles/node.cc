@@ -1001,12 +1001,25 @@ void Node::schedule_mode0() {
       log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(kv.first));
       continue;
     }
+    // host_share (planned engines): every node holding the layer's bytes below
+    // HBM (the leader's shared host segment, mapped by each rank) stages one
+    // slice of it; the leader is then a dest like any other.
+    std::vector<NodeID> stagers;
+    const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1);
+    const int64_t nchunks = (src.data_size + cb - 1) / cb;
+    if (cfg_.host_share && e_->planned())
+      for (auto& st : status_) {
+        auto it = st.second.find(kv.first);
+        if (it != st.second.end() && it->second.location != e_->target() && it->second.location != Location::Client)
+          stagers.push_back(st.first);
+      }
+    const bool sliced = stagers.size() >= 2 && nchunks >= int64_t(stagers.size());
     std::vector<NodeID> remote;
     for (NodeID d : kv.second) {
-      if (d == cfg_.id) {
+      if (d == cfg_.id && !sliced) {
         if (e_->planned()) add_job(d, d, kv.first, 0, -1);
         else send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
-      } else {
+      } else if (d != cfg_.id) {
         remote.push_back(d);
       }
     }
@@ -1016,9 +1029,23 @@ void Node::schedule_mode0() {
     }
     if (e_->planned()) {
       const int64_t total = src.data_size;
-      const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1);
       bool everyone = cfg_.collective && remote.size() >= 2 && remote.size() + 1 == status_.size();
-      if (everyone) {
+      if (sliced) {
+        // Slice i of the layer is staged by stager i over its own PCIe (a
+        // local load if it needs the layer) and sent from its HBM to every
+        // other dest; leftover chunks rotate over the stagers layer by layer.
+        const int64_t k = int64_t(stagers.size());
+        int64_t off = 0;
+        for (int64_t i = 0; i < k; ++i) {
+          const int64_t r = ((i - rot) % k + k) % k;
+          const int64_t cnt = nchunks / k + (r < nchunks % k ? 1 : 0);
+          const int64_t len = std::min(total - off, cnt * cb);
+          if (len <= 0) continue;
+          for (NodeID d : kv.second) add_job(stagers[size_t(i)], d, kv.first, off, len, 0);
+          off += len;
+        }
+        rot += nchunks % k;
+      } else if (everyone) {
         // Collective: one ncclBroadcast per layer (chunk-pipelined) rooted at the
         // leader; every rank of the communicator takes part.
         add_job(cfg_.id, kAllRanks, kv.first, 0, total, 0);
@@ -1026,7 +1053,6 @@ void Node::schedule_mode0() {
         // Bandwidth-optimal broadcast on a fully connected xGMI mesh: scatter
         // 1/k of the layer to each of k dests, then every dest relays its share
         // to the other k-1 (per-link load 2/k of the layer instead of 1).
-        const int64_t nchunks = (total + cb - 1) / cb;
         const int64_t k = int64_t(remote.size());
         int64_t off = 0;
         for (int64_t i = 0; i < k; ++i) {

@@ -64,6 +64,13 @@ struct NodeConfig {
   // the group as one budget (sched/maxflow.h).
   std::map<NodeID, int> disk_group;
   std::map<int, int64_t> disk_group_bw;
+  // Planned mode 0 (BASELINE config #2 from host memory): the leader's host
+  // layers sit in node-shared pinned memory that every rank has mapped, so
+  // every rank holding a layer's bytes stages a 1/k slice of it over its own
+  // PCIe and sends that slice to every dest - k host links feed the xGMI mesh
+  // instead of the leader's one (reference mode 0: the leader pushes
+  // everything, node.go:326-352; that stays the default).
+  bool host_share = false;
 };
 
 struct NodeStats {

@@ -106,6 +106,8 @@ class Runtime:
         source_pool: int = 0,
         node_disk_gbps: float = 0.0,
         node_key: str = "",
+        host_share: bool = False,
+        host_share_timeout_s: float = 600.0,
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -136,6 +138,15 @@ class Runtime:
         # disk readers of all ranks draw from one budget (engine/node_pacer.h,
         # keyed by node_key) and mode 3 plans the ranks' disk tiers as one group.
         self.node_disk_gbps = float(node_disk_gbps)
+        # Node-shared host tier (BASELINE config #2 from host memory): host-tier
+        # layers live in POSIX shared memory created by their holder and mapped
+        # (and HIP-registered) by every rank of the node; every rank then holds
+        # them as host-tier sources and mode 0 stages one slice per rank.
+        self.host_share = bool(host_share)
+        self.node_key = node_key or sim_key
+        self.host_share_timeout_s = host_share_timeout_s
+        self._shared: List[object] = []
+        self.shared_mapped: List[int] = []  # layers this rank maps from another rank's shared host tier
         self.verify = verify
         self.payload_seed = payload_seed
         self._barrier = barrier or (lambda: None)
@@ -294,6 +305,12 @@ class Runtime:
                     self._gen_layer(l, size, seed)
                     self.engine.set_seeded(l, True)
                     layers[l] = _core.layer_src_device(ptr, self.slot_sizes[l])
+                elif gpu and self.host_share:
+                    buf = _core.HostBuffer.shared(self._hs_name(self.node_id, l), size, True,
+                                                  self.engine_kind == "rccl")
+                    self._shared.append(buf)
+                    self._gen_layer(l, size, seed, host_buf=buf)
+                    layers[l] = self._host_src(buf, l, size, rate, st)
                 elif gpu:
                     key = (l % self.source_pool, size) if self.source_pool > 0 else None
                     if key is not None and key in self._pool:
@@ -306,16 +323,12 @@ class Runtime:
                         self._gen_layer(l, size, seed, host_buf=buf)
                         if key is not None:
                             self._pool[key] = buf
-                    src = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
-                    if self.slot_sizes[l] != size:  # packed: bf16 source, fp8 slot
-                        src.data_size = self.slot_sizes[l]
-                        meta = src.meta
-                        meta.size = self.slot_sizes[l]
-                        src.meta = meta
-                    layers[l] = src
+                    layers[l] = self._host_src(buf, l, size, rate, st)
                 else:
                     data = _core.fill_random_host(size, seed)
                     layers[l] = _core.LayerSrc.inmem(data, rate, _core.SourceType(st))
+        if gpu and self.host_share:
+            self._map_shared_layers(layers)
         client = self.cfg.client(self.node_id)
         if client is not None:  # AddClientLayers (config.go:119-131): metadata only
             for l, rate in client.layers.items():
@@ -339,6 +352,55 @@ class Runtime:
                 self.engine.set_source_packed(l, True)
             self.resumed.append(l)
         return layers
+
+    def _host_src(self, buf, l: int, size: int, rate: int, st: int):
+        src = _core.layer_src_from_buffer(buf, rate, _core.SourceType(st))
+        if self.slot_sizes[l] != size:  # packed: bf16 source, fp8 slot
+            src.data_size = self.slot_sizes[l]
+            meta = src.meta
+            meta.size = self.slot_sizes[l]
+            src.meta = meta
+        return src
+
+    def _hs_name(self, holder: int, layer) -> str:
+        return f"dld_hs_{self.node_key}_{holder}_{layer}"
+
+    def _map_shared_layers(self, layers) -> None:
+        """host_share: publish this rank's segments (a ready marker), then map every
+        other rank's host-tier layers as host-tier sources of this rank."""
+        mine = [l for st, per in self.me.initial_layers.items() if st not in (SOURCE_DISK, SOURCE_DEVICE, SOURCE_CLIENT)
+                for l in per]
+        if mine:
+            self._shared.append(_core.HostBuffer.shared(self._hs_name(self.node_id, "ready"), 4096, True, False))
+        pin = self.engine_kind == "rccl"
+        for n in self.cfg.nodes:
+            if n.id == self.node_id:
+                continue
+            theirs = [(l, size) for st, per in n.initial_layers.items()
+                      if st not in (SOURCE_DISK, SOURCE_DEVICE, SOURCE_CLIENT) for l, size in per.items()]
+            if not theirs or self.storage_path:
+                continue
+            deadline = time.monotonic() + self.host_share_timeout_s
+            while not _core.HostBuffer.shared_exists(self._hs_name(n.id, "ready")):
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"host_share: node {n.id} did not publish its host layers in "
+                                       f"{self.host_share_timeout_s:.0f} s")
+                time.sleep(0.02)
+            for l, size in theirs:
+                if l in layers:
+                    continue
+                buf = _core.HostBuffer.shared(self._hs_name(n.id, l), size, False, pin)
+                self._shared.append(buf)
+                layers[l] = self._host_src(buf, l, size, 0, 2)
+                self.shared_mapped.append(l)
+
+    def unlink_shared(self) -> None:
+        """Remove this rank's shared segment names once every rank has mapped them
+        (call after a barrier; mappings stay valid, nothing is left in /dev/shm)."""
+        for st, per in self.me.initial_layers.items():
+            for l in per:
+                _core.HostBuffer.shared_unlink(self._hs_name(self.node_id, l))
+        _core.HostBuffer.shared_unlink(self._hs_name(self.node_id, "ready"))
 
     # Planning estimates for the GPU topology (per direction): one xGMI link as
     # RCCL P2P drives it, and one GPU's PCIe host->HBM staging (57.5 GB/s
@@ -570,6 +632,7 @@ class Runtime:
             hbm_gbps = self.HBM_PLAN_GBPS if gpu else 0.0
         if hbm_gbps > 0:
             nc.hbm_bw = {n.id: int(hbm_gbps * 1e9) for n in self.cfg.nodes}
+        nc.host_share = self.host_share
         if self.node_disk_gbps > 0:  # every rank of this node reads the same NVMe
             nc.disk_group = {n.id: 0 for n in self.cfg.nodes}
             nc.disk_group_bw = {0: int(self.node_disk_gbps * 1e9)}
@@ -831,3 +894,4 @@ class Runtime:
         if self.engine is not None:
             self.engine.shutdown()
         self.transport.close()
+        self._shared.clear()  # unmaps (and unlinks the names this rank created)

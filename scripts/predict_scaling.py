@@ -40,7 +40,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
-            adapt_links: bool = True, disk_gbps: float = 13.3) -> dict:
+            adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -65,13 +65,13 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     try:
         return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                         seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
-                        disk_gbps / slowdown)
+                        disk_gbps / slowdown, host_share)
     finally:
         _core.set_log_level(level)
 
 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
-             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps):
+             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False):
     import shutil
     import tempfile
 
@@ -79,14 +79,15 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
     try:
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
-                           storage)
+                           storage, host_share)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
 
 
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
-                policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage):
+                policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
+                host_share=False):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -109,7 +110,11 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             cfg.links[s][d] = int(bw * frac)
     disk = dict(storage_path=storage, node_disk_gbps=disk_gbps / scale, node_key=key) if tier == "disk" else {}
     rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
-                   poison=False, engine_opts={"lanes": lanes}, pack=pack, **disk) for i in range(n)]
+                   poison=False, engine_opts={"lanes": lanes}, pack=pack, host_share=host_share, **disk)
+           for i in range(n)]
+    if host_share:
+        for r in rts:
+            r.unlink_shared()
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
         r.transport.set_registry(reg)
@@ -147,7 +152,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
             **({"node_disk_GBps": disk_gbps * slowdown} if tier == "disk" else {}),
             **({"pack": pack, "layers": layers, "layer_MiB": layer_bytes >> 20} if pack != "none" else {}),
-            "seeding": seeding, **({"policy": policy} if policy else {}),
+            "seeding": seeding, **({"policy": policy} if policy else {}), **({"host_share": True} if host_share else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
             "times_ms": [round(x / slowdown * 1e3, 1) for x in times],
             **({"flow_T_ms": [round(x / slowdown * 1e3, 1) for x in flow_Ts]} if any(flow_Ts) else {}),
@@ -173,6 +178,8 @@ def main() -> int:
     ap.add_argument("--disk-gbps", type=float, default=13.3, help="the node's NVMe read rate (profiles/r1_diskspeed.log)")
     ap.add_argument("--pack", choices=["none", "fp8"], default="none",
                     help="fp8: BASELINE config #5 (bf16 over PCIe, packed fp8 over the links)")
+    ap.add_argument("--host-share", action="store_true",
+                    help="with --mode0: the leader's host layers in node-shared memory, one slice staged per rank")
     ap.add_argument("--mode0", action="store_true",
                     help="BASELINE config #2 instead: mode 0 from the leader (relay vs ncclBroadcast, host vs HBM source)")
     args = ap.parse_args()
@@ -180,6 +187,11 @@ def main() -> int:
     if args.mode0:
         for lg in args.link_gbps:
             for n in args.ns:
+                if args.host_share:
+                    r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes,
+                                mode=0, slowdown=args.slowdown, seeding="leader", tier="host", host_share=True)
+                    print(json.dumps(r), flush=True)
+                    continue
                 for tier in ("device", "host"):
                     for relay, coll in ((True, False), (False, True)):
                         r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes,

@@ -447,3 +447,60 @@ def test_disk_tier_more_chunks_than_the_bounce_ring(tmp_path, n):
     cfg = make_workload(n, 2 * n, 12 * MiB, tier="disk", seeding="random", chunk_bytes=MiB)
     (res,), _ = run_cluster(cfg, 1, rt_kw={"storage_path": str(tmp_path)})
     assert all(r.engine_stats["verify_failures"] == 0 for r in res)
+
+
+@pytest.mark.parametrize("n", [3, 8])
+@pytest.mark.parametrize("pack", ["none", "fp8"])
+def test_mode0_host_share_stages_a_slice_per_rank(n, pack):
+    """BASELINE config #2 from host memory with --host-share: the leader's host
+    layers live in node-shared memory every rank maps, so each rank stages one
+    slice per layer over its own host link and sends it to every other dest.
+    Bytes arrive exact and verified (the leader's job CRCs check the slices its
+    peers stage), and the leader's own link carries 1/n of the bytes instead
+    of everything."""
+    import threading as th
+
+    L, size = 4, 8 * MiB
+    cfg = make_workload(n, L, size, tier="host", seeding="leader", chunk_bytes=MiB)
+    key = f"hs{next(_keys)}"
+    rts = [None] * n
+
+    def make(i):
+        rts[i] = Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+                         host_share=True, pack=pack)
+
+    ths = [th.Thread(target=make, args=(i,)) for i in range(n)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    try:
+        assert all(r is not None for r in rts)
+        assert all(sorted(r.shared_mapped) == list(range(L)) for r in rts[1:])
+        reg = {i: r.transport.address() for i, r in enumerate(rts)}
+        for r in rts:
+            r.transport.set_registry(reg)
+            r.unlink_shared()
+        for r in rts:
+            r.prepare(0)
+        res = [None] * n
+        go = [th.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(n)]
+        for t in go:
+            t.start()
+        for t in go:
+            t.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        for i, r in enumerate(rts):
+            for l in cfg.assignment.get(i, []):
+                assert r.layer_bytes(l) == expected_image(r, l, size), (i, l)
+            st = r.engine.stats()
+            assert st.verify_failures == 0 and st.unverified_pieces == 0
+        slot = rts[0].slot_sizes[0]
+        # every rank staged about 1/n of the bytes; the leader sent its slice to each receiver
+        staged = [r.engine.stats().bytes_staged for r in rts]
+        assert staged[0] <= L * size // n + L * 2 * MiB, staged
+        assert sum(rts[0].link_bytes()["sent"].values()) <= (n - 1) * L * (slot // n + slot // 8 + 1)
+    finally:
+        for r in rts:
+            if r is not None:
+                r.close()

@@ -61,7 +61,8 @@ def test_probe_measures_every_directed_link(n):
             assert set(o["concurrent"]) == peers and set(o["solo"]) == peers
         slow = out[0]["solo"][1]
         fast = [out[a]["solo"][b] for a in range(n) for b in range(n) if a != b and (a, b) != (0, 1)]
-        assert slow < 0.5 * min(fast), (slow, fast)
+        fast.sort()
+        assert slow < 0.5 * fast[len(fast) // 2], (slow, fast)  # a quarter-rate link, against the median
         # the probe leaves the engine ready for sessions
         res, err = _all(rts, lambda r: (r.prepare(1), r.execute(30))[1])
         assert all(x.ok for x in res), [x.error for x in res]
