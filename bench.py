@@ -64,6 +64,12 @@ def parse_args(argv=None):
     p.add_argument("--store", default="packed", choices=["packed", "bf16"],
                    help="with --pack fp8: bf16 = every resident chunk is also dequantized to bf16 in HBM by the "
                         "fused verify+unpack kernel (the receive path of an inference deployment)")
+    p.add_argument("--host-share", action="store_true",
+                   help="host-tier layers in node-shared pinned memory (POSIX shm, hipHostRegister in every rank); "
+                        "mode 0 then stages one slice of every layer per rank over its own PCIe (config #2)")
+    p.add_argument("--node-disk-gbps", type=float, default=None,
+                   help="--tier disk: the node's one NVMe read rate shared by every rank's disk readers and planned "
+                        "as one budget by mode 3 (default 13.3, profiles/r1_diskspeed.log; 0 = per-rank, unpaced)")
     p.add_argument("--reserve-cus", type=int, default=-1,
                    help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
@@ -273,12 +279,20 @@ def worker(args, world, rank, chan) -> int:
     log(f"HBM free {free / 2**30:.1f} / {tot / 2**30:.1f} GiB; setting up {args.layers} x {args.layer_mib} MiB"
         + (f" (attempt {chan.attempt}: {chan.label})" if chan is not None and chan.label else ""))
     t_setup = time.time()
+    # names the node-shared resources of this run (shm segments, disk pacer): same on every rank
+    import hashlib
+
+    run_tag = os.environ.get("DLD_SUP_PREFIX", "") + os.environ.get("MASTER_PORT", "") + os.environ.get(
+        "TORCHELASTIC_RUN_ID", "") if world > 1 else str(os.getpid())
+    node_key = "b" + hashlib.blake2b(run_tag.encode(), digest_size=6).hexdigest()
+    disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else (13.3 if args.tier == "disk" else 0.0)
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
                  store=args.store, group_timeout_s=min(300.0, args.timeout),
                  engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(rank)},
-                 inject_corrupt=faults.drop_chunk, source_pool=args.source_pool)
+                 inject_corrupt=faults.drop_chunk, source_pool=args.source_pool, host_share=args.host_share,
+                 node_key=node_key, node_disk_gbps=disk_gbps)
     beat("comm ready")
     if args.pack != "none":
         # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
@@ -288,6 +302,9 @@ def worker(args, world, rank, chan) -> int:
         addrs = [None] * world
         dist.all_gather_object(addrs, rt.transport.address())
         rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
+    if args.host_share:
+        barrier()  # every rank has mapped the shared segments: drop their names
+        rt.unlink_shared()
     log(f"setup done in {time.time() - t_setup:.1f}s")
 
     probe = {}
@@ -388,6 +405,8 @@ def worker(args, world, rank, chan) -> int:
                                f", {engine_note}" if engine_note else ""),
                 "pack": args.pack,
                 "payload": "bf16 layer shards as raw bytes, moved bit-exact (CRC32C per chunk)",
+                **({"host_share": True} if args.host_share else {}),
+                **({"node_disk_GBps": disk_gbps} if args.tier == "disk" else {}),
             },
         }
         if args.pack != "none":

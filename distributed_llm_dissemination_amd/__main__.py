@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import datetime
+import hashlib
 import json
 import os
 import signal
@@ -84,6 +85,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="rccl: independent comm lanes (RCCL communicator + HIP stream + dedicated HW queue "
                         "each); 0 = one lane per directed link on up to 8 ranks (14 at 8 ranks), world-1 "
                         "per-distance lanes beyond; a slow peer stalls only its own lane")
+    p.add_argument("--host-share", action="store_true",
+                   help="rccl: host-tier layers in node-shared pinned memory every rank maps; mode 0 stages one "
+                        "slice per rank over its own PCIe")
+    p.add_argument("--node-disk-gbps", type=float, default=0.0,
+                   help="rccl: one NVMe shared by every rank of the node at this read rate (disk readers share it; "
+                        "mode 3 plans it as one budget); 0 = per-rank disks")
     p.add_argument("--comm-init", default="parallel", choices=["parallel", "split"],
                    help="rccl: lane communicators from one unique id each, initialized together in one group "
                         "(parallel), or split from the world communicator one by one (split)")
@@ -231,7 +238,10 @@ def main(argv=None) -> int:
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
                  host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
                  persist_dir=args.persist_dir,
-                 engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(my_id)})
+                 engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(my_id)},
+                 host_share=args.host_share and args.engine == "rccl", node_disk_gbps=args.node_disk_gbps,
+                 node_key="c" + hashlib.blake2b((args.f + os.environ.get("MASTER_PORT", "")).encode(),
+                                                digest_size=6).hexdigest())
     if barrier is not None:
         # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
         import torch.distributed as dist
@@ -241,6 +251,9 @@ def main(argv=None) -> int:
         reg = dict(registry)
         reg.update({nid: addr for nid, addr in pairs})
         rt.transport.set_registry(reg)
+        if args.host_share:
+            barrier()  # every rank mapped the shared host layers: drop their names
+            rt.unlink_shared()
     if args.l:
         print(json.dumps({"level": "info", "node": my_id, "message": "layer set up"}), file=sys.stderr)
         rt.close()

@@ -12,6 +12,7 @@
 #   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
 #   insure     IPC variants, 14-lane rank death at 8 ranks, supervised bench --gpus 8 (+ forced fallback)
 #   init       parallel vs split lane-communicator set-up at 8 shared ranks; rank-death re-form
+#   r3rehearse host-share (config #2), disk tier + node NVMe budget (config #4) at 8 shared ranks; N = 1 A/Bs
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
@@ -83,6 +84,23 @@ case "$RECIPE" in
         > $OUT/bench8_$ci.json 2> $OUT/bench8_$ci.log || exit 1
       grep -E "Init timings|Init COMPLETE|communicators ready" $OUT/bench8_$ci.log > $OUT/init_$ci.txt || true
     done
+    ;;
+  r3rehearse)
+    # round-3 paths at 8 shared ranks and N = 1: config #2 with --host-share, config #4 (disk tier, node
+    # NVMe budget) in modes 1 and 3, the supervised default bench; N = 1 staging from shm vs hipHostMalloc
+    mkdir -p /tmp/dld_disk8 &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \
+      --chunk-mib 16 --mode 0 --seeding leader --host-share --probe-mib 16 > $OUT/b8_m0_hostshare.json 2> $OUT/b8_m0_hostshare.log &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \
+      --chunk-mib 16 --tier disk --storage /tmp/dld_disk8 --probe-mib 16 > $OUT/b8_disk_m1.json 2> $OUT/b8_disk_m1.log &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \
+      --chunk-mib 16 --tier disk --storage /tmp/dld_disk8 --mode 3 --probe-mib 16 > $OUT/b8_disk_m3.json 2> $OUT/b8_disk_m3.log &&
+    DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 --layer-mib 64 \
+      --chunk-mib 16 --probe-mib 16 > $OUT/b8_m1.json 2> $OUT/b8_m1.log &&
+    timeout -k 10 300 python bench.py --steps 3 --warmup 1 > $OUT/b1.json 2> $OUT/b1.log &&
+    timeout -k 10 300 python bench.py --steps 3 --warmup 1 --host-share > $OUT/b1_hostshare.json 2> $OUT/b1_hostshare.log &&
+    timeout -k 10 600 python bench.py --steps 2 --warmup 1 --tier disk --layers 16 --storage /tmp/dld_disk8 \
+      > $OUT/b1_disk.json 2> $OUT/b1_disk.log
     ;;
   shared24)
     timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
