@@ -301,16 +301,17 @@ void register_gpu_bindings(PyObject* module) {
   }, py::arg("src"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("dst"),
         py::arg("stream") = 0);
   m.def("fp8_verify_unpack_async", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block,
-                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream) {
+                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream, int store) {
     check(kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
                                   reinterpret_cast<uint16_t*>(out), reinterpret_cast<uint32_t*>(crc_out_dev),
-                                  reinterpret_cast<void*>(ws), as_stream(stream)),
+                                  reinterpret_cast<void*>(ws), as_stream(stream), 0, store),
           "fp8_verify_unpack");
-  });
+  }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
+     py::arg("crc_out"), py::arg("ws"), py::arg("stream") = 0, py::arg("store") = -1);
   // Fused verify + unpack (synchronous): writes the bf16 layer to `out`, returns
   // the CRC32C of every packed chunk.
   m.def("fp8_verify_unpack", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block, uint64_t out,
-                                uint64_t stream, int max_blocks) {
+                                uint64_t stream, int max_blocks, int store) {
     py::gil_scoped_release nogil;
     const int64_t pbytes = fp8::packed_size(src_bytes, src_chunk, block);
     const int64_t pchunk = fp8::packed_chunk(src_chunk, block);
@@ -322,7 +323,8 @@ void register_gpu_bindings(PyObject* module) {
           "hipHostMalloc");
     check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
     hipError_t e = kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
-                                           reinterpret_cast<uint16_t*>(out), dev, ws, as_stream(stream), max_blocks);
+                                           reinterpret_cast<uint16_t*>(out), dev, ws, as_stream(stream), max_blocks,
+                                           store);
     if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
     std::vector<uint32_t> crc(host, host + n);
     (void)hipFree(ws);
@@ -330,7 +332,7 @@ void register_gpu_bindings(PyObject* module) {
     check(e, "fp8_verify_unpack");
     return crc;
   }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
-        py::arg("stream") = 0, py::arg("max_blocks") = 0);
+        py::arg("stream") = 0, py::arg("max_blocks") = 0, py::arg("store") = -1);
 
   // ---- RCCL path on one GPU: a one-rank communicator driven through the same
   // Backend::group / crc calls the planned engine issues. `rounds` groups of

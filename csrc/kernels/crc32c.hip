@@ -74,6 +74,7 @@ constexpr int kBlocksPerSeg = kSegBytes / kBlockBytes;  // 4
 constexpr int kGapBytes = kBlockBytes - kPieceBytes;    // between a lane's pieces
 constexpr uint32_t kShLds = 131072;                     // shift tables after the byte tables
 constexpr uint32_t kLdsBytes = kShLds + 8 * 16 * 128;   // 144 KiB
+constexpr uint32_t kStageBytes = 16 * 1024;              // fused unpack: 1 KiB output staging per wave
 constexpr int kThreads = 1024;                          // one workgroup per CU, 4 waves per SIMD
 constexpr int kWaves = kThreads / 64;
 // Global constants: [T: 4 x 256 (T[k][v]: byte v then k zero bytes)]
@@ -383,9 +384,8 @@ __device__ inline uint32_t pk_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
 
-// 16 e4m3fn values (one 16-B word) times their block scale -> 16 bf16 (two 16-B words).
-__device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ dst) {
-  uint32_t o[8];
+// 16 e4m3fn values (one 16-B word) times their block scale -> 16 bf16 (32 B in o).
+__device__ inline void unpack16_regs(const u32x4_t& w, float s, uint32_t (&o)[8]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), false);
@@ -393,8 +393,35 @@ __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ d
     o[2 * i] = pk_bf16(lo[0] * s, lo[1] * s);
     o[2 * i + 1] = pk_bf16(hi[0] * s, hi[1] * s);
   }
+}
+__device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ dst) {
+  uint32_t o[8];
+  unpack16_regs(w, s, o);
   dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
   dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// A wave's 2 KiB of bf16 from one loaded word (lane m + 16 r holds output bytes
+// [128 m + 32 r, +32)) written as two fully coalesced 1 KiB stores (lane i:
+// bytes 16 i of each half) through a 1 KiB LDS slot of the wave: the lanes of
+// half h (m in 8h..8h+7) write their 32 B, every lane reads back 16 B and
+// stores. Stored directly, each of the two store instructions covers the 2 KiB
+// at half density (16 B in every 32). One wave's LDS operations run in issue
+// order, so no barrier is needed between its writes and reads.
+__device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* slot, uint4* __restrict__ region) {
+  const int lane = threadIdx.x & 63, m = lane & 15, r = lane >> 4;
+  uint4* w = reinterpret_cast<uint4*>(slot + 128 * (m & 7) + 32 * r);
+  const uint4* rd = reinterpret_cast<const uint4*>(slot) + lane;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if ((m >> 3) == h) {
+      w[0] = make_uint4(o[0], o[1], o[2], o[3]);
+      w[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    region[64 * h + lane] = *rd;
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 // Fused verify + unpack of fp8-packed chunks (core/fp8.h layout
@@ -411,7 +438,7 @@ __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ d
 // for all older loads - the next segment's prefetch included (vmcnt counts in
 // order): 3.93 -> 4.12 TB/s (profiles/r2_fused_ahead). Nontemporal bf16 stores
 // measured slower (3.61 TB/s, profiles/r2_fused_nt).
-template <int BLOCK>
+template <int BLOCK, bool STAGE = false>
 struct UnpackVisit {
   static constexpr int kR = kSegBytes / BLOCK >= 64 ? kSegBytes / BLOCK / 64 : 1;  // scale registers
   // BLOCK 32 would hold 16 scale registers and spill: it keeps the per-word load
@@ -422,6 +449,7 @@ struct UnpackVisit {
   int64_t n_q = 0;
   const float* scales = nullptr;
   uint16_t* obase = nullptr;
+  uint8_t* slot = nullptr;  // STAGE: this wave's 1 KiB of LDS
   float cs[kAhead ? kR : 1] = {}, ns[kAhead ? kR : 1] = {};  // scales of the current / next full segment
   __device__ void begin(const Seg& sg) {
     n_q = sg.chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
@@ -457,20 +485,31 @@ struct UnpackVisit {
     const int from = (base & 63) + (64 * (lane & 15) + 16 * (lane >> 4)) / BLOCK;
     const float s = __builtin_bit_cast(
         float, __builtin_amdgcn_ds_bpermute(from * 4, __builtin_bit_cast(int, cs[kAhead ? (base >> 6) : 0])));
+    if constexpr (STAGE) {
+      // the KiB this word covers: wave-uniform (lane offsets 0..1008 inside it)
+      const int64_t kib = e - (64 * (lane & 15) + 16 * (lane >> 4));
+      if (kib + 1024 <= n_q) {
+        uint32_t o[8];
+        unpack16_regs(w, s, o);
+        store_staged(o, slot, reinterpret_cast<uint4*>(obase + kib));
+        return;
+      }
+    }
     if (e < n_q) unpack16(w, s, reinterpret_cast<uint4*>(obase + e));
   }
 };
 
-template <int BLOCK>
+template <int BLOCK, bool STAGE>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
                               const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
                               uint16_t* __restrict__ out) {
-  __shared__ uint4 lds_raw[kLdsBytes / 16];
+  __shared__ uint4 lds_raw[(kLdsBytes + (STAGE ? kStageBytes : 0)) / 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
   load_lds(lds, sc);
   const Slice4 st(lds);
-  UnpackVisit<BLOCK> v{out_chunk_elems, out, geo.src};
+  UnpackVisit<BLOCK, STAGE> v{out_chunk_elems, out, geo.src};
+  v.slot = lds + kLdsBytes + (threadIdx.x >> 6) * 1024;
   slice_walk(geo, total_segs, sc, st, v, seg_out);
 }
 
@@ -699,7 +738,7 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
 }
 
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
-                             uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks) {
+                             uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks, int store) {
   if (src_bytes <= 0) return hipSuccess;
   if (src_chunk <= 0 || src_chunk % 4096 || src_bytes % (2 * block) || (reinterpret_cast<uintptr_t>(packed) & 15) ||
       (reinterpret_cast<uintptr_t>(out) & 15))
@@ -713,14 +752,19 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.fold, p.fold + p.spc * 64};
   const int64_t oc = src_chunk / 2;
   const dim3 grid = seg_grid(p.total_segs, max_blocks), tpb{kThreads};
+  if (store < 0) store = kFusedStoreDefault;
+#define DLD_VU(B)                                                                                           \
+  (store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
+              : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
   switch (block) {
-    case 32: verify_unpack_segments_kernel<32><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
-    case 64: verify_unpack_segments_kernel<64><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
-    case 128: verify_unpack_segments_kernel<128><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
-    case 256: verify_unpack_segments_kernel<256><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
-    case 512: verify_unpack_segments_kernel<512><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out); break;
+    case 32: DLD_VU(32); break;
+    case 64: DLD_VU(64); break;
+    case 128: DLD_VU(128); break;
+    case 256: DLD_VU(256); break;
+    case 512: DLD_VU(512); break;
     default: return hipErrorInvalidValue;
   }
+#undef DLD_VU
   crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, pchunk, p.spc,
                                                                      p.fold + 2 * p.spc * 64, crc_out);
   return hipGetLastError();

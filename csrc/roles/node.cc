@@ -995,6 +995,7 @@ void Node::schedule_mode0() {
     for (auto& l : kv.second)
       if (!at(status_[kv.first], l.first, e_->target())) need[l.first].push_back(kv.first);
   int64_t rot = 0;  // relay: which dests take a layer's leftover chunks rotates, so every link carries 1/k
+  int64_t srot = 0;  // host_share: which stagers serve a layer with fewer chunks than stagers rotates
   for (auto& kv : need) {
     LayerSrc src;
     if (!store_.get(kv.first, &src)) {
@@ -1013,7 +1014,7 @@ void Node::schedule_mode0() {
         if (it != st.second.end() && it->second.location != e_->target() && it->second.location != Location::Client)
           stagers.push_back(st.first);
       }
-    const bool sliced = stagers.size() >= 2 && nchunks >= int64_t(stagers.size());
+    const bool sliced = stagers.size() >= 2 && nchunks >= 2;
     std::vector<NodeID> remote;
     for (NodeID d : kv.second) {
       if (d == cfg_.id && !sliced) {
@@ -1034,17 +1035,20 @@ void Node::schedule_mode0() {
         // Slice i of the layer is staged by stager i over its own PCIe (a
         // local load if it needs the layer) and sent from its HBM to every
         // other dest; leftover chunks rotate over the stagers layer by layer.
-        const int64_t k = int64_t(stagers.size());
+        // A layer of fewer chunks than stagers goes to a rotating subset.
+        const int64_t S = int64_t(stagers.size()), k = std::min<int64_t>(S, nchunks);
         int64_t off = 0;
         for (int64_t i = 0; i < k; ++i) {
           const int64_t r = ((i - rot) % k + k) % k;
           const int64_t cnt = nchunks / k + (r < nchunks % k ? 1 : 0);
           const int64_t len = std::min(total - off, cnt * cb);
           if (len <= 0) continue;
-          for (NodeID d : kv.second) add_job(stagers[size_t(i)], d, kv.first, off, len, 0);
+          const NodeID s = stagers[size_t((i + srot) % S)];
+          for (NodeID d : kv.second) add_job(s, d, kv.first, off, len, 0);
           off += len;
         }
         rot += nchunks % k;
+        srot += k;
       } else if (everyone) {
         // Collective: one ncclBroadcast per layer (chunk-pipelined) rooted at the
         // leader; every rank of the communicator takes part.

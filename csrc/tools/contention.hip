@@ -12,6 +12,13 @@
 // its enqueue to its end (HIP events on its own idle stream), and the burst.
 // Verify stream without a CU mask vs one created with R CUs left free, with
 // the CRC grid at 256 workgroups or capped at the stream's 256 - R CUs.
+//
+// Bandwidth, not only launch delay: a 32-workgroup HBM -> HBM copy (16 B per
+// lane, grid-stride; the stand-in for one comm lane's RCCL P2P kernel moving a
+// chunk) on an all-CU dedicated queue, alone and while batched CRC bursts run
+// back to back on the verify stream (unmasked / masked with R CUs free). The
+// copy's GB/s (bytes copied per second) says whether the CU reservation leaves
+// a lane its bandwidth: 7 lanes at >= 60 GB/s each need >= 420 GB/s.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,11 +48,16 @@ __global__ void __launch_bounds__(256) probe_kernel(uint32_t* out, uint64_t tick
   if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
-static hipStream_t make_stream(int reserve) {
+__global__ void __launch_bounds__(256) copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                  int64_t n16) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += int64_t(gridDim.x) * 256) dst[i] = src[i];
+}
+
+static hipStream_t make_stream(int reserve, bool dedicated = false) {
   hipStream_t s = nullptr;
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  if (reserve <= 0) {
+  if (reserve <= 0 && !dedicated) {
     CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     return s;
   }
@@ -130,6 +142,39 @@ int main(int argc, char** argv) {
            "\"probe_p50_us\": %.1f, \"probe_p90_us\": %.1f, \"probe_max_us\": %.1f, \"crc_burst_p50_us\": %.1f}\n",
            r, cap, pct(lat, 0.5), pct(lat, 0.9), pct(lat, 1.0), pct(burst, 0.5));
     CHECK(hipStreamDestroy(verify));
+  }
+
+  // ---- copy bandwidth beside CRC bursts
+  const int64_t copy_bytes = 256ll << 20;  // 4 chunks' worth per copy launch
+  uint8_t *csrc = nullptr, *cdst = nullptr;
+  CHECK(hipMalloc(&csrc, size_t(copy_bytes)));
+  CHECK(hipMalloc(&cdst, size_t(copy_bytes)));
+  CHECK(hipMemset(csrc, 1, size_t(copy_bytes)));
+  hipStream_t lane = make_stream(0, true);  // all-CU dedicated queue, like a comm lane
+  for (int wgs : {32, 64}) {
+    const std::pair<int, int> ccases[] = {{-1, 0}, {0, 0}, {reserve, cus - reserve}};  // -1: no CRC
+    for (auto [r, cap] : ccases) {
+      hipStream_t verify = r >= 0 ? make_stream(r) : nullptr;
+      std::vector<float> gbps;
+      for (int t = 0; t < trials + 2; ++t) {
+        // 3 bursts of 7-chunk CRCs queued ahead, so the copy runs inside them
+        if (verify)
+          for (int b = 0; b < 3; ++b) CHECK(dissem::kern::crc32c_batch(items, int(nchunks), ws, verify, cap));
+        CHECK(hipEventRecord(e0, lane));
+        copy_kernel<<<wgs, 256, 0, lane>>>(reinterpret_cast<const uint4*>(csrc), reinterpret_cast<uint4*>(cdst),
+                                           copy_bytes / 16);
+        CHECK(hipEventRecord(e1, lane));
+        CHECK(hipStreamSynchronize(lane));
+        if (verify) CHECK(hipStreamSynchronize(verify));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (t >= 2) gbps.push_back(float(double(copy_bytes) / (double(ms) * 1e-3) / 1e9));
+      }
+      printf("{\"case\": \"copy_beside_crc\", \"copy_workgroups\": %d, \"crc\": %s, \"reserved_cus\": %d, "
+             "\"crc_grid_cap\": %d, \"copy_GBps_p50\": %.1f, \"copy_GBps_p10\": %.1f, \"copy_GBps_min\": %.1f}\n",
+             wgs, r < 0 ? "false" : "true", r < 0 ? 0 : r, cap, pct(gbps, 0.5), pct(gbps, 0.1), pct(gbps, 0.0));
+      if (verify) CHECK(hipStreamDestroy(verify));
+    }
   }
   return 0;
 }

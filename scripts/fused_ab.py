@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""A/B of the fused fp8 verify + unpack kernel's bf16 store path (crc32c.hip):
+store=0 writes each lane's 32 B straight from registers (two half-dense 2 KiB
+stores per loaded word), store=1 stages them through 1 KiB of LDS per wave and
+issues two fully coalesced 1 KiB stores. Same input, same CRCs and bf16 bytes
+(checked), timed with HIP events on 512 MiB of bf16 (264 MiB packed), plus the
+plain fp8 unpack and a torch copy of the same output size as references.
+
+    python scripts/fused_ab.py [--store 0|1] [--reps N]   # one variant only: for rocprofv3 --pmc passes
+"""
+
+import argparse
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+from distributed_llm_dissemination_amd import _core  # noqa: E402
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--store", type=int, nargs="*", default=[0, 1])
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    chunk, block = 64 << 20, 128
+    src = 512 << 20
+    buf = torch.empty(src, dtype=torch.uint8, device="cuda")
+    _core.fill_random(buf.data_ptr(), src, 11)
+    pbytes = _core.fp8_packed_size(src, chunk, block)
+    packed = torch.empty(pbytes, dtype=torch.uint8, device="cuda")
+    _core.fp8_pack_chunks(buf.data_ptr(), src, chunk, block, packed.data_ptr())
+    pchunk = chunk // 2 + chunk // 2 // block * 4
+    nch = (pbytes + pchunk - 1) // pchunk
+    ws = torch.empty(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device="cuda")
+    out = {"src_MiB": src >> 20, "packed_MiB": round(pbytes / 2**20, 1)}
+    ref_bytes = ref_crc = None
+    for st in args.store:
+        y = torch.zeros(src, dtype=torch.uint8, device="cuda")
+        crc = torch.zeros(nch, dtype=torch.int32, device="cuda")
+        fn = lambda: _core.fp8_verify_unpack_async(packed.data_ptr(), src, chunk, block, y.data_ptr(),  # noqa: E731
+                                                    crc.data_ptr(), ws.data_ptr(), 0, st)
+        t = timed(fn, args.reps)
+        out[f"store{st}_us"] = round(t * 1e6, 1)
+        out[f"store{st}_GBps"] = round((pbytes + src) / t / 1e9, 1)
+        if ref_bytes is None:
+            ref_bytes, ref_crc = y.clone(), crc.clone()
+        else:
+            out[f"store{st}_identical"] = bool(torch.equal(y, ref_bytes) and torch.equal(crc, ref_crc))
+    if len(args.store) > 1:
+        want = _core.crc32c_chunks(packed.data_ptr(), pbytes, pchunk)
+        out["crc_matches_reference"] = [x & 0xFFFFFFFF for x in ref_crc.tolist()] == list(want)
+        q = torch.empty(src // 2, dtype=torch.uint8, device="cuda")
+        scl = torch.empty(src // 2 // block, dtype=torch.float32, device="cuda")
+        x = buf.view(torch.bfloat16)
+        _core.fp8_pack(x.data_ptr(), src // 2, q.data_ptr(), scl.data_ptr(), block)
+        y2 = torch.empty(src, dtype=torch.uint8, device="cuda")
+        t = timed(lambda: _core.fp8_unpack(q.data_ptr(), scl.data_ptr(), src // 2, y2.data_ptr(), block), args.reps)
+        out["plain_unpack_GBps"] = round((src // 2 + src // 2 // 32 + src) / t / 1e9, 1)
+        a = torch.empty(pbytes, dtype=torch.uint8, device="cuda")
+        t = timed(lambda: y2.copy_(buf), args.reps)
+        out["torch_copy_512MiB_GBps"] = round(2 * src / t / 1e9, 1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

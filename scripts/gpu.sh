@@ -13,6 +13,7 @@
 #   insure     IPC variants, 14-lane rank death at 8 ranks, supervised bench --gpus 8 (+ forced fallback)
 #   init       parallel vs split lane-communicator set-up at 8 shared ranks; rank-death re-form
 #   r3rehearse host-share (config #2), disk tier + node NVMe budget (config #4) at 8 shared ranks; N = 1 A/Bs
+#   r3kernels  fused verify+unpack store A/B + counters, copy bandwidth beside CRC, NUMA A/B
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
@@ -101,6 +102,30 @@ case "$RECIPE" in
     timeout -k 10 300 python bench.py --steps 3 --warmup 1 --host-share > $OUT/b1_hostshare.json 2> $OUT/b1_hostshare.log &&
     timeout -k 10 600 python bench.py --steps 2 --warmup 1 --tier disk --layers 16 --storage /tmp/dld_disk8 \
       > $OUT/b1_disk.json 2> $OUT/b1_disk.log
+    ;;
+  r3kernels)
+    # fused fp8 verify+unpack store-path A/B (numerics, timing, counters), copy bandwidth beside
+    # CRC bursts (bin/contention), and the NUMA-binding A/B (3 x 2 interleaved arms, 5 steps each)
+    timeout -k 10 300 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log || exit 1
+    timeout -s KILL 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1
+    for st in 0 1; do
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VALU --output-format csv -d $OUT/pmc_sq_$st -o sq -- \
+        python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_sq_$st.log 2>&1 || exit 1
+      timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE TA_BUSY_avr TD_BUSY_avr --output-format csv -d $OUT/pmc_mem_$st \
+        -o mem -- python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_mem_$st.log 2>&1 ||
+        { rc=$?; [ $rc -ge 124 ] && exit 1; }  # an unknown counter name fails fast; a kill ends the recipe
+    done
+    timeout -k 10 180 bin/contention -trials 30 -reserve 32 > $OUT/contention.jsonl 2>&1 || exit 1
+    for i in 1 2 3; do
+      timeout -k 10 200 python bench.py --steps 5 --warmup 1 > $OUT/numa_bound_$i.json 2> $OUT/numa_bound_$i.log &&
+      DISSEM_NUMA_BIND=0 timeout -k 10 200 python bench.py --steps 5 --warmup 1 > $OUT/numa_off_$i.json \
+        2> $OUT/numa_off_$i.log || exit 1
+    done
+    DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 --layer-mib 128 \
+      --chunk-mib 16 --mode 0 --seeding leader --host-share --probe-mib 16 > $OUT/b8_m0_hostshare.json \
+      2> $OUT/b8_m0_hostshare.log
     ;;
   shared24)
     timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&

@@ -223,16 +223,19 @@ def test_fp8_pack_chunks_matches_host_layout(gpu, size, chunk, block):
     # partial segments between full ones)
     (48 << 20, 16 << 20, 128, 3), ((24 << 20) + 4096, 1 << 20, 256, 7), (16 << 20, (1 << 20) + 4096, 64, 1),
     (8 << 20, 4 << 20, 32, 2), ((8 << 20) + 1024, 64 << 10, 512, 5)])
-def test_fp8_fused_verify_unpack(gpu, size, chunk, block, max_blocks):
+@pytest.mark.parametrize("store", [0, 1])
+def test_fp8_fused_verify_unpack(gpu, size, chunk, block, max_blocks, store):
     """One pass: CRC32C of every packed chunk + bf16 dequantization; compared with
-    the CRC kernel, the host CRC and the standalone unpack kernel (same math)."""
+    the CRC kernel, the host CRC and the standalone unpack kernel (same math).
+    store 1: the bf16 leaves through the per-wave LDS staging slot (coalesced 1 KiB stores)."""
     raw = _dev_bytes(size)
     gpu.fill_random(raw.data_ptr(), size, 11)  # random bf16 bit patterns, NaN/Inf included
     packed_n = gpu.fp8_packed_size(size, chunk, block)
     packed = _dev_bytes(packed_n)
     gpu.fp8_pack_chunks(raw.data_ptr(), size, chunk, block, packed.data_ptr())
     out = _dev_bytes(size)
-    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr(), max_blocks=max_blocks)
+    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr(), max_blocks=max_blocks,
+                                 store=store)
     pchunk = chunk // 2 + chunk // 2 // block * 4
     assert crcs == gpu.crc32c_chunks(packed.data_ptr(), packed_n, pchunk)
     host = packed.cpu().numpy().tobytes()

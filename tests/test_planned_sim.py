@@ -504,3 +504,36 @@ def test_mode0_host_share_stages_a_slice_per_rank(n, pack):
         for r in rts:
             if r is not None:
                 r.close()
+
+
+def test_mode0_host_share_layers_with_fewer_chunks_than_ranks():
+    """8 ranks, layers of 4 chunks: each layer is staged by 4 of the 8 ranks,
+    the subset rotating from layer to layer so every rank stages about 1/8."""
+    import threading as th
+
+    n, L, size = 8, 8, 4 * MiB
+    cfg = make_workload(n, L, size, tier="host", seeding="leader", chunk_bytes=MiB)
+    key = f"hs{next(_keys)}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key, host_share=True)
+           for i in range(n)]
+    try:
+        reg = {i: r.transport.address() for i, r in enumerate(rts)}
+        for r in rts:
+            r.transport.set_registry(reg)
+        for r in rts:
+            r.prepare(0)
+        res = [None] * n
+        go = [th.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(30))) for i in range(n)]
+        for t in go:
+            t.start()
+        for t in go:
+            t.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        for i, r in enumerate(rts):
+            for l in range(L):
+                assert r.layer_bytes(l) == expected_image(r, l, size)
+        staged = [r.engine.stats().bytes_staged for r in rts]
+        assert staged == [L * size // n] * n, staged
+    finally:
+        for r in rts:
+            r.close()
