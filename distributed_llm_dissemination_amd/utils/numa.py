@@ -85,10 +85,12 @@ def bind_to_gpu(device: int) -> Dict[str, int]:
     """Pin this thread's CPUs and page preference to the GPU's NUMA node.
 
     Returns {"numa_node", "cpus", "mempolicy"} describing what was applied
-    ({} when nothing was); DISSEM_NUMA_BIND=0 turns it off."""
+    ({} when nothing was); DISSEM_NUMA_BIND=0 turns it off, DISSEM_NUMA_NODE=k
+    binds to node k instead (A/B runs: a deliberately remote node)."""
     if os.environ.get("DISSEM_NUMA_BIND", "1") == "0" or not hasattr(os, "sched_setaffinity"):
         return {}
-    node = gpu_numa_node(device)
+    forced = os.environ.get("DISSEM_NUMA_NODE", "")
+    node = int(forced) if forced else gpu_numa_node(device)
     if node < 0 or node >= 64:
         return {}
     cpus = node_cpus(node) & os.sched_getaffinity(0)
