@@ -270,10 +270,12 @@ __device__ __forceinline__ u32x4_t seg_load(__amdgpu_buffer_rsrc_t r, int lo, in
 // byte offset in the chunk.
 template <class Geo, class Visit>
 __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, const uint32_t* __restrict__ sc,
-                                           const Slice4& st, Visit& visit, uint32_t* __restrict__ seg_out) {
+                                           const Slice4& st, Visit& visit, uint32_t* __restrict__ seg_out,
+                                           int waves_per_wg = kWaves) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = __builtin_amdgcn_readfirstlane(int(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-  const int64_t nwaves = int64_t(gridDim.x) * kWaves;
+  const int64_t wave =
+      __builtin_amdgcn_readfirstlane(int(blockIdx.x * waves_per_wg + ((threadIdx.x >> 6) % waves_per_wg)));
+  const int64_t nwaves = int64_t(gridDim.x) * waves_per_wg;
   const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
   int64_t g = wave;
   if (g >= total_segs) return;
@@ -519,6 +521,71 @@ verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t ou
   slice_walk(geo, total_segs, sc, st, v, seg_out);
 }
 
+// store = 2: the same CRC walk on half of the waves (0-7) while the other half
+// (8-15) stream the same segments' q bytes through the plain unpack (8 B of
+// fp8 in, 16 B of bf16 out per lane: every load and store instruction fully
+// coalesced), one segment behind or ahead, so the packed bytes come twice from
+// L2 / the Infinity Cache instead of twice from HBM. In the fused walk every
+// wave does both jobs in sequence: its CRC (LDS lookups, VALU) and its stores
+// do not overlap, and the kernel takes about the sum of a CRC pass and an
+// unpack pass (profiles/r3_kernels).
+template <int BLOCK>
+__device__ __forceinline__ void unpack_walk(const ChunkGeo& geo, int64_t total_segs, int64_t out_chunk_elems,
+                                            uint16_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = __builtin_amdgcn_readfirstlane(int(blockIdx.x * 8 + ((threadIdx.x >> 6) & 7)));
+  const int64_t nwaves = int64_t(gridDim.x) * 8;
+  for (int64_t g = wave; g < total_segs; g += nwaves) {
+    const Seg sg = geo(g);
+    const int64_t n_q = sg.chunk_len / (BLOCK + 4) * BLOCK;
+    if (sg.seg_start >= n_q) continue;  // the chunk's scales: nothing to unpack
+    const float* scales = reinterpret_cast<const float*>(geo.src + sg.chunk_start + n_q);
+    uint16_t* obase = out + sg.chunk * out_chunk_elems;
+    const int64_t end = min(sg.seg_start + sg.len, n_q);
+    const uint2* q = reinterpret_cast<const uint2*>(sg.p);
+    constexpr int kU = 8;  // 8 x 512 B of loads in flight per wave
+    for (int64_t base = 0; sg.seg_start + base < end; base += kU * 512) {
+      uint2 v[kU];
+      float sc[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t e = sg.seg_start + base + u * 512 + 8 * lane;
+        v[u] = e < end ? q[(base + u * 512) / 8 + lane] : make_uint2(0, 0);
+        sc[u] = e < end ? scales[e / BLOCK] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t e = sg.seg_start + base + u * 512 + 8 * lane;
+        if (e >= end) continue;
+        const float s = sc[u];
+        const auto f0 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].x), false);
+        const auto f1 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].x), true);
+        const auto f2 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].y), false);
+        const auto f3 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].y), true);
+        *reinterpret_cast<uint4*>(obase + e) = make_uint4(pk_bf16(f0[0] * s, f0[1] * s), pk_bf16(f1[0] * s, f1[1] * s),
+                                                          pk_bf16(f2[0] * s, f2[1] * s), pk_bf16(f3[0] * s, f3[1] * s));
+      }
+    }
+  }
+}
+
+template <int BLOCK>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+verify_unpack_split_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
+                           const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
+                           uint16_t* __restrict__ out) {
+  __shared__ uint4 lds_raw[kLdsBytes / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  load_lds(lds, sc);
+  if ((threadIdx.x >> 6) < 8) {
+    const Slice4 st(lds);
+    NoVisit v;
+    slice_walk(geo, total_segs, sc, st, v, seg_out, 8);
+  } else {
+    unpack_walk<BLOCK>(geo, total_segs, out_chunk_elems, out);
+  }
+}
+
 // One 256-thread block per chunk: XOR of the chunk's (pre-shifted) segment
 // values plus the init/xorout term. init[0]: full chunks, init[1]: short last chunk.
 __global__ void __launch_bounds__(256) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
@@ -759,9 +826,12 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   const int64_t oc = src_chunk / 2;
   const dim3 grid = seg_grid(p.total_segs, max_blocks), tpb{kThreads};
   if (store < 0) store = kFusedStoreDefault;
+  // the split kernel's CRC half walks 8 segments per workgroup at a time
+  const dim3 grid2(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + 7) / 8, max_blocks > 0 ? max_blocks : 256))));
 #define DLD_VU(B)                                                                                           \
-  (store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
-              : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
+  (store == 2   ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
+   : store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
+                : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
   switch (block) {
     case 32: DLD_VU(32); break;
     case 64: DLD_VU(64); break;

@@ -74,7 +74,9 @@ hipError_t fp8_pack_chunks(const void* src, int64_t src_bytes, int64_t src_chunk
 // `workspace`: crc32c_workspace_bytes(packed bytes, packed chunk) bytes.
 // store: how the bf16 output leaves the CU - 0 = each lane's 32 B straight from
 // registers (two half-dense 2 KiB stores per word), 1 = through 1 KiB of LDS per
-// wave as fully coalesced 1 KiB stores; -1 = kFusedStoreDefault.
+// wave as fully coalesced 1 KiB stores, 2 = split roles: half of each
+// workgroup's waves CRC the segments while the other half unpack them;
+// -1 = kFusedStoreDefault.
 constexpr int kFusedStoreDefault = 0;
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
                              uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks = 0, int store = -1);

@@ -2,7 +2,8 @@
 """A/B of the fused fp8 verify + unpack kernel's bf16 store path (crc32c.hip):
 store=0 writes each lane's 32 B straight from registers (two half-dense 2 KiB
 stores per loaded word), store=1 stages them through 1 KiB of LDS per wave and
-issues two fully coalesced 1 KiB stores. Same input, same CRCs and bf16 bytes
+issues two fully coalesced 1 KiB stores, store=2 splits each workgroup's waves
+into CRC walkers and unpack streamers over the same segments. Same input, same CRCs and bf16 bytes
 (checked), timed with HIP events on 512 MiB of bf16 (264 MiB packed), plus the
 plain fp8 unpack and a torch copy of the same output size as references.
 
@@ -33,7 +34,7 @@ def timed(fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--store", type=int, nargs="*", default=[0, 1])
+    ap.add_argument("--store", type=int, nargs="*", default=[0, 1, 2])
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
     chunk, block = 64 << 20, 128
