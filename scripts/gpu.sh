@@ -77,6 +77,9 @@ case "$RECIPE" in
     DISSEM_FULL_REHEARSAL=1 DISSEM_TEST_LOGDIR=$OUT/death8 timeout -k 10 400 $PYTEST tests/test_gpu_multirank.py \
       -k "rank_death" > $OUT/pytest_death.log 2>&1
     ;;
+  cvt)
+    timeout -k 10 60 bin/cvtprobe > $OUT/cvtprobe.jsonl 2>&1
+    ;;
   initdbg)
     # RCCL's own init timing breakdown (NCCL_DEBUG=INFO, INIT) for both lane set-ups at 8 shared ranks
     for ci in parallel split; do
