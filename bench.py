@@ -411,7 +411,7 @@ def worker(args, world, rank, chan) -> int:
         }
         if args.pack != "none":
             out["dtype"] = "fp8"
-            out["config"]["payload"] = "bf16 sources packed on the GPU to fp8 e4m3fn, one f32 scale per block"
+            out["config"]["payload"] = "bf16 sources packed on the GPU to fp8 e4m3fn, one power-of-two scale per block"
             out["config"]["model"] = f"{args.layers}x{args.layer_mib}MiB bf16 layers (Llama-3.1-405B-sized shards), fp8 in HBM"
             out["config"]["bf16_source_bytes_per_step"] = src_bytes
             out["config"]["bf16_equivalent_GBps"] = round(src_bytes * args.steps / total / 1e9, 3)

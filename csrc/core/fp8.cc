@@ -61,13 +61,16 @@ void pack_host(const uint16_t* in, int64_t n, uint8_t* q, float* scales, int blo
       float x = bf16_to_f32(in[b * block + i]);
       if (std::isfinite(x)) amax = std::fmax(amax, std::fabs(x));
     }
-    const float inv = amax > 0.f ? 448.0f / amax : 1.0f;
+    uint32_t ab;
+    memcpy(&ab, &amax, 4);
+    const int e = scale_exp(ab);
+    const float inv = std::ldexp(1.0f, -e);  // exact: x * 2^-E only moves the exponent
     for (int i = 0; i < block; ++i) {
       float y = bf16_to_f32(in[b * block + i]) * inv;
       if (y == y) y = std::fmin(std::fmax(y, -448.0f), 448.0f);
       q[b * block + i] = f32_to_e4m3(y);
     }
-    scales[b] = amax > 0.f ? amax / 448.0f : 1.0f;
+    scales[b] = std::ldexp(1.0f, e);
   }
 }
 

@@ -5,8 +5,12 @@
 // A bf16 layer is cut on the source chunk grid (`src_chunk` bytes). Source
 // chunk c of n bf16 elements packs into one packed chunk:
 //     [ q: n bytes of OCP e4m3fn ][ scales: n/block f32 ]
-// with one scale per `block` consecutive elements (scale = amax/448 over the
-// block's finite values, 1 if none). Packed chunks are laid end to end, so the
+// with one scale per `block` consecutive elements. The scale is a power of two,
+// 2^E with E the smallest integer such that amax <= 448 * 2^E over the block's
+// finite values (E = 0 if none, E >= -126): an E8M0-valued scale (stored as
+// f32), so gfx950's scaled conversions (v_cvt_scalef32_pk_bf16_fp8, which
+// apply only the scale's exponent) dequantize a pair of values in one
+// instruction, and q * 2^E is exact in bf16. Packed chunks are laid end to end, so the
 // packed layer has its own uniform chunk grid of packed_chunk(src_chunk) bytes
 // and every transfer, CRC and retry runs on that grid unchanged.
 #pragma once
@@ -41,6 +45,16 @@ inline int64_t source_size(int64_t packed, int64_t src_chunk, int block) {
   const int64_t t = tail * 2 * block / (block + 4);
   if (packed_len(t, block) != tail) throw std::runtime_error("size is not a packed fp8 layer size");
   return full * src_chunk + t;
+}
+
+// E of a block's scale 2^E from its finite amax (>= 0): exact integer logic on
+// the f32 bits (448 = 1.75 * 2^8), identical in the gfx950 pack kernel.
+inline int scale_exp(uint32_t amax_bits) {
+  if (amax_bits == 0) return 0;
+  const int ef = int(amax_bits >> 23);
+  if (ef == 0) return -126;  // f32 subnormal amax: the lowest normal scale
+  const int e = ef - 127 - 8 + ((amax_bits & 0x7FFFFFu) > 0x600000u ? 1 : 0);
+  return e < -126 ? -126 : e;
 }
 
 // Host reference (bit-exact with the gfx950 kernel except where the hardware

@@ -60,6 +60,7 @@
 #include <vector>
 
 #include "core/crc32c.h"
+#include "kernels/fp8_cvt.h"
 #include "kernels/kernels.h"
 
 namespace dissem {
@@ -377,23 +378,12 @@ crc32c_segments_kernel(const ChunkGeo geo, int64_t total_segs, const uint32_t* _
   slice_walk(geo, total_segs, sc, st, v, seg_out);
 }
 
-// Two f32 -> packed bf16 (a in the low half), round-to-nearest-even, NaN kept
-// quiet: gfx950's v_cvt_pk_bf16_f32, one VALU per pair (the integer RNE
-// sequence it replaces took ~6 per value and made the fused kernel spill).
-__device__ inline uint32_t pk_bf16(float a, float b) {
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
-}
-
-// 16 e4m3fn values (one 16-B word) times their block scale -> 16 bf16 (32 B in o).
+// 16 e4m3fn values (one 16-B word) times their power-of-two block scale -> 16 bf16 (32 B in o).
 __device__ inline void unpack16_regs(const u32x4_t& w, float s, uint32_t (&o)[8]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), false);
-    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(int(w[i]), true);
-    o[2 * i] = pk_bf16(lo[0] * s, lo[1] * s);
-    o[2 * i + 1] = pk_bf16(hi[0] * s, hi[1] * s);
+    o[2 * i] = fp8x2_to_bf16x2<false>(w[i], s);
+    o[2 * i + 1] = fp8x2_to_bf16x2<true>(w[i], s);
   }
 }
 __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ dst) {
@@ -558,12 +548,9 @@ __device__ __forceinline__ void unpack_walk(const ChunkGeo& geo, int64_t total_s
         const int64_t e = sg.seg_start + base + u * 512 + 8 * lane;
         if (e >= end) continue;
         const float s = sc[u];
-        const auto f0 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].x), false);
-        const auto f1 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].x), true);
-        const auto f2 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].y), false);
-        const auto f3 = __builtin_amdgcn_cvt_pk_f32_fp8(int(v[u].y), true);
-        *reinterpret_cast<uint4*>(obase + e) = make_uint4(pk_bf16(f0[0] * s, f0[1] * s), pk_bf16(f1[0] * s, f1[1] * s),
-                                                          pk_bf16(f2[0] * s, f2[1] * s), pk_bf16(f3[0] * s, f3[1] * s));
+        *reinterpret_cast<uint4*>(obase + e) =
+            make_uint4(fp8x2_to_bf16x2<false>(v[u].x, s), fp8x2_to_bf16x2<true>(v[u].x, s),
+                       fp8x2_to_bf16x2<false>(v[u].y, s), fp8x2_to_bf16x2<true>(v[u].y, s));
       }
     }
   }

@@ -1,11 +1,14 @@
 // bf16 <-> OCP fp8 e4m3fn block-scaled pack/unpack (BASELINE config #5: the
 // 405B-sized run ships layers as fp8 on the wire to halve xGMI bytes).
 //
-// gfx950 converts with v_cvt_pk_fp8_f32 / v_cvt_pk_f32_fp8, which use the OCP
-// e4m3fn encoding on CDNA4 (not MI300's fnuz). One f32 scale per `block`
-// elements: scale = amax/448 over the block's finite values (1 if none), so
-// q = x * (448/amax) fits the e4m3fn range; +-inf saturate to +-448 and NaN
-// stays NaN (0x7F) - random bf16 payload bit patterns contain both.
+// OCP e4m3fn encoding (CDNA4's, not MI300's fnuz). One power-of-two scale 2^E
+// per `block` elements (core/fp8.h: the smallest E with amax <= 448 * 2^E over
+// the block's finite values), stored as f32. Pack scales by the exact 2^-E and
+// converts with v_cvt_pk_fp8_f32 (+-inf saturate to +-448, NaN stays NaN
+// 0x7F - random bf16 payload bit patterns contain both); unpack is
+// v_cvt_scalef32_pk_bf16_fp8: fp8 pair -> scaled bf16 pair in one instruction
+// (the scale's exponent is applied, exact for a power of two), where the f32
+// path took 4 VALU per pair (convert, 2 multiplies, pack to bf16).
 //
 // Each thread moves 8 elements: a 16-B bf16 load and an 8-B fp8 store (pack),
 // or the reverse (unpack). A block of `block` elements is handled by
@@ -14,6 +17,7 @@
 
 #include <algorithm>
 
+#include "kernels/fp8_cvt.h"
 #include "kernels/kernels.h"
 
 namespace dissem {
@@ -23,13 +27,13 @@ namespace {
 
 __device__ inline float bf16_to_f32(uint16_t b) { return __uint_as_float(uint32_t(b) << 16); }
 
-// Two f32 -> packed bf16 (a in the low half), round-to-nearest-even, NaN kept
-// quiet: gfx950's v_cvt_pk_bf16_f32, one VALU per pair (the integer RNE
-// sequence it replaces took ~6 per value and made the fused kernel spill).
-__device__ inline uint32_t pk_bf16(float a, float b) {
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+// E of the block scale 2^E from the block's finite amax: core/fp8.h scale_exp.
+__device__ inline int scale_exp(uint32_t amax_bits) {
+  if (amax_bits == 0) return 0;
+  const int ef = int(amax_bits >> 23);
+  if (ef == 0) return -126;
+  const int e = ef - 127 - 8 + ((amax_bits & 0x7FFFFFu) > 0x600000u ? 1 : 0);
+  return e < -126 ? -126 : e;
 }
 
 __device__ inline bool finite(float x) { return (__float_as_uint(x) & 0x7F800000u) != 0x7F800000u; }
@@ -78,7 +82,8 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__
   for (int i = 0; i < 8; ++i)
     if (finite(x[i])) amax = fmaxf(amax, fabsf(x[i]));
   amax = group_max<LANES>(amax);
-  const float inv = amax > 0.f ? 448.0f / amax : 1.0f;
+  const int e = scale_exp(__float_as_uint(amax));
+  const float inv = __uint_as_float(uint32_t(127 - e) << 23);  // 2^-E, E in [-126, 120]
   float y[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -92,7 +97,7 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__
   hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], hi, true);
   if (!active) return;
   out[t] = make_uint2(uint32_t(lo), uint32_t(hi));
-  if ((threadIdx.x % LANES) == 0) scales[t / LANES] = amax > 0.f ? amax / 448.0f : 1.0f;
+  if ((threadIdx.x % LANES) == 0) scales[t / LANES] = __uint_as_float(uint32_t(127 + e) << 23);
 }
 
 template <int LANES>
@@ -103,12 +108,8 @@ __global__ void __launch_bounds__(256) fp8_unpack_kernel(const uint2* __restrict
   if (t >= nthreads) return;
   const uint2 q = in[t];
   const float s = scales[t / LANES];
-  const auto f0 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.x), false);
-  const auto f1 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.x), true);
-  const auto f2 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.y), false);
-  const auto f3 = __builtin_amdgcn_cvt_pk_f32_fp8(int(q.y), true);
-  auto pk = [s](float a, float b) { return pk_bf16(a * s, b * s); };
-  out[t] = make_uint4(pk(f0[0], f0[1]), pk(f1[0], f1[1]), pk(f2[0], f2[1]), pk(f3[0], f3[1]));
+  out[t] = make_uint4(fp8x2_to_bf16x2<false>(q.x, s), fp8x2_to_bf16x2<true>(q.x, s),
+                      fp8x2_to_bf16x2<false>(q.y, s), fp8x2_to_bf16x2<true>(q.y, s));
 }
 
 }  // namespace

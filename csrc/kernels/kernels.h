@@ -62,7 +62,7 @@ hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_by
 hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int max_blocks = 0);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements
-// (scale = amax/448; non-finite inputs: +-inf saturate, NaN stays NaN), and back.
+// (power-of-two scale 2^E, core/fp8.h; +-inf saturate, NaN stays NaN), and back.
 hipError_t fp8_pack(const uint16_t* bf16, int64_t n, uint8_t* fp8, float* scales, int block, hipStream_t s);
 hipError_t fp8_unpack(const uint8_t* fp8, const float* scales, int64_t n, uint16_t* bf16, int block, hipStream_t s);
 // Whole layer into the chunked packed layout of core/fp8.h (one pack launch per chunk).

@@ -89,7 +89,8 @@ def crc32c_values(crcs: torch.Tensor) -> List[int]:
 
 
 def fp8_pack(x: torch.Tensor, block: int = 128) -> Tuple[torch.Tensor, torch.Tensor]:
-    """bf16 -> OCP fp8 e4m3fn with one f32 scale (amax/448) per `block` values.
+    """bf16 -> OCP fp8 e4m3fn with one power-of-two f32 scale per `block` values
+    (2^E, the smallest E >= -126 with the block's finite amax <= 448 * 2^E; core/fp8.h).
     Non-finite inputs: +-inf saturate to +-448*scale, NaN stays NaN.
     Returns (q: float8_e4m3fn [n], scales: float32 [n / block])."""
     _check_dev(x, "x", torch.bfloat16)

@@ -130,6 +130,19 @@ case "$RECIPE" in
       --chunk-mib 16 --mode 0 --seeding leader --host-share --probe-mib 16 > $OUT/b8_m0_hostshare.json \
       2> $OUT/b8_m0_hostshare.log
     ;;
+  r3mx)
+    # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters
+    timeout -k 10 400 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py tests/test_gpu_engine.py -k "fp8 or fused" \
+      > $OUT/pytest_fp8.log 2>&1 &&
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log || exit 1
+    for st in 0 1; do
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VALU --output-format csv -d $OUT/pmc_sq_$st -o sq -- \
+        python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_sq_$st.log 2>&1 || exit 1
+    done
+    timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 \
+      --steps 2 --warmup 1 > $OUT/bench_fp8_store_bf16.json 2> $OUT/bench_fp8_store_bf16.log
+    ;;
   r3fused2)
     # swizzled LDS staging slot (store=1) vs direct stores, counters; NUMA: GPU's node vs the other node
     timeout -k 10 300 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&

@@ -122,16 +122,27 @@ def test_crc32c_detects_single_bit_flip(gpu):
     assert a[:3] == b[:3] and a[3] != b[3]
 
 
+def _scale_exp(amax: torch.Tensor) -> torch.Tensor:
+    """core/fp8.h scale: the smallest E >= -126 with amax <= 448 * 2^E (0 if amax == 0), exact in f64."""
+    a = amax.double()
+    _, k = torch.frexp(a)  # a = m * 2^k, m in [0.5, 1)
+    e = k.long() - 10
+    for _ in range(4):  # 448 * 2^(k - 10) < a always; the answer is k - 9 or k - 8
+        e = torch.where(a > 448.0 * torch.pow(2.0, e.double()), e + 1, e)
+    e = e.clamp(min=-126)
+    return torch.where(a > 0, e, torch.zeros_like(e))
+
+
 def _fp8_reference(x_bf16: torch.Tensor, block: int):
-    """fp32 reference of the pack: per-block amax over finite values, scale = amax/448."""
+    """fp32 reference of the pack: per-block amax over finite values, scale 2^E (_scale_exp)."""
     x = x_bf16.float().view(-1, block)
     fin = torch.isfinite(x)
     amax = torch.where(fin, x.abs(), torch.zeros_like(x)).amax(dim=1)
-    inv = torch.where(amax > 0, 448.0 / amax, torch.ones_like(amax))
-    y = x * inv[:, None]
+    e = _scale_exp(amax)
+    y = x * torch.pow(2.0, -e.double()).float()[:, None]
     y = torch.where(torch.isnan(y), y, y.clamp(-448.0, 448.0))
     q = y.to(torch.float8_e4m3fn)
-    scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    scale = torch.pow(2.0, e.double()).float()
     return q.view(torch.uint8).reshape(-1), scale
 
 
@@ -151,8 +162,7 @@ def test_fp8_pack_matches_torch(gpu, block):
     # (e.g. 168.0000153 -> 160 instead of 176): the code may then be the other
     # neighbor. Everything else must match IEEE round-to-nearest-even exactly.
     xf = x.float().cpu().view(-1, block)
-    inv = 448.0 / xf.abs().amax(1)
-    y = (xf * inv[:, None]).flatten()
+    y = (xf / sr[:, None]).flatten()
     dec = lambda c: c.view(torch.float8_e4m3fn).float()  # noqa: E731
     for i in bad.tolist():
         a, b = dec(qg[i : i + 1]).item(), dec(qr[i : i + 1]).item()
