@@ -65,9 +65,10 @@ void pack_host(const uint16_t* in, int64_t n, uint8_t* q, float* scales, int blo
     memcpy(&ab, &amax, 4);
     const int e = scale_exp(ab);
     const float inv = std::ldexp(1.0f, -e);  // exact: x * 2^-E only moves the exponent
+    const float hi = sat_limit(e);
     for (int i = 0; i < block; ++i) {
       float y = bf16_to_f32(in[b * block + i]) * inv;
-      if (y == y) y = std::fmin(std::fmax(y, -448.0f), 448.0f);
+      if (y == y) y = std::fmin(std::fmax(y, -hi), hi);
       q[b * block + i] = f32_to_e4m3(y);
     }
     scales[b] = std::ldexp(1.0f, e);

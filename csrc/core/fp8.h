@@ -10,7 +10,7 @@
 // finite values (E = 0 if none, E >= -126): an E8M0-valued scale (stored as
 // f32), so gfx950's scaled conversions (v_cvt_scalef32_pk_bf16_fp8, which
 // apply only the scale's exponent) dequantize a pair of values in one
-// instruction, and q * 2^E is exact in bf16. Packed chunks are laid end to end, so the
+// instruction, and q * 2^E is exact in bf16 (sat_limit keeps it finite). Packed chunks are laid end to end, so the
 // packed layer has its own uniform chunk grid of packed_chunk(src_chunk) bytes
 // and every transfer, CRC and retry runs on that grid unchanged.
 #pragma once
@@ -56,6 +56,11 @@ inline int scale_exp(uint32_t amax_bits) {
   const int e = ef - 127 - 8 + ((amax_bits & 0x7FFFFFu) > 0x600000u ? 1 : 0);
   return e < -126 ? -126 : e;
 }
+
+// Largest code magnitude of a block with scale 2^E: 448, except 240 at E = 120
+// (only blocks whose amax is within 2^-4 of bf16's max get there), where
+// 256 * 2^120 would overflow bf16 on unpack (the bf16 maximum is 255 * 2^120).
+inline float sat_limit(int e) { return e >= 120 ? 240.0f : 448.0f; }
 
 // Host reference (bit-exact with the gfx950 kernel except where the hardware
 // converter double-rounds values within 2^-18 of a rounding tie).

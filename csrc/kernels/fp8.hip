@@ -4,7 +4,8 @@
 // OCP e4m3fn encoding (CDNA4's, not MI300's fnuz). One power-of-two scale 2^E
 // per `block` elements (core/fp8.h: the smallest E with amax <= 448 * 2^E over
 // the block's finite values), stored as f32. Pack scales by the exact 2^-E and
-// converts with v_cvt_pk_fp8_f32 (+-inf saturate to +-448, NaN stays NaN
+// converts with v_cvt_pk_fp8_f32 (+-inf saturate to +-448 - 240 in the top
+// binade, core/fp8.h sat_limit - and NaN stays NaN
 // 0x7F - random bf16 payload bit patterns contain both); unpack is
 // v_cvt_scalef32_pk_bf16_fp8: fp8 pair -> scaled bf16 pair in one instruction
 // (the scale's exponent is applied, exact for a power of two), where the f32
@@ -84,12 +85,13 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__
   amax = group_max<LANES>(amax);
   const int e = scale_exp(__float_as_uint(amax));
   const float inv = __uint_as_float(uint32_t(127 - e) << 23);  // 2^-E, E in [-126, 120]
+  const float lim = e >= 120 ? 240.0f : 448.0f;                  // core/fp8.h sat_limit
   float y[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     y[i] = x[i] * inv;
     // Saturate finite and infinite values; NaN is left for the converter (-> NaN).
-    if (y[i] == y[i]) y[i] = __builtin_amdgcn_fmed3f(y[i], 448.0f, -448.0f);
+    if (y[i] == y[i]) y[i] = __builtin_amdgcn_fmed3f(y[i], lim, -lim);
   }
   int lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], 0, false);
   lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], lo, true);

@@ -61,3 +61,23 @@ def test_host_unpack_is_exact_product():
     assert torch.equal(y.double(), want)
     err = (y.float() - x.float()).abs()
     assert bool((err <= x.float().abs() * 2**-4 + s.repeat_interleave(block) * 2**-9).all())
+
+
+def test_host_roundtrip_random_bit_patterns():
+    """Random payload bytes as bf16 (NaN, +-inf, the top binade): NaN stays NaN, +-inf saturate,
+    nothing finite unpacks to inf (blocks with E = 120 saturate their codes at 240)."""
+    src, chunk, block = MiB, MiB, 128
+    raw = _core.fill_random_host(src, 3)
+    x = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()).view(torch.bfloat16).float()
+    packed = _core.fp8_pack_layer_host(raw, chunk, block)
+    y = torch.from_numpy(np.frombuffer(_core.fp8_unpack_layer_host(packed, src, chunk, block),
+                                       dtype=np.uint8).copy()).view(torch.bfloat16).float()
+    _, s = _split(packed, src, chunk, block)
+    assert bool((s == 2.0**120).any())  # the top binade is exercised
+    assert torch.equal(torch.isnan(x), torch.isnan(y))
+    fin = torch.isfinite(x)
+    assert bool(torch.isfinite(y[fin]).all())
+    err = (y - x).abs()
+    assert bool(((err <= x.abs() * 0.0625 + s.repeat_interleave(block) * 2**-9) | ~fin).all())
+    inf = torch.isinf(x)
+    assert torch.equal(y[inf].sign(), x[inf].sign())
