@@ -33,7 +33,7 @@ PYTEST="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 
 case "$RECIPE" in
   check)
-    timeout -k 10 900 $PYTEST tests -m gpu > $OUT/pytest_gpu.log 2>&1 &&
+    timeout -k 10 900 $PYTEST --durations=30 tests -m gpu > $OUT/pytest_gpu.log 2>&1 &&
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 &&
     timeout -k 10 600 python bench.py --steps 3 --warmup 1 > $OUT/bench.json 2> $OUT/bench.log
     ;;
@@ -88,6 +88,19 @@ case "$RECIPE" in
         > $OUT/bench8_$ci.json 2> $OUT/bench8_$ci.log || exit 1
       grep -E "Init timings|Init COMPLETE|communicators ready" $OUT/bench8_$ci.log > $OUT/init_$ci.txt || true
     done
+    ;;
+  init2)
+    # lane-communicator set-up with RCCL's ring/tree connections deferred to first use
+    # (NCCL_RUNTIME_CONNECT=1; the lanes' P2P connections are still made eagerly by connect_all)
+    for ci in parallel split; do
+      NCCL_RUNTIME_CONNECT=1 NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=INIT DISSEM_SHARED_GPU=1 timeout -k 10 300 \
+        python bench.py --gpus 8 --steps 1 --warmup 0 --layers 8 --layer-mib 16 --chunk-mib 16 --probe-mib 0 \
+        --comm-init $ci --no-fallback > $OUT/bench8_rc_$ci.json 2> $OUT/bench8_rc_$ci.log || exit 1
+      grep -E "Init timings" $OUT/bench8_rc_$ci.log > $OUT/init_rc_$ci.txt || true
+    done
+    NCCL_RUNTIME_CONNECT=1 DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 \
+      --layers 8 --layer-mib 16 --chunk-mib 16 --mode 0 --seeding leader --bcast collective \
+      > $OUT/bench8_rc_bcast.json 2> $OUT/bench8_rc_bcast.log
     ;;
   r3rehearse)
     # round-3 paths at 8 shared ranks and N = 1: config #2 with --host-share, config #4 (disk tier, node
