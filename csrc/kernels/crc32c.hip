@@ -269,7 +269,9 @@ __device__ __forceinline__ u32x4_t seg_load(__amdgpu_buffer_rsrc_t r, int lo, in
 // compiler sinks those loads behind the math), so 16 KiB stay in flight per
 // wave. Visit sees every 16-B word (as loaded, before the transpose) with its
 // byte offset in the chunk.
-template <class Geo, class Visit>
+// CRC = false (diagnostic A/B only: its segment values are garbage) keeps the
+// walk, the loads and the visits and drops the CRC math.
+template <class Geo, class Visit, bool CRC = true>
 __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, const uint32_t* __restrict__ sc,
                                            const Slice4& st, Visit& visit, uint32_t* __restrict__ seg_out,
                                            int waves_per_wg = kWaves) {
@@ -314,10 +316,12 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
       for (int b = 0; b < kBlocksPerSeg; ++b) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) visit.word(w[4 * b + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo, 4 * b + j);
-        row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
-        s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
+        if constexpr (CRC) {
+          row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
+          s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
 #pragma unroll
-        for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
+          for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (b == 0) {  // the next segment's scales go out ahead of its data
           visit.prefetch(nxt, nfull);
@@ -327,7 +331,7 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
         for (int j = 0; j < 4; ++j) w[4 * b + j] = seg_load(rn, lo, 4 * b + j);
         __builtin_amdgcn_sched_barrier(0);
       }
-      s = wave_xor_dpp(multmodp_unrolled(rowc, s));
+      if constexpr (CRC) s = wave_xor_dpp(multmodp_unrolled(rowc, s));
     } else {
       s = slice_partial(cur, sc, st, lane, visit);
     }
@@ -497,7 +501,7 @@ struct UnpackVisit {
   }
 };
 
-template <int BLOCK, bool STAGE>
+template <int BLOCK, bool STAGE, bool CRC = true>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
                               const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
@@ -508,7 +512,7 @@ verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t ou
   const Slice4 st(lds);
   UnpackVisit<BLOCK, STAGE> v{out_chunk_elems, out, geo.src};
   v.slot = lds + kLdsBytes + (threadIdx.x >> 6) * 1024;
-  slice_walk(geo, total_segs, sc, st, v, seg_out);
+  slice_walk<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC>(geo, total_segs, sc, st, v, seg_out);
 }
 
 // store = 2: the same CRC walk on half of the waves (0-7) while the other half
@@ -819,13 +823,21 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   (store == 2   ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
    : store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
                 : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
-  switch (block) {
-    case 32: DLD_VU(32); break;
-    case 64: DLD_VU(64); break;
-    case 128: DLD_VU(128); break;
-    case 256: DLD_VU(256); break;
-    case 512: DLD_VU(512); break;
-    default: return hipErrorInvalidValue;
+  if (store == 3 || store == 4) {  // diagnostic: the same walk without the CRC math (CRCs are garbage)
+    if (block != 128) return hipErrorInvalidValue;
+    if (store == 3)
+      verify_unpack_segments_kernel<128, true, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
+    else
+      verify_unpack_segments_kernel<128, false, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
+  } else {
+    switch (block) {
+      case 32: DLD_VU(32); break;
+      case 64: DLD_VU(64); break;
+      case 128: DLD_VU(128); break;
+      case 256: DLD_VU(256); break;
+      case 512: DLD_VU(512); break;
+      default: return hipErrorInvalidValue;
+    }
   }
 #undef DLD_VU
   crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, pchunk, p.spc,

@@ -3,7 +3,8 @@
 store=0 writes each lane's 32 B straight from registers (two half-dense 2 KiB
 stores per loaded word), store=1 stages them through 1 KiB of LDS per wave and
 issues two fully coalesced 1 KiB stores, store=2 splits each workgroup's waves
-into CRC walkers and unpack streamers over the same segments. Same input, same CRCs and bf16 bytes
+into CRC walkers and unpack streamers over the same segments; store=3/4 are store=1/0 with the CRC
+math removed (diagnostic: what the walk, loads and stores cost alone). Same input, same CRCs and bf16 bytes
 (checked), timed with HIP events on 512 MiB of bf16 (264 MiB packed), plus the
 plain fp8 unpack and a torch copy of the same output size as references.
 
@@ -34,7 +35,7 @@ def timed(fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--store", type=int, nargs="*", default=[0, 1, 2])
+    ap.add_argument("--store", type=int, nargs="*", default=[0, 1, 2, 3, 4])
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
     chunk, block = 64 << 20, 128
@@ -60,7 +61,8 @@ def main():
         if ref_bytes is None:
             ref_bytes, ref_crc = y.clone(), crc.clone()
         else:
-            out[f"store{st}_identical"] = bool(torch.equal(y, ref_bytes) and torch.equal(crc, ref_crc))
+            same = torch.equal(y, ref_bytes) and (st >= 3 or torch.equal(crc, ref_crc))
+            out[f"store{st}_identical"] = bool(same)
     if len(args.store) > 1:
         want = _core.crc32c_chunks(packed.data_ptr(), pbytes, pchunk)
         out["crc_matches_reference"] = [x & 0xFFFFFFFF for x in ref_crc.tolist()] == list(want)
@@ -71,7 +73,11 @@ def main():
         y2 = torch.empty(src, dtype=torch.uint8, device="cuda")
         t = timed(lambda: _core.fp8_unpack(q.data_ptr(), scl.data_ptr(), src // 2, y2.data_ptr(), block), args.reps)
         out["plain_unpack_GBps"] = round((src // 2 + src // 2 // 32 + src) / t / 1e9, 1)
-        a = torch.empty(pbytes, dtype=torch.uint8, device="cuda")
+        c2 = torch.empty(nch, dtype=torch.int32, device="cuda")
+        t = timed(lambda: _core.crc32c_chunks_async(packed.data_ptr(), pbytes, pchunk, c2.data_ptr(), ws.data_ptr()),
+                  args.reps)
+        out["crc_only_packed_us"] = round(t * 1e6, 1)
+        out["plain_unpack_us"] = round((src // 2 + src // 2 // 32 + src) / (out["plain_unpack_GBps"] * 1e9) * 1e6, 1)
         t = timed(lambda: y2.copy_(buf), args.reps)
         out["torch_copy_512MiB_GBps"] = round(2 * src / t / 1e9, 1)
     print(json.dumps(out))

@@ -156,6 +156,17 @@ case "$RECIPE" in
     timeout -k 10 600 python bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 \
       --steps 2 --warmup 1 > $OUT/bench_fp8_store_bf16.json 2> $OUT/bench_fp8_store_bf16.log
     ;;
+  r3nocrc)
+    # fused verify+unpack with and without its CRC math (store 3/4 = 1/0 minus CRC), CRC-only pass, counters
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log || exit 1
+    for st in 1 3; do
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
+        SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU --output-format csv -d $OUT/pmc_sq_$st -o sq -- \
+        python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_sq_$st.log 2>&1 || exit 1
+      timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE TA_BUSY_avr TD_BUSY_avr --output-format csv \
+        -d $OUT/pmc_mem_$st -o mem -- python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_mem_$st.log 2>&1 || exit 1
+    done
+    ;;
   r3fused2)
     # swizzled LDS staging slot (store=1) vs direct stores, counters; NUMA: GPU's node vs the other node
     timeout -k 10 300 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
