@@ -301,13 +301,14 @@ void register_gpu_bindings(PyObject* module) {
   }, py::arg("src"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("dst"),
         py::arg("stream") = 0);
   m.def("fp8_verify_unpack_async", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block,
-                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream, int store) {
+                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream, int store,
+                                      int max_blocks) {
     check(kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
                                   reinterpret_cast<uint16_t*>(out), reinterpret_cast<uint32_t*>(crc_out_dev),
-                                  reinterpret_cast<void*>(ws), as_stream(stream), 0, store),
+                                  reinterpret_cast<void*>(ws), as_stream(stream), max_blocks, store),
           "fp8_verify_unpack");
   }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
-     py::arg("crc_out"), py::arg("ws"), py::arg("stream") = 0, py::arg("store") = -1);
+     py::arg("crc_out"), py::arg("ws"), py::arg("stream") = 0, py::arg("store") = -1, py::arg("max_blocks") = 0);
   // Fused verify + unpack (synchronous): writes the bf16 layer to `out`, returns
   // the CRC32C of every packed chunk.
   m.def("fp8_verify_unpack", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block, uint64_t out,

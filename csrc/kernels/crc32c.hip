@@ -712,9 +712,19 @@ uint32_t* device_consts() {
 // One workgroup per CU (LDS-bound), 16 segments per workgroup at a time,
 // grid-stride beyond that. Kernel trace on 1 GiB (profiles/r2_crc_slice):
 // 186.5 us with 256 workgroups, 185.0 with 512, 187.8 with 1024.
+// Workgroups for a segment walk: as few rounds of kWaves segments per
+// workgroup as `cap` allows, then as few workgroups as still need only that
+// many rounds. A wave takes segments g, g + nwaves, ..., so a last round that
+// only some waves reach costs a whole round: 16896 segments (512 MiB of
+// bf16 packed) on 256 x 16 waves are 4.125 rounds, 5 for the kernel; 212
+// workgroups do the same 5 rounds with every wave busy, and the freed CUs'
+// share of HBM goes to the rest: fused verify+unpack 4.30 -> 4.61 TB/s
+// (profiles/r3_tail).
 dim3 seg_grid(int64_t total_segs, int max_blocks) {
   const int64_t cap = max_blocks > 0 ? max_blocks : 256;
-  return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>((total_segs + kWaves - 1) / kWaves, cap))));
+  const int64_t rounds = std::max<int64_t>(1, (total_segs + cap * kWaves - 1) / (cap * kWaves));
+  const int64_t blocks = (total_segs + kWaves * rounds - 1) / (kWaves * rounds);
+  return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>(blocks, cap))));
 }
 
 struct Plan {

@@ -37,9 +37,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--store", type=int, nargs="*", default=[0, 1, 2, 3, 4])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--src-mib", type=int, default=512)
+    ap.add_argument("--max-blocks", type=int, default=0, help="cap on the fused kernel's workgroups (0: one per CU)")
     args = ap.parse_args()
     chunk, block = 64 << 20, 128
-    src = 512 << 20
+    src = args.src_mib << 20
     buf = torch.empty(src, dtype=torch.uint8, device="cuda")
     _core.fill_random(buf.data_ptr(), src, 11)
     pbytes = _core.fp8_packed_size(src, chunk, block)
@@ -48,13 +50,14 @@ def main():
     pchunk = chunk // 2 + chunk // 2 // block * 4
     nch = (pbytes + pchunk - 1) // pchunk
     ws = torch.empty(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device="cuda")
-    out = {"src_MiB": src >> 20, "packed_MiB": round(pbytes / 2**20, 1)}
+    out = {"src_MiB": src >> 20, "packed_MiB": round(pbytes / 2**20, 1), "segments": -(-pchunk // 16384) * nch,
+           "max_blocks": args.max_blocks}
     ref_bytes = ref_crc = None
     for st in args.store:
         y = torch.zeros(src, dtype=torch.uint8, device="cuda")
         crc = torch.zeros(nch, dtype=torch.int32, device="cuda")
         fn = lambda: _core.fp8_verify_unpack_async(packed.data_ptr(), src, chunk, block, y.data_ptr(),  # noqa: E731
-                                                    crc.data_ptr(), ws.data_ptr(), 0, st)
+                                                    crc.data_ptr(), ws.data_ptr(), 0, st, args.max_blocks)
         t = timed(fn, args.reps)
         out[f"store{st}_us"] = round(t * 1e6, 1)
         out[f"store{st}_GBps"] = round((pbytes + src) / t / 1e9, 1)
@@ -79,7 +82,7 @@ def main():
         out["crc_only_packed_us"] = round(t * 1e6, 1)
         out["plain_unpack_us"] = round((src // 2 + src // 2 // 32 + src) / (out["plain_unpack_GBps"] * 1e9) * 1e6, 1)
         t = timed(lambda: y2.copy_(buf), args.reps)
-        out["torch_copy_512MiB_GBps"] = round(2 * src / t / 1e9, 1)
+        out["torch_copy_GBps"] = round(2 * src / t / 1e9, 1)
     print(json.dumps(out))
 
 

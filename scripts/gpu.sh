@@ -167,6 +167,19 @@ case "$RECIPE" in
         -d $OUT/pmc_mem_$st -o mem -- python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_mem_$st.log 2>&1 || exit 1
     done
     ;;
+  r3tail)
+    # segment rounds: 512 MiB = 16896 segments = 4.125 rounds of 4096 waves; 4 GiB = 33 whole rounds
+    timeout -k 10 120 python scripts/fused_ab.py --store 1 3 > $OUT/ab_512.json 2> $OUT/ab_512.log &&
+    timeout -k 10 120 python scripts/fused_ab.py --store 1 3 --max-blocks 212 > $OUT/ab_512_mb212.json 2> $OUT/ab_512_mb212.log &&
+    timeout -k 10 200 python scripts/fused_ab.py --store 1 3 --src-mib 4096 --reps 5 > $OUT/ab_4096.json 2> $OUT/ab_4096.log
+    ;;
+  r3tail2)
+    # balanced segment rounds by default (seg_grid): fused A/B at 512 MiB and 4 GiB, CRC-only, kernel bench, tests
+    timeout -k 10 300 $PYTEST tests/test_gpu_kernels.py -k "crc or fused" > $OUT/pytest.log 2>&1 &&
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/ab_512.json 2> $OUT/ab_512.log &&
+    timeout -k 10 200 python scripts/fused_ab.py --store 1 3 --src-mib 4096 --reps 5 > $OUT/ab_4096.json 2> $OUT/ab_4096.log &&
+    timeout -k 10 200 python scripts/kernel_bench.py > $OUT/kernel_bench.json 2> $OUT/kernel_bench.log
+    ;;
   r3fused2)
     # swizzled LDS staging slot (store=1) vs direct stores, counters; NUMA: GPU's node vs the other node
     timeout -k 10 300 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&
