@@ -214,8 +214,8 @@ case "$RECIPE" in
     pids=()
     for r in $(seq 0 $((NR - 1))); do
       DISSEM_SHARED_GPU=1 RANK=$r LOCAL_RANK=0 WORLD_SIZE=$NR MASTER_ADDR=127.0.0.1 MASTER_PORT=29517 \
-        timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/rank$r -o q -- \
-        python3 bench.py --gpus $NR --steps 1 --warmup 1 --layers $((NR * 2)) --layer-mib 64 --chunk-mib 16 \
+        timeout -s KILL 300 rocprofv3 --kernel-trace --marker-trace --output-format csv -d $OUT/rank$r -o q -- \
+        python3 bench.py --gpus $NR --steps 2 --warmup 1 --layers $((NR * 2)) --layer-mib 64 --chunk-mib 16 \
         > $OUT/rank$r.json 2> $OUT/rank$r.log &
       pids+=($!)
     done
