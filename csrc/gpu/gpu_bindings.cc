@@ -167,7 +167,13 @@ void register_gpu_bindings(PyObject* module) {
         py::gil_scoped_release nogil;
         const std::string nm = name.empty() || name[0] != '/' ? "/" + name : name;
         int fd = shm_open(nm.c_str(), O_RDWR | (create ? O_CREAT | O_EXCL : 0), 0600);
-        if (fd < 0) throw std::runtime_error("shm_open " + nm + ": " + strerror(errno));
+        if (fd < 0) {
+          const int e = errno;
+          throw std::runtime_error("shm_open " + nm + ": " + strerror(e) +
+                                   (e == EEXIST ? " (left by an earlier run that did not finish: remove /dev/shm" + nm +
+                                                      " and the run's other /dev/shm/dld_* segments)"
+                                                : ""));
+        }
         if (create && ftruncate(fd, off_t(n)) != 0) {
           const int e = errno;
           close(fd);
