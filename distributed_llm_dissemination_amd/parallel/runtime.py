@@ -73,6 +73,16 @@ class SessionResult:
     engine_stats: Dict[str, float] = field(default_factory=dict)
 
 
+class _DeviceBytes:
+    """__cuda_array_interface__ of `n` bytes of HBM owned by a Runtime's engine
+    (torch.as_tensor keeps this object, and so the Runtime, alive)."""
+
+    def __init__(self, owner, ptr: int, n: int):
+        self._owner = owner
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (int(ptr), False),
+                                         "version": 3, "strides": None, "stream": None}
+
+
 class Runtime:
     def __init__(
         self,
@@ -108,6 +118,7 @@ class Runtime:
         node_key: str = "",
         host_share: bool = False,
         host_share_timeout_s: float = 600.0,
+        layer_source: Optional[Callable[[int, int], object]] = None,
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -134,6 +145,12 @@ class Runtime:
         # carries random bytes and its own CRC manifest.
         self.source_pool = int(source_pool)
         self._pool: Dict[int, object] = {}
+        # The bytes of the layers this rank seeds: layer_source(layer, size) ->
+        # any buffer of `size` bytes (bytes, numpy array, CPU tensor; e.g. a
+        # models/weights.py blob). Default: random bytes (splitmix64, layer_seed).
+        self.layer_source = layer_source
+        if layer_source is not None and self.source_pool:
+            raise ValueError("layer_source and source_pool are exclusive (a pool reuses one buffer for many layers)")
         # One NVMe shared by every rank of this node (BASELINE config #4): the
         # disk readers of all ranks draw from one budget (engine/node_pacer.h,
         # keyed by node_key) and mode 3 plans the ranks' disk tiers as one group.
@@ -162,6 +179,8 @@ class Runtime:
                 raise ValueError(f"--pack fp8 needs layer sizes and the chunk size to be multiples of {unit} B "
                                  f"(2 bytes x {pack_block}-element scale blocks); layers {sorted(bad)[:8]} are not")
         self.epoch = 0
+        self._closed = False
+        self.device: Optional[int] = None
         self.keep: List[object] = []  # buffers that must outlive sessions
         # Closed-loop link rates (planned engines): EWMA of this rank's measured
         # send rate to each peer node (B/s), reported with its announce.
@@ -206,6 +225,7 @@ class Runtime:
                 if self.world > 1 and nccl_uid is None:
                     raise ValueError("rccl engine with world > 1 needs an nccl unique id from the bootstrap")
                 _core.set_device(dev)
+                self.device = dev
                 self.engine = _core.gpu_engine(pcfg, dev, nccl_uid or b"")
             else:
                 # Simulated fabric: ranks in this process sharing `sim_key` exchange bytes
@@ -238,29 +258,56 @@ class Runtime:
             return _core.crc32c_chunks(ptr, size, self.grid)
         return _core.host_crc32c_chunks(ptr, size, self.grid)
 
+    def _source(self, layer: int, size: int) -> memoryview:
+        """layer_source's bytes for a layer, checked for size."""
+        import torch
+
+        obj = self.layer_source(layer, size)
+        if isinstance(obj, torch.Tensor):
+            obj = obj.detach().cpu().contiguous().view(torch.uint8).numpy()
+        mv = memoryview(obj).cast("B")
+        if mv.nbytes != size:
+            raise ValueError(f"layer_source({layer}) gave {mv.nbytes} B, the layer is {size} B")
+        return mv
+
+    def _source_bytes(self, layer: int, size: int, seed: int, off: int = 0, n: Optional[int] = None) -> bytes:
+        n = size - off if n is None else n
+        if self.layer_source is not None:
+            return bytes(self._source(layer, size)[off:off + n])
+        return _core.fill_random_host(n, seed, off) if off else _core.fill_random_host(n, seed)
+
+    def _fill_from_source(self, dev: int, layer: int, size: int, seed: int, host_buf=None) -> None:
+        """rccl: the layer's source bytes into device memory `dev` (and `host_buf`)."""
+        if self.layer_source is None:
+            _core.fill_random(dev, size, seed)
+            _core.device_synchronize()
+            if host_buf is not None:
+                _core.memcpy(host_buf.ptr, dev, size)
+            return
+        stage = host_buf if host_buf is not None else _core.HostBuffer.malloc(size)
+        stage.view()[:] = self._source(layer, size)
+        _core.memcpy(dev, stage.ptr, size)
+
     def _gen_layer(self, layer: int, size: int, seed: int, host_buf=None) -> None:
-        """Generate a layer's source bytes (random bf16 bit patterns when packing),
-        optionally copy them to `host_buf`, put the target-tier image (packed with
-        --pack fp8) into the layer's HBM slot and record its CRC manifest."""
+        """Generate a layer's source bytes (layer_source, or random bf16 bit
+        patterns), optionally copy them to `host_buf`, put the target-tier image
+        (packed with --pack fp8) into the layer's HBM slot and record its CRC
+        manifest."""
         slot = self.engine.device_ptr(layer)
         ssz = self.slot_sizes[layer]
         if self.engine_kind == "rccl":
             if self.pack == "fp8":
                 tmp = _core.device_malloc(size)
                 try:
-                    _core.fill_random(tmp, size, seed)
-                    if host_buf is not None:
-                        _core.memcpy(host_buf.ptr, tmp, size)
+                    self._fill_from_source(tmp, layer, size, seed, host_buf)
                     _core.fp8_pack_chunks(tmp, size, self.chunk_bytes, self.pack_block, slot)
                     _core.device_synchronize()
                 finally:
                     _core.device_free(tmp)
             else:
-                self._dev_fill(slot, size, seed)
-                if host_buf is not None:
-                    _core.memcpy(host_buf.ptr, slot, size)
+                self._fill_from_source(slot, layer, size, seed, host_buf)
         else:
-            data = _core.fill_random_host(size, seed)
+            data = self._source_bytes(layer, size, seed)
             if host_buf is not None:
                 _core.sim_write(host_buf.ptr, data)
             if self.pack == "fp8":
@@ -325,7 +372,7 @@ class Runtime:
                             self._pool[key] = buf
                     layers[l] = self._host_src(buf, l, size, rate, st)
                 else:
-                    data = _core.fill_random_host(size, seed)
+                    data = self._source_bytes(l, size, seed)
                     layers[l] = _core.LayerSrc.inmem(data, rate, _core.SourceType(st))
         if gpu and self.host_share:
             self._map_shared_layers(layers)
@@ -550,13 +597,13 @@ class Runtime:
         d = os.path.join(root, "layers", str(self.node_id))
         os.makedirs(d, exist_ok=True)
         path = os.path.join(d, f"{layer}.layer")
-        if not os.path.exists(path) or os.path.getsize(path) != size:
+        if self.layer_source is not None or not os.path.exists(path) or os.path.getsize(path) != size:
             tmp = path + ".tmp"
             with open(tmp, "wb") as f:
                 step = 256 * MiB
                 for off in range(0, size, step):
                     n = min(step, size - off)
-                    f.write(_core.fill_random_host(n, seed, off))
+                    f.write(self._source_bytes(layer, size, seed, off, n))
             os.replace(tmp, path)
         return path
 
@@ -890,7 +937,47 @@ class Runtime:
             raise RuntimeError(f"layer {layer}: packed chunks do not match the CRC manifest")
         return out
 
+    # ------------------------------------------------------ serving views
+    def layer_tensor(self, layer: int, unpacked: bool = False):
+        """The layer as this rank holds it in HBM, as a uint8 torch tensor.
+
+        rccl engine: a zero-copy view of the layer's HBM slot (the packed image
+        with --pack fp8; ``unpacked=True`` with --store bf16: the dequantized bf16
+        image the fused verify+unpack wrote), valid until close(). The view keeps
+        this Runtime alive. Other engines: a CPU copy of the same bytes."""
+        import torch
+
+        if self.engine is None:
+            return torch.frombuffer(bytearray(self.layer_bytes(layer)), dtype=torch.uint8)
+        if unpacked and self.pack == "fp8":
+            if self.store != "bf16":
+                raise ValueError("unpacked views need --store bf16 (use unpacked_layer_bytes for a copy)")
+            ptr, n = self.engine.unpacked_ptr(layer), self.sizes[layer]
+        else:
+            ptr, n = self.engine.device_ptr(layer), self.slot_sizes[layer]
+        if not ptr:
+            raise RuntimeError(f"layer {layer} is not resident on rank {self.rank}")
+        if self.engine_kind == "sim":
+            return torch.frombuffer(bytearray(_core.sim_read(ptr, n)), dtype=torch.uint8)
+        if self._closed:
+            raise RuntimeError("runtime is closed")
+        dev = torch.device("cuda", self.device)
+        return torch.as_tensor(_DeviceBytes(self, ptr, n), device=dev)
+
+    def layer_params(self, layer: int, spec):
+        """Named bf16 parameter views of a layer that holds a models/weights.py
+        blob: zero-copy in HBM on the rccl engine (the dequantized image with
+        --pack fp8 --store bf16), CPU copies otherwise."""
+        from ..models.weights import unflatten
+
+        if self.pack == "fp8" and self.store != "bf16":
+            import torch
+
+            return unflatten(torch.frombuffer(bytearray(self.unpacked_layer_bytes(layer)), dtype=torch.uint8), spec)
+        return unflatten(self.layer_tensor(layer, unpacked=True), spec)
+
     def close(self) -> None:
+        self._closed = True
         if self.engine is not None:
             self.engine.shutdown()
         self.transport.close()

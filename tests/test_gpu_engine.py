@@ -114,3 +114,43 @@ def test_hbm_capacity_is_checked_before_allocating():
     cfg = make_workload(1, 80, 4 << 30, tier="device", chunk_bytes=64 << 20)
     with pytest.raises(ValueError, match="HBM"):
         Runtime(cfg, 0, engine="rccl", chunk_bytes=64 << 20, registry={0: "127.0.0.1:0"})
+
+
+@pytest.mark.parametrize("pack", ["none", "fp8"])
+def test_layer_weights_zero_copy_in_hbm(gpu, pack):
+    """A Llama-family decoder layer (models/weights.py) staged into HBM by a session,
+    read back as named bf16 parameters that alias the HBM slot (or, with fp8, the
+    dequantized image the fused verify+unpack wrote) and run on the GPU."""
+    import torch
+
+    from distributed_llm_dissemination_amd.models.weights import (PRESETS, decoder_forward, flatten, layer_nbytes,
+                                                                 random_layer, unflatten)
+
+    spec = PRESETS["tiny"]
+    size = layer_nbytes(spec)
+    blobs = {l: flatten(random_layer(spec, 7 + l), spec) for l in range(2)}
+    cfg = make_workload(1, 2, size, tier="host", chunk_bytes=64 * 1024)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=64 * 1024, registry={0: "127.0.0.1:0"}, pack=pack,
+                 store="bf16" if pack == "fp8" else "packed", layer_source=lambda l, n: blobs[l])
+    try:
+        res = rt.run(1, timeout=60)
+        assert res.ok, res.error
+        x = torch.randn(1, 16, spec.hidden).to(torch.bfloat16)
+        for l in range(2):
+            p = rt.layer_params(l, spec)
+            t = rt.layer_tensor(l, unpacked=True)
+            assert t.is_cuda and t.numel() == size
+            want_ptr = rt.engine.unpacked_ptr(l) if pack == "fp8" else rt.engine.device_ptr(l)
+            assert t.data_ptr() == want_ptr and p["input_layernorm"].data_ptr() == want_ptr  # zero-copy
+            want = unflatten(blobs[l], spec)
+            if pack == "none":
+                assert all(torch.equal(p[k].cpu(), want[k]) for k in want)
+            else:
+                ref = gpu.fp8_unpack_layer_host(gpu.fp8_pack_layer_host(blobs[l].numpy().tobytes(), 64 * 1024, 128),
+                                                size, 64 * 1024, 128)
+                assert t.cpu().numpy().tobytes() == ref
+            y = decoder_forward(x.cuda(), p, spec).float().cpu()
+            y0 = decoder_forward(x, {k: p[k].cpu() for k in p}, spec).float()
+            assert float((y - y0).norm() / y0.norm()) < 2e-2
+    finally:
+        rt.close()
