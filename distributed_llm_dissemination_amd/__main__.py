@@ -73,6 +73,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="with --pack fp8: bf16 = also keep each layer dequantized to bf16 in HBM (fused "
                         "verify+unpack kernel on every landed chunk)")
     p.add_argument("--verify", default="crc32c", choices=["none", "crc32c"])
+    p.add_argument("--weights", default="", metavar="PRESET",
+                   help="layers hold random-init decoder-layer weights of this model (models/weights.py presets: "
+                        "tiny, llama3-8b, llama3-70b, llama3.1-405b; LayerSize must equal the preset's layer "
+                        "bytes) instead of random bytes; after delivery each rank runs its layers' forward pass "
+                        "on the received parameters")
     p.add_argument("--streams-per-peer", type=int, default=1,
                    help="P2P ops per peer and direction in one RCCL group")
     p.add_argument("--reserve-cus", type=int, default=-1,
@@ -231,6 +236,19 @@ def main(argv=None) -> int:
     client = cfg.client(my_id)
     if client is not None:
         registry[_core.CLIENT_ID] = client.addr
+    weights = None
+    if args.weights:
+        from .models.weights import PRESETS, layer_nbytes
+
+        if args.weights not in PRESETS:
+            print(f"error: --weights {args.weights}: presets are {', '.join(PRESETS)}", file=sys.stderr)
+            return 2
+        weights = PRESETS[args.weights]
+        bad = {l: n for l, n in cfg.layer_sizes().items() if n != layer_nbytes(weights)}
+        if bad:
+            print(f"error: --weights {args.weights} needs LayerSize {layer_nbytes(weights)} "
+                  f"(layers {sorted(bad)[:8]} differ)", file=sys.stderr)
+            return 2
     rt = Runtime(cfg, my_id, engine=args.engine, storage_path=args.s,
                  chunk_bytes=args.chunk_bytes or (args.chunk_mib << 20),
                  verify=not args.no_verify and args.verify != "none", registry=registry, barrier=barrier,
@@ -241,7 +259,8 @@ def main(argv=None) -> int:
                  engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(my_id)},
                  host_share=args.host_share and args.engine == "rccl", node_disk_gbps=args.node_disk_gbps,
                  node_key="c" + hashlib.blake2b((args.f + os.environ.get("MASTER_PORT", "")).encode(),
-                                                digest_size=6).hexdigest())
+                                                digest_size=6).hexdigest(),
+                 layer_source=_weights_source(weights) if weights is not None else None)
     if barrier is not None:
         # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
         import torch.distributed as dist
@@ -294,6 +313,8 @@ def main(argv=None) -> int:
     if not res.ok:
         print(json.dumps({"level": "error", "node": my_id, "error": res.error, "message": f"{role} failed"}),
               file=sys.stderr)
+    elif weights is not None and cfg.assignment.get(my_id):
+        _check_weights(rt, weights, cfg.assignment[my_id], my_id)
     if args.persist_dir and cfg.assignment.get(my_id) and (res.ok or rt.engine is not None):
         # After a failed session the planned engines keep what did land, chunk
         # by chunk: the next run with the same --persist-dir resumes from there.
@@ -317,6 +338,33 @@ def main(argv=None) -> int:
     time.sleep(0.05)  # let startup messages flush before sockets close
     rt.close()
     return 0 if res.ok else 1
+
+
+def _weights_source(spec):
+    """layer_source for --weights: layer l = random-init weights seeded by l."""
+    from .models.weights import flatten, random_layer
+
+    return lambda l, n: flatten(random_layer(spec, 1000 + l), spec)
+
+
+def _check_weights(rt, spec, layers, my_id: int) -> None:
+    """Serving smoke: each assigned layer as named parameters (zero-copy views in
+    HBM on the rccl engine), one forward pass, compared with the same pass on the
+    seeded weights."""
+    import torch
+
+    from .models.weights import decoder_forward, random_layer
+
+    x = torch.randn(1, 8, spec.hidden, generator=torch.Generator().manual_seed(0)).to(torch.bfloat16)
+    worst = 0.0
+    for l in sorted(layers):
+        p = rt.layer_params(l, spec)
+        dev = next(iter(p.values())).device
+        y = decoder_forward(x.to(dev), p, spec).float().cpu()
+        y0 = decoder_forward(x, random_layer(spec, 1000 + l), spec).float()
+        worst = max(worst, float((y - y0).norm() / y0.norm()))
+    print(json.dumps({"level": "info", "node": my_id, "layers": len(layers), "preset": spec.name,
+                      "max_rel_err": worst, "message": "weights forward check"}), file=sys.stderr, flush=True)
 
 
 def run_client(cfg, node_id: int) -> int:

@@ -159,3 +159,20 @@ def test_persist_dir_resume_skips_network(tmp_path):
     outs = run_nodes(cfg, [0, 1], 1, ["--persist-dir", pdir])
     assert all(rc == 0 for rc, _, _ in outs), [e[-2000:] for _, _, e in outs]
     assert "start receiving layer" not in outs[1][2]  # promoted from the persisted copies
+
+
+@pytest.mark.slow
+def test_two_process_weights_preset(tmp_path):
+    """--weights: the layers are random-init Llama-family decoder layers (models/weights.py);
+    the receiver reads its layers back as named parameters and runs their forward pass."""
+    from distributed_llm_dissemination_amd.models.weights import PRESETS, layer_nbytes
+
+    ports = free_ports(2)
+    cfg = write_config(tmp_path, ports, layers=2, size=layer_nbytes(PRESETS["tiny"]))
+    (rc0, out0, err0), (rc1, out1, err1) = run_nodes(cfg, [0, 1], 1, extra=("--weights", "tiny"))
+    assert rc0 == 0, err0
+    assert rc1 == 0, err1
+    check = [json.loads(line) for line in err1.splitlines() if "weights forward check" in line]
+    assert check and check[0]["layers"] == 2 and check[0]["max_rel_err"] == 0.0
+    bad = run_nodes(write_config(tmp_path, ports, layers=1, size=4096), [0], 1, extra=("--weights", "tiny"))
+    assert bad[0][0] == 2 and "needs LayerSize" in bad[0][2]
