@@ -129,13 +129,13 @@ def test_predicted_scaling_follows_the_link_bound():
 
 def test_slow_link_costs_at_most_a_seventh_with_the_link_aware_plan():
     """One directed link at half speed (8 ranks, headline mode 1, 1/1024 size,
-    timing slowed 4x). Lanes are per directed link, so the slow link holds back
+    timing slowed 16x so thread overhead stays out). Lanes are per directed link, so the slow link holds back
     only its own transfers; the leader's link-aware plan (owner policy
     "links" with the config's Links) then moves chunk slices of the layers it
     carries onto relays - ranks that receive the same layer directly - until
     the slowest link no longer sets the pace: <= 1/7 extra time, where a plan
     that ignores the link takes ~2x."""
-    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=2, slowdown=4,
+    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=2, slowdown=16,
               policy={"owner_policy": "links"})
     base = predict_scaling.predict(8, **kw)["ms_per_step"]
     slow = predict_scaling.predict(8, slow_link=((0, 1), 0.5), adapt_links=False, **kw)["ms_per_step"]
@@ -200,7 +200,7 @@ def test_closed_loop_routes_around_an_unconfigured_slow_link():
     per-link busy throughput into an EWMA and announces it, so the leader's
     second plan relays around the slow link: <= 1/7 extra time (reference
     analog: node.go:774-793 times jobs, :1044-1053 steers by those times)."""
-    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=2, slowdown=4,
+    kw = dict(layers=32, scale=1024, link_gbps=50.0, pcie_gbps=57.5, mode=1, steps=2, slowdown=16,
               policy={"owner_policy": "links"})
     base = predict_scaling.predict(8, **kw)["ms_per_step"]
     r = predict_scaling.predict(8, slow_link=((0, 1), 0.5), **kw)
