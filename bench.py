@@ -88,6 +88,9 @@ def parse_args(argv=None):
     p.add_argument("--no-adapt-links", action="store_true",
                    help="plan every session on the fixed link estimates instead of the per-link rates the ranks "
                         "measured (probe + earlier sessions' busy throughput, EWMA)")
+    p.add_argument("--no-hierarchical", action="store_true",
+                   help="ranks on several hosts: plan every dest from the holders directly instead of importing a "
+                        "layer once per host and relaying it over that host's xGMI (mode 1, links policy)")
     p.add_argument("--no-fallback", action="store_true",
                    help="N > 1 under torchrun: run the worker in this process (no supervised fresh-process "
                         "attempts with fallback data-plane settings)")
@@ -214,7 +217,7 @@ def worker(args, world, rank, chan) -> int:
     json_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
-    from distributed_llm_dissemination_amd.utils.launch import rank_device, shared_gpu
+    from distributed_llm_dissemination_amd.utils.launch import advertised, gather_hosts, listen_addr, rank_device, shared_gpu
 
     beat = chan.heartbeat if chan is not None else (lambda phase: None)
     beat("start")
@@ -259,6 +262,8 @@ def worker(args, world, rank, chan) -> int:
         barrier = dist.barrier
     else:
         barrier = lambda: None  # noqa: E731
+    # ranks on several machines (multi-node torchrun): host-aware lanes and plans
+    hosts = gather_hosts(rank) if world > 1 else None
     beat("setup")
     if chan is not None and chan.attempt in faults.fail_attempts.get(rank, []):
         failed(f"fault injection: fail-attempt={rank}@{chan.attempt}")
@@ -287,12 +292,12 @@ def worker(args, world, rank, chan) -> int:
     node_key = "b" + hashlib.blake2b(run_tag.encode(), digest_size=6).hexdigest()
     disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else (13.3 if args.tier == "disk" else 0.0)
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
-                 verify=not args.no_verify, payload_seed=args.seed, registry={rank: "127.0.0.1:0"},
+                 verify=not args.no_verify, payload_seed=args.seed, registry={rank: listen_addr(bool(hosts))},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
                  store=args.store, group_timeout_s=min(300.0, args.timeout),
                  engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(rank)},
                  inject_corrupt=faults.drop_chunk, source_pool=args.source_pool, host_share=args.host_share,
-                 node_key=node_key, node_disk_gbps=disk_gbps)
+                 node_key=node_key, node_disk_gbps=disk_gbps, hosts=hosts)
     beat("comm ready")
     if args.pack != "none":
         # bytes that land in HBM (and cross PCIe/xGMI) are the packed ones
@@ -300,7 +305,7 @@ def worker(args, world, rank, chan) -> int:
         total_bytes = src_bytes * rt.slot_sizes[0] // rt.sizes[0]
     if world > 1:
         addrs = [None] * world
-        dist.all_gather_object(addrs, rt.transport.address())
+        dist.all_gather_object(addrs, advertised(rt.transport.address()))
         rt.transport.set_registry({i: a for i, a in enumerate(addrs)})
     if args.host_share:
         barrier()  # every rank has mapped the shared segments: drop their names
@@ -322,7 +327,7 @@ def worker(args, world, rank, chan) -> int:
     policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, 2 * (world - 1)),
                   owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective",
-                  adapt_links=not args.no_adapt_links)
+                  adapt_links=not args.no_adapt_links, hierarchical=not args.no_hierarchical)
 
     def step(timed: bool, i: int):
         beat(f"{'step' if timed else 'warmup'} {i}")
@@ -429,6 +434,8 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["comm_init_ms_max"] = round(max(init_ms), 1)
             out["config"]["comm_connect_ms_rank0"] = round(es.comm_connect_ms, 1)
             out["config"]["comm_init"] = args.comm_init
+            if hosts:
+                out["config"]["hosts"] = len(set(hosts.values()))
         if world > 1:
             # GB/s per directed link: averaged over the timed wall time, and while
             # its send groups were on the device (busy).

@@ -267,17 +267,25 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("nccl_max_ctas", &PlannedConfig::nccl_max_ctas)
       .def_readwrite("nccl_register", &PlannedConfig::nccl_register)
       .def_readwrite("lanes", &PlannedConfig::lanes)
+      .def_readwrite("hosts", &PlannedConfig::hosts)
+      .def_readwrite("host_lane_classes", &PlannedConfig::host_lane_classes)
       .def_readwrite("unpack_store", &PlannedConfig::unpack_store)
       .def_readwrite("link_rate", &PlannedConfig::link_rate)
       .def_readwrite("comm_init", &PlannedConfig::comm_init)
       .def_readwrite("node_disk_rate", &PlannedConfig::node_disk_rate)
       .def_readwrite("node_disk_key", &PlannedConfig::node_disk_key);
-  m.def("resolve_lanes", [](int world, int lanes) {
+  m.def("resolve_lanes", [](int world, int lanes, int hosts, int classes) {
     PlannedConfig c;
     c.world = world;
     c.lanes = lanes;
+    c.hosts = hosts;
+    c.host_lane_classes = classes;
     return resolve_lanes(c);
-  }, py::arg("world"), py::arg("lanes") = 0);
+  }, py::arg("world"), py::arg("lanes") = 0, py::arg("hosts") = 1, py::arg("classes") = 0);
+  m.def("lane_of", [](int src, int dst, int world, int lanes, int hosts, int classes) {
+    return lane_of_hosts(src, dst, world, lanes, hosts, classes);
+  }, py::arg("src"), py::arg("dst"), py::arg("world"), py::arg("lanes"), py::arg("hosts") = 1,
+     py::arg("classes") = 0);
   py::class_<PlannedStats>(m, "PlannedStats")
       .def_readonly("bytes_sent", &PlannedStats::bytes_sent)
       .def_readonly("bytes_recv", &PlannedStats::bytes_recv)
@@ -369,7 +377,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("link", &SimTiming::link)
       .def_readwrite("stage_bps", &SimTiming::stage_bps)
       .def_readwrite("copy_bytes", &SimTiming::copy_bytes)
-      .def_readwrite("p2p_rounds", &SimTiming::p2p_rounds);
+      .def_readwrite("p2p_rounds", &SimTiming::p2p_rounds)
+      .def_readwrite("host", &SimTiming::host)
+      .def_readwrite("nic_bps", &SimTiming::nic_bps);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
   m.def("sim_read", [](uint64_t ptr, int64_t n) {
@@ -458,7 +468,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("adapt_links", &NodeConfig::adapt_links)
       .def_readwrite("disk_group", &NodeConfig::disk_group)
       .def_readwrite("disk_group_bw", &NodeConfig::disk_group_bw)
-      .def_readwrite("host_share", &NodeConfig::host_share);
+      .def_readwrite("host_share", &NodeConfig::host_share)
+      .def_readwrite("host", &NodeConfig::host);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)

@@ -19,6 +19,7 @@
 //    multi-rank schedules, deadlock freedom and timing without GPUs.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -152,6 +153,37 @@ inline int lane_of(int src, int dst, int world, int lanes) {
   return (d - 1) % lanes;
 }
 
+// Several hosts (multi-node): `hosts` hosts of g = world / hosts ranks each,
+// rank r on host r / g (torchrun's rank order). A pair on one host uses the
+// directed lanes of a host's xGMI mesh (by local index). A pair across hosts
+// uses a lane of its (host distance, local distance class, sender color):
+// the cycle coloring over hosts keeps a GPU's sends to and recvs from another
+// host on different lanes, and `classes` (1..g) spreads a GPU's remote peers
+// over that many lanes per direction (classes = g: one lane per directed link,
+// = directed_lanes(world) lanes in all; fewer classes share a lane between
+// remote peers, which then wait on each other in key order).
+// classes <= 0: auto, about 8 cross-host lanes in all (2 hosts: 4 classes per
+// direction; the 2 x 8-GPU sim: 22 lanes run as fast as 30, 16 lanes ~2x
+// slower, profiles/r3_multihost/).
+inline int host_lane_classes(int world, int hosts, int classes) {
+  const int g = world / hosts;
+  if (classes <= 0) classes = 8 / ((hosts - 1) * lane_colors(hosts));
+  return std::max(1, std::min(classes, g));
+}
+inline int host_lanes(int world, int hosts, int classes) {
+  if (hosts <= 1 || world % hosts) return directed_lanes(world);
+  const int g = world / hosts, k = host_lane_classes(world, hosts, classes);
+  return directed_lanes(g) + (hosts - 1) * k * lane_colors(hosts);
+}
+inline int lane_of_hosts(int src, int dst, int world, int lanes, int hosts, int classes) {
+  if (hosts <= 1 || world % hosts || lanes != host_lanes(world, hosts, classes)) return lane_of(src, dst, world, lanes);
+  const int g = world / hosts, hs = src / g, hd = dst / g, k = host_lane_classes(world, hosts, classes);
+  if (hs == hd) return lane_of(src % g, dst % g, g, directed_lanes(g));
+  const int dh = ((hd - hs) % hosts + hosts) % hosts, c = lane_colors(hosts);
+  const int dl = ((dst % g - src % g) % g + g) % g;
+  return directed_lanes(g) + ((dh - 1) * k + dl % k) * c + lane_color(hs, dh, hosts, c);
+}
+
 struct SimFabricStats {
   int64_t matched = 0, bytes = 0;
 };
@@ -167,6 +199,12 @@ struct SimTiming {
   // after round d completed. Irregular groups can then deadlock where
   // independent ops would not; one-distance groups (lanes = world-1) cannot.
   bool p2p_rounds = false;
+  // Several hosts (multi-node runs): rank -> host id (empty: one host). A
+  // transfer between ranks on different hosts also occupies the sender's NIC
+  // (egress) and the receiver's NIC (ingress), each nic_bps per direction, at
+  // min(link, NIC): one NIC per GPU, shared by all of that GPU's remote peers.
+  std::vector<int> host;
+  double nic_bps = 0;
 };
 
 // In-process simulated fabric: ranks of one "communicator" share `comm_key`.

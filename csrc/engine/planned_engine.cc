@@ -1243,6 +1243,7 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
     if (!std::binary_search(dead.begin(), dead.end(), r)) nodes.push_back(cfg_.rank_nodes[size_t(r)]);
   cfg_.rank_nodes = nodes;
   cfg_.world = int(nodes.size());
+  cfg_.hosts = 1;  // the survivors no longer fill whole hosts: per-distance lanes (as the backend's)
   cfg_.rank = new_rank;
   node_rank_.clear();
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;

@@ -68,6 +68,10 @@ struct PlannedConfig {
   // group's ops in rounds of one distance each, so a multi-distance group can
   // wait on itself across ranks (SimTiming::p2p_rounds reproduces it).
   int lanes = 0;
+  // Multi-node runs: the ranks sit in this many hosts of world / hosts GPUs
+  // each, in rank order (backend.h host_lanes); 1 = one host.
+  int hosts = 1;
+  int host_lane_classes = 0;       // lanes per direction to each other host (backend.h host_lanes; 0 = auto)
   std::map<NodeID, int64_t> link_rate;  // cap this rank's sends to a node (B/s; slow-link injection)
   int group_peers = 1;             // ops per peer and direction per group
   int disk_readers = 4;            // NVMe reader threads (O_DIRECT pread into pinned bounce buffers)
@@ -126,6 +130,11 @@ struct PlannedConfig {
 // equals directed_lanes).
 inline int resolve_lanes(const PlannedConfig& c) {
   if (c.world <= 1) return 1;
+  // several hosts: host-aware lanes while they stay few (a communicator and a
+  // hardware queue each), else the per-distance lanes below
+  if (c.lanes <= 0 && c.hosts > 1 && c.world % c.hosts == 0 && c.world / c.hosts <= 8 &&
+      host_lanes(c.world, c.hosts, c.host_lane_classes) <= 32)
+    return host_lanes(c.world, c.hosts, c.host_lane_classes);
   if (c.lanes <= 0) return c.world <= 8 ? directed_lanes(c.world) : std::min(c.world - 1, 7);
   return std::min(c.lanes, directed_lanes(c.world));
 }
@@ -317,7 +326,8 @@ class PlannedEngine : public DataEngine {
            bounce_busy_.empty();
   }
   int lane_for(int peer, bool send) const {
-    return send ? lane_of(cfg_.rank, peer, cfg_.world, lanes_) : lane_of(peer, cfg_.rank, cfg_.world, lanes_);
+    return send ? lane_of_hosts(cfg_.rank, peer, cfg_.world, lanes_, cfg_.hosts, cfg_.host_lane_classes)
+                : lane_of_hosts(peer, cfg_.rank, cfg_.world, lanes_, cfg_.hosts, cfg_.host_lane_classes);
   }
   // Events shared by several chunks (a lane mark after a recv group): refcounted.
   void ev_hold(Ev e) {

@@ -12,7 +12,8 @@
 // len / link_bps after the link's previous transfer (full duplex, links
 // independent); a staging copy occupies the rank's copy queue for
 // len / stage_bps. With copy_bytes = false no payload moves (timing-only runs
-// of full-size schedules in little memory).
+// of full-size schedules in little memory). Multi-host fabrics (host, nic_bps)
+// also charge a cross-host transfer to both ends' NICs.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -61,10 +62,15 @@ struct Fabric {
   std::set<int> crashed;  // fault injection: ranks whose posts no longer move bytes
   SimTiming timing;
   std::map<std::pair<int, int>, Clock::time_point> link_free;  // timing model: directed link busy until
+  std::map<int, Clock::time_point> nic_out_free, nic_in_free;   // timing model: per-rank NIC busy until
 
   double link_rate(int src, int dst) const {
     auto it = timing.link.find({src, dst});
     return it != timing.link.end() ? it->second : timing.link_bps;
+  }
+  bool cross_host(int src, int dst) const {
+    const auto& h = timing.host;
+    return src < int(h.size()) && dst < int(h.size()) && h[size_t(src)] != h[size_t(dst)];
   }
 
   void post(int lane, int src, int dst, bool send, Posted* op) {
@@ -87,11 +93,15 @@ struct Fabric {
         if (timing.copy_bytes) memcpy(r->ptr, s->ptr, size_t(s->len));
         stats.matched++;
         stats.bytes += s->len;
-        const double bps = link_rate(src, dst);
+        double bps = link_rate(src, dst);
+        const bool nic = timing.nic_bps > 0 && cross_host(src, dst);
+        if (nic) bps = bps > 0 ? std::min(bps, timing.nic_bps) : timing.nic_bps;
         if (bps > 0) {
           auto& free_at = link_free[{src, dst}];
-          const auto start = std::max(Clock::now(), free_at);
+          auto start = std::max(Clock::now(), free_at);
+          if (nic) start = std::max({start, nic_out_free[src], nic_in_free[dst]});
           free_at = start + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(s->len) / bps));
+          if (nic) nic_out_free[src] = nic_in_free[dst] = free_at;
           s->done_at = r->done_at = free_at;
         }
       }

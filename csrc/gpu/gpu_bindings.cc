@@ -402,6 +402,8 @@ void register_gpu_bindings(PyObject* module) {
     hc.nccl_max_ctas = cfg.nccl_max_ctas;
     hc.nccl_register = cfg.nccl_register;
     hc.lanes = resolve_lanes(cfg);
+    hc.hosts = cfg.hosts;
+    hc.host_lane_classes = cfg.host_lane_classes;
     if (cfg.comm_init != "parallel" && cfg.comm_init != "split")
       throw std::runtime_error("comm_init must be parallel or split, not " + cfg.comm_init);
     hc.parallel_init = cfg.comm_init == "parallel";

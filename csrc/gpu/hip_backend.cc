@@ -144,7 +144,8 @@ class HipBackend : public Backend {
     if (one_group) NCCL_OK(ncclGroupStart());
     for (int d = 1; d < world; ++d) {
       const int to = (cfg_.rank + d) % world, from = (cfg_.rank - d + world) % world;
-      const size_t ls = size_t(lane_of(cfg_.rank, to, world, lanes)), lr = size_t(lane_of(from, cfg_.rank, world, lanes));
+      const size_t ls = size_t(lane_of_hosts(cfg_.rank, to, world, lanes, cfg_.hosts, cfg_.host_lane_classes)),
+                   lr = size_t(lane_of_hosts(from, cfg_.rank, world, lanes, cfg_.hosts, cfg_.host_lane_classes));
       uint8_t* rbuf = sbuf + 4096 * size_t(std::min(d, 15));  // distinct landing per recv of the group
       if (!one_group) NCCL_OK(ncclGroupStart());
       NCCL_OK(ncclSend(sbuf, 64, ncclUint8, to, nccl_[ls], comm_[ls]));
@@ -367,6 +368,7 @@ class HipBackend : public Backend {
     for (int r = 0; r < cfg_.rank; ++r)
       if (std::find(dead.begin(), dead.end(), r) == dead.end()) ++new_rank;
     cfg_.world -= int(dead.size());
+    cfg_.hosts = 1;  // the survivors no longer fill whole hosts (as the engine's lane map)
     cfg_.rank = new_rank;
     {
       std::lock_guard<std::mutex> lk(mu_);

@@ -36,6 +36,8 @@ struct HipBackendConfig {
   int reserve_cus = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
   int lanes = 1;                               // comm lanes (communicator + stream each)
+  int hosts = 1;                               // multi-node: hosts of world / hosts ranks (backend.h host_lanes)
+  int host_lane_classes = 0;
   bool nccl_register = false;                  // ncclCommRegister every layer slot
   bool parallel_init = true;                   // per-lane ids: init all lane communicators in one group
 };

@@ -71,6 +71,11 @@ struct NodeConfig {
   // instead of the leader's one (reference mode 0: the leader pushes
   // everything, node.go:326-352; that stays the default).
   bool host_share = false;
+  // Multi-node runs: node -> host (GPUs of one host share an xGMI mesh; hosts
+  // are joined by one NIC per GPU). Empty / one value: a single host. With
+  // several, mode 1's "links" policy imports a layer once per host and relays
+  // it inside the host (Node::schedule_imports).
+  std::map<NodeID, int> host;
 };
 
 struct NodeStats {
@@ -172,6 +177,13 @@ class Node {
   };
   using RelayPlan = std::map<std::pair<NodeID, LayerID>, std::vector<PlanPart>>;  // (dest, layer) -> parts
   void relay_rebalance(RelayPlan& plan, const std::function<double(NodeID, NodeID)>& cap);
+  // multi-host (cfg_.host): (host, layer) -> dests of that host needing the layer + their missing ranges
+  using ImportMap =
+      std::map<std::pair<int, LayerID>, std::vector<std::pair<NodeID, std::vector<std::pair<int64_t, int64_t>>>>>;
+  void schedule_imports(const ImportMap& imports, RelayPlan& plan, const std::function<double(NodeID, NodeID)>& cap);
+  void relay_across_hosts(LayerID layer, int64_t total, const std::vector<NodeID>& remote, std::map<int, int64_t>& rot);
+  int host_of(NodeID n) const;
+  bool multi_host() const;
   void schedule_mode2();
   void schedule_mode3();
   // mode 2 (node.go:628-1073); a job is (layer, dest, byte range)

@@ -232,6 +232,11 @@ def main(argv=None) -> int:
                 dist.broadcast_object_list(box, src=0)
                 uid = box[0]
             barrier = dist.barrier
+    hosts = None
+    if world > 1:
+        from .utils.launch import gather_hosts
+
+        hosts = gather_hosts(my_id)  # multi-node torchrun: host-aware lanes and plans
     registry = cfg.registry()
     client = cfg.client(my_id)
     if client is not None:
@@ -260,13 +265,15 @@ def main(argv=None) -> int:
                  host_share=args.host_share and args.engine == "rccl", node_disk_gbps=args.node_disk_gbps,
                  node_key="c" + hashlib.blake2b((args.f + os.environ.get("MASTER_PORT", "")).encode(),
                                                 digest_size=6).hexdigest(),
-                 layer_source=_weights_source(weights) if weights is not None else None)
+                 layer_source=_weights_source(weights) if weights is not None else None, hosts=hosts)
     if barrier is not None:
         # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
         import torch.distributed as dist
 
         pairs = [None] * dist.get_world_size()
-        dist.all_gather_object(pairs, (my_id, rt.transport.address()))
+        from .utils.launch import advertised
+
+        dist.all_gather_object(pairs, (my_id, advertised(rt.transport.address())))
         reg = dict(registry)
         reg.update({nid: addr for nid, addr in pairs})
         rt.transport.set_registry(reg)

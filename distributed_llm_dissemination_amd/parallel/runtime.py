@@ -119,6 +119,7 @@ class Runtime:
         host_share: bool = False,
         host_share_timeout_s: float = 600.0,
         layer_source: Optional[Callable[[int, int], object]] = None,
+        hosts: Optional[Dict[int, object]] = None,
     ):
         self.cfg = cfg
         self.node_id = node_id
@@ -168,6 +169,14 @@ class Runtime:
         self.payload_seed = payload_seed
         self._barrier = barrier or (lambda: None)
         self.node_ids = sorted(n.id for n in cfg.nodes)
+        # node -> host group: GPUs of one host share its xGMI mesh, hosts are
+        # joined by one NIC per GPU (config "Host", or `hosts` - e.g. every
+        # rank's hostname under a multi-node torchrun - which takes precedence)
+        if hosts:
+            groups: Dict[object, int] = {}
+            self.hosts = {n: groups.setdefault(hosts.get(n, ""), len(groups)) for n in self.node_ids}
+        else:
+            self.hosts = cfg.hosts()
         self.rank = self.node_ids.index(node_id)
         self.world = len(self.node_ids)
         self.sizes = cfg.layer_sizes()
@@ -212,6 +221,7 @@ class Runtime:
             pcfg.max_retries = max_retries
             pcfg.group_timeout_s = group_timeout_s
             pcfg.group_peers = group_peers
+            pcfg.hosts = self.uniform_hosts()
             if self.node_disk_gbps > 0:
                 pcfg.node_disk_rate = int(self.node_disk_gbps * 1e9)
                 pcfg.node_disk_key = node_key or sim_key
@@ -458,6 +468,9 @@ class Runtime:
     # rate (profiles/r1_fp8/kernel_bench.json: 5.3 TB/s) - never binding next to
     # 7 xGMI links, but the graph states it (SURVEY C13')
     HBM_PLAN_GBPS = 5000.0
+    # One GPU's NIC per direction on a multi-node cluster (a 400 Gb/s NIC per
+    # GPU): the rate of a link between GPUs of different hosts in the plan.
+    NIC_PLAN_GBPS = 50.0
 
     # Headroom kept free of layer slots: CRC workspaces, fp8 staging scratch,
     # RCCL's own buffers, PyTorch's context.
@@ -632,6 +645,7 @@ class Runtime:
         link_bw: Optional[Dict[tuple, int]] = None,
         hbm_gbps: Optional[float] = None,
         adapt_links: bool = True,
+        hierarchical: bool = True,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed).
 
@@ -646,7 +660,12 @@ class Runtime:
         ``adapt_links`` (closed loop): this rank announces its measured send
         rate to each peer (``link_report``: EWMA over earlier sessions and the
         pre-flight probe), and the leader plans on every rank's reports in place
-        of the estimates above."""
+        of the estimates above.
+
+        ``hierarchical`` (multi-host runs): mode 1's "links" policy imports a
+        layer once per host and relays it over that host's xGMI mesh
+        (Node::schedule_imports); False plans every dest from the holders
+        directly, as on one host."""
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()
@@ -680,9 +699,11 @@ class Runtime:
         if hbm_gbps > 0:
             nc.hbm_bw = {n.id: int(hbm_gbps * 1e9) for n in self.cfg.nodes}
         nc.host_share = self.host_share
-        if self.node_disk_gbps > 0:  # every rank of this node reads the same NVMe
-            nc.disk_group = {n.id: 0 for n in self.cfg.nodes}
-            nc.disk_group_bw = {0: int(self.node_disk_gbps * 1e9)}
+        if hierarchical and len(set(self.hosts.values())) > 1:
+            nc.host = dict(self.hosts)
+        if self.node_disk_gbps > 0:  # every rank of a host reads that host's one NVMe
+            nc.disk_group = {n.id: self.hosts.get(n.id, 0) for n in self.cfg.nodes}
+            nc.disk_group_bw = {h: int(self.node_disk_gbps * 1e9) for h in set(self.hosts.values())}
         nc.adapt_links = adapt_links
         if adapt_links:
             nc.link_report = self.link_report()
@@ -753,6 +774,20 @@ class Runtime:
         self._last_node = node  # on failure keep it alive for inspection
         return res
 
+    def uniform_hosts(self) -> int:
+        """H when the ranks fill H hosts with the same number of GPUs each, in
+        rank order (torchrun's layout; the engine's host-aware comm lanes,
+        backend.h host_lanes), else 1."""
+        seq = [self.hosts.get(n, 0) for n in self.node_ids]
+        h = len(set(seq))
+        if h <= 1 or self.world % h:
+            return 1
+        g = self.world // h
+        blocks = [seq[i * g:(i + 1) * g] for i in range(h)]
+        if any(len(set(b)) != 1 for b in blocks) or len({b[0] for b in blocks}) != h:
+            return 1
+        return h
+
     # ------------------------------------------------- closed-loop link rates
     LINK_EWMA_ALPHA = 0.5   # weight of the newest measurement
     LINK_SNAP = 0.15        # reports within this fraction of the median are reported as the median
@@ -806,17 +841,30 @@ class Runtime:
                       "group_us_hist", "land_us_hist")
         }
 
-    def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0) -> Dict[tuple, int]:
-        """Per directed (node, node) link capacity for the mode-3 planner from the
-        GPU topology (SURVEY C4/C13'): xGMI links at `xgmi_gbps` divided by their
-        hop count, anything else at `pcie_gbps`. Node i runs on device `device`
-        from the config, else its rank (one process per GPU of this node)."""
-        dev = {n.id: (n.device if n.device is not None else self.node_ids.index(n.id)) for n in self.cfg.nodes}
+    def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0,
+                         nic_gbps: Optional[float] = None) -> Dict[tuple, int]:
+        """Per directed (node, node) link capacity for the planners from the GPU
+        topology (SURVEY C4/C13'): xGMI links at `xgmi_gbps` divided by their
+        hop count, other same-host pairs at `pcie_gbps`, pairs on different
+        hosts at `nic_gbps` (default NIC_PLAN_GBPS). Node i runs on device
+        `device` from the config, else its index among its host's nodes (one
+        process per GPU; this host's topology stands for every host's)."""
+        nic = self.NIC_PLAN_GBPS if nic_gbps is None else nic_gbps
+        local: Dict[int, int] = {}
+        per_host: Dict[int, int] = {}
+        for n in self.node_ids:
+            h = self.hosts.get(n, 0)
+            local[n] = per_host.get(h, 0)
+            per_host[h] = local[n] + 1
+        dev = {n.id: (n.device if n.device is not None else local[n.id]) for n in self.cfg.nodes}
         links = {(i, j): (kind, hops) for i, j, kind, hops, _ in _core.gpu_topology()}
         out = {}
         for a in self.node_ids:
             for b in self.node_ids:
                 if a == b:
+                    continue
+                if self.hosts.get(a, 0) != self.hosts.get(b, 0):
+                    out[(a, b)] = int(nic * 1e9)
                     continue
                 kind, hops = links.get((dev[a], dev[b]), ("other", 1))
                 gbps = xgmi_gbps / max(1, hops) if kind == "xgmi" else pcie_gbps

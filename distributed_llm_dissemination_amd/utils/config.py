@@ -10,9 +10,11 @@ Go's encoding/json matches keys case-insensitively ("Id" == "ID"); so do we.
 Unlike the reference (quirk Q15), malformed files raise instead of yielding an
 empty config.
 
-Extensions (all optional): per node ``"Device"`` (GPU ordinal), top-level
-``"Links"`` (``{"<src>": {"<dst>": bytes_per_s}}`` directed link bandwidths for
-the topology-aware mode-3 planner) and ``"ChunkBytes"``.
+Extensions (all optional): per node ``"Device"`` (GPU ordinal) and ``"Host"``
+(the machine the node's GPU sits in: GPUs of one host share its xGMI mesh,
+hosts are joined by the network; default: one host), top-level ``"Links"``
+(``{"<src>": {"<dst>": bytes_per_s}}`` directed link bandwidths for the
+topology-aware planners) and ``"ChunkBytes"``.
 """
 
 from __future__ import annotations
@@ -58,6 +60,7 @@ class NodeConf:
     sources: Dict[int, int] = field(default_factory=dict)  # source type -> rate (B/s)
     initial_layers: Dict[int, Dict[int, int]] = field(default_factory=dict)  # source -> layer -> size
     device: Optional[int] = None
+    host: Optional[str] = None
 
     def layer_ids(self) -> List[int]:
         return sorted({l for per in self.initial_layers.values() for l in per})
@@ -101,6 +104,12 @@ class Config:
     def network_bw(self) -> Dict[int, int]:
         return {n.id: n.network_bw for n in self.nodes}
 
+    def hosts(self) -> Dict[int, int]:
+        """node id -> host group (0, 1, ... in order of first appearance); every
+        node on host 0 when no node names its Host."""
+        groups: Dict[str, int] = {}
+        return {n.id: groups.setdefault(n.host or "", len(groups)) for n in self.nodes}
+
     def registry(self) -> Dict[int, str]:
         return {n.id: n.addr for n in self.nodes}
 
@@ -132,6 +141,7 @@ class Config:
                         for st, per in n.initial_layers.items()
                     },
                     **({"Device": n.device} if n.device is not None else {}),
+                    **({"Host": n.host} if n.host is not None else {}),
                 }
                 for n in self.nodes
             ],
@@ -196,6 +206,7 @@ def parse_config(raw: Dict[str, Any]) -> Config:
             if flat:
                 initial[SOURCE_MEM] = flat
         dev = _get(nr, "Device")
+        host = _get(nr, "Host")
         nodes.append(
             NodeConf(
                 id=nid,
@@ -205,6 +216,7 @@ def parse_config(raw: Dict[str, Any]) -> Config:
                 sources=sources,
                 initial_layers=initial,
                 device=None if dev is None else _int(dev, "Device"),
+                host=None if host is None else str(host),
             )
         )
     ids = [n.id for n in nodes]

@@ -14,6 +14,7 @@
 #   init       parallel vs split lane-communicator set-up at 8 shared ranks; rank-death re-form
 #   r3rehearse host-share (config #2), disk tier + node NVMe budget (config #4) at 8 shared ranks; N = 1 A/Bs
 #   r3kernels  fused verify+unpack store A/B + counters, copy bandwidth beside CRC, NUMA A/B
+#   multihost  8 shared ranks rehearsed as 2 hosts x 4 GPUs: host-aware lanes, hierarchical vs flat mode 1
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
@@ -197,6 +198,17 @@ case "$RECIPE" in
       DISSEM_NUMA_NODE=1 timeout -k 10 200 python bench.py --steps 5 --warmup 1 > $OUT/numa_node1_$i.json \
         2> $OUT/numa_node1_$i.log || exit 1
     done
+    ;;
+  multihost)
+    # 8 ranks on one GPU rehearsed as 2 hosts x 4 GPUs (DISSEM_FAKE_HOSTS=2): host-aware comm lanes
+    # (14: 6 per host mesh + 8 across) and the hierarchical mode-1 plan over real RCCL; then the flat plan
+    rc=0
+    for spec in "" "--no-hierarchical"; do
+      tag=m1$(echo "$spec" | tr -c 'a-z0-9' '_')
+      DISSEM_SHARED_GPU=1 DISSEM_FAKE_HOSTS=2 timeout -k 10 240 python bench.py --gpus 8 --steps 2 --warmup 1 \
+        --layers 16 --layer-mib 64 --chunk-mib 16 --mode 1 $spec > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
+    done
+    [ $rc -eq 0 ]
     ;;
   shared24)
     timeout -k 10 200 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 &&

@@ -12,6 +12,7 @@ session takes its full-size wall time in a fraction of the memory.
     python scripts/predict_scaling.py --link-gbps 50 64 --ns 1 2 4 8
     python scripts/predict_scaling.py --ns 8 --mode0                 # BASELINE config #2
     python scripts/predict_scaling.py --ns 8 --pack fp8 --layers 126 --layer-mib 3072 --slowdown 8   # config #5
+    python scripts/predict_scaling.py --ns 16 --hosts 2 --slowdown 8 [--flat]   # 2 hosts x 8 GPUs
 
 Prints one JSON line per (link rate, N): predicted ms per step and the
 aggregate GB/s value bench.py would report (N x 80 GiB / T).
@@ -40,7 +41,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             link_gbps: float = 50.0, scale: int = 256, mode: int = 1, lanes: int = 0, steps: int = 2,
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
-            adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False) -> dict:
+            adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
+            nic_gbps: float = 50.0, host_lane_classes: int = 0) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -56,6 +58,9 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     readers through ONE node-wide budget of disk_gbps (the node's single NVMe,
     engine/node_pacer.h), then staged over that rank's PCIe; mode 3 plans the
     ranks' disk tiers as one group.
+    hosts: the N ranks sit in this many hosts (N / hosts GPUs each, an xGMI mesh
+    inside a host); a transfer between hosts also occupies both GPUs' NICs at
+    nic_gbps per direction (one NIC per GPU).
     slowdown: run every rate this many times slower and divide the measured time
     by it (keeps the simulator's own per-op thread overhead small next to the
     modeled transfer times)."""
@@ -65,13 +70,14 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     try:
         return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                         seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
-                        disk_gbps / slowdown, host_share)
+                        disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes)
     finally:
         _core.set_log_level(level)
 
 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
-             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False):
+             policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False,
+             hosts=1, nic_gbps=50.0, host_lane_classes=0):
     import shutil
     import tempfile
 
@@ -79,7 +85,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
     try:
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
-                           storage, host_share)
+                           storage, host_share, hosts, nic_gbps, host_lane_classes)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
@@ -87,7 +93,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
 
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
                 policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
-                host_share=False):
+                host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -98,19 +104,29 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     if slow_link is not None:
         (s, d), frac = slow_link
         t.link = {(s, d): link_gbps * 1e9 / scale * frac}
+    per_host = max(1, n // max(1, hosts))
+    host_of = [min(i // per_host, hosts - 1) for i in range(n)]
+    if hosts > 1:
+        t.host = host_of
+        t.nic_bps = nic_gbps * 1e9 / scale
     _core.sim_set_timing(key, t)
     lb, cb = layer_bytes // scale, chunk // scale
     cfg = make_workload(n, layers, lb, tier=tier, seeding=seeding, chunk_bytes=cb)
+    if hosts > 1:
+        for nd in cfg.nodes:
+            nd.host = f"host{host_of[nd.id]}"
     if plan_links:
         # the plan's rates are the simulated ones (scaled): mode 3 paces jobs at size/T
         bw = int(plan_link_gbps * 1e9 / scale)
-        cfg.links = {s: {d: bw for d in range(n) if d != s} for s in range(n)}
+        nic_bw = int(nic_gbps * 1e9 / scale)
+        cfg.links = {s: {d: (bw if host_of[s] == host_of[d] else min(bw, nic_bw)) for d in range(n) if d != s}
+                     for s in range(n)}
         if slow_link is not None:
             (s, d), frac = slow_link
             cfg.links[s][d] = int(bw * frac)
     disk = dict(storage_path=storage, node_disk_gbps=disk_gbps / scale, node_key=key) if tier == "disk" else {}
     rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
-                   poison=False, engine_opts={"lanes": lanes}, pack=pack, host_share=host_share, **disk)
+                   poison=False, engine_opts={"lanes": lanes, "host_lane_classes": host_lane_classes}, pack=pack, host_share=host_share, **disk)
            for i in range(n)]
     if host_share:
         for r in rts:
@@ -152,6 +168,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
             **({"node_disk_GBps": disk_gbps * slowdown} if tier == "disk" else {}),
             **({"pack": pack, "layers": layers, "layer_MiB": layer_bytes >> 20} if pack != "none" else {}),
+            **({"hosts": hosts, "nic_GBps": nic_gbps * slowdown} if hosts > 1 else {}),
             "seeding": seeding, **({"policy": policy} if policy else {}), **({"host_share": True} if host_share else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
             "times_ms": [round(x / slowdown * 1e3, 1) for x in times],
@@ -180,6 +197,11 @@ def main() -> int:
                     help="fp8: BASELINE config #5 (bf16 over PCIe, packed fp8 over the links)")
     ap.add_argument("--host-share", action="store_true",
                     help="with --mode0: the leader's host layers in node-shared memory, one slice staged per rank")
+    ap.add_argument("--hosts", type=int, default=1,
+                    help="the N ranks on this many hosts (one NIC per GPU at --nic-gbps between hosts)")
+    ap.add_argument("--nic-gbps", type=float, default=50.0)
+    ap.add_argument("--flat", action="store_true",
+                    help="with --hosts: every dest imports from the holders itself (no per-host import + relay)")
     ap.add_argument("--mode0", action="store_true",
                     help="BASELINE config #2 instead: mode 0 from the leader (relay vs ncclBroadcast, host vs HBM source)")
     args = ap.parse_args()
@@ -203,10 +225,11 @@ def main() -> int:
         for n in args.ns:
             r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,
                         slowdown=args.slowdown, layers=args.layers, layer_bytes=args.layer_mib << 20, pack=args.pack,
-                        tier=args.tier, disk_gbps=args.disk_gbps)
+                        tier=args.tier, disk_gbps=args.disk_gbps, hosts=args.hosts, nic_gbps=args.nic_gbps,
+                        policy={"owner_policy": "links", "hierarchical": not args.flat} if args.hosts > 1 else None)
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
-            if args.pack == "none":
+            if args.pack == "none" and args.hosts == 1:
                 total = args.layers * (args.layer_mib << 20)
                 bound = total / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)
                 if args.tier == "disk":  # every byte leaves the node's one NVMe once

@@ -332,7 +332,8 @@ def test_topology_link_bw_from_probe(monkeypatch):
     monkeypatch.setattr(_core, "gpu_topology", lambda: topo, raising=False)
     nodes = [SimpleNamespace(id=10 + r, device=None) for r in range(4)]
     nodes[1].device, nodes[2].device = 2, 1  # config Device overrides the rank order
-    fake = SimpleNamespace(cfg=SimpleNamespace(nodes=nodes), node_ids=[10, 11, 12, 13])
+    fake = SimpleNamespace(cfg=SimpleNamespace(nodes=nodes), node_ids=[10, 11, 12, 13], hosts={},
+                           NIC_PLAN_GBPS=Runtime.NIC_PLAN_GBPS)
     bw = Runtime.topology_link_bw(fake, 50.0, pcie_gbps=20.0)
     assert bw[(10, 11)] == 50e9 and bw[(11, 10)] == 50e9
     assert bw[(11, 12)] == 20e9 and bw[(12, 11)] == 20e9  # devices 2 <-> 1: PCIe peer path
