@@ -379,7 +379,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("copy_bytes", &SimTiming::copy_bytes)
       .def_readwrite("p2p_rounds", &SimTiming::p2p_rounds)
       .def_readwrite("host", &SimTiming::host)
-      .def_readwrite("nic_bps", &SimTiming::nic_bps);
+      .def_readwrite("nic_bps", &SimTiming::nic_bps)
+      .def_readwrite("wait_s", &SimTiming::wait_s);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
   m.def("sim_read", [](uint64_t ptr, int64_t n) {

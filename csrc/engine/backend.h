@@ -162,12 +162,14 @@ inline int lane_of(int src, int dst, int world, int lanes) {
 // over that many lanes per direction (classes = g: one lane per directed link,
 // = directed_lanes(world) lanes in all; fewer classes share a lane between
 // remote peers, which then wait on each other in key order).
-// classes <= 0: auto, about 8 cross-host lanes in all (2 hosts: 4 classes per
-// direction; the 2 x 8-GPU sim: 22 lanes run as fast as 30, 16 lanes ~2x
-// slower, profiles/r3_multihost/).
+// classes <= 0: auto, as many as fit 32 lanes in all (2 hosts x 8 GPUs: 8
+// classes = one lane per directed link, 30 lanes; 3-4 hosts: 3 classes). The
+// 2 x 8-GPU sim (profiles/r3_multihost/): mode 1 runs about as fast with 4
+// classes (22 lanes) as with 8, 2x slower with 1 (16 lanes); the three-level
+// mode-0 broadcast 663 ms with 8 classes vs 880-920 with 4.
 inline int host_lane_classes(int world, int hosts, int classes) {
   const int g = world / hosts;
-  if (classes <= 0) classes = 8 / ((hosts - 1) * lane_colors(hosts));
+  if (classes <= 0) classes = (32 - directed_lanes(g)) / ((hosts - 1) * lane_colors(hosts));
   return std::max(1, std::min(classes, g));
 }
 inline int host_lanes(int world, int hosts, int classes) {
@@ -205,6 +207,10 @@ struct SimTiming {
   // min(link, NIC): one NIC per GPU, shared by all of that GPU's remote peers.
   std::vector<int> host;
   double nic_bps = 0;
+  // A group not complete after this many seconds counts as deadlocked. Timed
+  // runs of congested schedules can queue a transfer behind longer than the
+  // default (the link and NIC reservations are FIFO).
+  double wait_s = 30;
 };
 
 // In-process simulated fabric: ranks of one "communicator" share `comm_key`.

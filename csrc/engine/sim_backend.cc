@@ -316,7 +316,7 @@ class SimBackend : public Backend {
     comm_.at(size_t(lane))->push([=] {
       for (size_t i = 0; i < deps.size(); ++i) {
         auto& d = deps[i];
-        if (!d || !wait_event(d, kTimeout)) {
+        if (!d || !wait_event(d, fab->timing.wait_s)) {
           set_error(std::string("group dependency failed: event ") + std::to_string(waits[i]) +
                     (d ? (d->state.load() < 0 ? " failed" : " timed out") : " was already released"));
           ev->state = -1;
@@ -370,12 +370,12 @@ class SimBackend : public Backend {
         std::vector<std::unique_ptr<Posted>> cur;
         for (size_t i = first; i < posted.size(); ++i) cur.push_back(std::move(posted[i]));
         posted.resize(first);
-        const bool ok = fab->wait_all(cur, kTimeout);
+        const bool ok = fab->wait_all(cur, fab->timing.wait_s);
         for (auto& c : cur) posted.push_back(std::move(c));
         if (!ok) break;
       }
       }
-      if (!fab->wait_all(posted, kTimeout)) {
+      if (!fab->wait_all(posted, fab->timing.wait_s)) {
         fab->cancel(posted);
         set_error("P2P group did not complete (deadlock or size mismatch)");
         ev->state = -1;
@@ -396,7 +396,7 @@ class SimBackend : public Backend {
     auto [id, ev] = make_event();
     auto dep = lookup(after);
     verify_.push([=] {
-      if (dep && !wait_event(dep, kTimeout)) {
+      if (dep && !wait_event(dep, fab_->timing.wait_s)) {
         ev->state = -1;
         return;
       }
@@ -412,7 +412,7 @@ class SimBackend : public Backend {
     auto dep = lookup(after);
     const bool copy = fab_->timing.copy_bytes;
     verify_.push([=] {
-      if (dep && !wait_event(dep, kTimeout)) {
+      if (dep && !wait_event(dep, fab_->timing.wait_s)) {
         ev->state = -1;
         return;
       }
@@ -474,7 +474,6 @@ class SimBackend : public Backend {
   }
 
  private:
-  static constexpr double kTimeout = 30.0;
   std::pair<Ev, std::shared_ptr<SimEvent>> make_event() {
     auto e = std::make_shared<SimEvent>();
     std::lock_guard<std::mutex> lk(ev_mu_);

@@ -1442,8 +1442,10 @@ NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
   // A sender's rate for this job is its tier's LimitRate capped by its link to
   // the dest when the plan knows it (measured or configured): on equal links
   // this is the reference's choice.
+  // Several hosts: a holder on the dest's host (xGMI) before any across the
+  // network (the NIC a GPU shares with all of its remote peers).
   NodeID best = 0;
-  bool found = false;
+  bool found = false, best_local = false;
   int64_t best_rate = 0;
   int64_t min_count = INT64_MAX;
   for (auto& kv : load_) {
@@ -1457,10 +1459,14 @@ NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
     if (auto lb = cfg_.link_bw.find({sender, dest}); lb != cfg_.link_bw.end() && lb->second > 0 && sender != dest)
       eff = std::min(eff, lb->second);
     int64_t count = kv.second;
-    if (!found || eff > best_rate || (eff == best_rate && (count < min_count || (count == min_count && sender < best)))) {
+    const bool local = host_of(sender) == host_of(dest);
+    if (!found || (local && !best_local) ||
+        (local == best_local &&
+         (eff > best_rate || (eff == best_rate && (count < min_count || (count == min_count && sender < best)))))) {
       best = sender;
       best_rate = eff;
       min_count = count;
+      best_local = local;
       found = true;
     }
   }

@@ -664,8 +664,8 @@ class Runtime:
 
         ``hierarchical`` (multi-host runs): mode 1's "links" policy imports a
         layer once per host and relays it over that host's xGMI mesh
-        (Node::schedule_imports); False plans every dest from the holders
-        directly, as on one host."""
+        (Node::schedule_imports), and mode 0's relay broadcast runs as a
+        three-level tree (Node::relay_across_hosts); False plans as on one host."""
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()

@@ -99,6 +99,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     _n[0] += 1
     t = _core.SimTiming()
     t.copy_bytes = False
+    t.wait_s = 600.0  # congested schedules queue transfers behind their links and NICs for long
     t.stage_bps = pcie_gbps * 1e9 / scale
     t.link_bps = link_gbps * 1e9 / scale
     if slow_link is not None:
@@ -218,7 +219,8 @@ def main() -> int:
                     for relay, coll in ((True, False), (False, True)):
                         r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes,
                                     mode=0, slowdown=args.slowdown, seeding="leader", tier=tier,
-                                    policy={"relay": relay, "collective": coll})
+                                    policy={"relay": relay, "collective": coll, "hierarchical": not args.flat},
+                                    hosts=args.hosts, nic_gbps=args.nic_gbps)
                         print(json.dumps(r), flush=True)
         return 0
     for lg in args.link_gbps:

@@ -195,3 +195,12 @@ def test_mode0_broadcast_across_hosts(hosts, n):
     finally:
         for r in rts:
             r.close()
+
+
+@pytest.mark.parametrize("n,hosts", [(16, 2), (24, 3)])
+def test_host_lanes_survive_rccl_round_model(n, hosts):
+    """RCCL runs a group's P2P ops in rounds of one ring distance each
+    (SimTiming.p2p_rounds). Hierarchical mode 1 on host-aware lanes - at 3
+    hosts of 8 several remote peers share a cross-host lane - completes
+    byte-exact under that model."""
+    run_hosts(n, hosts, 24, 2 * MiB, MiB, hierarchical=True, timing=dict(p2p_rounds=True, copy_bytes=True, wait_s=20))
