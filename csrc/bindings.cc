@@ -470,7 +470,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("disk_group", &NodeConfig::disk_group)
       .def_readwrite("disk_group_bw", &NodeConfig::disk_group_bw)
       .def_readwrite("host_share", &NodeConfig::host_share)
-      .def_readwrite("host", &NodeConfig::host);
+      .def_readwrite("host", &NodeConfig::host)
+      .def_readwrite("nic_bw", &NodeConfig::nic_bw);
   py::class_<NodeStats>(m, "NodeStats")
       .def_readonly("time_to_deliver_s", &NodeStats::time_to_deliver_s)
       .def_readonly("bytes_planned", &NodeStats::bytes_planned)
@@ -561,8 +562,11 @@ PYBIND11_MODULE(_core, m) {
                          const std::map<std::pair<NodeID, NodeID>, int64_t>& links, int64_t align,
                          bool integer_seconds, bool allow_self, const std::map<NodeID, int64_t>& stage,
                          bool stage_once, const std::map<NodeID, int>& disk_group,
-                         const std::map<int, int64_t>& disk_group_bps, const std::string& solver) {
+                         const std::map<int, int64_t>& disk_group_bps, const std::string& solver,
+                         const std::map<NodeID, int>& host, const std::map<NodeID, int64_t>& nic) {
     FlowProblem p;
+    p.host = host;
+    p.nic_bps = nic;
     p.stage_bps = stage;
     p.stage_once = stage_once;
     p.disk_group = disk_group;
@@ -584,7 +588,8 @@ PYBIND11_MODULE(_core, m) {
      py::arg("integer_seconds") = false, py::arg("allow_self") = false,
      py::arg("stage") = std::map<NodeID, int64_t>{}, py::arg("stage_once") = false,
      py::arg("disk_group") = std::map<NodeID, int>{}, py::arg("disk_group_bps") = std::map<int, int64_t>{},
-     py::arg("solver") = "auto");
+     py::arg("solver") = "auto", py::arg("host") = std::map<NodeID, int>{},
+     py::arg("nic") = std::map<NodeID, int64_t>{});
 
   // Dense two-phase simplex (sched/lp.h); rows as lists of ((col, coef) pairs, rhs).
   m.def("solve_lp", [](int n, const std::vector<double>& c,

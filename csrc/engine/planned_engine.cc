@@ -1315,6 +1315,7 @@ void PlannedEngine::poll() {
       }
       backend_->release(head.ev);
       infl.pop_front();
+      ++completions_;
     }
     if (failed_ || recovering_) break;
   }
@@ -1513,6 +1514,17 @@ void PlannedEngine::run() {
             fail("async error: " + e);
           }
         }
+      }
+      // A quiet data plane with work left (nothing issued or completed for
+      // suspect_s): say what every lane waits for - also on ranks whose lanes
+      // hold no old group, which the suspect report above never covers.
+      if (progress || completions_ != quiet_mark_ || idle()) {
+        quiet_mark_ = completions_;
+        quiet_since_ = now;
+      } else if (cfg_.suspect_s > 0 && now - quiet_since_ > std::chrono::duration<double>(cfg_.suspect_s)) {
+        quiet_since_ = now;
+        log::warn(int64_t(self_node_)).s("state", describe_stall()).f("quiet_s", cfg_.suspect_s)
+            .msg("data plane waiting: no group issued or completed");
       }
       if (!progress && !idle()) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }

@@ -434,6 +434,8 @@ class PlannedEngine : public DataEngine {
           .count();
     }
   };
+  int64_t completions_ = 0, quiet_mark_ = 0;  // completed groups; the count at the last progress check
+  std::chrono::steady_clock::time_point quiet_since_ = std::chrono::steady_clock::now();
   std::atomic<const char*> call_what_{nullptr};
   std::atomic<int64_t> call_since_us_{0};
   std::atomic<int> call_lane_{0};

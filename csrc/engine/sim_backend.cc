@@ -97,12 +97,24 @@ struct Fabric {
         const bool nic = timing.nic_bps > 0 && cross_host(src, dst);
         if (nic) bps = bps > 0 ? std::min(bps, timing.nic_bps) : timing.nic_bps;
         if (bps > 0) {
+          // Each resource serves its transfers in match order: the directed
+          // link, and across hosts the sender's NIC egress and the receiver's
+          // NIC ingress as two queues of their own (a packet network keeps both
+          // ends busy; a transfer waiting on one end never idles the other).
+          // The transfer is done when its last queue is.
+          const auto now = Clock::now();
+          const auto dur = std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(s->len) / bps));
           auto& free_at = link_free[{src, dst}];
-          auto start = std::max(Clock::now(), free_at);
-          if (nic) start = std::max({start, nic_out_free[src], nic_in_free[dst]});
-          free_at = start + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(s->len) / bps));
-          if (nic) nic_out_free[src] = nic_in_free[dst] = free_at;
-          s->done_at = r->done_at = free_at;
+          free_at = std::max(now, free_at) + dur;
+          auto done = free_at;
+          if (nic) {
+            auto& o = nic_out_free[src];
+            auto& i = nic_in_free[dst];
+            o = std::max(now, o) + dur;
+            i = std::max(now, i) + dur;
+            done = std::max({done, o, i});
+          }
+          s->done_at = r->done_at = done;
         }
       }
       s->done = r->done = true;

@@ -1717,6 +1717,10 @@ void Node::schedule_mode3() {
   p.integer_seconds = cfg_.integer_seconds;
   p.disk_group = cfg_.disk_group;
   p.disk_group_bps = cfg_.disk_group_bw;
+  if (multi_host()) {
+    p.host = cfg_.host;
+    p.nic_bps = cfg_.nic_bw;
+  }
   if (e_->planned()) {
     // GPU data plane: a layer is loaded into HBM once and forwarded from there;
     // a self-job's load feeds the dest's own sends of that layer too.

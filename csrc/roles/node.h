@@ -76,6 +76,7 @@ struct NodeConfig {
   // several, mode 1's "links" policy imports a layer once per host and relays
   // it inside the host (Node::schedule_imports).
   std::map<NodeID, int> host;
+  std::map<NodeID, int64_t> nic_bw;  // several hosts: each node's NIC (B/s per direction), mode 3's budget
 };
 
 struct NodeStats {

@@ -326,6 +326,7 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
   for (auto& kv : p.link_bps) upd(kv.second);
   for (auto& kv : p.stage_bps) upd(kv.second);
   for (auto& kv : p.disk_group_bps) upd(kv.second);
+  for (auto& kv : p.nic_bps) upd(kv.second);
   for (auto& hs : p.holdings)
     for (auto& lm : hs.second) upd(lm.second.limit_rate);
   LpProblem lp;
@@ -395,7 +396,11 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
     auto it = m.find(k);
     return it == m.end() ? int64_t(0) : it->second;
   };
-  std::map<NodeID, std::vector<std::pair<int, double>>> egress, ingress, stage;
+  std::map<NodeID, std::vector<std::pair<int, double>>> egress, ingress, stage, nic_out, nic_in;
+  auto host_of = [&](NodeID n) {
+    auto it = p.host.find(n);
+    return it == p.host.end() ? 0 : it->second;
+  };
   std::map<std::pair<NodeID, NodeID>, std::vector<std::pair<int, double>>> link;
   std::map<std::pair<NodeID, int>, std::vector<std::pair<int, double>>> tier;
   std::map<int, std::vector<std::pair<int, double>>> group;
@@ -405,6 +410,10 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
     egress[x.s].push_back({col, 1.0});
     ingress[x.d].push_back({col, 1.0});
     if (x.s != x.d) link[{x.s, x.d}].push_back({col, 1.0});
+    if (host_of(x.s) != host_of(x.d)) {
+      nic_out[x.s].push_back({col, 1.0});
+      nic_in[x.d].push_back({col, 1.0});
+    }
     const bool y = ycol.count({x.c, x.s}) > 0;
     if (!y || !p.stage_once) {  // read per transfer
       tier[{x.s, x.t}].push_back({col, 1.0});
@@ -429,6 +438,8 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
   for (auto& kv : egress) budget(rate_of(p.egress_bps, kv.first), kv.second);
   for (auto& kv : ingress) budget(rate_of(p.ingress_bps, kv.first), kv.second);
   for (auto& kv : stage) budget(rate_of(p.stage_bps, kv.first), kv.second);
+  for (auto& kv : nic_out) budget(rate_of(p.nic_bps, kv.first), kv.second);
+  for (auto& kv : nic_in) budget(rate_of(p.nic_bps, kv.first), kv.second);
   for (auto& kv : link) {
     auto it = p.link_bps.find(kv.first);
     if (it != p.link_bps.end()) budget(it->second, kv.second);
@@ -504,6 +515,14 @@ bool needs_lp(const FlowProblem& p) {
   if (p.solver == "lp") return true;
   if (p.solver == "flow") return false;
   const int kDevice = int(SourceType::Device), kDisk = int(SourceType::Disk);
+  // a NIC shared by a node's traffic to every other host: the LP's rows
+  {
+    std::set<int> hosts;
+    for (auto& kv : p.host) hosts.insert(kv.second);
+    if (hosts.size() > 1)
+      for (auto& kv : p.nic_bps)
+        if (kv.second > 0) return true;
+  }
   std::map<LayerID, std::map<NodeID, int64_t>> dests;  // layer -> dest -> bytes
   for (auto& dm : p.demands) {
     int64_t& z = dests[dm.layer][dm.dest];

@@ -83,6 +83,11 @@ struct FlowProblem {
   // to the dest's tier, staging and disk group, shared with whatever the dest
   // forwards of the same layer to others.
   std::map<NodeID, std::map<LayerID, int64_t>> self_loads;
+  // Several hosts: node -> host, and each node's NIC rate (B/s, per direction)
+  // that bounds what it sends to and receives from nodes of OTHER hosts (one
+  // NIC per GPU; traffic inside a host rides its xGMI links). Solved by the LP.
+  std::map<NodeID, int> host;
+  std::map<NodeID, int64_t> nic_bps;
   std::string solver = "auto";  // "flow", "lp" or "auto"
 };
 

@@ -646,6 +646,7 @@ class Runtime:
         hbm_gbps: Optional[float] = None,
         adapt_links: bool = True,
         hierarchical: bool = True,
+        nic_gbps: Optional[float] = None,
     ) -> None:
         """Reset the data plane and start a fresh Node for the next epoch (untimed).
 
@@ -665,7 +666,9 @@ class Runtime:
         ``hierarchical`` (multi-host runs): mode 1's "links" policy imports a
         layer once per host and relays it over that host's xGMI mesh
         (Node::schedule_imports), and mode 0's relay broadcast runs as a
-        three-level tree (Node::relay_across_hosts); False plans as on one host."""
+        three-level tree (Node::relay_across_hosts), and mode 3 budgets each
+        node's traffic to other hosts by its NIC (``nic_gbps``, default
+        NIC_PLAN_GBPS); False plans as on one host."""
         self.epoch += 1
         if self.engine is not None:
             self.engine.reset_session()
@@ -701,6 +704,9 @@ class Runtime:
         nc.host_share = self.host_share
         if hierarchical and len(set(self.hosts.values())) > 1:
             nc.host = dict(self.hosts)
+            # mode 3 budgets every node's traffic to other hosts by its NIC
+            nc.nic_bw = {n: int((nic_gbps if nic_gbps is not None else self.NIC_PLAN_GBPS) * 1e9)
+                         for n in self.node_ids}
         if self.node_disk_gbps > 0:  # every rank of a host reads that host's one NVMe
             nc.disk_group = {n.id: self.hosts.get(n.id, 0) for n in self.cfg.nodes}
             nc.disk_group_bw = {h: int(self.node_disk_gbps * 1e9) for h in set(self.hosts.values())}

@@ -203,11 +203,16 @@ case "$RECIPE" in
     # 8 ranks on one GPU rehearsed as 2 hosts x 4 GPUs (DISSEM_FAKE_HOSTS=2): host-aware comm lanes
     # (14: 6 per host mesh + 8 across) and the hierarchical mode-1 plan over real RCCL; then the flat plan
     rc=0
-    for spec in "" "--no-hierarchical"; do
-      tag=m1$(echo "$spec" | tr -c 'a-z0-9' '_')
+    for spec in "1" "1 --no-hierarchical" "0 --seeding leader" "0 --seeding leader --no-hierarchical" "2"; do
+      set -- $spec
+      mode=$1; shift
+      tag=m${mode}$(echo "$*" | tr -c 'a-z0-9' '_')
       DISSEM_SHARED_GPU=1 DISSEM_FAKE_HOSTS=2 timeout -k 10 240 python bench.py --gpus 8 --steps 2 --warmup 1 \
-        --layers 16 --layer-mib 64 --chunk-mib 16 --mode 1 $spec > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
+        --layers 16 --layer-mib 64 --chunk-mib 16 --mode "$mode" "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.log || { rc=$?; break; }
     done
+    # the one-host headline path on the same tree (lane map unchanged at N = 8)
+    [ $rc -eq 0 ] && DISSEM_SHARED_GPU=1 timeout -k 10 240 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
+        --layer-mib 64 --chunk-mib 16 --mode 1 > $OUT/bench_onehost_m1.json 2> $OUT/bench_onehost_m1.log || rc=$?
     [ $rc -eq 0 ]
     ;;
   shared24)

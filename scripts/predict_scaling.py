@@ -142,6 +142,8 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
         for _ in range(steps):
             for r in rts:
                 extra = {"stage_gbps": pcie_gbps / scale} if plan_links else {}
+                if plan_links and hosts > 1:
+                    extra["nic_gbps"] = nic_gbps / scale
                 r.prepare(mode, **{"pull_window": max(1, n - 1), "adapt_links": adapt_links, **extra, **(policy or {})})
             res = [None] * n
 

@@ -340,3 +340,27 @@ def test_topology_link_bw_from_probe(monkeypatch):
     assert bw[(10, 13)] == 25e9  # devices 0 -> 3: two xGMI hops
     assert bw[(13, 12)] == 50e9
     assert len(bw) == 12
+
+
+def test_nic_budget_across_hosts(core):
+    """Several hosts (mode 3): every node's traffic to and from OTHER hosts
+    shares its NIC; traffic inside a host does not. Nodes 0, 1 (host 0) hold
+    2 x 1 GB each, nodes 2, 3 (host 1) need all 4 plus each other's nothing:
+    each dest pulls 4 GB through a 10 GB/s NIC -> T = 0.4 s, where per-pair
+    links alone (100 GB/s) would promise 0.02 s."""
+    G = 10**9
+    dev = core.LayerMeta(core.Location.Inmem, 0, core.SourceType.Device, G)
+    holdings = {0: {0: dev, 1: dev}, 1: {2: dev, 3: dev}, 2: {}, 3: {}}
+    demands = [(l, d, G) for l in range(4) for d in (2, 3)]
+    links = {(s, d): 100 * G for s in range(4) for d in range(4) if s != d}
+    alone = core.solve_flow(holdings, demands, links=links)
+    assert alone.T == pytest.approx(0.02, rel=1e-3)
+    nic = core.solve_flow(holdings, demands, links=links, host={0: 0, 1: 0, 2: 1, 3: 1},
+                          nic={n: 10 * G for n in range(4)})
+    assert nic.solver == "lp" and nic.feasible
+    assert nic.T == pytest.approx(0.4, rel=1e-3)
+    check_ranges(nic, holdings, demands)
+    # one host: the NIC rows do not apply
+    same = core.solve_flow(holdings, demands, links=links, host={n: 0 for n in range(4)},
+                           nic={n: 10 * G for n in range(4)})
+    assert same.T == pytest.approx(0.02, rel=1e-3)
