@@ -233,7 +233,7 @@ def worker(args, world, rank, chan) -> int:
 
     faults = parse_inject(args.inject)
 
-    _core.set_log_level(2)
+    _core.set_log_level(int(os.environ.get("DISSEM_LOG_LEVEL", "2")))  # 1 = info, 0 = debug
 
     def log(msg):
         print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)

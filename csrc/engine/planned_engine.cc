@@ -26,7 +26,10 @@
 // every mode at up to 8 ranks, with one lane and with world-1 lanes.
 #include "engine/planned_engine.h"
 
+#include <execinfo.h>
 #include <fcntl.h>
+#include <pthread.h>
+#include <signal.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -43,6 +46,17 @@
 namespace dissem {
 
 namespace {
+// Diagnostics: the monitor asks a stuck issue thread for its native stack
+// (async-signal-safe: backtrace + backtrace_symbols_fd straight to stderr;
+// resolve the .so offsets with addr2line).
+void dump_stack_handler(int) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  static const char hdr[] = "=== issue thread stack ===\n";
+  (void)!write(2, hdr, sizeof hdr - 1);
+  backtrace_symbols_fd(frames, n, 2);
+}
+
 size_t log2_bucket(std::chrono::steady_clock::time_point since) {
   const int64_t us =
       std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - since).count();
@@ -87,6 +101,27 @@ void PlannedEngine::monitor_loop() {
   int64_t reported = 0;
   while (!stop_req_) {
     std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    {
+      // the issue thread loops every ~20 us while it has work: a loop counter that
+      // stands still for 5 s means it is stuck outside any marked backend call
+      const int64_t t = loop_ticks_.load();
+      const auto now = std::chrono::steady_clock::now();
+      if (t != last_ticks_) {
+        last_ticks_ = t;
+        ticks_since_ = now;
+      } else if (now - ticks_since_ > std::chrono::seconds(5) && !call_what_.load() && !idle_flag_.load()) {
+        ticks_since_ = now;
+        log::warn(int64_t(self_node_)).i("loop_ticks", t).msg("issue thread not looping (stuck outside backend calls)");
+        if (!stack_dumped_ && getenv("DISSEM_STACK_DUMP")) {
+          stack_dumped_ = true;
+          struct sigaction sa {};
+          sa.sa_handler = dump_stack_handler;
+          sigemptyset(&sa.sa_mask);
+          sigaction(SIGUSR2, &sa, nullptr);
+          pthread_kill(th_.native_handle(), SIGUSR2);
+        }
+      }
+    }
     const char* what = call_what_.load();
     const int64_t since = call_since_us_.load();
     if (!what || since == reported) continue;
@@ -910,6 +945,10 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
     if (p.kind == Kind::Send && !p.bcast) fwd_pending_[{p.layer, p.chunk}].insert(key_of(p));
     ops_[size_t(p.lane)].push_back(p);
   }
+  int64_t ns = 0, nr = 0;
+  for (auto& p : pieces) (p.kind == Kind::Send ? ns : nr) += p.kind == Kind::Local ? 0 : 1;
+  log::info(int64_t(self_node_)).u("batch", batch).i("jobs", int64_t(jobs.size())).i("sends", ns).i("recvs", nr)
+      .msg("transfer batch queued");
 }
 
 bool PlannedEngine::issue_some() {
@@ -1492,6 +1531,8 @@ void PlannedEngine::run() {
         std::this_thread::sleep_for(std::chrono::milliseconds(5));
         continue;
       }
+      loop_ticks_.fetch_add(1, std::memory_order_relaxed);
+      idle_flag_ = idle();
       pump_disk();
       bool progress = issue_some();
       poll();

@@ -434,6 +434,11 @@ class PlannedEngine : public DataEngine {
           .count();
     }
   };
+  std::atomic<int64_t> loop_ticks_{0};  // issue-thread loop iterations (monitor: liveness)
+  std::atomic<bool> idle_flag_{true};
+  int64_t last_ticks_ = -1;             // monitor thread only
+  bool stack_dumped_ = false;           // monitor thread only (DISSEM_STACK_DUMP)
+  std::chrono::steady_clock::time_point ticks_since_ = std::chrono::steady_clock::now();
   int64_t completions_ = 0, quiet_mark_ = 0;  // completed groups; the count at the last progress check
   std::chrono::steady_clock::time_point quiet_since_ = std::chrono::steady_clock::now();
   std::atomic<const char*> call_what_{nullptr};

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -125,6 +126,51 @@ void register_gpu_bindings(PyObject* module) {
       }
     return out;
   });
+  // Regression probe (round 3): the first CRC of a new chunk size must not
+  // wait for other streams. A blocking stream holds a kernel that spins until
+  // the host releases it (an RCCL kernel waiting on a peer); meanwhile a CRC of
+  // a never-seen size is launched on another stream. Returns (host ms of that
+  // launch call, spin iterations, crc, spin stream drained). Before the fix the
+  // launch blocked in a null-stream hipMemcpy until the spin ran out.
+  m.def("crc_launch_beside_blocked_stream", [](int64_t bytes, uint64_t max_iters) {
+    py::gil_scoped_release nogil;
+    hipStream_t blocked = nullptr, work = nullptr;
+    check(hipStreamCreate(&blocked), "hipStreamCreate");  // default flags: blocking, like the lanes
+    check(hipStreamCreateWithFlags(&work, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+    uint32_t* flag = nullptr;
+    uint32_t *flag_dev = nullptr, *out = nullptr;
+    uint64_t* iters = nullptr;
+    check(hipHostMalloc(reinterpret_cast<void**>(&flag), 4, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+    *flag = 0;
+    check(hipHostGetDevicePointer(reinterpret_cast<void**>(&flag_dev), flag, 0), "hipHostGetDevicePointer");
+    check(hipMalloc(reinterpret_cast<void**>(&iters), 8), "hipMalloc");
+    check(hipMalloc(reinterpret_cast<void**>(&out), 4), "hipMalloc");
+    uint8_t* data = nullptr;
+    check(hipMalloc(reinterpret_cast<void**>(&data), size_t(bytes)), "hipMalloc");
+    check(kern::fill_random(data, bytes, 7, work), "fill");
+    check(hipStreamSynchronize(work), "sync");
+    void* ws = nullptr;
+    check(hipMalloc(&ws, kern::crc32c_workspace_bytes(bytes, bytes)), "hipMalloc");
+    check(kern::spin_until(flag_dev, max_iters, iters, blocked), "spin");
+    const auto t0 = std::chrono::steady_clock::now();
+    check(kern::crc32c_chunks(data, bytes, bytes, out, ws, work), "crc32c_chunks");
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    __atomic_store_n(flag, 1u, __ATOMIC_RELEASE);
+    check(hipStreamSynchronize(blocked), "sync blocked");
+    check(hipStreamSynchronize(work), "sync work");
+    uint32_t crc = 0;
+    uint64_t it = 0;
+    check(hipMemcpy(&crc, out, 4, hipMemcpyDeviceToHost), "copy");
+    check(hipMemcpy(&it, iters, 8, hipMemcpyDeviceToHost), "copy");
+    (void)hipFree(ws);
+    (void)hipFree(data);
+    (void)hipFree(out);
+    (void)hipFree(iters);
+    (void)hipHostFree(flag);
+    (void)hipStreamDestroy(blocked);
+    (void)hipStreamDestroy(work);
+    return std::make_tuple(ms, it, crc);
+  }, py::arg("bytes"), py::arg("max_iters") = 600000);
   m.def("device_synchronize", [] {
     py::gil_scoped_release nogil;
     check(hipDeviceSynchronize(), "hipDeviceSynchronize");

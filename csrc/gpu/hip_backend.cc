@@ -73,6 +73,10 @@ class HipBackend : public Backend {
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&crc_dev_), crc_host_, 0));
+    // CRC tables and the full-chunk fold tables before any RCCL traffic (the
+    // packed grid too when fp8 chunks may be checked)
+    HIP_OK(kern::crc32c_warm(cfg_.max_crc_bytes, verify_));
+    HIP_OK(hipStreamSynchronize(verify_));
     if (cfg_.world > 1 || cfg_.self_comm) {
       std::string ids = cfg_.nccl_uid;
       if (cfg_.world == 1 && ids.empty()) ids = nccl_unique_id(int(nccl_.size()));
@@ -227,11 +231,14 @@ class HipBackend : public Backend {
     const int q = copy2_ && (flip_ ^= true) ? 1 : 0;
     hipStream_t s = q ? copy2_ : copy_;
     if (n_src > scratch_bytes_[q]) {
+      // Sized for a whole source chunk on first use, so it never grows in a
+      // session: hipFree synchronizes the device, comm lanes included.
       HIP_OK(hipStreamSynchronize(s));
       if (scratch_[q]) HIP_OK(hipFree(scratch_[q]));
       scratch_[q] = nullptr;
-      HIP_OK(hipMalloc(&scratch_[q], size_t(n_src)));
-      scratch_bytes_[q] = n_src;
+      const int64_t want = std::max(n_src, cfg_.max_crc_bytes);
+      HIP_OK(hipMalloc(&scratch_[q], size_t(want)));
+      scratch_bytes_[q] = want;
     }
     HIP_OK(hipMemcpyAsync(scratch_[q], src, size_t(n_src), hipMemcpyHostToDevice, s));
     const int64_t n = n_src / 2;

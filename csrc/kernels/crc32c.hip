@@ -55,6 +55,7 @@
 
 #include <algorithm>
 #include <map>
+#include <cstring>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -645,13 +646,62 @@ __global__ void __launch_bounds__(256) crc32c_batch_fold_kernel(const BatchArgs 
 }
 
 // Per-device constant tables and per-(chunk, last chunk) fold tables.
+//
+// Built on first use and uploaded WITHOUT a host-synchronous copy: a
+// hipMemcpy here ran on the null stream in the middle of a session (the first
+// CRC of a rank that starts by receiving), waited for the comm lanes' RCCL
+// kernels, and hung a rank whose peers waited for it (profiles/r3_multihost/).
+// Tables go into pinned host and device arenas (bump-allocated, never reused
+// or freed) and are copied with hipMemcpyAsync on the caller's stream; an
+// event recorded behind the copy orders any later user on another stream.
+struct ConstEntry {
+  uint32_t* d = nullptr;
+  hipEvent_t ready = nullptr;
+};
 struct DeviceConsts {
   std::mutex mu;
-  std::map<int, uint32_t*> by_device;
+  std::map<int, ConstEntry> by_device;
   // (device, chunk_bytes, last_len) -> [shift: spc x 64][shift_last: spc x 64][init: 2]
-  std::map<std::tuple<int, int64_t, int64_t>, uint32_t*> fold;
+  std::map<std::tuple<int, int64_t, int64_t>, ConstEntry> fold;
+  struct Arena {
+    uint8_t* dev = nullptr;
+    uint8_t* host = nullptr;
+    size_t cap = 0, used = 0;
+  };
+  std::map<int, Arena> arena;  // per device
 };
 DeviceConsts g_consts;
+
+// Caller holds g_consts.mu. A new arena (the rare case: first use, or one
+// more after 64 MiB of tables) is the only allocation on this path.
+ConstEntry upload_consts(int dev, const std::vector<uint32_t>& h, hipStream_t s) {
+  const size_t n = (h.size() * 4 + 255) & ~size_t(255);
+  auto& a = g_consts.arena[dev];
+  if (!a.dev || a.used + n > a.cap) {
+    const size_t cap = std::max(n, size_t(64) << 20);
+    void *d = nullptr, *hp = nullptr;
+    if (hipMalloc(&d, cap) != hipSuccess) return {};
+    if (hipHostMalloc(&hp, cap, hipHostMallocDefault) != hipSuccess) return {};
+    a = DeviceConsts::Arena{static_cast<uint8_t*>(d), static_cast<uint8_t*>(hp), cap, 0};
+  }
+  uint8_t* hd = a.host + a.used;
+  uint8_t* dd = a.dev + a.used;
+  a.used += n;
+  memcpy(hd, h.data(), h.size() * 4);
+  ConstEntry e;
+  e.d = reinterpret_cast<uint32_t*>(dd);
+  if (hipMemcpyAsync(dd, hd, h.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess) return {};
+  if (hipEventCreateWithFlags(&e.ready, hipEventDisableTiming) != hipSuccess) return {};
+  if (hipEventRecord(e.ready, s) != hipSuccess) return {};
+  return e;
+}
+
+// Tables for use on stream s (a no-op wait once their upload has run).
+uint32_t* use_on(const ConstEntry& e, hipStream_t s) {
+  if (!e.d) return nullptr;
+  if (hipStreamWaitEvent(s, e.ready, 0) != hipSuccess) return nullptr;
+  return e.d;
+}
 
 // Per full segment k of a `len`-byte chunk and lane l: x^(8 * (bytes from the
 // end of lane l's last piece to the chunk end)) = x^(8*64*(63 - l)) * x^(8 * (len - end of k)).
@@ -669,32 +719,31 @@ void lane_shifts(int64_t len, int64_t spc, uint32_t* out) {
   }
 }
 
-uint32_t* fold_consts(int64_t chunk_bytes, int64_t last_len) {
+uint32_t* fold_consts(int64_t chunk_bytes, int64_t last_len, hipStream_t s) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_consts.mu);
   auto key = std::make_tuple(dev, chunk_bytes, last_len);
   auto it = g_consts.fold.find(key);
-  if (it != g_consts.fold.end()) return it->second;
+  if (it != g_consts.fold.end()) return use_on(it->second, s);
   const int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
   std::vector<uint32_t> h(size_t(2 * spc * 64 + 2));
   lane_shifts(chunk_bytes, spc, h.data());
   lane_shifts(last_len, spc, h.data() + spc * 64);
   h[size_t(2 * spc * 64)] = crc32c_init_term(uint64_t(chunk_bytes));
   h[size_t(2 * spc * 64 + 1)] = crc32c_init_term(uint64_t(last_len));
-  uint32_t* d = nullptr;
-  if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
-  if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
-  g_consts.fold[key] = d;
-  return d;
+  const ConstEntry e = upload_consts(dev, h, s);
+  if (!e.d) return nullptr;
+  g_consts.fold[key] = e;
+  return e.d;
 }
 
-uint32_t* device_consts() {
+uint32_t* device_consts(hipStream_t s) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_consts.mu);
   auto it = g_consts.by_device.find(dev);
-  if (it != g_consts.by_device.end()) return it->second;
+  if (it != g_consts.by_device.end()) return use_on(it->second, s);
   std::vector<uint32_t> T(16 * 256), h(kConstWords);
   crc32c_slice16_tables(T.data());
   for (int i = 0; i < 4 * 256; ++i) h[size_t(kT + i)] = T[size_t(i)];
@@ -702,11 +751,10 @@ uint32_t* device_consts() {
   for (int n = 0; n < 8; ++n)
     for (uint32_t v = 0; v < 16; ++v) h[size_t(kGap + n * 16 + int(v))] = crc32c_multmodp(xg, v << (4 * n));
   for (int m = 0; m < 1024; ++m) h[size_t(kPow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
-  uint32_t* d = nullptr;
-  if (hipMalloc(&d, h.size() * 4) != hipSuccess) return nullptr;
-  if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
-  g_consts.by_device[dev] = d;
-  return d;
+  const ConstEntry e = upload_consts(dev, h, s);
+  if (!e.d) return nullptr;
+  g_consts.by_device[dev] = e;
+  return e.d;
 }
 
 // One workgroup per CU (LDS-bound), 16 segments per workgroup at a time,
@@ -732,17 +780,23 @@ struct Plan {
   uint32_t *consts, *fold;
 };
 
-hipError_t plan(int64_t bytes, int64_t chunk_bytes, Plan* p) {
+hipError_t plan(int64_t bytes, int64_t chunk_bytes, Plan* p, hipStream_t s) {
   p->spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
   p->nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
   const int64_t last_len = bytes - (p->nchunks - 1) * chunk_bytes;
   p->total_segs = (p->nchunks - 1) * p->spc + (last_len + kSegBytes - 1) / kSegBytes;
-  p->consts = device_consts();
-  p->fold = fold_consts(chunk_bytes, last_len);
+  p->consts = device_consts(s);
+  p->fold = fold_consts(chunk_bytes, last_len, s);
   return p->consts && p->fold ? hipSuccess : hipErrorOutOfMemory;
 }
 
 }  // namespace
+
+hipError_t crc32c_warm(int64_t chunk_bytes, hipStream_t s) {
+  if (!device_consts(s)) return hipErrorOutOfMemory;
+  if (chunk_bytes > 0 && !fold_consts(chunk_bytes, chunk_bytes, s)) return hipErrorOutOfMemory;
+  return hipSuccess;
+}
 
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes) {
   if (bytes <= 0 || chunk_bytes <= 0) return 16;
@@ -766,7 +820,7 @@ hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_by
   if (bytes <= chunk_bytes) chunk_bytes = bytes;
   else if (chunk_bytes % 16) return hipErrorInvalidValue;
   Plan p;
-  if (hipError_t e = plan(bytes, chunk_bytes, &p); e != hipSuccess) return e;
+  if (hipError_t e = plan(bytes, chunk_bytes, &p, s); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
   const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.fold, p.fold + p.spc * 64};
   crc32c_segments_kernel<<<seg_grid(p.total_segs, max_blocks), dim3(kThreads), 0, s>>>(geo, p.total_segs, p.consts,
@@ -787,13 +841,13 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
   BatchArgs a{};
   a.n = 0;
   a.seg_base[0] = 0;
-  uint32_t* consts = device_consts();
+  uint32_t* consts = device_consts(s);
   if (!consts) return hipErrorOutOfMemory;
   for (int i = 0; i < n; ++i) {
     const CrcItem& it = items[i];
     if (it.bytes <= 0) continue;
     if (reinterpret_cast<uintptr_t>(it.src) & 15) return hipErrorInvalidValue;  // any length
-    uint32_t* fold = fold_consts(it.bytes, it.bytes);
+    uint32_t* fold = fold_consts(it.bytes, it.bytes, s);
     if (!fold) return hipErrorOutOfMemory;
     const int64_t spc = (it.bytes + kSegBytes - 1) / kSegBytes;
     const int j = a.n++;
@@ -821,7 +875,7 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   const int64_t full = src_bytes / src_chunk, tail = src_bytes % src_chunk;
   const int64_t bytes = full * pchunk + (tail ? tail / 2 + tail / 2 / block * 4 : 0);
   Plan p;
-  if (hipError_t e = plan(bytes, pchunk, &p); e != hipSuccess) return e;
+  if (hipError_t e = plan(bytes, pchunk, &p, s); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
   const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.fold, p.fold + p.spc * 64};
   const int64_t oc = src_chunk / 2;

@@ -168,5 +168,24 @@ void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset) {
   }
 }
 
+// Test helper: one wave that holds its stream until the host sets `flag`
+// (host-mapped, coherent) or max_iters sleeps have passed - a stand-in for an
+// RCCL kernel waiting on a peer. Always exits; writes how long it waited.
+__global__ void __launch_bounds__(64) spin_until_kernel(const volatile uint32_t* flag, uint64_t max_iters,
+                                                         uint64_t* iters) {
+  if (threadIdx.x != 0) return;
+  uint64_t i = 0;
+  while (i < max_iters && *flag == 0) {
+    __builtin_amdgcn_s_sleep(127);
+    ++i;
+  }
+  *iters = i;
+}
+
+hipError_t spin_until(const uint32_t* flag, uint64_t max_iters, uint64_t* iters, hipStream_t s) {
+  spin_until_kernel<<<dim3(1), dim3(64), 0, s>>>(flag, max_iters, iters);
+  return hipGetLastError();
+}
+
 }  // namespace kern
 }  // namespace dissem

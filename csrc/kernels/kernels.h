@@ -23,6 +23,8 @@ namespace kern {
 // 16 B per lane stores; byte-identical to kern::fill_random_host.
 hipError_t fill_random(void* dst, int64_t bytes, uint64_t seed, hipStream_t s);
 void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset = 0);
+// Test helper: hold stream s until *flag != 0 (host-mapped) or max_iters ~3 us sleeps.
+hipError_t spin_until(const uint32_t* flag, uint64_t max_iters, uint64_t* iters, hipStream_t s);
 // Read-bandwidth probe: XOR of [src, src+bytes) into blocks*4 dwords at out
 // (bytes % 16 == 0); `depth` 16-B loads in flight per lane (1, 2, 4, 8).
 hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, int depth, hipStream_t s);
@@ -38,6 +40,10 @@ hipError_t read_seg(const void* src, int64_t bytes, uint32_t* out, int blocks, i
 // device memory. src 16-B aligned; chunk_bytes a multiple of 16 unless the span
 // is one chunk (bytes <= chunk_bytes: any length, e.g. a layer's last chunk).
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes);
+// Build and upload (stream-ordered on s) the CRC tables and the fold tables of
+// `chunk_bytes` chunks ahead of time; later launches then never allocate. Any
+// table first needed later is uploaded the same way, never with a host sync.
+hipError_t crc32c_warm(int64_t chunk_bytes, hipStream_t s);
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
                          hipStream_t s);
 // Batched: the standard CRC32C of each of up to kCrcBatchMax independent

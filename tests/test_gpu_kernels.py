@@ -285,3 +285,17 @@ def test_rccl_selftest_p2p_and_broadcast(gpu, n, chunk):
     assert len(src) == (n + chunk - 1) // chunk
     assert p2p == src
     assert bcast == src
+
+
+def test_crc_table_upload_never_waits_for_other_streams(gpu):
+    """Round-3 hang: the first CRC of a new chunk size uploaded its tables with
+    a null-stream hipMemcpy, which waited for every blocking stream - the comm
+    lanes' RCCL kernels included - in the middle of a session. A kernel that
+    spins on a host flag holds a blocking stream (an RCCL kernel waiting on a
+    peer); a CRC of a never-seen size on another stream must launch without
+    waiting for it, and still be right."""
+    n = (40 << 20) + 3 * 4096 + 48  # a size no other test checks: fresh fold tables
+    ms, iters, crc = gpu.crc_launch_beside_blocked_stream(n)
+    assert ms < 250, ms           # before the fix: until the spin ran out (~2 s)
+    assert iters < 600000, iters  # released by the host, not by its bound
+    assert crc == gpu.crc32c(gpu.fill_random_host(n, 7))
