@@ -237,6 +237,7 @@ def main(argv=None) -> int:
         from .utils.launch import gather_hosts
 
         hosts = gather_hosts(my_id)  # multi-node torchrun: host-aware lanes and plans
+    from .utils.launch import listen_addr as _listen_addr
     registry = cfg.registry()
     client = cfg.client(my_id)
     if client is not None:
@@ -265,7 +266,8 @@ def main(argv=None) -> int:
                  host_share=args.host_share and args.engine == "rccl", node_disk_gbps=args.node_disk_gbps,
                  node_key="c" + hashlib.blake2b((args.f + os.environ.get("MASTER_PORT", "")).encode(),
                                                 digest_size=6).hexdigest(),
-                 layer_source=_weights_source(weights) if weights is not None else None, hosts=hosts)
+                 layer_source=_weights_source(weights) if weights is not None else None, hosts=hosts,
+                 listen_addr=None if me.addr or not hosts else _listen_addr(True))
     if barrier is not None:
         # torchrun: nodes without a fixed Addr listen on ephemeral ports; share them.
         import torch.distributed as dist
