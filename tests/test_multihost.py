@@ -207,3 +207,51 @@ def test_host_lanes_survive_rccl_round_model(n, hosts):
     hosts of 8 several remote peers share a cross-host lane - completes
     byte-exact under that model."""
     run_hosts(n, hosts, 24, 2 * MiB, MiB, hierarchical=True, timing=dict(p2p_rounds=True, copy_bytes=True, wait_s=20))
+
+
+def _gather_worker(rank, world, port, fake, out):
+    import os
+
+    import torch.distributed as dist
+
+    from distributed_llm_dissemination_amd.utils.launch import FAKE_HOSTS_ENV, gather_hosts, listen_addr
+
+    if fake:
+        os.environ[FAKE_HOSTS_ENV] = str(fake)
+    else:
+        os.environ.pop(FAKE_HOSTS_ENV, None)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        hosts = gather_hosts(10 + rank)
+        out.put((rank, hosts, listen_addr(bool(hosts))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fake", [0, 2])
+def test_gather_hosts_over_gloo(fake):
+    """Under torchrun every rank learns every rank's host: one machine -> None
+    (single-host plans and lanes); DISSEM_FAKE_HOSTS=2 splits 4 ranks into 2
+    hosts of consecutive ranks, still listening on loopback."""
+    import multiprocessing as mp
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_worker, args=(r, 4, port, fake, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    got = dict((r, (h, a)) for r, h, a in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(4):
+        hosts, addr = got[r]
+        assert addr == "127.0.0.1:0"
+        if fake:
+            assert hosts == {10: "host0", 11: "host0", 12: "host1", 13: "host1"}
+        else:
+            assert hosts is None
