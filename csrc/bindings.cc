@@ -555,6 +555,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("feasible", &FlowPlan::feasible)
       .def_readonly("solver", &FlowPlan::solver)
       .def_readonly("lp_pivots", &FlowPlan::lp_pivots)
+      .def_readonly("lp_status", &FlowPlan::lp_status)
       .def_readonly("jobs", &FlowPlan::jobs);
   m.def("solve_flow", [](const std::map<NodeID, LayerIDs>& holdings,
                          const std::vector<std::tuple<LayerID, NodeID, int64_t>>& demands,

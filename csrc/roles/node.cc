@@ -1734,6 +1734,15 @@ void Node::schedule_mode3() {
   log::info(int64_t(cfg_.id)).msg("assigning a job...");
   int64_t t0 = log::now_us();
   FlowPlan plan = solve_flow(p);
+  if (!plan.feasible && plan.solver == "lp") {
+    // The LP did not solve (numerics on extreme measured rates, or its pivot
+    // limit): plan with the flow instead - it relaxes the budgets it cannot
+    // state, so its T may be optimistic, but every demand gets a sender.
+    log::warn(int64_t(cfg_.id)).s("lp_status", plan.lp_status).i("lp_pivots", plan.lp_pivots)
+        .msg("mode 3: the LP failed, planning with the max-flow instead");
+    p.solver = "flow";
+    plan = solve_flow(p);
+  }
   log::info(int64_t(cfg_.id)).f("computation time[ms]", double(log::now_us() - t0) / 1e3).i("solves", plan.solves)
       .s("solver", plan.solver).i("lp_pivots", plan.lp_pivots).msg("Job assignment completed");
   log::info(int64_t(cfg_.id)).f("required minimum time(s)", plan.T).b("feasible", plan.feasible)

@@ -389,7 +389,7 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
     std::map<int, double> merged;
     for (auto& e : cols) merged[e.first] += e.second;
     for (auto& e : merged) r.a.push_back(e);
-    r.a.push_back({0, -double(rate) / R0});
+    r.a.push_back({0, -double(rate)});  // scaled by the candidate R0 below
     lp.le.push_back(r);
   };
   auto rate_of = [](const std::map<NodeID, int64_t>& m, NodeID k) {
@@ -459,8 +459,38 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
     auto it = p.disk_group_bps.find(kv.first);
     if (it != p.disk_group_bps.end()) budget(it->second, kv.second);
   }
-  LpResult r = solve_lp(lp);
+  // T's column carries -rate / R0. R0 = the largest rate keeps every
+  // coefficient <= 1, but when the rates span orders of magnitude (measured
+  // link rates next to planning constants) the optimum's scaled T grows large
+  // and the dense simplex can lose it to round-off (it has reported such
+  // instances "unbounded"/"infeasible" where scipy finds the optimum): retry
+  // with the median and the smallest rate as the scale.
+  std::vector<double> rates;
+  for (auto& row : lp.le)
+    for (auto& e : row.a)
+      if (e.first == 0 && e.second < 0) rates.push_back(-e.second);
+  std::sort(rates.begin(), rates.end());
+  std::vector<double> scales{R0};
+  if (!rates.empty()) {
+    scales.push_back(rates[rates.size() / 2]);
+    scales.push_back(rates.front());
+  }
+  LpResult r;
+  LpProblem scaled;
+  for (double sc : scales) {
+    scaled = lp;
+    for (auto& row : scaled.le)
+      for (auto& e : row.a)
+        if (e.first == 0) e.second /= sc;
+    r = solve_lp(scaled);
+    plan.lp_pivots += r.pivots;
+    if (r.ok) {
+      R0 = sc;
+      break;
+    }
+  }
   if (getenv("DLD_LP_DUMP")) {
+    const LpProblem& lp = scaled;
     fprintf(stderr, "LP n=%d B0=%g R0=%g\n", lp.n, B0, R0);
     for (auto& row : lp.eq) {
       fprintf(stderr, "EQ");
@@ -474,7 +504,7 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
     }
     fprintf(stderr, "status %s obj %g\n", r.status.c_str(), r.obj);
   }
-  plan.lp_pivots = r.pivots;
+  plan.lp_status = r.status;
   if (!r.ok) return plan;
   double T = r.x[0] * B0 / R0;
   if (p.integer_seconds) T = std::max(1.0, std::ceil(T - 1e-9));

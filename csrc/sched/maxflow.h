@@ -99,6 +99,7 @@ struct FlowPlan {
   bool feasible = false;
   std::string solver;      // "flow" or "lp"
   int lp_pivots = 0;
+  std::string lp_status;   // the LP's outcome ("optimal", "infeasible", "iteration limit", ...)
   std::vector<FlowJob> jobs;
 };
 

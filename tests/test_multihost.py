@@ -255,3 +255,42 @@ def test_gather_hosts_over_gloo(fake):
             assert hosts == {10: "host0", 11: "host0", 12: "host1", 13: "host1"}
         else:
             assert hosts is None
+
+
+def test_mode3_across_hosts_every_session_plans():
+    """Mode 3 on 2 hosts x 4 GPUs plans with NIC budgets (LP); the closed loop
+    then feeds measured link rates that span orders of magnitude next to the
+    planning constants. Every session must still get a plan (the LP retries
+    with other scalings of T, then falls back to the max-flow) and deliver."""
+    n, hosts = 8, 2
+    key = f"mh3{next(_keys)}"
+    host_of = [i // 4 for i in range(n)]
+    t = _core.SimTiming()
+    t.host = host_of
+    t.wait_s = 20
+    _core.sim_set_timing(key, t)
+    cfg = make_workload(n, 16, 4 * MiB, tier="host", seeding="random", chunk_bytes=MiB)
+    for nd in cfg.nodes:
+        nd.host = f"h{host_of[nd.id]}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key) for i in range(n)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for _ in range(3):
+            for r in rts:
+                r.prepare(3)
+            res = [None] * n
+            ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(60))) for i in range(n)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            assert all(x.ok for x in res), [x.error for x in res]
+            assert res[0].flow_T > 0
+            for i, r in enumerate(rts):
+                for l in cfg.assignment[i]:
+                    assert r.layer_bytes(l) == _core.fill_random_host(4 * MiB, layer_seed(0, l)), (i, l)
+    finally:
+        for r in rts:
+            r.close()
