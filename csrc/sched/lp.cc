@@ -37,13 +37,13 @@ struct Tableau {
   // Minimize the objective in the last row over the columns `allowed` lets in.
   // Returns "optimal", "unbounded" or "iteration limit".
   template <class Allowed>
-  const char* run(Allowed allowed, int ncols, int& pivots, int max_pivots) {
+  const char* run(Allowed allowed, int ncols, int& pivots, int max_pivots, bool always_bland = false) {
     int degenerate = 0;
     for (;;) {
       if (pivots >= max_pivots) return "iteration limit";
       double* obj = row(m);
       int c = -1;
-      const bool bland = degenerate > 50;
+      const bool bland = always_bland || degenerate > 50;
       double best = -kEps;
       for (int j = 0; j < ncols; ++j) {
         if (!allowed(j) || obj[j] >= -kEps) continue;
@@ -78,7 +78,25 @@ struct Tableau {
 
 }  // namespace
 
+namespace {
+LpResult solve_once(const LpProblem& p, int max_pivots, bool bland);
+}
+
 LpResult solve_lp(const LpProblem& p, int max_pivots) {
+  // Dantzig's rule first (fast); an instance it loses to round-off on long
+  // degenerate stretches (a spurious "unbounded"/"infeasible", seen with
+  // measured link rates next to planning constants) is solved again with
+  // Bland's rule from the start, which never cycles.
+  LpResult r = solve_once(p, max_pivots, false);
+  if (r.ok) return r;
+  LpResult b = solve_once(p, max_pivots, true);
+  b.pivots += r.pivots;
+  if (!b.ok) b.status = r.status + " / bland: " + b.status;
+  return b;
+}
+
+namespace {
+LpResult solve_once(const LpProblem& p, int max_pivots, bool bland) {
   LpResult res;
   const int n = p.n, neq = int(p.eq.size()), nle = int(p.le.size());
   const int m = neq + nle;
@@ -118,7 +136,7 @@ LpResult solve_lp(const LpProblem& p, int max_pivots) {
       for (int j = 0; j < art0; ++j) obj[j] -= ri[j];
       obj[T.W - 1] -= ri[T.W - 1];
     }
-    const char* st = T.run([&](int j) { return j < art0; }, ncols, res.pivots, max_pivots);
+    const char* st = T.run([&](int j) { return j < art0; }, ncols, res.pivots, max_pivots, bland);
     if (std::string(st) != "optimal") {
       res.status = st;
       return res;
@@ -150,7 +168,7 @@ LpResult solve_lp(const LpProblem& p, int max_pivots) {
       const double* ri = T.row(i);
       for (int j = 0; j < T.W; ++j) obj[j] -= cb * ri[j];
     }
-    const char* st = T.run([&](int j) { return j < art0; }, ncols, res.pivots, max_pivots);
+    const char* st = T.run([&](int j) { return j < art0; }, ncols, res.pivots, max_pivots, bland);
     res.status = st;
     if (std::string(st) != "optimal") return res;
   }
@@ -162,5 +180,6 @@ LpResult solve_lp(const LpProblem& p, int max_pivots) {
   for (int j = 0; j < n; ++j) res.obj += p.c[size_t(j)] * res.x[size_t(j)];
   return res;
 }
+}  // namespace
 
 }  // namespace dissem

@@ -89,6 +89,29 @@ def test_bench_modes(n, mode, extra, request):
     assert st["verify_failures"] == 0 and st["unverified_pieces"] == 0
 
 
+@pytest.mark.parametrize("mode,extra", [(1, []), (0, ["--seeding", "leader"])])
+def test_bench_fake_hosts(mode, extra):
+    """4 ranks posing as 2 hosts x 2 GPUs (DISSEM_FAKE_HOSTS=2) over real RCCL:
+    host-aware comm lanes, mode 1's once-per-host imports with xGMI relays and
+    mode 0's three-level tree. Mode 0 with the leader holding every layer is the
+    run that hung before the CRC tables were uploaded without a host sync
+    (profiles/r3_multihost/hang_diag/): the other host's ranks start by
+    receiving, so their first check comes after posted receives."""
+    if _ngpus() < 1:
+        pytest.skip("needs a GPU")
+    os.environ["DISSEM_FAKE_HOSTS"] = "2"
+    try:
+        r = _torchrun(4, ["bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1", "--layers", "8",
+                          "--layer-mib", "64", "--chunk-mib", "16", "--probe-mib", "16", "--mode", str(mode)] + extra)
+    finally:
+        del os.environ["DISSEM_FAKE_HOSTS"]
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["config"]["hosts"] == 2 and out["config"].get("fallback") is None
+    st = out["config"]["engine_stats_rank0"]
+    assert st["verify_failures"] == 0 and st["unverified_pieces"] == 0 and st["order_violations"] == 0
+
+
 @pytest.mark.parametrize("size", [32 << 20, (32 << 20) + 13])
 def test_cli_torchrun_rccl(n, size, tmp_path):
     """The CLI over RCCL; the second size is not a multiple of 16 (like the
