@@ -130,3 +130,16 @@ def test_rank_death_eight_ranks_mode3_flow():
     res, _ = _cluster(cfg, dead_rank=5, die_after=2, mode=3)
     assert res[0].recoveries == 1
     assert res[0].dropped == len(cfg.assignment[5])
+
+
+def test_rank_death_on_two_hosts_hierarchical():
+    """2 hosts x 4 GPUs (host-aware lanes, hierarchical mode 1 with imports and
+    xGMI relays): a rank of the second host dies mid-session. The survivors
+    drop to per-distance lanes over the shrunk communicator and the leader's
+    re-plan still imports once per host - every survivor ends byte-exact."""
+    cfg = make_workload(8, 16, 4 * MiB, tier="host", seeding="uniform", copies=2, seed=5, chunk_bytes=MiB)
+    for nd in cfg.nodes:
+        nd.host = f"h{nd.id // 4}"
+    res, _ = _cluster(cfg, dead_rank=6, die_after=2, owner_policy="links")
+    assert res[0].recoveries == 1
+    assert res[0].dropped == len(cfg.assignment[6])
