@@ -173,12 +173,34 @@ struct Fabric {
 std::mutex g_fab_mu;
 std::map<std::string, std::shared_ptr<Fabric>> g_fabrics;
 
-std::shared_ptr<Fabric> fabric(const std::string& key, const Fabric* inherit = nullptr) {
+// A shrunk communicator runs over the same links and hosts, its ranks
+// renumbered without the dead ones: rank-indexed timing follows them.
+SimTiming survivors_timing(const SimTiming& t, const std::vector<int>& dead, int old_world) {
+  SimTiming out = t;
+  std::vector<int> to(size_t(old_world), -1);
+  for (int r = 0, k = 0; r < old_world; ++r)
+    if (std::find(dead.begin(), dead.end(), r) == dead.end()) to[size_t(r)] = k++;
+  if (!t.host.empty()) {
+    out.host.clear();
+    for (int r = 0; r < old_world && r < int(t.host.size()); ++r)
+      if (to[size_t(r)] >= 0) out.host.push_back(t.host[size_t(r)]);
+  }
+  out.link.clear();
+  for (auto& kv : t.link) {
+    const int a = kv.first.first, b = kv.first.second;
+    if (a < old_world && b < old_world && to[size_t(a)] >= 0 && to[size_t(b)] >= 0)
+      out.link[{to[size_t(a)], to[size_t(b)]}] = kv.second;
+  }
+  return out;
+}
+
+std::shared_ptr<Fabric> fabric(const std::string& key, const Fabric* inherit = nullptr,
+                               const std::vector<int>& dead = {}, int old_world = 0) {
   std::lock_guard<std::mutex> lk(g_fab_mu);
   auto& f = g_fabrics[key];
   if (!f) {
     f = std::make_shared<Fabric>();
-    if (inherit) f->timing = inherit->timing;  // a shrunk communicator runs over the same links
+    if (inherit) f->timing = survivors_timing(inherit->timing, dead, old_world);
   }
   return f;
 }
@@ -462,13 +484,14 @@ class SimBackend : public Backend {
     int new_rank = 0;
     for (int r = 0; r < rank_; ++r)
       if (std::find(dead.begin(), dead.end(), r) == dead.end()) ++new_rank;
+    const int old_world = world_;
     world_ -= int(dead.size());
     rank_ = new_rank;
     {
       std::lock_guard<std::mutex> lk(ev_mu_);
       error_.clear();
     }
-    fab_ = fabric(key_ + "/shrink" + std::to_string(generation), fab_.get());
+    fab_ = fabric(key_ + "/shrink" + std::to_string(generation), fab_.get(), dead, old_world);
     return rank_;
   }
 
