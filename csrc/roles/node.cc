@@ -1522,6 +1522,9 @@ bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID
       if (sender == node || jd.second.state != JobState::Pending || load_[sender] == 0 ||
           (node_rate != 0 && node_rate < sender_rate))
         continue;
+      // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
+      const NodeID dest = jd.first.first;
+      if (host_of(node) != host_of(dest) && host_of(sender) == host_of(dest) && multi_host()) continue;
       double ttf = perf_.count(sender) ? perf_[sender].first * double(load_[sender]) : 1e300;
       Cand c{l.first, jd.first, sender, cnt, ttf};
       if (!have || c.owners < best.owners || (c.owners == best.owners && c.ttf > best.ttf)) {
@@ -1625,6 +1628,33 @@ void Node::schedule_mode2() {
       }
     }
   for (auto& kv : status_) load_.emplace(kv.first, 0);
+  // Several hosts (planned engines): a layer that no GPU of a host holds is
+  // pulled across the network by one GPU of that host - the entry, the dest
+  // with the fewest imports so far - and every other dest of the host pulls it
+  // from the entry once it holds it (its ack makes it an owner and kicks it),
+  // over xGMI. Jobs from an entry are not stolen across hosts.
+  const bool hier = e_->planned() && multi_host();
+  std::map<std::pair<int, LayerID>, NodeID> entry;
+  if (hier) {
+    std::map<NodeID, int> imports;
+    for (LayerID layer : sorted) {
+      auto lj = jobs_.find(layer);
+      if (lj == jobs_.end()) continue;
+      std::map<int, std::set<NodeID>> remote_dests;  // host -> dests with no holder on it
+      for (auto& jd : lj->second) {
+        const NodeID d = jd.first.first;
+        const NodeID s = min_loaded_sender(layer, d);
+        if (s != kClientID && host_of(s) != host_of(d)) remote_dests[host_of(d)].insert(d);
+      }
+      for (auto& hv : remote_dests) {
+        NodeID e = *hv.second.begin();
+        for (NodeID d : hv.second)
+          if (imports[d] < imports[e]) e = d;
+        imports[e]++;
+        entry[{hv.first, layer}] = e;
+      }
+    }
+  }
   for (LayerID layer : sorted) {
     auto lj = jobs_.find(layer);
     if (lj == jobs_.end()) continue;
@@ -1633,6 +1663,10 @@ void Node::schedule_mode2() {
       if (sender == kClientID) {
         log::error(int64_t(cfg_.id)).u("layer", layer).msg("no owner holds the layer");
         continue;
+      }
+      if (hier && host_of(sender) != host_of(jd.first.first)) {
+        auto en = entry.find({host_of(jd.first.first), layer});
+        if (en != entry.end() && en->second != jd.first.first) sender = en->second;
       }
       jd.second.sender = sender;
       jd.second.state = JobState::Pending;

@@ -294,3 +294,43 @@ def test_mode3_across_hosts_every_session_plans():
     finally:
         for r in rts:
             r.close()
+
+
+@pytest.mark.parametrize("hosts,n,window", [(2, 6, 1), (3, 6, 5), (2, 8, 7)])
+def test_mode2_pulls_once_per_host(hosts, n, window):
+    """Mode 2 (pull / steal) on several hosts: one GPU of a host that lacks a
+    layer pulls it across the network; its host peers pull it from that GPU
+    once it holds it (its ack kicks it), and no job a host serves itself is
+    stolen across hosts. Byte-exact, and every layer enters each other host
+    exactly once (the flat pull: about once per GPU)."""
+    key = f"mh2{next(_keys)}"
+    per = n // hosts
+    host_of = [i // per for i in range(n)]
+    size = 4 * MiB
+    cfg = make_workload(n, 12, size, tier="host", seeding="random", chunk_bytes=MiB)
+    for nd in cfg.nodes:
+        nd.host = f"h{host_of[nd.id]}"
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key) for i in range(n)]
+    reg = {i: r.transport.address() for i, r in enumerate(rts)}
+    for r in rts:
+        r.transport.set_registry(reg)
+    try:
+        for r in rts:
+            r.prepare(2, pull_window=window)
+        res = [None] * n
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, rts[i].execute(60))) for i in range(n)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert all(x.ok for x in res), [x.error for x in res]
+        for i, r in enumerate(rts):
+            for l in cfg.assignment[i]:
+                assert r.layer_bytes(l) == _core.fill_random_host(size, layer_seed(0, l)), (i, l)
+        sent = [r.link_stats()["sent"] for r in rts]
+        holders = {l: i for i, nd in enumerate(cfg.nodes) for per_src in nd.initial_layers.values() for l in per_src}
+        once = sum(size for l, h in holders.items() for H in set(host_of) if host_of[h] != H)
+        assert cross_bytes(sent, host_of) == once
+    finally:
+        for r in rts:
+            r.close()
