@@ -364,3 +364,18 @@ def test_nic_budget_across_hosts(core):
     same = core.solve_flow(holdings, demands, links=links, host={n: 0 for n in range(4)},
                            nic={n: 10 * G for n in range(4)})
     assert same.T == pytest.approx(0.02, rel=1e-3)
+
+
+def test_lp_does_not_cycle_on_beales_example(core):
+    """Beale's degenerate LP cycles forever under Dantzig's rule without an
+    anti-cycling rule; the simplex (sched/lp.cc) switches to Bland's rule on
+    long degenerate stretches, and re-solves with Bland from the start when
+    Dantzig's run ends in a spurious verdict. Optimum: -5/4 (x1 = x3 = 1; scipy agrees)."""
+    c = [-0.75, 20.0, -0.5, 6.0]
+    le = [([(0, 0.25), (1, -8.0), (2, -1.0), (3, 9.0)], 0.0),
+          ([(0, 0.5), (1, -12.0), (2, -0.5), (3, 3.0)], 0.0),
+          ([(2, 1.0)], 1.0)]
+    ok, status, obj, x, pivots = core.solve_lp(4, c, [], le)
+    assert ok and status == "optimal", status
+    assert obj == pytest.approx(-1.25, abs=1e-9)
+    assert x[0] == pytest.approx(1.0) and x[2] == pytest.approx(1.0)
