@@ -1442,6 +1442,13 @@ NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
   // A sender's rate for this job is its tier's LimitRate capped by its link to
   // the dest when the plan knows it (measured or configured): on equal links
   // this is the reference's choice.
+  // A dest that holds the layer in another tier loads it itself (as modes 1
+  // and 3 do): a transfer from a peer would land on top of its own staging
+  // of the same chunks (a race TSAN caught in the rank-death selftest).
+  if (!suspects_.count(dest)) {
+    auto sd = status_.find(dest);
+    if (sd != status_.end() && sd->second.count(layer) && load_.count(dest)) return dest;
+  }
   // Several hosts: a holder on the dest's host (xGMI) before any across the
   // network (the NIC a GPU shares with all of its remote peers).
   NodeID best = 0;
@@ -1784,6 +1791,46 @@ void Node::schedule_mode3() {
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     stats_.flow_T = plan.T;
+  }
+  // Safety net: every demand's byte ranges must cover the layer, or its dest
+  // never completes it and the session hangs. A plan that leaves a gap (the
+  // LP's rounding of tiny shares onto the chunk grid can) gets the gap from
+  // the demand's largest sender, at the plan's pace.
+  if (plan.feasible) {
+    std::map<std::pair<LayerID, NodeID>, std::vector<std::pair<int64_t, int64_t>>> cover;
+    std::map<std::pair<LayerID, NodeID>, std::pair<NodeID, int64_t>> biggest;
+    for (auto& j : plan.jobs) {
+      cover[{j.layer, j.dest}].push_back({j.offset, j.offset + j.size});
+      auto& b = biggest[{j.layer, j.dest}];
+      if (j.size > b.second) b = {j.sender, j.size};
+    }
+    int64_t filled = 0;
+    for (auto& d : p.demands) {
+      auto& v = cover[{d.layer, d.dest}];
+      std::sort(v.begin(), v.end());
+      int64_t pos = 0;
+      std::vector<std::pair<int64_t, int64_t>> gaps;
+      for (auto& r : v) {
+        if (r.first > pos) gaps.push_back({pos, r.first});
+        pos = std::max(pos, r.second);
+      }
+      if (pos < d.size) gaps.push_back({pos, d.size});
+      auto bg = biggest.find({d.layer, d.dest});
+      NodeID src = bg != biggest.end() ? bg->second.first : kClientID;
+      if (src == kClientID)
+        for (auto& hs : p.holdings)
+          if (hs.first != d.dest && hs.second.count(d.layer)) {
+            src = hs.first;
+            break;
+          }
+      if (src == kClientID) continue;
+      for (auto& g : gaps) {
+        plan.jobs.push_back(FlowJob{src, d.layer, d.dest, g.second - g.first, g.first});
+        filled += g.second - g.first;
+      }
+    }
+    if (filled)
+      log::warn(int64_t(cfg_.id)).i("gap_bytes", filled).msg("mode 3: the plan left bytes uncovered; filled from a sender");
   }
   for (auto& j : plan.jobs) {
     Message f;
