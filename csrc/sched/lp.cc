@@ -86,13 +86,27 @@ LpResult solve_lp(const LpProblem& p, int max_pivots) {
   // Dantzig's rule first (fast); an instance it loses to round-off on long
   // degenerate stretches (a spurious "unbounded"/"infeasible", seen with
   // measured link rates next to planning constants) is solved again with
-  // Bland's rule from the start, which never cycles.
+  // Bland's rule from the start, which never cycles, and then with every row
+  // equilibrated (divided by its largest coefficient: the same feasible set,
+  // pivots of one magnitude).
   LpResult r = solve_once(p, max_pivots, false);
   if (r.ok) return r;
   LpResult b = solve_once(p, max_pivots, true);
   b.pivots += r.pivots;
-  if (!b.ok) b.status = r.status + " / bland: " + b.status;
-  return b;
+  if (b.ok) return b;
+  LpProblem q = p;
+  for (auto* rows : {&q.eq, &q.le})
+    for (auto& row : *rows) {
+      double mx = 0;
+      for (auto& e : row.a) mx = std::max(mx, std::fabs(e.second));
+      if (mx <= 0) continue;
+      for (auto& e : row.a) e.second /= mx;
+      row.b /= mx;
+    }
+  LpResult e = solve_once(q, max_pivots, true);
+  e.pivots += b.pivots;
+  if (!e.ok) e.status = r.status + " / bland: " + b.status + " / equilibrated: " + e.status;
+  return e;
 }
 
 namespace {
