@@ -14,7 +14,7 @@
 #   init       parallel vs split lane-communicator set-up at 8 shared ranks; rank-death re-form
 #   r3rehearse host-share (config #2), disk tier + node NVMe budget (config #4) at 8 shared ranks; N = 1 A/Bs
 #   r3kernels  fused verify+unpack store A/B + counters, copy bandwidth beside CRC, NUMA A/B
-#   multihost  8 shared ranks rehearsed as 2 hosts x 4 GPUs: host-aware lanes, hierarchical vs flat mode 1
+#   multihost  8 shared ranks rehearsed as 2 hosts x 4 GPUs: host-aware lanes, hierarchical vs flat modes 1/0, modes 2/3
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
 #   crc        CRC32C kernels: numerics, A/B throughput, kernel trace, LDS/VALU counters
@@ -203,7 +203,7 @@ case "$RECIPE" in
     # 8 ranks on one GPU rehearsed as 2 hosts x 4 GPUs (DISSEM_FAKE_HOSTS=2): host-aware comm lanes
     # (14: 6 per host mesh + 8 across) and the hierarchical mode-1 plan over real RCCL; then the flat plan
     rc=0
-    for spec in "1" "1 --no-hierarchical" "0 --seeding leader" "0 --seeding leader --no-hierarchical" "2"; do
+    for spec in "1" "1 --no-hierarchical" "0 --seeding leader" "0 --seeding leader --no-hierarchical" "2" "3"; do
       set -- $spec
       mode=$1; shift
       tag=m${mode}$(echo "$*" | tr -c 'a-z0-9' '_')
