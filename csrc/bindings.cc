@@ -480,6 +480,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("bytes_received", &NodeStats::bytes_received)
       .def_readonly("flow_T", &NodeStats::flow_T)
       .def_readonly("plan_ms", &NodeStats::plan_ms)
+      .def_readonly("plan_cached", &NodeStats::plan_cached)
+      .def_readonly("plan_sched_ms", &NodeStats::plan_sched_ms)
+      .def_readonly("plan_dispatch_ms", &NodeStats::plan_dispatch_ms)
       .def_readonly("nacks", &NodeStats::nacks)
       .def_readonly("redispatched", &NodeStats::redispatched)
       .def_readonly("suspects", &NodeStats::suspects)

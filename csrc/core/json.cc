@@ -1,6 +1,7 @@
 #include "core/json.h"
 
 #include <cctype>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -136,8 +137,11 @@ void Json::dump_to(std::string& out) const {
     case Kind::Null: out += "null"; break;
     case Kind::Bool: out += b_ ? "true" : "false"; break;
     case Kind::Int: {
-      if (neg_) out.push_back('-');
-      out += std::to_string(mag_);
+      char buf[24];
+      char* e = buf;
+      if (neg_) *e++ = '-';
+      e = std::to_chars(e, buf + sizeof buf, mag_).ptr;
+      out.append(buf, size_t(e - buf));
       break;
     }
     case Kind::Float: {
@@ -292,21 +296,21 @@ struct Parser {
       ++p;
     }
     if (p == end) throw JsonIncomplete();
-    std::string tok(s, p);
-    if (tok == "-" || tok.empty()) fail("bad number");
+    const char* digits = s + (neg ? 1 : 0);
+    if (digits == p) fail("bad number");
     if (!is_float) {
-      errno = 0;
-      const char* digits = tok.c_str() + (neg ? 1 : 0);
-      char* ep = nullptr;
-      unsigned long long mag = strtoull(digits, &ep, 10);
-      if (*ep != 0) fail("bad integer");
-      if (errno == ERANGE) return Json(strtod(tok.c_str(), nullptr));
+      // in place: no token copy (control-plane batches carry thousands of integers)
+      uint64_t mag = 0;
+      auto r = std::from_chars(digits, p, mag);
+      if (r.ec == std::errc::result_out_of_range) return Json(strtod(std::string(s, p).c_str(), nullptr));
+      if (r.ec != std::errc() || r.ptr != p) fail("bad integer");
       if (neg) {
         if (mag > (1ull << 63)) return Json(-double(mag));
         return Json(int64_t(uint64_t(0) - uint64_t(mag)));
       }
-      return Json(uint64_t(mag));
+      return Json(mag);
     }
+    std::string tok(s, p);
     char* ep = nullptr;
     double d = strtod(tok.c_str(), &ep);
     if (*ep != 0) fail("bad float");
@@ -330,7 +334,7 @@ struct Parser {
           ws();
           if (peek() != ':') fail("expected ':'");
           ++p;
-          obj[k] = value();
+          obj.insert_or_assign(std::move(k), value());
           ws();
           char d = peek();
           ++p;
@@ -387,6 +391,49 @@ size_t Json::parse_prefix(const char* buf, size_t len, Json& out) {
     return 0;
   }
   return size_t(ps.p - buf);
+}
+
+size_t Json::scan_prefix(const char* buf, size_t len) {
+  const char* p = buf;
+  const char* end = buf + len;
+  auto ws = [&] {
+    while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  };
+  ws();
+  if (p == end) return 0;
+  int depth = 0;
+  for (;;) {
+    if (p == end) return 0;
+    const char c = *p;
+    if (c == '"') {
+      ++p;
+      for (;;) {
+        if (p == end) return 0;
+        if (*p == '\\') {
+          if (end - p < 2) return 0;
+          p += 2;
+          continue;
+        }
+        if (*p++ == '"') break;
+      }
+    } else if (c == '{' || c == '[') {
+      if (++depth > 256) throw std::runtime_error("json parse error: nesting too deep");
+      ++p;
+    } else if (c == '}' || c == ']') {
+      if (--depth < 0) throw std::runtime_error("json parse error: unbalanced");
+      ++p;
+    } else if (c == ',' || c == ':' || c == ' ' || c == '\n' || c == '\r' || c == '\t') {
+      if (depth == 0) throw std::runtime_error("json parse error: unexpected separator");
+      ++p;
+    } else {
+      // a scalar (number or literal): complete once a delimiter follows it
+      while (p < end && *p != ',' && *p != ']' && *p != '}' && *p != ' ' && *p != '\n' && *p != '\r' &&
+             *p != '\t' && *p != ':')
+        ++p;
+      if (p == end) return 0;
+    }
+    if (depth == 0) return size_t(p - buf);
+  }
 }
 
 Json Json::parse(const std::string& text) {

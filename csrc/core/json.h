@@ -74,6 +74,12 @@ class Json {
   // value is incomplete (need more bytes), throws on malformed input. Leading
   // whitespace is skipped and counted.
   static size_t parse_prefix(const char* buf, size_t len, Json& out);
+  // The extent of one value at the front of buf[0..len) without building it:
+  // bytes it spans (leading whitespace included), 0 if incomplete. Checks
+  // nesting and string syntax only (the decoder validates the rest); lets a
+  // stream reader find a message's end once instead of re-parsing a large
+  // message on every partial read.
+  static size_t scan_prefix(const char* buf, size_t len);
 
  private:
   Kind kind_;

@@ -1,5 +1,8 @@
 #include "core/wire.h"
 
+#include <charconv>
+#include <string_view>
+
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
@@ -219,9 +222,12 @@ Json encode_payload(const Message& m) {
         e.push_back(Json(j.size));
         e.push_back(Json(j.total));
         e.push_back(Json(j.chunk_bytes));
-        Json c = Json::array();
-        for (uint32_t x : j.crc) c.push_back(Json(unsigned(x)));
-        e.push_back(c);
+        std::string hx(j.crc.size() * 8, '0');
+        for (size_t i = 0; i < j.crc.size(); ++i) {
+          static const char* dg = "0123456789abcdef";
+          for (int k = 0; k < 8; ++k) hx[i * 8 + size_t(k)] = dg[(j.crc[i] >> (4 * (7 - k))) & 15];
+        }
+        e.push_back(Json(hx));
         if (j.rate) e.push_back(Json(j.rate));
         arr.push_back(e);
       }
@@ -306,7 +312,259 @@ Json encode_payload(const Message& m) {
   return p;
 }
 
+namespace {
+// Transfer batches are the largest control messages (every job of a session,
+// each with its chunks' CRCs) and sit between "timer start" and the first
+// byte on a link: written straight to text, the same bytes the Json DOM
+// dump gives (sorted keys: envelope payload/src/type, payload Batch/Epoch/Jobs/SrcID).
+// Writes into a buffer sized for the worst case up front (no per-append checks).
+struct Out {
+  char* p;
+  template <class T>
+  void num(T v) {
+    p = std::to_chars(p, p + 24, v).ptr;
+  }
+  void lit(const char* t) {
+    const size_t n = strlen(t);
+    memcpy(p, t, n);
+    p += n;
+  }
+  void ch(char c) { *p++ = c; }
+  // CRCs as one string of 8 hex digits each (a job's chunk CRCs are most of a
+  // batch: fixed-width hex is ~10x cheaper to write and read than decimals)
+  void hex(const std::vector<uint32_t>& v) {
+    static const char* d = "0123456789abcdef";
+    for (uint32_t x : v)
+      for (int k = 7; k >= 0; --k) *p++ = d[(x >> (4 * k)) & 15];
+  }
+};
+
+std::string encode_xfer_batch(const Message& m) {
+  size_t crcs = 0;
+  for (auto& j : m.jobs) crcs += j.crc.size();
+  std::string s;
+  s.resize(128 + m.jobs.size() * (10 * 21 + 8) + crcs * 8);
+  Out o{s.data()};
+  o.lit("{\"payload\":{\"Batch\":");
+  o.num(uint64_t(m.batch));
+  if (m.epoch) {
+    o.lit(",\"Epoch\":");
+    o.num(uint64_t(m.epoch));
+  }
+  o.lit(",\"Jobs\":[");
+  for (size_t i = 0; i < m.jobs.size(); ++i) {
+    const XferJob& j = m.jobs[i];
+    if (i) o.ch(',');
+    o.ch('[');
+    o.num(uint64_t(j.seq));
+    o.ch(',');
+    o.num(uint64_t(j.src));
+    o.ch(',');
+    o.num(uint64_t(j.dst));
+    o.ch(',');
+    o.num(uint64_t(j.layer));
+    o.ch(',');
+    o.num(j.offset);
+    o.ch(',');
+    o.num(j.size);
+    o.ch(',');
+    o.num(j.total);
+    o.ch(',');
+    o.num(j.chunk_bytes);
+    o.ch(',');
+    o.ch('"');
+    o.hex(j.crc);
+    o.ch('"');
+    if (j.rate) {
+      o.ch(',');
+      o.num(j.rate);
+    }
+    o.ch(']');
+  }
+  o.lit("],\"SrcID\":");
+  o.num(uint64_t(m.src));
+  o.lit("},\"src\":\"");
+  o.num(uint64_t(m.src));
+  o.lit("\",\"type\":");
+  o.num(uint64_t(unsigned(m.type)));
+  o.ch('}');
+  s.resize(size_t(o.p - s.data()));
+  return s;
+}
+
+bool parse_crc_hex(std::string_view h, std::vector<uint32_t>* out) {
+  if (h.size() % 8) return false;
+  out->reserve(h.size() / 8);
+  for (size_t i = 0; i < h.size(); i += 8) {
+    uint32_t v = 0;
+    for (size_t k = 0; k < 8; ++k) {
+      const char c = h[i + k];
+      uint32_t d;
+      if (c >= '0' && c <= '9') d = uint32_t(c - '0');
+      else if (c >= 'a' && c <= 'f') d = uint32_t(c - 'a' + 10);
+      else if (c >= 'A' && c <= 'F') d = uint32_t(c - 'A' + 10);
+      else return false;
+      v = (v << 4) | d;
+    }
+    out->push_back(v);
+  }
+  return true;
+}
+
+// A cursor over envelope text for the transfer-batch fast path. Any shape it
+// does not expect makes it give up (ok = false): the caller then decodes the
+// same bytes through the Json DOM, so it only ever saves time.
+struct Cur {
+  const char* p;
+  const char* e;
+  bool ok = true;
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  }
+  bool eat(char c) {
+    ws();
+    if (p < e && *p == c) {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+  void need(char c) {
+    if (!eat(c)) ok = false;
+  }
+  bool key(std::string_view* k) {  // "name" then ':'
+    ws();
+    if (p >= e || *p != '"') return ok = false;
+    const char* b = ++p;
+    while (p < e && *p != '"') {
+      if (*p == '\\') return ok = false;
+      ++p;
+    }
+    if (p >= e) return ok = false;
+    *k = std::string_view(b, size_t(p - b));
+    ++p;
+    need(':');
+    return ok;
+  }
+  template <class T>
+  T num() {
+    ws();
+    T v{};
+    auto r = std::from_chars(p, e, v);
+    if (r.ec != std::errc()) {
+      ok = false;
+      return T{};
+    }
+    p = r.ptr;
+    return v;
+  }
+  // skip one value of any kind (strings, numbers, nested containers)
+  void skip() {
+    ws();
+    size_t n = Json::scan_prefix(p, size_t(e - p));
+    if (n == 0) ok = false;
+    p += n;
+  }
+};
+
+bool decode_xfer_payload(Cur& c, Message& m) {
+  if (!c.eat('{')) return false;
+  if (c.eat('}')) return true;
+  do {
+    std::string_view k;
+    if (!c.key(&k)) return false;
+    if (k == "Batch") {
+      m.batch = c.num<uint64_t>();
+    } else if (k == "Epoch") {
+      m.epoch = c.num<uint64_t>();
+    } else if (k == "SrcID") {
+      m.src = c.num<uint64_t>();
+    } else if (k == "Jobs") {
+      if (!c.eat('[')) return false;
+      m.jobs.reserve(256);
+      if (!c.eat(']')) {
+        do {
+          XferJob j;
+          if (!c.eat('[')) return false;
+          j.seq = c.num<uint64_t>();
+          c.need(',');
+          j.src = c.num<uint64_t>();
+          c.need(',');
+          j.dst = c.num<uint64_t>();
+          c.need(',');
+          j.layer = c.num<uint64_t>();
+          c.need(',');
+          j.offset = c.num<int64_t>();
+          c.need(',');
+          j.size = c.num<int64_t>();
+          c.need(',');
+          j.total = c.num<int64_t>();
+          c.need(',');
+          j.chunk_bytes = c.num<int64_t>();
+          c.need(',');
+          if (c.eat('"')) {
+            const char* b = c.p;
+            while (c.p < c.e && *c.p != '"') ++c.p;
+            if (c.p >= c.e || !parse_crc_hex(std::string_view(b, size_t(c.p - b)), &j.crc)) return false;
+            ++c.p;
+          } else {
+            if (!c.eat('[')) return false;
+            if (!c.eat(']')) {
+              do j.crc.push_back(c.num<uint32_t>());
+              while (c.ok && c.eat(','));
+              c.need(']');
+            }
+          }
+          if (c.eat(',')) j.rate = c.num<int64_t>();
+          c.need(']');
+          if (!c.ok) return false;
+          m.jobs.push_back(std::move(j));
+        } while (c.eat(','));
+        c.need(']');
+      }
+    } else {
+      return false;  // a field this path does not know: the DOM decoder handles it
+    }
+  } while (c.ok && c.eat(','));
+  c.need('}');
+  return c.ok;
+}
+}  // namespace
+
+MessagePtr decode_envelope_text(const char* buf, size_t len) {
+  {
+    Cur c{buf, buf + len};
+    auto m = std::make_shared<Message>();
+    bool batch = false, typed = false;
+    if (c.eat('{') && !c.eat('}')) {
+      do {
+        std::string_view k;
+        if (!c.key(&k)) break;
+        if (k == "payload") {
+          batch = decode_xfer_payload(c, *m);
+          if (!batch) break;
+        } else if (k == "src") {
+          c.ws();
+          c.skip();  // "src" is informative: SrcID in the payload is the sender
+        } else if (k == "type") {
+          typed = c.num<unsigned>() == unsigned(MsgType::XferBatch);
+          if (!typed) break;
+        } else {
+          c.ok = false;
+        }
+      } while (c.ok && c.eat(','));
+      if (batch && typed && c.ok && c.eat('}')) {
+        m->type = MsgType::XferBatch;
+        m->src_str = node_str(m->src);
+        return m;
+      }
+    }
+  }
+  return decode_envelope(Json::parse(std::string(buf, len)));
+}
+
 std::string encode_envelope(const Message& m) {
+  if (m.type == MsgType::XferBatch) return encode_xfer_batch(m);
   Json env = Json::object();
   env["type"] = Json(unsigned(m.type));
   env["src"] = Json(m.type == MsgType::Simple ? m.src_addr : node_str(m.src));
@@ -359,7 +617,11 @@ MessagePtr decode_envelope(const Json& env) {
           j.size = a.at(5).as_i64();
           j.total = a.at(6).as_i64();
           j.chunk_bytes = a.at(7).as_i64();
-          for (auto& x : a.at(8).as_array()) j.crc.push_back(uint32_t(x.as_u64()));
+          if (a.at(8).is_string()) {
+            if (!parse_crc_hex(a.at(8).as_str(), &j.crc)) throw std::runtime_error("bad CRC hex in xfer job");
+          } else {
+            for (auto& x : a.at(8).as_array()) j.crc.push_back(uint32_t(x.as_u64()));
+          }
           if (a.size() > 9) j.rate = a.at(9).as_i64();
           m->jobs.push_back(std::move(j));
         }

@@ -114,6 +114,9 @@ std::string encode_envelope(const Message& m);
 Json encode_layer_header(const Message& m);
 // Decode an envelope. Layer envelopes decode into a header-only Layer message.
 MessagePtr decode_envelope(const Json& env);
+// Decode one envelope's text (exactly one JSON value): transfer batches take a
+// direct path, anything else goes through the Json DOM.
+MessagePtr decode_envelope_text(const char* buf, size_t len);
 
 std::string node_str(NodeID id);
 NodeID parse_node_id(const std::string& s);

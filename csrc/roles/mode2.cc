@@ -1,0 +1,275 @@
+// Mode 2: pull-retransmit scheduler (reference: node.go:628-1073) - rarest-first
+// jobs, min-load initial senders, work stealing by throughput, extended to
+// byte-range jobs and a per-sender window.
+#include "roles/node.h"
+
+#include <algorithm>
+#include <climits>
+#include <set>
+#include <tuple>
+
+#include "core/log.h"
+#include "core/trace.h"
+#include "roles/node_internal.h"
+
+namespace dissem {
+
+// ------------------------------------------------------------------- mode 2
+
+NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
+  // node.go:948-978 (the code picks the FASTEST source; quirk Q16 keeps that).
+  // A sender's rate for this job is its tier's LimitRate capped by its link to
+  // the dest when the plan knows it (measured or configured): on equal links
+  // this is the reference's choice.
+  // A dest that holds the layer in another tier loads it itself (as modes 1
+  // and 3 do): a transfer from a peer would land on top of its own staging
+  // of the same chunks (a race TSAN caught in the rank-death selftest).
+  if (!suspects_.count(dest)) {
+    auto sd = status_.find(dest);
+    if (sd != status_.end() && sd->second.count(layer) && load_.count(dest)) return dest;
+  }
+  // Several hosts: a holder on the dest's host (xGMI) before any across the
+  // network (the NIC a GPU shares with all of its remote peers).
+  NodeID best = 0;
+  bool found = false, best_local = false;
+  int64_t best_rate = 0;
+  int64_t min_count = INT64_MAX;
+  for (auto& kv : load_) {
+    NodeID sender = kv.first;
+    if (suspects_.count(sender)) continue;  // missed a deadline: no new work
+    auto st = status_.find(sender);
+    if (st == status_.end()) continue;
+    auto it = st->second.find(layer);
+    if (it == st->second.end()) continue;
+    int64_t eff = it->second.limit_rate == 0 ? INT64_MAX : it->second.limit_rate;
+    if (auto lb = cfg_.link_bw.find({sender, dest}); lb != cfg_.link_bw.end() && lb->second > 0 && sender != dest)
+      eff = std::min(eff, lb->second);
+    int64_t count = kv.second;
+    const bool local = host_of(sender) == host_of(dest);
+    if (!found || (local && !best_local) ||
+        (local == best_local &&
+         (eff > best_rate || (eff == best_rate && (count < min_count || (count == min_count && sender < best)))))) {
+      best = sender;
+      best_rate = eff;
+      min_count = count;
+      best_local = local;
+      found = true;
+    }
+  }
+  return found ? best : kClientID;
+}
+
+bool Node::rarest_own_job(NodeID node, LayerID* layer, JobKey* key) {
+  // node.go:981-1010 (ties: lowest layer id, then lowest (dest, offset))
+  bool ok = false;
+  size_t min_owners = SIZE_MAX;
+  auto st = status_.find(node);
+  if (st == status_.end()) return false;
+  for (auto& l : st->second) {
+    auto lj = jobs_.find(l.first);
+    if (lj == jobs_.end()) continue;
+    for (auto& jd : lj->second) {
+      if (jd.second.sender != node || jd.second.state != JobState::Pending) continue;
+      size_t cnt = owners_[l.first].size();
+      if (!ok || cnt < min_owners || (cnt == min_owners && l.first < *layer)) {
+        min_owners = cnt;
+        *layer = l.first;
+        *key = jd.first;
+        ok = true;
+      }
+    }
+  }
+  return ok;
+}
+
+bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID* victim) {
+  // node.go:1012-1073
+  struct Cand {
+    LayerID layer;
+    JobKey dest;
+    NodeID sender;
+    size_t owners;
+    double ttf;
+  };
+  bool have = false;
+  Cand best{};
+  auto st = status_.find(node);
+  if (st == status_.end()) return false;
+  for (auto& l : st->second) {
+    auto lj = jobs_.find(l.first);
+    if (lj == jobs_.end()) continue;
+    size_t cnt = owners_[l.first].size();
+    for (auto& jd : lj->second) {
+      NodeID sender = jd.second.sender;
+      int64_t sender_rate = 0;
+      if (auto s2 = status_.find(sender); s2 != status_.end())
+        if (auto x = s2->second.find(l.first); x != s2->second.end()) sender_rate = x->second.limit_rate;
+      int64_t node_rate = l.second.limit_rate;
+      if (sender == node || jd.second.state != JobState::Pending || load_[sender] == 0 ||
+          (node_rate != 0 && node_rate < sender_rate))
+        continue;
+      // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
+      const NodeID dest = jd.first.first;
+      if (host_of(node) != host_of(dest) && host_of(sender) == host_of(dest) && multi_host()) continue;
+      double ttf = perf_.count(sender) ? perf_[sender].first * double(load_[sender]) : 1e300;
+      Cand c{l.first, jd.first, sender, cnt, ttf};
+      if (!have || c.owners < best.owners || (c.owners == best.owners && c.ttf > best.ttf)) {
+        best = c;
+        have = true;
+      }
+    }
+  }
+  if (!have) return false;
+  *layer = best.layer;
+  *key = best.dest;
+  *victim = best.sender;
+  return true;
+}
+
+void Node::dispatch_range(LayerID layer, NodeID sender, NodeID dest, int64_t off, int64_t size) {
+  if (off == 0 && size >= layer_size(layer)) {
+    retransmit(layer, sender, dest);  // whole layer: the reference's Retransmit
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.jobs_dispatched++;
+  }
+  if (e_->planned()) {
+    add_job(sender, dest, layer, off, size);
+    return;
+  }
+  track(sender, dest, layer, off, size);
+  if (sender == cfg_.id) {
+    send_layer(dest, layer, off, size, 0);
+    return;
+  }
+  Message f;  // a byte range: FlowRetransmit carries offset + size
+  f.type = MsgType::FlowRetransmit;
+  f.layer = layer;
+  f.dest = dest;
+  f.offset = off;
+  f.data_size = size;
+  send_msg(sender, f);
+}
+
+bool Node::assign_new_job(NodeID node) {
+  // node.go:909-945
+  LayerID layer = 0;
+  JobKey key{0, 0};
+  NodeID victim = 0;
+  if (suspects_.count(node)) return false;
+  if (rarest_own_job(node, &layer, &key)) {
+    Job& j = jobs_[layer][key];
+    j.state = JobState::Sending;
+    j.t_us = log::now_us();
+    load_[node] = std::max<int64_t>(0, load_[node] - 1);
+    inflight_[node]++;
+    log::debug(int64_t(cfg_.id)).u("node", node).u("layer", layer).i("offset", key.second)
+        .msg("pass a job initially assigned");
+    dispatch_range(layer, node, key.first, key.second, j.size);
+    return true;
+  }
+  if (rarest_stealable_job(node, &layer, &key, &victim)) {
+    log::debug(int64_t(cfg_.id)).u("layer", layer)
+        .msg("steal a job from the most loaded node (" + std::to_string(victim) + ") to node " + std::to_string(node));
+    load_[victim] = std::max<int64_t>(0, load_[victim] - 1);
+    Job& j = jobs_[layer][key];
+    j.sender = node;
+    j.state = JobState::Sending;
+    j.t_us = log::now_us();
+    inflight_[node]++;
+    dispatch_range(layer, node, key.first, key.second, j.size);
+    return true;
+  }
+  log::debug(int64_t(cfg_.id)).u("node", node).msg("there is no job left to assign");
+  return false;
+}
+
+void Node::schedule_mode2() {
+  // node.go:810-904
+  for (auto& kv : status_)
+    for (auto& l : kv.second) owners_[l.first].insert(kv.first);
+  std::vector<LayerID> sorted;
+  for (auto& kv : owners_) sorted.push_back(kv.first);
+  std::stable_sort(sorted.begin(), sorted.end(), [&](LayerID a, LayerID b) {
+    if (owners_[a].size() != owners_[b].size()) return owners_[a].size() < owners_[b].size();
+    return a < b;  // rarest first, tiebreak by id
+  });
+  // Jobs are (layer, dest, range). With pull_job_bytes the layer is cut into
+  // ranges (chunk-aligned on planned engines) so stealing can rebalance inside
+  // a layer; 0 keeps the reference's one job per (layer, dest).
+  int64_t jb = cfg_.pull_job_bytes;
+  if (jb > 0 && e_->planned() && e_->chunk_bytes() > 0)
+    jb = std::max<int64_t>(1, (jb + e_->chunk_bytes() - 1) / e_->chunk_bytes()) * e_->chunk_bytes();
+  for (auto& kv : assignment_)
+    for (auto& l : kv.second) {
+      if (at(status_[kv.first], l.first, e_->target())) continue;
+      const int64_t size = layer_size(l.first);
+      const int64_t step = jb > 0 ? jb : std::max<int64_t>(size, 1);
+      for (int64_t off = 0; off < std::max<int64_t>(size, 1); off += step) {
+        Job j;
+        j.size = std::min(step, size - off);
+        jobs_[l.first][{kv.first, off}] = j;
+      }
+    }
+  for (auto& kv : status_) load_.emplace(kv.first, 0);
+  // Several hosts (planned engines): a layer that no GPU of a host holds is
+  // pulled across the network by one GPU of that host - the entry, the dest
+  // with the fewest imports so far - and every other dest of the host pulls it
+  // from the entry once it holds it (its ack makes it an owner and kicks it),
+  // over xGMI. Jobs from an entry are not stolen across hosts.
+  const bool hier = e_->planned() && multi_host();
+  std::map<std::pair<int, LayerID>, NodeID> entry;
+  if (hier) {
+    std::map<NodeID, int> imports;
+    for (LayerID layer : sorted) {
+      auto lj = jobs_.find(layer);
+      if (lj == jobs_.end()) continue;
+      std::map<int, std::set<NodeID>> remote_dests;  // host -> dests with no holder on it
+      for (auto& jd : lj->second) {
+        const NodeID d = jd.first.first;
+        const NodeID s = min_loaded_sender(layer, d);
+        if (s != kClientID && host_of(s) != host_of(d)) remote_dests[host_of(d)].insert(d);
+      }
+      for (auto& hv : remote_dests) {
+        NodeID e = *hv.second.begin();
+        for (NodeID d : hv.second)
+          if (imports[d] < imports[e]) e = d;
+        imports[e]++;
+        entry[{hv.first, layer}] = e;
+      }
+    }
+  }
+  for (LayerID layer : sorted) {
+    auto lj = jobs_.find(layer);
+    if (lj == jobs_.end()) continue;
+    for (auto& jd : lj->second) {
+      NodeID sender = min_loaded_sender(layer, jd.first.first);
+      if (sender == kClientID) {
+        log::error(int64_t(cfg_.id)).u("layer", layer).msg("no owner holds the layer");
+        continue;
+      }
+      if (hier && host_of(sender) != host_of(jd.first.first)) {
+        auto en = entry.find({host_of(jd.first.first), layer});
+        if (en != entry.end() && en->second != jd.first.first) sender = en->second;
+      }
+      jd.second.sender = sender;
+      jd.second.state = JobState::Pending;
+      load_[sender]++;
+      log::info(int64_t(cfg_.id)).msg("job assignment: layer: " + std::to_string(layer) +
+                                      ", sender: " + std::to_string(sender));
+    }
+  }
+  // Kick every node that has queued jobs or is a destination (quirk Q10:
+  // the reference kicks only assignment keys, stranding pure senders).
+  std::set<NodeID> kick;
+  for (auto& kv : assignment_) kick.insert(kv.first);
+  for (auto& kv : load_)
+    if (kv.second > 0) kick.insert(kv.first);
+  for (NodeID n : kick)
+    while (inflight_[n] < cfg_.pull_window && assign_new_job(n)) {
+    }
+}
+
+}  // namespace dissem

@@ -1,9 +1,12 @@
 #include "roles/node.h"
+#include "roles/node_internal.h"
+#include "roles/plan_cache.h"
 
 #include <algorithm>
 #include <climits>
 #include <cstring>
 #include <set>
+#include <thread>
 #include <tuple>
 
 #include "core/log.h"
@@ -12,12 +15,6 @@
 
 namespace dissem {
 
-namespace {
-bool at(const LayerIDs& ids, LayerID l, Location loc) {
-  auto it = ids.find(l);
-  return it != ids.end() && it->second.location == loc;
-}
-}  // namespace
 
 Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEngine> e, const LayersSrc& layers,
            const Assignment& assignment, bool is_leader)
@@ -42,7 +39,10 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
     const LayerIDs inv = store_.inventory();
     const PartialLayers part = store_.partial();
     for (auto& kv : e_->manifest()) {
-      if (inv.count(kv.first)) manifests_[kv.first] = kv.second;
+      if (inv.count(kv.first)) {
+        manifests_[kv.first] = kv.second;
+        manifest_holders_[kv.first].insert(cfg_.id);
+      }
       auto pit = part.find(kv.first);
       if (pit != part.end()) merge_partial_manifest(kv.first, kv.second, pit->second);
     }
@@ -452,12 +452,14 @@ void Node::on_announce(const MessagePtr& m) {
     add_node(m->src);
     for (auto& kv : m->link_rates) measured_links_[{m->src, kv.first}] = kv.second;
   }
+  if (!started_) t_->warm(m->src);  // the first dispatch after "timer start" pays no connect
   for (auto& kv : m->manifest) {
     auto pit = m->partial_layers.find(kv.first);
     if (pit != m->partial_layers.end()) {  // a partial copy vouches for its own chunks only
       merge_partial_manifest(kv.first, kv.second, pit->second);
       continue;
     }
+    manifest_holders_[kv.first].insert(m->src);
     auto it = manifests_.find(kv.first);
     if (it == manifests_.end()) {
       manifests_[kv.first] = kv.second;
@@ -469,6 +471,89 @@ void Node::on_announce(const MessagePtr& m) {
   for (auto& kv : assignment_)
     if (!status_.count(kv.first)) return;
   start_distribution();
+}
+
+namespace {
+struct KeyWriter {
+  std::string& s;
+  template <class T>
+  void put(const T& v) {
+    s.append(reinterpret_cast<const char*>(&v), sizeof v);
+  }
+  void put(const std::string& v) {
+    put(uint64_t(v.size()));
+    s.append(v);
+  }
+  template <class K, class V>
+  void put(const std::map<K, V>& m) {
+    put(uint64_t(m.size()));
+    for (auto& kv : m) {
+      put(kv.first);
+      put(kv.second);
+    }
+  }
+  template <class A, class B>
+  void put(const std::pair<A, B>& p) {
+    put(p.first);
+    put(p.second);
+  }
+  template <class T>
+  void put(const std::vector<T>& v) {
+    put(uint64_t(v.size()));
+    for (auto& x : v) put(x);
+  }
+  template <class T>
+  void put(const std::set<T>& v) {
+    put(uint64_t(v.size()));
+    for (auto& x : v) put(x);
+  }
+  void put(const LayerMeta& m) {
+    put(int(m.location));
+    put(m.limit_rate);
+    put(int(m.source_type));
+    put(m.size);
+  }
+  void put(const CrcManifest& m) {
+    put(m.chunk_bytes);
+    put(m.crc);
+  }
+};
+}  // namespace
+
+// Everything a deterministic scheduler reads, as bytes (roles/plan_cache.h).
+std::string Node::plan_key() {
+  std::string s;
+  s.reserve(64 << 10);
+  KeyWriter w{s};
+  w.put(cfg_.mode);
+  w.put(cfg_.id);
+  w.put(cfg_.owner_policy);
+  w.put(cfg_.align);
+  w.put(cfg_.integer_seconds);
+  w.put(cfg_.relay);
+  w.put(cfg_.collective);
+  w.put(cfg_.host_share);
+  w.put(e_->chunk_bytes());
+  w.put(int(e_->target()));
+  w.put(cfg_.network_bw);
+  w.put(cfg_.link_bw);
+  w.put(cfg_.stage_bw);
+  w.put(cfg_.hbm_bw);
+  w.put(cfg_.disk_group);
+  w.put(cfg_.disk_group_bw);
+  w.put(cfg_.host);
+  w.put(cfg_.nic_bw);
+  w.put(status_);
+  w.put(partial_);
+  w.put(assignment_);
+  w.put(manifests_);
+  w.put(uint64_t(partial_crc_.size()));
+  for (auto& kv : partial_crc_) {
+    w.put(kv.first);
+    w.put(kv.second.first);
+    w.put(kv.second.second);
+  }
+  return s;
 }
 
 void Node::start_distribution() {
@@ -497,14 +582,45 @@ void Node::start_distribution() {
   int64_t t0 = log::now_us();
   {
     trace::Scoped plan("dissem.plan");
-    switch (cfg_.mode) {
-      case 0: schedule_mode0(); break;
-      case 1: schedule_mode1(); break;
-      case 2: schedule_mode2(); break;
-      case 3: schedule_mode3(); break;
-      default: log::error(int64_t(cfg_.id)).msg("unknown mode");
+    // Deterministic schedulers on the planned data plane replay an identical
+    // earlier plan (roles/plan_cache.h).
+    const bool cacheable = e_->planned() && ((cfg_.mode == 1 && cfg_.owner_policy == "links") || cfg_.mode == 3);
+    std::string key;
+    std::shared_ptr<const CachedPlan> hit;
+    if (cacheable) {
+      key = plan_key();
+      hit = PlanCache::instance().get(key);
     }
+    if (hit) {
+      pending_jobs_.reserve(hit->jobs.size());
+      for (auto& j : hit->jobs) pending_jobs_.push_back({j.first, j.second});
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.jobs_dispatched += hit->dispatched;
+      stats_.flow_T = hit->flow_T;
+      stats_.plan_cached = true;
+    } else {
+      const int64_t d0 = stats_.jobs_dispatched;
+      switch (cfg_.mode) {
+        case 0: schedule_mode0(); break;
+        case 1: schedule_mode1(); break;
+        case 2: schedule_mode2(); break;
+        case 3: schedule_mode3(); break;
+        default: log::error(int64_t(cfg_.id)).msg("unknown mode");
+      }
+      if (cacheable) {
+        CachedPlan cp;
+        for (auto& pj : pending_jobs_) cp.jobs.push_back({pj.job, pj.phase});
+        std::lock_guard<std::mutex> lk(sig_mu_);
+        cp.dispatched = stats_.jobs_dispatched - d0;
+        cp.flow_T = stats_.flow_T;
+        PlanCache::instance().put(key, std::move(cp));
+      }
+    }
+    const int64_t t1 = log::now_us();
     flush_batch();
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.plan_sched_ms = double(t1 - t0) / 1e3;
+    stats_.plan_dispatch_ms = double(log::now_us() - t1) / 1e3;
   }
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
@@ -927,39 +1043,76 @@ void Node::merge_partial_manifest(LayerID layer, const CrcManifest& m,
 void Node::flush_batch() {
   // Assign global sequence numbers: by phase (relay hops after the hops that
   // feed them), then round-robin over (src, dst) pairs so that consecutive
-  // sequence numbers spread over distinct xGMI links.
+  // sequence numbers spread over distinct xGMI links. This runs between
+  // "timer start" and the first byte on any link: jobs are moved, not copied,
+  // and the leader's own batch goes last (its engine starts staging the
+  // moment it lands, beside the encoding of everyone else's).
   if (pending_jobs_.empty()) return;
   trace::Scoped tr("dissem.flush_batch");
-  std::map<int, std::map<std::pair<NodeID, NodeID>, std::vector<XferJob>>> by_phase;
-  for (auto& pj : pending_jobs_) by_phase[pj.phase][{pj.job.src, pj.job.dst}].push_back(pj.job);
-  pending_jobs_.clear();
+  std::map<std::pair<int, std::pair<NodeID, NodeID>>, std::vector<size_t>> groups;  // (phase, (src, dst)) -> jobs
+  for (size_t i = 0; i < pending_jobs_.size(); ++i)
+    groups[{pending_jobs_[i].phase, {pending_jobs_[i].job.src, pending_jobs_[i].job.dst}}].push_back(i);
   std::map<NodeID, Message> per_rank;
-  for (auto& ph : by_phase) {
+  for (auto g = groups.begin(); g != groups.end();) {
+    const int phase = g->first.first;
+    auto end = g;
+    while (end != groups.end() && end->first.first == phase) ++end;
     for (size_t round = 0;; ++round) {
       bool any = false;
-      for (auto& pr : ph.second) {
-        if (round >= pr.second.size()) continue;
+      for (auto pr = g; pr != end; ++pr) {
+        if (round >= pr->second.size()) continue;
         any = true;
-        XferJob j = pr.second[round];
+        XferJob& j = pending_jobs_[pr->second[round]].job;
         j.seq = next_seq_++;
-        per_rank[j.src].jobs.push_back(j);
         if (j.dst == kAllRanks) {
           for (auto& st : status_)
             if (st.first != j.src) per_rank[st.first].jobs.push_back(j);
-        } else if (j.dst != j.src) {
-          per_rank[j.dst].jobs.push_back(j);
+          per_rank[j.src].jobs.push_back(std::move(j));
+        } else if (j.dst == j.src) {
+          per_rank[j.src].jobs.push_back(std::move(j));
+        } else {
+          // a sender that announced the layer's manifest checks its staging
+          // against its own CRCs: its copy of the job goes without them
+          auto mh = manifest_holders_.find(j.layer);
+          const bool own = mh != manifest_holders_.end() && mh->second.count(j.src);
+          XferJob sj;
+          sj.seq = j.seq;
+          sj.src = j.src;
+          sj.dst = j.dst;
+          sj.layer = j.layer;
+          sj.offset = j.offset;
+          sj.size = j.size;
+          sj.total = j.total;
+          sj.chunk_bytes = j.chunk_bytes;
+          sj.rate = j.rate;
+          if (!own) sj.crc = j.crc;
+          per_rank[j.src].jobs.push_back(std::move(sj));
+          per_rank[j.dst].jobs.push_back(std::move(j));
         }
       }
       if (!any) break;
     }
+    g = end;
   }
+  pending_jobs_.clear();
   const uint64_t batch = next_batch_++;
   int64_t njobs = 0;
-  for (auto& kv : per_rank) {
-    kv.second.type = MsgType::XferBatch;
-    kv.second.batch = batch;
-    njobs += int64_t(kv.second.jobs.size());
-    send_msg(kv.first, kv.second);
+  std::vector<std::pair<NodeID, Message>> out;
+  out.reserve(per_rank.size());
+  for (auto& kv : per_rank)
+    if (kv.first != cfg_.id) out.emplace_back(kv.first, std::move(kv.second));
+  if (auto self = per_rank.find(cfg_.id); self != per_rank.end()) out.emplace_back(self->first, std::move(self->second));
+  for (auto& o : out) {
+    o.second.type = MsgType::XferBatch;
+    o.second.batch = batch;
+    o.second.src = cfg_.id;
+    o.second.epoch = cfg_.epoch;
+    njobs += int64_t(o.second.jobs.size());
+  }
+  try {
+    t_->send_many(out);
+  } catch (const std::exception& e) {
+    log::error(int64_t(cfg_.id)).s("error", e.what()).msg("failed to send xfer_batch");
   }
   log::debug(int64_t(cfg_.id)).u("batch", batch).i("job_copies", njobs).msg("dispatched transfer batch");
 }
@@ -986,871 +1139,6 @@ void Node::retransmit(LayerID layer, NodeID owner, NodeID dest) {
   r.layer = layer;
   r.dest = dest;
   send_msg(owner, r);
-}
-
-void Node::schedule_mode0() {
-  // node.go:326-352: the leader pushes every missing (dest, layer) itself.
-  std::map<LayerID, std::vector<NodeID>> need;
-  for (auto& kv : assignment_)
-    for (auto& l : kv.second)
-      if (!at(status_[kv.first], l.first, e_->target())) need[l.first].push_back(kv.first);
-  int64_t rot = 0;  // relay: which dests take a layer's leftover chunks rotates, so every link carries 1/k
-  int64_t srot = 0;  // host_share: which stagers serve a layer with fewer chunks than stagers rotates
-  std::map<int, int64_t> host_rot;  // several hosts: which GPUs of a host take the slices rotates
-  for (auto& kv : need) {
-    LayerSrc src;
-    if (!store_.get(kv.first, &src)) {
-      log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(kv.first));
-      continue;
-    }
-    // host_share (planned engines): every node holding the layer's bytes below
-    // HBM (the leader's shared host segment, mapped by each rank) stages one
-    // slice of it; the leader is then a dest like any other.
-    std::vector<NodeID> stagers;
-    const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1);
-    const int64_t nchunks = (src.data_size + cb - 1) / cb;
-    if (cfg_.host_share && e_->planned())
-      for (auto& st : status_) {
-        auto it = st.second.find(kv.first);
-        if (it != st.second.end() && it->second.location != e_->target() && it->second.location != Location::Client)
-          stagers.push_back(st.first);
-      }
-    const bool sliced = stagers.size() >= 2 && nchunks >= 2;
-    std::vector<NodeID> remote;
-    for (NodeID d : kv.second) {
-      if (d == cfg_.id && !sliced) {
-        if (e_->planned()) add_job(d, d, kv.first, 0, -1);
-        else send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
-      } else if (d != cfg_.id) {
-        remote.push_back(d);
-      }
-    }
-    {
-      std::lock_guard<std::mutex> lk(sig_mu_);
-      stats_.jobs_dispatched += int64_t(kv.second.size());
-    }
-    if (e_->planned()) {
-      const int64_t total = src.data_size;
-      bool everyone = cfg_.collective && remote.size() >= 2 && remote.size() + 1 == status_.size();
-      if (sliced) {
-        // Slice i of the layer is staged by stager i over its own PCIe (a
-        // local load if it needs the layer) and sent from its HBM to every
-        // other dest; leftover chunks rotate over the stagers layer by layer.
-        // A layer of fewer chunks than stagers goes to a rotating subset.
-        const int64_t S = int64_t(stagers.size()), k = std::min<int64_t>(S, nchunks);
-        int64_t off = 0;
-        for (int64_t i = 0; i < k; ++i) {
-          const int64_t r = ((i - rot) % k + k) % k;
-          const int64_t cnt = nchunks / k + (r < nchunks % k ? 1 : 0);
-          const int64_t len = std::min(total - off, cnt * cb);
-          if (len <= 0) continue;
-          const NodeID s = stagers[size_t((i + srot) % S)];
-          for (NodeID d : kv.second) add_job(s, d, kv.first, off, len, 0);
-          off += len;
-        }
-        rot += nchunks % k;
-        srot += k;
-      } else if (everyone) {
-        // Collective: one ncclBroadcast per layer (chunk-pipelined) rooted at the
-        // leader; every rank of the communicator takes part.
-        add_job(cfg_.id, kAllRanks, kv.first, 0, total, 0);
-      } else if (cfg_.relay && remote.size() >= 2 && multi_host()) {
-        relay_across_hosts(kv.first, total, remote, host_rot);
-      } else if (cfg_.relay && remote.size() >= 2 && total >= int64_t(remote.size()) * cb) {
-        // Bandwidth-optimal broadcast on a fully connected xGMI mesh: scatter
-        // 1/k of the layer to each of k dests, then every dest relays its share
-        // to the other k-1 (per-link load 2/k of the layer instead of 1).
-        const int64_t k = int64_t(remote.size());
-        int64_t off = 0;
-        for (int64_t i = 0; i < k; ++i) {
-          // nchunks % k dests get one chunk more; a fixed choice would give the
-          // same dests (and their relay links) 3/16 of every 16-chunk layer
-          // instead of 1/7 at k = 7
-          const int64_t r = ((i - rot) % k + k) % k;
-          int64_t cnt = nchunks / k + (r < nchunks % k ? 1 : 0);
-          int64_t len = std::min(total - off, cnt * cb);
-          add_job(cfg_.id, remote[size_t(i)], kv.first, off, len, 0);
-          for (int64_t j = 0; j < k; ++j)
-            if (j != i) add_job(remote[size_t(i)], remote[size_t(j)], kv.first, off, len, 1);
-          off += len;
-        }
-        rot += nchunks % k;
-      } else {
-        for (NodeID d : remote) add_job(cfg_.id, d, kv.first, 0, -1);
-      }
-    } else if (remote.size() >= 2 && e_->supports_broadcast() && src.meta.location != Location::Client) {
-      for (NodeID d : remote) track(cfg_.id, d, kv.first, 0, src.data_size);
-      e_->broadcast_layer(kv.first, src.data_size, remote);
-    } else {
-      for (NodeID d : remote) {
-        track(cfg_.id, d, kv.first, 0, src.data_size);
-        send_layer(d, kv.first, 0, -1, src.meta.limit_rate);
-      }
-    }
-  }
-}
-
-void Node::schedule_mode1() {
-  // node.go:554-608: a random current owner retransmits each missing layer.
-  for (auto& kv : status_)
-    for (auto& l : kv.second) owners_[l.first].insert(kv.first);  // initialized on demand (quirk Q3)
-  const bool links = cfg_.owner_policy == "links";
-  // Link capacities (config Links / probed topology); unknown links count as
-  // the fastest known one, and with none known every link is equal.
-  double cap_max = 0;
-  for (auto& kv : cfg_.link_bw) cap_max = std::max(cap_max, double(kv.second));
-  auto cap = [&](NodeID s, NodeID d) {
-    auto it = cfg_.link_bw.find({s, d});
-    return it != cfg_.link_bw.end() && it->second > 0 ? double(it->second) : (cap_max > 0 ? cap_max : 1.0);
-  };
-  RelayPlan plan;
-  // Multi-host jobs (planned engines, "links" policy): (host, layer) -> the
-  // dests on that host that need the layer and their missing ranges.
-  const bool hier = links && e_->planned() && multi_host();
-  ImportMap imports;
-  for (auto& kv : assignment_) {
-    NodeID dest = kv.first;
-    for (auto& l : kv.second) {
-      LayerID layer = l.first;
-      if (at(status_[dest], layer, e_->target())) continue;
-      auto oit = owners_.find(layer);
-      if (oit != owners_.end() && !oit->second.empty()) {
-        if (oit->second.count(dest)) {
-          // The dest holds it in a lower tier (disk/host/client): promote locally.
-          retransmit(layer, dest, dest);
-          continue;
-        }
-        // Chunk-granular resume: a dest that announced part of this layer (its
-        // persisted chunks) loads those ranges locally and receives only the gaps.
-        std::vector<std::pair<int64_t, int64_t>> gaps{{0, layer_size(layer)}};
-        if (e_->planned()) {
-          auto pit = partial_.find(dest);
-          auto lit = pit == partial_.end() ? PartialLayers::const_iterator() : pit->second.find(layer);
-          if (pit != partial_.end() && lit != pit->second.end() && !lit->second.empty()) {
-            gaps.clear();
-            int64_t pos = 0;
-            for (auto r : lit->second) {
-              r.second = std::min(r.second, layer_size(layer));
-              if (r.first >= r.second) continue;
-              if (r.first > pos) gaps.push_back({pos, r.first});
-              {
-                std::lock_guard<std::mutex> lk(sig_mu_);
-                stats_.jobs_dispatched++;
-              }
-              add_job(dest, dest, layer, r.first, r.second - r.first);
-              pos = std::max(pos, r.second);
-            }
-            if (pos < layer_size(layer)) gaps.push_back({pos, layer_size(layer)});
-            if (gaps.empty()) continue;
-          }
-        }
-        int64_t need = 0;
-        for (auto& g : gaps) need += g.second - g.first;
-        const bool ranged = gaps.size() != 1 || need != layer_size(layer);
-        std::vector<NodeID> cand(oit->second.begin(), oit->second.end());
-        if (hier) {
-          // Several hosts: a holder on the dest's own host serves it over xGMI;
-          // a layer no GPU of that host holds is imported once per host
-          // (schedule_imports) instead of once per GPU over the NICs.
-          std::vector<NodeID> local;
-          for (NodeID c : cand)
-            if (host_of(c) == host_of(dest)) local.push_back(c);
-          if (local.empty()) {
-            imports[{host_of(dest), layer}].push_back({dest, gaps});
-            continue;
-          }
-          cand.swap(local);
-        }
-        NodeID owner;
-        if (links) {
-          // xGMI-aware: every GPU pair has its own link, so spread each dest's
-          // inbound bytes over distinct links - least projected link time
-          // (bytes / capacity) first, then least total egress, then lowest id.
-          owner = cand[0];
-          std::pair<double, int64_t> best{1e300, INT64_MAX};
-          for (NodeID c : cand) {
-            std::pair<double, int64_t> k{double(link_bytes_[{c, dest}] + need) / cap(c, dest), owner_bytes_[c]};
-            if (k < best) {
-              best = k;
-              owner = c;
-            }
-          }
-          link_bytes_[{owner, dest}] += need;
-        } else if (cfg_.owner_policy == "balanced") {
-          int64_t best = INT64_MAX;
-          std::vector<NodeID> ties;
-          for (NodeID c : cand) {
-            int64_t b = owner_bytes_[c];
-            if (b < best) {
-              best = b;
-              ties.assign(1, c);
-            } else if (b == best) {
-              ties.push_back(c);
-            }
-          }
-          owner = ties[size_t(rng_() % ties.size())];
-        } else {
-          owner = cand[size_t(rng_() % cand.size())];  // uniform (quirk Q5)
-        }
-        owner_bytes_[owner] += need;
-        if (links && e_->planned()) {
-          for (auto& g : gaps) plan[{dest, layer}].push_back(PlanPart{owner, g.first, g.second - g.first, 0});
-        } else if (ranged) {
-          for (auto& g : gaps) {
-            {
-              std::lock_guard<std::mutex> lk(sig_mu_);
-              stats_.jobs_dispatched++;
-            }
-            add_job(owner, dest, layer, g.first, g.second - g.first);
-          }
-        } else {
-          retransmit(layer, owner, dest);
-        }
-      } else {
-        LayerSrc src;
-        if (!store_.get(layer, &src)) {
-          log::warn(int64_t(cfg_.id)).msg("no layers found for layerID:" + std::to_string(layer));
-          continue;
-        }
-        retransmit(layer, cfg_.id, dest);
-      }
-    }
-  }
-  if (cap_max > 0 && !plan.empty()) relay_rebalance(plan, cap);
-  if (!imports.empty()) schedule_imports(imports, plan, cap);
-  if (plan.empty()) return;
-  for (auto& kv : plan)
-    for (auto& p : kv.second) {
-      {
-        std::lock_guard<std::mutex> lk(sig_mu_);
-        stats_.jobs_dispatched++;
-      }
-      add_job(p.src, kv.first.first, kv.first.second, p.off, p.size, p.phase);
-    }
-}
-
-void Node::relay_rebalance(RelayPlan& plan, const std::function<double(NodeID, NodeID)>& cap) {
-  // A slow link (config Links / measured topology) must not set the session
-  // time: move chunk-sized slices of the layers it carries onto relays. A relay
-  // is a rank that receives the same layer straight from an owner in this plan
-  // (phase 0); it forwards the slice in phase 1, chunk-pipelined behind its own
-  // recv (the planned engine orders a relay after the recv it forwards). Each
-  // move takes one slice off the link with the longest projected time onto the
-  // relay->dest link whose time stays lowest, while that lowers the maximum.
-  const int64_t unit = std::max<int64_t>(cfg_.align, 1);
-  std::map<std::pair<NodeID, NodeID>, int64_t> bytes;
-  std::set<std::pair<NodeID, LayerID>> relayed_into, relays_from;
-  for (auto& kv : plan)
-    for (auto& p : kv.second) bytes[{p.src, kv.first.first}] += p.size;
-  auto t = [&](NodeID s, NodeID d, int64_t extra) { return double(bytes[{s, d}] + extra) / cap(s, d); };
-  int64_t moves = 0;
-  for (int iter = 0; iter < 1000000; ++iter) {
-    std::pair<NodeID, NodeID> worst{};
-    double tw = -1;
-    for (auto& kv : bytes)
-      if (kv.second > 0 && t(kv.first.first, kv.first.second, 0) > tw) {
-        tw = t(kv.first.first, kv.first.second, 0);
-        worst = kv.first;
-      }
-    if (tw <= 0) break;
-    const NodeID s = worst.first, d = worst.second;
-    bool moved = false;
-    for (auto& kv : plan) {
-      if (kv.first.first != d || relays_from.count(kv.first)) continue;
-      const LayerID layer = kv.first.second;
-      auto& parts = kv.second;
-      for (size_t i = 0; i < parts.size() && !moved; ++i) {
-        PlanPart& p = parts[i];
-        if (p.phase != 0 || p.src != s) continue;
-        // The slice is the part's last grid chunk: cut on the chunk grid, so an
-        // odd layer end moves as one short whole chunk (never two partial
-        // pieces of one chunk from different senders).
-        const int64_t end = p.off + p.size, cut = (end - 1) / unit * unit;
-        if (cut <= p.off) continue;
-        const int64_t slice = end - cut;
-        // the best relay: receives this layer directly (phase 0 only) in this plan
-        NodeID best = 0;
-        double tb = 1e300;
-        for (auto& other : plan) {
-          const NodeID x = other.first.first;
-          if (other.first.second != layer || x == d || x == s || relayed_into.count(other.first)) continue;
-          if (host_of(x) != host_of(d)) continue;  // relays stay on the dest's host (xGMI)
-          const double tx = t(x, d, slice);
-          if (tx < tb) {
-            tb = tx;
-            best = x;
-          }
-        }
-        if (tb >= tw) continue;  // no relay improves on this link
-        p.size -= slice;
-        parts.push_back(PlanPart{best, cut, slice, 1});
-        bytes[{s, d}] -= slice;
-        bytes[{best, d}] += slice;
-        relayed_into.insert(kv.first);
-        relays_from.insert({best, layer});
-        moved = true;
-        ++moves;
-      }
-      if (moved) break;
-    }
-    if (!moved) break;
-  }
-  if (moves)
-    log::info(int64_t(cfg_.id)).i("relayed_slices", moves).i("slice_bytes", unit).msg("mode 1: relays around slow links");
-}
-
-void Node::relay_across_hosts(LayerID layer, int64_t total, const std::vector<NodeID>& remote,
-                              std::map<int, int64_t>& rot) {
-  // Planned mode 0 on several hosts: a three-level broadcast. The leader
-  // scatters the layer over its own host's xGMI (one chunk-grid slice per
-  // GPU of its host that needs it); each of those GPUs relays its slice to
-  // its host peers and forwards it over its NIC to one GPU of every other
-  // host, which relays it inside that host. No byte enters a host twice, and
-  // the export is spread over the leader host's NICs instead of the leader's
-  // one (a flat relay would send every slice into a remote host once per GPU).
-  const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1), nchunks = (total + cb - 1) / cb;
-  const int me = host_of(cfg_.id);
-  std::vector<NodeID> local;
-  std::map<int, std::vector<NodeID>> far;
-  for (NodeID d : remote) (host_of(d) == me ? local : far[host_of(d)]).push_back(d);
-  // the GPUs that take the first-level slices: the leader host's dests, or the
-  // leader itself when none of its host's GPUs needs the layer
-  const bool self_export = local.empty();
-  const std::vector<NodeID> tier1 = self_export ? std::vector<NodeID>{cfg_.id} : local;
-  const int64_t k = std::max<int64_t>(1, std::min<int64_t>(int64_t(tier1.size()), nchunks));
-  int64_t off = 0;
-  for (int64_t i = 0; i < k; ++i) {
-    const int64_t cnt = nchunks / k + (i < nchunks % k ? 1 : 0);
-    const int64_t len = std::min(total - off, cnt * cb);
-    if (len <= 0) continue;
-    const NodeID a = tier1[size_t((i + rot[me]) % int64_t(tier1.size()))];
-    if (!self_export) {
-      add_job(cfg_.id, a, layer, off, len, 0);
-      for (NodeID d : local)
-        if (d != a) add_job(a, d, layer, off, len, 1);
-    }
-    const int phase = self_export ? 0 : 1;
-    for (auto& hv : far) {
-      const auto& gpus = hv.second;
-      const NodeID entry = gpus[size_t((i + rot[hv.first]) % int64_t(gpus.size()))];
-      add_job(a, entry, layer, off, len, phase);
-      for (NodeID d : gpus)
-        if (d != entry) add_job(entry, d, layer, off, len, phase + 1);
-    }
-    off += len;
-  }
-  rot[me] += k;
-  for (auto& hv : far) rot[hv.first] += k;
-}
-
-int Node::host_of(NodeID n) const {
-  auto it = cfg_.host.find(n);
-  return it == cfg_.host.end() ? 0 : it->second;
-}
-
-bool Node::multi_host() const {
-  std::set<int> hosts;
-  for (auto& kv : status_) hosts.insert(host_of(kv.first));
-  return hosts.size() > 1;
-}
-
-void Node::schedule_imports(const ImportMap& imports, RelayPlan& plan,
-                            const std::function<double(NodeID, NodeID)>& cap) {
-  // Hierarchical dissemination across hosts. A layer that no GPU of host H
-  // holds crosses the network once per host, not once per GPU: it is cut on
-  // the chunk grid into one slice per dest of H that needs it; slice i goes
-  // from a holder on another host to dest i of H over their NICs (phase 0) and
-  // dest i relays it to the other dests of H over xGMI (phase 1, chunk-
-  // pipelined behind its own recv, as mode 0's scatter + relay). Every GPU's
-  // NIC then carries 1/k of each imported layer and its xGMI links the rest.
-  // The slice of a layer a dest takes is the next in a rotation over the
-  // dests with the least NIC ingress so far; the holder of each slice is the
-  // one with the least NIC egress so far (reference: a layer always goes
-  // owner -> dest directly, node.go:554-608, which on a multi-node MI355X
-  // cluster sends every byte over the NIC once per GPU).
-  const int64_t unit = std::max<int64_t>(cfg_.align, 1);
-  std::map<NodeID, int64_t> nic_in, nic_out;
-  int64_t imported = 0;
-  for (auto& kv : imports) {
-    const LayerID layer = kv.first.second;
-    const int64_t total = layer_size(layer);
-    auto oit = owners_.find(layer);
-    if (oit == owners_.end() || oit->second.empty()) continue;
-    std::vector<NodeID> holders(oit->second.begin(), oit->second.end());
-    auto pick_holder = [&](NodeID dest) {
-      NodeID best = holders[0];
-      std::pair<int64_t, double> bk{INT64_MAX, 1e300};
-      for (NodeID h : holders) {
-        std::pair<int64_t, double> k{nic_out[h], double(link_bytes_[{h, dest}]) / cap(h, dest)};
-        if (k < bk) {
-          bk = k;
-          best = h;
-        }
-      }
-      return best;
-    };
-    // Dests missing the whole layer share it by slices; a dest with a partial
-    // copy (chunk-granular resume) receives its own gaps directly.
-    std::vector<NodeID> whole;
-    for (auto& dg : kv.second) {
-      const bool full = dg.second.size() == 1 && dg.second[0].first == 0 && dg.second[0].second == total;
-      if (full) {
-        whole.push_back(dg.first);
-        continue;
-      }
-      for (auto& g : dg.second) {
-        const NodeID h = pick_holder(dg.first);
-        plan[{dg.first, layer}].push_back(PlanPart{h, g.first, g.second - g.first, 0});
-        nic_out[h] += g.second - g.first;
-        nic_in[dg.first] += g.second - g.first;
-        link_bytes_[{h, dg.first}] += g.second - g.first;
-      }
-    }
-    if (whole.empty()) continue;
-    const int64_t nchunks = (total + unit - 1) / unit;
-    const int64_t k = std::min<int64_t>(int64_t(whole.size()), std::max<int64_t>(nchunks, 1));
-    // entries: the k dests with the least NIC ingress so far take the slices
-    std::stable_sort(whole.begin(), whole.end(), [&](NodeID a, NodeID b) { return nic_in[a] < nic_in[b]; });
-    int64_t off = 0;
-    for (int64_t i = 0; i < k; ++i) {
-      const int64_t cnt = nchunks / k + (i < nchunks % k ? 1 : 0);
-      const int64_t len = std::min(total - off, cnt * unit);
-      if (len <= 0) continue;
-      const NodeID entry = whole[size_t(i)];
-      const NodeID h = pick_holder(entry);
-      plan[{entry, layer}].push_back(PlanPart{h, off, len, 0});
-      nic_out[h] += len;
-      nic_in[entry] += len;
-      link_bytes_[{h, entry}] += len;
-      for (NodeID d : whole)
-        if (d != entry) {
-          plan[{d, layer}].push_back(PlanPart{entry, off, len, 1});
-          link_bytes_[{entry, d}] += len;
-        }
-      off += len;
-    }
-    imported++;
-  }
-  if (imported)
-    log::info(int64_t(cfg_.id)).i("imported_layer_copies", imported).msg("mode 1: layers imported once per host, relayed over xGMI");
-}
-
-// ------------------------------------------------------------------- mode 2
-
-NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
-  // node.go:948-978 (the code picks the FASTEST source; quirk Q16 keeps that).
-  // A sender's rate for this job is its tier's LimitRate capped by its link to
-  // the dest when the plan knows it (measured or configured): on equal links
-  // this is the reference's choice.
-  // A dest that holds the layer in another tier loads it itself (as modes 1
-  // and 3 do): a transfer from a peer would land on top of its own staging
-  // of the same chunks (a race TSAN caught in the rank-death selftest).
-  if (!suspects_.count(dest)) {
-    auto sd = status_.find(dest);
-    if (sd != status_.end() && sd->second.count(layer) && load_.count(dest)) return dest;
-  }
-  // Several hosts: a holder on the dest's host (xGMI) before any across the
-  // network (the NIC a GPU shares with all of its remote peers).
-  NodeID best = 0;
-  bool found = false, best_local = false;
-  int64_t best_rate = 0;
-  int64_t min_count = INT64_MAX;
-  for (auto& kv : load_) {
-    NodeID sender = kv.first;
-    if (suspects_.count(sender)) continue;  // missed a deadline: no new work
-    auto st = status_.find(sender);
-    if (st == status_.end()) continue;
-    auto it = st->second.find(layer);
-    if (it == st->second.end()) continue;
-    int64_t eff = it->second.limit_rate == 0 ? INT64_MAX : it->second.limit_rate;
-    if (auto lb = cfg_.link_bw.find({sender, dest}); lb != cfg_.link_bw.end() && lb->second > 0 && sender != dest)
-      eff = std::min(eff, lb->second);
-    int64_t count = kv.second;
-    const bool local = host_of(sender) == host_of(dest);
-    if (!found || (local && !best_local) ||
-        (local == best_local &&
-         (eff > best_rate || (eff == best_rate && (count < min_count || (count == min_count && sender < best)))))) {
-      best = sender;
-      best_rate = eff;
-      min_count = count;
-      best_local = local;
-      found = true;
-    }
-  }
-  return found ? best : kClientID;
-}
-
-bool Node::rarest_own_job(NodeID node, LayerID* layer, JobKey* key) {
-  // node.go:981-1010 (ties: lowest layer id, then lowest (dest, offset))
-  bool ok = false;
-  size_t min_owners = SIZE_MAX;
-  auto st = status_.find(node);
-  if (st == status_.end()) return false;
-  for (auto& l : st->second) {
-    auto lj = jobs_.find(l.first);
-    if (lj == jobs_.end()) continue;
-    for (auto& jd : lj->second) {
-      if (jd.second.sender != node || jd.second.state != JobState::Pending) continue;
-      size_t cnt = owners_[l.first].size();
-      if (!ok || cnt < min_owners || (cnt == min_owners && l.first < *layer)) {
-        min_owners = cnt;
-        *layer = l.first;
-        *key = jd.first;
-        ok = true;
-      }
-    }
-  }
-  return ok;
-}
-
-bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID* victim) {
-  // node.go:1012-1073
-  struct Cand {
-    LayerID layer;
-    JobKey dest;
-    NodeID sender;
-    size_t owners;
-    double ttf;
-  };
-  bool have = false;
-  Cand best{};
-  auto st = status_.find(node);
-  if (st == status_.end()) return false;
-  for (auto& l : st->second) {
-    auto lj = jobs_.find(l.first);
-    if (lj == jobs_.end()) continue;
-    size_t cnt = owners_[l.first].size();
-    for (auto& jd : lj->second) {
-      NodeID sender = jd.second.sender;
-      int64_t sender_rate = 0;
-      if (auto s2 = status_.find(sender); s2 != status_.end())
-        if (auto x = s2->second.find(l.first); x != s2->second.end()) sender_rate = x->second.limit_rate;
-      int64_t node_rate = l.second.limit_rate;
-      if (sender == node || jd.second.state != JobState::Pending || load_[sender] == 0 ||
-          (node_rate != 0 && node_rate < sender_rate))
-        continue;
-      // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
-      const NodeID dest = jd.first.first;
-      if (host_of(node) != host_of(dest) && host_of(sender) == host_of(dest) && multi_host()) continue;
-      double ttf = perf_.count(sender) ? perf_[sender].first * double(load_[sender]) : 1e300;
-      Cand c{l.first, jd.first, sender, cnt, ttf};
-      if (!have || c.owners < best.owners || (c.owners == best.owners && c.ttf > best.ttf)) {
-        best = c;
-        have = true;
-      }
-    }
-  }
-  if (!have) return false;
-  *layer = best.layer;
-  *key = best.dest;
-  *victim = best.sender;
-  return true;
-}
-
-void Node::dispatch_range(LayerID layer, NodeID sender, NodeID dest, int64_t off, int64_t size) {
-  if (off == 0 && size >= layer_size(layer)) {
-    retransmit(layer, sender, dest);  // whole layer: the reference's Retransmit
-    return;
-  }
-  {
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    stats_.jobs_dispatched++;
-  }
-  if (e_->planned()) {
-    add_job(sender, dest, layer, off, size);
-    return;
-  }
-  track(sender, dest, layer, off, size);
-  if (sender == cfg_.id) {
-    send_layer(dest, layer, off, size, 0);
-    return;
-  }
-  Message f;  // a byte range: FlowRetransmit carries offset + size
-  f.type = MsgType::FlowRetransmit;
-  f.layer = layer;
-  f.dest = dest;
-  f.offset = off;
-  f.data_size = size;
-  send_msg(sender, f);
-}
-
-bool Node::assign_new_job(NodeID node) {
-  // node.go:909-945
-  LayerID layer = 0;
-  JobKey key{0, 0};
-  NodeID victim = 0;
-  if (suspects_.count(node)) return false;
-  if (rarest_own_job(node, &layer, &key)) {
-    Job& j = jobs_[layer][key];
-    j.state = JobState::Sending;
-    j.t_us = log::now_us();
-    load_[node] = std::max<int64_t>(0, load_[node] - 1);
-    inflight_[node]++;
-    log::debug(int64_t(cfg_.id)).u("node", node).u("layer", layer).i("offset", key.second)
-        .msg("pass a job initially assigned");
-    dispatch_range(layer, node, key.first, key.second, j.size);
-    return true;
-  }
-  if (rarest_stealable_job(node, &layer, &key, &victim)) {
-    log::debug(int64_t(cfg_.id)).u("layer", layer)
-        .msg("steal a job from the most loaded node (" + std::to_string(victim) + ") to node " + std::to_string(node));
-    load_[victim] = std::max<int64_t>(0, load_[victim] - 1);
-    Job& j = jobs_[layer][key];
-    j.sender = node;
-    j.state = JobState::Sending;
-    j.t_us = log::now_us();
-    inflight_[node]++;
-    dispatch_range(layer, node, key.first, key.second, j.size);
-    return true;
-  }
-  log::debug(int64_t(cfg_.id)).u("node", node).msg("there is no job left to assign");
-  return false;
-}
-
-void Node::schedule_mode2() {
-  // node.go:810-904
-  for (auto& kv : status_)
-    for (auto& l : kv.second) owners_[l.first].insert(kv.first);
-  std::vector<LayerID> sorted;
-  for (auto& kv : owners_) sorted.push_back(kv.first);
-  std::stable_sort(sorted.begin(), sorted.end(), [&](LayerID a, LayerID b) {
-    if (owners_[a].size() != owners_[b].size()) return owners_[a].size() < owners_[b].size();
-    return a < b;  // rarest first, tiebreak by id
-  });
-  // Jobs are (layer, dest, range). With pull_job_bytes the layer is cut into
-  // ranges (chunk-aligned on planned engines) so stealing can rebalance inside
-  // a layer; 0 keeps the reference's one job per (layer, dest).
-  int64_t jb = cfg_.pull_job_bytes;
-  if (jb > 0 && e_->planned() && e_->chunk_bytes() > 0)
-    jb = std::max<int64_t>(1, (jb + e_->chunk_bytes() - 1) / e_->chunk_bytes()) * e_->chunk_bytes();
-  for (auto& kv : assignment_)
-    for (auto& l : kv.second) {
-      if (at(status_[kv.first], l.first, e_->target())) continue;
-      const int64_t size = layer_size(l.first);
-      const int64_t step = jb > 0 ? jb : std::max<int64_t>(size, 1);
-      for (int64_t off = 0; off < std::max<int64_t>(size, 1); off += step) {
-        Job j;
-        j.size = std::min(step, size - off);
-        jobs_[l.first][{kv.first, off}] = j;
-      }
-    }
-  for (auto& kv : status_) load_.emplace(kv.first, 0);
-  // Several hosts (planned engines): a layer that no GPU of a host holds is
-  // pulled across the network by one GPU of that host - the entry, the dest
-  // with the fewest imports so far - and every other dest of the host pulls it
-  // from the entry once it holds it (its ack makes it an owner and kicks it),
-  // over xGMI. Jobs from an entry are not stolen across hosts.
-  const bool hier = e_->planned() && multi_host();
-  std::map<std::pair<int, LayerID>, NodeID> entry;
-  if (hier) {
-    std::map<NodeID, int> imports;
-    for (LayerID layer : sorted) {
-      auto lj = jobs_.find(layer);
-      if (lj == jobs_.end()) continue;
-      std::map<int, std::set<NodeID>> remote_dests;  // host -> dests with no holder on it
-      for (auto& jd : lj->second) {
-        const NodeID d = jd.first.first;
-        const NodeID s = min_loaded_sender(layer, d);
-        if (s != kClientID && host_of(s) != host_of(d)) remote_dests[host_of(d)].insert(d);
-      }
-      for (auto& hv : remote_dests) {
-        NodeID e = *hv.second.begin();
-        for (NodeID d : hv.second)
-          if (imports[d] < imports[e]) e = d;
-        imports[e]++;
-        entry[{hv.first, layer}] = e;
-      }
-    }
-  }
-  for (LayerID layer : sorted) {
-    auto lj = jobs_.find(layer);
-    if (lj == jobs_.end()) continue;
-    for (auto& jd : lj->second) {
-      NodeID sender = min_loaded_sender(layer, jd.first.first);
-      if (sender == kClientID) {
-        log::error(int64_t(cfg_.id)).u("layer", layer).msg("no owner holds the layer");
-        continue;
-      }
-      if (hier && host_of(sender) != host_of(jd.first.first)) {
-        auto en = entry.find({host_of(jd.first.first), layer});
-        if (en != entry.end() && en->second != jd.first.first) sender = en->second;
-      }
-      jd.second.sender = sender;
-      jd.second.state = JobState::Pending;
-      load_[sender]++;
-      log::info(int64_t(cfg_.id)).msg("job assignment: layer: " + std::to_string(layer) +
-                                      ", sender: " + std::to_string(sender));
-    }
-  }
-  // Kick every node that has queued jobs or is a destination (quirk Q10:
-  // the reference kicks only assignment keys, stranding pure senders).
-  std::set<NodeID> kick;
-  for (auto& kv : assignment_) kick.insert(kv.first);
-  for (auto& kv : load_)
-    if (kv.second > 0) kick.insert(kv.first);
-  for (NodeID n : kick)
-    while (inflight_[n] < cfg_.pull_window && assign_new_job(n)) {
-    }
-}
-
-// ------------------------------------------------------------------- mode 3
-
-void Node::schedule_mode3() {
-  // node.go:1200-1288 + flow.go
-  FlowProblem p;
-  const Location tgt = e_->target();
-  std::vector<FlowDemand> demands;
-  struct SelfJob {
-    NodeID dest;
-    LayerID layer;
-    int64_t size, rate;
-  };
-  std::vector<SelfJob> self_jobs;
-  for (auto& kv : assignment_) {
-    for (auto& l : kv.second) {
-      auto& st = status_[kv.first];
-      if (at(st, l.first, tgt)) continue;
-      auto it = st.find(l.first);
-      if (it != st.end()) {
-        self_jobs.push_back({kv.first, l.first, layer_size(l.first), it->second.limit_rate});
-      } else {
-        demands.push_back({l.first, kv.first, layer_size(l.first)});
-      }
-    }
-  }
-  for (auto& sj : self_jobs) {
-    Message f;
-    f.type = MsgType::FlowRetransmit;
-    f.layer = sj.layer;
-    f.dest = sj.dest;
-    f.data_size = sj.size;
-    f.offset = 0;
-    f.rate = sj.rate;
-    {
-      std::lock_guard<std::mutex> lk(sig_mu_);
-      stats_.jobs_dispatched++;
-    }
-    if (e_->planned()) {
-      add_job(sj.dest, sj.dest, sj.layer, 0, sj.size);
-    } else {
-      track(sj.dest, sj.dest, sj.layer, 0, sj.size);
-      send_msg(sj.dest, f);
-    }
-  }
-  if (demands.empty()) {
-    log::info(int64_t(cfg_.id)).msg("No jobs to assign other than self-assignment");
-    return;
-  }
-  p.demands = demands;
-  p.holdings = status_;
-  for (auto& kv : cfg_.network_bw) {
-    p.egress_bps[kv.first] = kv.second;
-    p.ingress_bps[kv.first] = kv.second;
-  }
-  for (auto& kv : cfg_.hbm_bw) {
-    if (kv.second <= 0) continue;
-    auto it = p.ingress_bps.find(kv.first);
-    if (it == p.ingress_bps.end() || it->second <= 0 || it->second > kv.second) p.ingress_bps[kv.first] = kv.second;
-  }
-  p.link_bps = cfg_.link_bw;
-  p.stage_bps = cfg_.stage_bw;
-  p.align = cfg_.align;
-  p.integer_seconds = cfg_.integer_seconds;
-  p.disk_group = cfg_.disk_group;
-  p.disk_group_bps = cfg_.disk_group_bw;
-  if (multi_host()) {
-    p.host = cfg_.host;
-    p.nic_bps = cfg_.nic_bw;
-  }
-  if (e_->planned()) {
-    // GPU data plane: a layer is loaded into HBM once and forwarded from there;
-    // a self-job's load feeds the dest's own sends of that layer too.
-    p.stage_once = true;
-    for (auto& sj : self_jobs) {
-      auto st = status_[sj.dest].find(sj.layer);
-      if (st != status_[sj.dest].end() && st->second.source_type != SourceType::Device)
-        p.self_loads[sj.dest][sj.layer] = sj.size;
-    }
-  }
-  log::info(int64_t(cfg_.id)).msg("assigning a job...");
-  int64_t t0 = log::now_us();
-  FlowPlan plan = solve_flow(p);
-  if (!plan.feasible && plan.solver == "lp") {
-    // The LP did not solve (numerics on extreme measured rates, or its pivot
-    // limit): plan with the flow instead - it relaxes the budgets it cannot
-    // state, so its T may be optimistic, but every demand gets a sender.
-    log::warn(int64_t(cfg_.id)).s("lp_status", plan.lp_status).i("lp_pivots", plan.lp_pivots)
-        .msg("mode 3: the LP failed, planning with the max-flow instead");
-    p.solver = "flow";
-    plan = solve_flow(p);
-  }
-  log::info(int64_t(cfg_.id)).f("computation time[ms]", double(log::now_us() - t0) / 1e3).i("solves", plan.solves)
-      .s("solver", plan.solver).i("lp_pivots", plan.lp_pivots).msg("Job assignment completed");
-  log::info(int64_t(cfg_.id)).f("required minimum time(s)", plan.T).b("feasible", plan.feasible)
-      .msg("job assignment calculated");
-  {
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    stats_.flow_T = plan.T;
-  }
-  // Safety net: every demand's byte ranges must cover the layer, or its dest
-  // never completes it and the session hangs. A plan that leaves a gap (the
-  // LP's rounding of tiny shares onto the chunk grid can) gets the gap from
-  // the demand's largest sender, at the plan's pace.
-  if (plan.feasible) {
-    std::map<std::pair<LayerID, NodeID>, std::vector<std::pair<int64_t, int64_t>>> cover;
-    std::map<std::pair<LayerID, NodeID>, std::pair<NodeID, int64_t>> biggest;
-    for (auto& j : plan.jobs) {
-      cover[{j.layer, j.dest}].push_back({j.offset, j.offset + j.size});
-      auto& b = biggest[{j.layer, j.dest}];
-      if (j.size > b.second) b = {j.sender, j.size};
-    }
-    int64_t filled = 0;
-    for (auto& d : p.demands) {
-      auto& v = cover[{d.layer, d.dest}];
-      std::sort(v.begin(), v.end());
-      int64_t pos = 0;
-      std::vector<std::pair<int64_t, int64_t>> gaps;
-      for (auto& r : v) {
-        if (r.first > pos) gaps.push_back({pos, r.first});
-        pos = std::max(pos, r.second);
-      }
-      if (pos < d.size) gaps.push_back({pos, d.size});
-      auto bg = biggest.find({d.layer, d.dest});
-      NodeID src = bg != biggest.end() ? bg->second.first : kClientID;
-      if (src == kClientID)
-        for (auto& hs : p.holdings)
-          if (hs.first != d.dest && hs.second.count(d.layer)) {
-            src = hs.first;
-            break;
-          }
-      if (src == kClientID) continue;
-      for (auto& g : gaps) {
-        plan.jobs.push_back(FlowJob{src, d.layer, d.dest, g.second - g.first, g.first});
-        filled += g.second - g.first;
-      }
-    }
-    if (filled)
-      log::warn(int64_t(cfg_.id)).i("gap_bytes", filled).msg("mode 3: the plan left bytes uncovered; filled from a sender");
-  }
-  for (auto& j : plan.jobs) {
-    Message f;
-    f.type = MsgType::FlowRetransmit;
-    f.layer = j.layer;
-    f.dest = j.dest;
-    f.data_size = j.size;
-    f.offset = j.offset;
-    f.rate = plan.T > 0 ? int64_t(double(j.size) / plan.T) : 0;  // node.go:1281 (pace to finish together)
-    {
-      std::lock_guard<std::mutex> lk(sig_mu_);
-      stats_.jobs_dispatched++;
-    }
-    if (e_->planned()) {
-      add_job(j.sender, j.dest, j.layer, j.offset, j.size, 0, f.rate);
-    } else {
-      track(j.sender, j.dest, j.layer, j.offset, j.size);
-      send_msg(j.sender, f);
-    }
-  }
 }
 
 // ------------------------------------------------------------------- client

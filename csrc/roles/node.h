@@ -86,7 +86,10 @@ struct NodeStats {
   int64_t layers_received = 0;
   int64_t bytes_received = 0;
   double flow_T = 0;             // mode 3 planned completion time (s)
-  double plan_ms = 0;            // scheduling time
+  double plan_ms = 0;            // leader: scheduling time (plan + dispatch of the transfer batches)
+  double plan_sched_ms = 0;      // leader: of which the scheduler (or the plan cache lookup)
+  double plan_dispatch_ms = 0;   // leader: of which encoding + sending the transfer batches
+  bool plan_cached = false;      // leader: the plan was an identical earlier session's (roles/plan_cache.h)
   int64_t nacks = 0;             // leader: chunk re-sends requested by receivers (CRC mismatch)
   int64_t redispatched = 0;      // leader: jobs re-sent from another owner after their deadline
   int64_t suspects = 0;          // leader: senders that missed a deadline
@@ -166,6 +169,7 @@ class Node {
   NodeID alternative_owner(LayerID layer, NodeID dest, NodeID avoid);
   void ticker();
   int64_t layer_size(LayerID l);
+  std::string plan_key();
   void retransmit(LayerID layer, NodeID owner, NodeID dest);
   void add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase = 0, int64_t rate = 0);
   void flush_batch();
@@ -236,6 +240,7 @@ class Node {
   uint64_t next_seq_ = 1, next_batch_ = 1;
   std::map<std::pair<NodeID, NodeID>, int64_t> measured_links_;  // leader: reported link rates (B/s)
   std::map<LayerID, CrcManifest> manifests_;  // whole copies' manifests
+  std::map<LayerID, std::set<NodeID>> manifest_holders_;  // who announced a whole copy's manifest
   // chunk CRCs vouched for by partial copies: layer -> (grid, chunk -> crc)
   std::map<LayerID, std::pair<int64_t, std::map<int64_t, uint32_t>>> partial_crc_;
   void merge_partial_manifest(LayerID layer, const CrcManifest& m,

@@ -18,21 +18,44 @@ namespace {
 
 constexpr int64_t kInf = int64_t(4e18);
 
+// Dinic on a sparse residual graph whose capacities are affine in T: an edge
+// carries fixed + floor(rate * T) bytes, or is unbounded. The graph is built
+// once per plan; each T re-sets the capacities and re-runs the flow, and the
+// source side of the final residual graph is a minimum cut, whose fixed and
+// rate parts drive the parametric search for T (solve_flow below).
 struct Dinic {
   struct E {
     int to;
     int64_t cap;
   };
+  struct P {  // capacity parameters of a forward edge
+    double rate = 0;
+    int64_t fixed = 0;
+    bool inf = false;
+  };
   std::vector<E> e;
+  std::vector<P> par;  // per forward edge (index id / 2)
   std::vector<std::vector<int>> g;
   std::vector<int> level, it;
   explicit Dinic(int n) : g(size_t(n)), level(size_t(n)), it(size_t(n)) {}
-  int add(int u, int v, int64_t c) {
-    e.push_back({v, c});
+  int add(int u, int v, P prm) {
+    e.push_back({v, 0});
     g[size_t(u)].push_back(int(e.size()) - 1);
     e.push_back({u, 0});
     g[size_t(v)].push_back(int(e.size()) - 1);
+    par.push_back(prm);
     return int(e.size()) - 2;
+  }
+  static int64_t cap_at(const P& q, double T) {
+    if (q.inf) return kInf;
+    const double c = double(q.fixed) + std::floor(q.rate * T);
+    return c >= 4e18 ? kInf : int64_t(c);
+  }
+  void set_T(double T) {
+    for (size_t i = 0; i < par.size(); ++i) {
+      e[2 * i].cap = cap_at(par[i], T);
+      e[2 * i + 1].cap = 0;
+    }
   }
   bool bfs(int s, int t) {
     std::fill(level.begin(), level.end(), -1);
@@ -75,155 +98,30 @@ struct Dinic {
         if (flow >= kInf) return flow;
       }
     }
-    return flow;
+    return flow;  // `level` now marks the source side of a minimum cut
+  }
+  // The minimum cut left by run(): its fixed bytes, its rate (B/s of T) and
+  // its edge count; false if an unbounded edge crosses it.
+  bool cut(double* fixed, double* rate, int* edges) const {
+    *fixed = *rate = 0;
+    *edges = 0;
+    for (size_t i = 0; i < par.size(); ++i) {
+      const int u = e[2 * i + 1].to, v = e[2 * i].to;
+      if (level[size_t(u)] < 0 || level[size_t(v)] >= 0) continue;
+      if (par[i].inf) return false;
+      *fixed += double(par[i].fixed);
+      *rate += par[i].rate;
+      ++*edges;
+    }
+    return true;
   }
   int64_t flow_on(int id) const { return e[size_t(id ^ 1)].cap; }
 };
 
-int64_t cap_for(int64_t rate_bps, double T) {
-  if (rate_bps <= 0) return kInf;
-  double c = double(rate_bps) * T;
-  if (c >= 4e18) return kInf;
-  return int64_t(std::floor(c));
-}
-
-struct Built {
-  std::unique_ptr<Dinic> d;
-  int src = 0, sink = 1;
-  // (sender, layer, dest) -> edge id carrying its bytes
-  std::map<std::tuple<NodeID, LayerID, NodeID>, int> job_edges;
-};
-
-Built build(const FlowProblem& p, double T) {
-  // demands indexed by layer
-  std::map<LayerID, std::vector<const FlowDemand*>> by_layer;
-  for (auto& dm : p.demands) by_layer[dm.layer].push_back(&dm);
-  std::map<std::pair<LayerID, NodeID>, int64_t> dsize;
-  for (auto& dm : p.demands) dsize[{dm.layer, dm.dest}] = std::max(dsize[{dm.layer, dm.dest}], dm.size);
-  const bool topo = !p.link_bps.empty();
-  const int kDevice = int(SourceType::Device);
-  // Candidate (sender, tier, layer, dest) edges, and per (sender, dest) the
-  // demanded bytes by tier (to split a link shared by several tiers).
-  struct Cand {
-    NodeID s;
-    int t;
-    LayerID l;
-    NodeID d;
-  };
-  std::vector<Cand> cands;
-  std::map<std::pair<NodeID, NodeID>, std::map<int, int64_t>> sd_tiers;
-  std::set<std::tuple<NodeID, LayerID, NodeID>> seen;
-  for (auto& hs : p.holdings) {
-    const NodeID s = hs.first;
-    for (auto& lm : hs.second) {
-      auto bl = by_layer.find(lm.first);
-      if (bl == by_layer.end()) continue;
-      const int t = int(lm.second.source_type);
-      for (auto* dm : bl->second) {
-        if (dm->dest == s && !p.allow_self) continue;
-        if (!seen.insert({s, lm.first, dm->dest}).second) continue;
-        cands.push_back({s, t, lm.first, dm->dest});
-        sd_tiers[{s, dm->dest}][t] += dsize[{lm.first, dm->dest}];
-      }
-    }
-  }
-  // Vertex numbering: 0 source, 1 sink.
-  int n = 2;
-  std::map<NodeID, int> vs, vstage, vdest;
-  std::map<std::pair<NodeID, int>, int> vst;
-  std::map<std::tuple<NodeID, int, NodeID>, int> vlink;  // (s, tier or -1 = shared, d)
-  std::map<std::pair<LayerID, NodeID>, int> vd;
-  for (auto& kv : dsize) {
-    vd[kv.first] = n++;
-    if (!vdest.count(kv.first.second)) vdest[kv.first.second] = n++;
-  }
-  auto link_key = [&](const Cand& c) {
-    return std::make_tuple(c.s, sd_tiers[{c.s, c.d}].size() > 1 ? c.t : -1, c.d);
-  };
-  for (auto& c : cands) {
-    if (!vs.count(c.s)) vs[c.s] = n++;
-    if (c.t != kDevice && !vstage.count(c.s)) vstage[c.s] = n++;
-    if (!vst.count({c.s, c.t})) vst[{c.s, c.t}] = n++;
-    if (topo && c.s != c.d && !vlink.count(link_key(c))) vlink[link_key(c)] = n++;
-  }
-  Built b;
-  b.d = std::make_unique<Dinic>(n);
-  Dinic& d = *b.d;
-  auto rate_of = [](const std::map<NodeID, int64_t>& m, NodeID k) {
-    auto it = m.find(k);
-    return it == m.end() ? int64_t(0) : it->second;
-  };
-  for (auto& kv : vs) d.add(b.src, kv.second, cap_for(rate_of(p.egress_bps, kv.first), T));
-  // Staging is paid once per byte a sender loads into HBM, however many dests it
-  // then forwards it to over xGMI; a flow charges every transfer, so the
-  // budget is scaled by the sender's fan-out (its candidate bytes over the
-  // distinct layer bytes it could load) - exact when its layers share one
-  // fan-out.
-  std::map<NodeID, double> cand_bytes, layer_bytes;
-  std::set<std::pair<NodeID, LayerID>> counted;
-  for (auto& c : cands) {
-    if (c.t == kDevice) continue;
-    cand_bytes[c.s] += double(dsize[{c.l, c.d}]);
-    if (counted.insert({c.s, c.l}).second) {
-      int64_t mx = 0;
-      for (auto* dm : by_layer[c.l]) mx = std::max(mx, dm->size);
-      layer_bytes[c.s] += double(mx);
-    }
-  }
-  for (auto& kv : vstage) {
-    const int64_t r = rate_of(p.stage_bps, kv.first);
-    const double fan = layer_bytes[kv.first] > 0 ? std::max(1.0, cand_bytes[kv.first] / layer_bytes[kv.first]) : 1.0;
-    d.add(vs[kv.first], kv.second, r > 0 ? cap_for(int64_t(double(r) * fan), T) : kInf);
-  }
-  // Tier capacity: the tier's configured rate (all its layers share one device).
-  std::map<std::pair<NodeID, int>, int64_t> tier_rate;
-  for (auto& hs : p.holdings)
-    for (auto& lm : hs.second) {
-      auto key = std::make_pair(hs.first, int(lm.second.source_type));
-      if (!vst.count(key)) continue;
-      int64_t r = lm.second.limit_rate;
-      auto it = tier_rate.find(key);
-      if (it == tier_rate.end()) tier_rate[key] = r;
-      else if (it->second > 0 && (r <= 0 || r > it->second)) it->second = r;  // 0 = unlimited wins
-    }
-  for (auto& kv : vst) {
-    const NodeID s = kv.first.first;
-    const bool dev = kv.first.second == kDevice;
-    const int parent = dev ? vs[s] : vstage[s];
-    int64_t r = tier_rate[kv.first];
-    if (p.stage_once && !dev && r > 0 && layer_bytes[s] > 0)  // read once, forwarded to every dest
-      r = int64_t(double(r) * std::max(1.0, cand_bytes[s] / layer_bytes[s]));
-    d.add(parent, kv.second, cap_for(r, T));
-  }
-  for (auto& kv : vlink) {
-    const NodeID s = std::get<0>(kv.first), dst = std::get<2>(kv.first);
-    const int t = std::get<1>(kv.first);
-    auto lk = p.link_bps.find({s, dst});
-    int64_t cap = cap_for(lk == p.link_bps.end() ? 0 : lk->second, T);
-    const auto& tiers = sd_tiers[{s, dst}];
-    if (t >= 0 && cap < kInf) {
-      // several tiers share this link: each gets its share of the demanded bytes
-      int64_t tot = 0;
-      for (auto& x : tiers) tot += x.second;
-      cap = tot > 0 ? int64_t(double(cap) * double(tiers.at(t)) / double(tot)) : cap;
-    }
-    // a shared vertex is fed by every tier of the sender that serves this dest
-    if (t >= 0) {
-      d.add(vst[{s, t}], kv.second, cap);
-    } else {
-      const int only = tiers.begin()->first;
-      d.add(vst[{s, only}], kv.second, cap);
-    }
-  }
-  for (auto& c : cands) {
-    auto key = std::make_tuple(c.s, c.l, c.d);
-    const int from = (topo && c.s != c.d) ? vlink[link_key(c)] : vst[{c.s, c.t}];
-    b.job_edges[key] = d.add(from, vd[{c.l, c.d}], kInf);
-  }
-  for (auto& kv : vd) d.add(kv.second, vdest[kv.first.second], dsize[kv.first]);
-  for (auto& kv : vdest) d.add(kv.second, b.sink, cap_for(rate_of(p.ingress_bps, kv.first), T));
-  return b;
-}
+Dinic::P unlimited() { return Dinic::P{0, 0, true}; }
+Dinic::P fixed_bytes(int64_t b) { return Dinic::P{0, b, false}; }
+// rate <= 0: unlimited (the reference's LimitRate 0, quirk Q1)
+Dinic::P per_second(double rate) { return rate > 0 ? Dinic::P{rate, 0, false} : unlimited(); }
 
 int64_t required_bytes(const FlowProblem& p) {
   std::map<std::pair<LayerID, NodeID>, int64_t> dsize;
@@ -234,9 +132,10 @@ int64_t required_bytes(const FlowProblem& p) {
 }
 
 // Layers with the same holders (and tiers) and the same demands (dest, bytes):
-// one LP class. Its demand per dest is the sum over its layers, and an LP
-// solution splits back onto the layers in equal shares - exact, as every
-// layer of a class has the same constraints.
+// one class. Every layer of a class has the same constraints in the flow and
+// in the LP, so both solve over classes (80 layers with one random holder
+// each are 8 classes at 8 ranks) and split a class's bytes back onto its
+// layers (split_class below) - the optimum is the per-layer problem's.
 struct LpClass {
   std::vector<std::pair<NodeID, int>> holders;   // (sender, tier)
   std::vector<std::pair<NodeID, int64_t>> dests; // (dest, bytes per layer)
@@ -278,33 +177,181 @@ std::vector<LpClass> lp_classes(const FlowProblem& p) {
   return out;
 }
 
-// Byte counts per (sender, layer, dest) -> ranges: per demand, aligned sizes
-// (remainder to the biggest), offsets in sender order, so a sender that serves
-// one layer to several dests sends each of them the same region where it can.
-void extract_jobs(std::map<std::pair<LayerID, NodeID>, std::vector<FlowJob>>& per_demand, int64_t align,
-                  FlowPlan& plan) {
-  for (auto& kv : per_demand) {
-    auto& jobs = kv.second;
-    if (align > 1 && jobs.size() > 1) {
-      int64_t total = 0;
-      for (auto& j : jobs) total += j.size;
-      int64_t acc = 0;
-      size_t biggest = 0;
-      for (size_t i = 0; i < jobs.size(); ++i) {
-        jobs[i].size = (jobs[i].size / align) * align;
-        acc += jobs[i].size;
-        if (jobs[i].size > jobs[biggest].size) biggest = i;
-      }
-      jobs[biggest].size += total - acc;
-      jobs.erase(std::remove_if(jobs.begin(), jobs.end(), [](const FlowJob& j) { return j.size <= 0; }), jobs.end());
+// One class's bytes for one dest, per sender (sender order = ascending id),
+// cut into per-layer ranges. The class's layers are laid end to end as one
+// stream of L x size bytes and each sender takes the next run of its share,
+// with every cut rounded to the chunk grid inside its layer: most layers
+// come whole from one sender and a share splits at most the two layers at
+// its ends (L + senders pieces, not L x senders). A sender that serves
+// several dests of a class the same share sends each of them the same region,
+// so it loads those bytes once. The ranges partition every layer exactly.
+void split_class(const LpClass& c, NodeID dest, int64_t size, std::vector<std::pair<NodeID, int64_t>> shares,
+                 int64_t align, FlowPlan& plan) {
+  const int64_t L = int64_t(c.layers.size());
+  const int64_t total = L * size;
+  if (total <= 0) return;
+  std::sort(shares.begin(), shares.end());
+  shares.erase(std::remove_if(shares.begin(), shares.end(), [](auto& x) { return x.second <= 0; }), shares.end());
+  if (shares.empty()) return;
+  int64_t sum = 0;
+  for (auto& x : shares) sum += x.second;
+  // integer bytes: the shares add up to the class demand (remainder to the biggest)
+  size_t big = 0;
+  for (size_t i = 1; i < shares.size(); ++i)
+    if (shares[i].second > shares[big].second) big = i;
+  shares[big].second += total - sum;
+  const int64_t a = std::max<int64_t>(align, 1);
+  auto snap = [&](int64_t q) {  // a cut at stream position q, on the grid of its layer
+    if (q <= 0 || q >= total) return std::min(std::max<int64_t>(q, 0), total);
+    const int64_t li = q / size, off = q - li * size;
+    int64_t r = (off + a / 2) / a * a;
+    if (r > size) r = size;
+    if (size - r < a / 2 && size - r < r - off + a) r = size;  // the layer's short last chunk stays whole
+    return li * size + r;
+  };
+  int64_t pos = 0, acc = 0;
+  for (size_t k = 0; k < shares.size(); ++k) {
+    acc += shares[k].second;
+    const int64_t end = k + 1 == shares.size() ? total : std::max(pos, snap(acc));
+    for (int64_t q = pos; q < end;) {
+      const int64_t li = q / size, off = q - li * size;
+      const int64_t n = std::min(end - q, size - off);
+      plan.jobs.push_back(FlowJob{shares[k].first, c.layers[size_t(li)], dest, n, off});
+      q += n;
     }
-    int64_t off = 0;  // ranges partition the layer, senders in id order
-    for (auto& j : jobs) {
-      j.offset = off;
-      off += j.size;
-      plan.jobs.push_back(j);
+    pos = end;
+  }
+}
+
+// The parametric flow graph: vertices per class demand instead of per layer.
+struct FlowGraph {
+  std::unique_ptr<Dinic> d;
+  int src = 0, sink = 1;
+  struct Job {
+    NodeID s;
+    size_t cls;
+    NodeID dst;
+    int edge;
+  };
+  std::vector<Job> jobs;
+};
+
+FlowGraph build(const FlowProblem& p, const std::vector<LpClass>& classes) {
+  const bool topo = !p.link_bps.empty();
+  const int kDevice = int(SourceType::Device);
+  struct Cand {
+    NodeID s;
+    int t;
+    size_t c;
+    NodeID d;
+    int64_t bytes;  // the class's demand at d
+  };
+  std::vector<Cand> cands;
+  // per (sender, dest): demanded bytes by tier (to split a link shared by several tiers)
+  std::map<std::pair<NodeID, NodeID>, std::map<int, int64_t>> sd_tiers;
+  std::map<NodeID, double> cand_bytes, layer_bytes;  // staging fan-out per sender
+  for (size_t ci = 0; ci < classes.size(); ++ci) {
+    const LpClass& c = classes[ci];
+    const int64_t L = int64_t(c.layers.size());
+    int64_t mx = 0;
+    for (auto& dz : c.dests) mx = std::max(mx, dz.second);
+    for (auto& h : c.holders) {
+      bool any = false;
+      for (auto& dz : c.dests) {
+        if (dz.first == h.first && !p.allow_self) continue;
+        const int64_t b = dz.second * L;
+        cands.push_back({h.first, h.second, ci, dz.first, b});
+        sd_tiers[{h.first, dz.first}][h.second] += b;
+        if (h.second != kDevice) cand_bytes[h.first] += double(b);
+        any = true;
+      }
+      if (any && h.second != kDevice) layer_bytes[h.first] += double(mx * L);
     }
   }
+  int n = 2;
+  std::map<NodeID, int> vs, vstage, vdest;
+  std::map<std::pair<NodeID, int>, int> vst;
+  std::map<std::tuple<NodeID, int, NodeID>, int> vlink;  // (s, tier or -1 = shared, d)
+  std::map<std::pair<size_t, NodeID>, int> vd;
+  std::map<std::pair<size_t, NodeID>, int64_t> vd_bytes;
+  for (auto& c : cands) {
+    if (!vd.count({c.c, c.d})) {
+      vd[{c.c, c.d}] = n++;
+      vd_bytes[{c.c, c.d}] = c.bytes;
+    }
+    if (!vdest.count(c.d)) vdest[c.d] = n++;
+  }
+  auto link_key = [&](const Cand& c) {
+    return std::make_tuple(c.s, sd_tiers[{c.s, c.d}].size() > 1 ? c.t : -1, c.d);
+  };
+  for (auto& c : cands) {
+    if (!vs.count(c.s)) vs[c.s] = n++;
+    if (c.t != kDevice && !vstage.count(c.s)) vstage[c.s] = n++;
+    if (!vst.count({c.s, c.t})) vst[{c.s, c.t}] = n++;
+    if (topo && c.s != c.d && !vlink.count(link_key(c))) vlink[link_key(c)] = n++;
+  }
+  FlowGraph b;
+  b.d = std::make_unique<Dinic>(n);
+  Dinic& d = *b.d;
+  auto rate_of = [](const std::map<NodeID, int64_t>& m, NodeID k) {
+    auto it = m.find(k);
+    return it == m.end() ? int64_t(0) : it->second;
+  };
+  for (auto& kv : vs) d.add(b.src, kv.second, per_second(double(rate_of(p.egress_bps, kv.first))));
+  // Staging is paid once per byte a sender loads into HBM, however many dests it
+  // then forwards it to over xGMI; a flow charges every transfer, so the
+  // budget is scaled by the sender's fan-out (its candidate bytes over the
+  // distinct layer bytes it could load) - exact when its layers share one
+  // fan-out (needs_lp sends the other cases to the LP).
+  auto fan = [&](NodeID s) {
+    return layer_bytes[s] > 0 ? std::max(1.0, cand_bytes[s] / layer_bytes[s]) : 1.0;
+  };
+  for (auto& kv : vstage) {
+    const int64_t r = rate_of(p.stage_bps, kv.first);
+    d.add(vs[kv.first], kv.second, r > 0 ? per_second(double(r) * fan(kv.first)) : unlimited());
+  }
+  // Tier capacity: the tier's configured rate (all its layers share one device).
+  std::map<std::pair<NodeID, int>, int64_t> tier_rate;
+  for (auto& hs : p.holdings)
+    for (auto& lm : hs.second) {
+      auto key = std::make_pair(hs.first, int(lm.second.source_type));
+      if (!vst.count(key)) continue;
+      int64_t r = lm.second.limit_rate;
+      auto it = tier_rate.find(key);
+      if (it == tier_rate.end()) tier_rate[key] = r;
+      else if (it->second > 0 && (r <= 0 || r > it->second)) it->second = r;  // 0 = unlimited wins
+    }
+  for (auto& kv : vst) {
+    const NodeID s = kv.first.first;
+    const bool dev = kv.first.second == kDevice;
+    const int parent = dev ? vs[s] : vstage[s];
+    double r = double(tier_rate[kv.first]);
+    if (p.stage_once && !dev && r > 0) r *= fan(s);  // read once, forwarded to every dest
+    d.add(parent, kv.second, per_second(r));
+  }
+  for (auto& kv : vlink) {
+    const NodeID s = std::get<0>(kv.first), dst = std::get<2>(kv.first);
+    const int t = std::get<1>(kv.first);
+    auto lk = p.link_bps.find({s, dst});
+    double rate = lk == p.link_bps.end() ? 0.0 : double(lk->second);
+    const auto& tiers = sd_tiers[{s, dst}];
+    if (t >= 0 && rate > 0) {
+      // several tiers share this link: each gets its share of the demanded bytes
+      int64_t tot = 0;
+      for (auto& x : tiers) tot += x.second;
+      if (tot > 0) rate *= double(tiers.at(t)) / double(tot);
+    }
+    // a shared vertex is fed by every tier of the sender that serves this dest
+    const int from = t >= 0 ? vst[{s, t}] : vst[{s, tiers.begin()->first}];
+    d.add(from, kv.second, per_second(rate));
+  }
+  for (auto& c : cands) {
+    const int from = (topo && c.s != c.d) ? vlink[link_key(c)] : vst[{c.s, c.t}];
+    b.jobs.push_back({c.s, c.c, c.d, d.add(from, vd[{c.c, c.d}], unlimited())});
+  }
+  for (auto& kv : vd) d.add(kv.second, vdest[kv.first.second], fixed_bytes(vd_bytes[kv.first]));
+  for (auto& kv : vdest) d.add(kv.second, b.sink, per_second(double(rate_of(p.ingress_bps, kv.first))));
+  return b;
 }
 
 FlowPlan solve_flow_lp(const FlowProblem& p) {
@@ -512,30 +559,14 @@ FlowPlan solve_flow_lp(const FlowProblem& p) {
   plan.max_flow = plan.required;
   plan.feasible = true;
   plan.solves = 1;
-  // Class bytes back to layers (each layer of a class takes its share of every x).
-  std::map<std::pair<LayerID, NodeID>, std::vector<FlowJob>> per_demand;
+  // Class bytes back to layers: per (class, dest) the senders' shares, cut into ranges.
+  std::map<std::pair<size_t, NodeID>, std::vector<std::pair<NodeID, int64_t>>> shares;
   for (size_t i = 0; i < xs.size(); ++i) {
     const double bytes = r.x[size_t(xs[i].col)] * B0;
-    if (bytes <= 0.5) continue;
-    const LpClass& c = classes[xs[i].c];
-    for (LayerID l : c.layers)
-      per_demand[{l, xs[i].d}].push_back(FlowJob{xs[i].s, l, xs[i].d, int64_t(bytes / double(c.layers.size())), 0});
+    shares[{xs[i].c, xs[i].d}].push_back({xs[i].s, int64_t(std::llround(std::max(0.0, bytes)))});
   }
-  // Integer bytes: every demand's shares add up to its size exactly (remainder to the biggest share).
-  std::map<std::pair<LayerID, NodeID>, int64_t> dsize;
-  for (auto& dm : p.demands) dsize[{dm.layer, dm.dest}] = std::max(dsize[{dm.layer, dm.dest}], dm.size);
-  for (auto& kv : per_demand) {
-    auto& jobs = kv.second;
-    std::sort(jobs.begin(), jobs.end(), [](const FlowJob& a, const FlowJob& b) { return a.sender < b.sender; });
-    int64_t acc = 0;
-    size_t biggest = 0;
-    for (size_t i = 0; i < jobs.size(); ++i) {
-      acc += jobs[i].size;
-      if (jobs[i].size > jobs[biggest].size) biggest = i;
-    }
-    jobs[biggest].size += dsize[kv.first] - acc;
-  }
-  extract_jobs(per_demand, p.align, plan);
+  for (size_t ci = 0; ci < classes.size(); ++ci)
+    for (auto& dz : classes[ci].dests) split_class(classes[ci], dz.first, dz.second, shares[{ci, dz.first}], p.align, plan);
   return plan;
 }
 
@@ -599,7 +630,9 @@ bool needs_lp(const FlowProblem& p) {
 }
 
 int64_t max_flow_at(const FlowProblem& p, double T) {
-  Built b = build(p, T);
+  const auto classes = lp_classes(p);
+  FlowGraph b = build(p, classes);
+  b.d->set_T(T);
   return b.d->run(b.src, b.sink);
 }
 
@@ -613,59 +646,55 @@ FlowPlan solve_flow(const FlowProblem& p) {
     plan.feasible = true;
     return plan;
   }
+  const auto classes = lp_classes(p);
+  FlowGraph b = build(p, classes);
+  Dinic& d = *b.d;
+  const double D = double(plan.required);
   auto flow = [&](double T) {
     ++plan.solves;
-    return max_flow_at(p, T);
+    d.set_T(T);
+    return d.run(b.src, b.sink);
   };
-  // Upper bound by doubling (flow.go:155-167).
-  double hi = p.integer_seconds ? 1.0 : 1e-3;
-  bool found = false;
-  for (int i = 0; i < 128; ++i) {
-    if (flow(hi) >= plan.required) {
-      found = true;
-      break;
+  // Parametric search (Newton / Dinkelbach on the min cut): the max flow at T
+  // is the minimum over cuts of fixed + rate * T, concave and piecewise
+  // linear. From a T below the optimum, the minimum cut at T reaches the
+  // demand at T' = (D - fixed) / rate, which is still <= the optimum; every
+  // step moves to a new cut of the optimum's envelope, so a few max-flows
+  // (not the reference's ~60-step doubling + bisection, flow.go:155-191) give
+  // the smallest T exactly. The floor of each edge's rate * T loses < 1 byte,
+  // so a step adds one byte per cut edge.
+  double T = 1e-12;
+  int64_t f = flow(T);
+  for (int it = 0; f < plan.required && it < 256; ++it) {
+    double fixed = 0, rate = 0;
+    int edges = 0;
+    if (!d.cut(&fixed, &rate, &edges) || rate <= 0) break;  // no T-dependent edge: infeasible
+    const double Tn = (D - fixed + double(edges)) / rate;
+    if (!(Tn > T)) {  // rounding: nudge up
+      T = T * (1 + 1e-12) + 1e-15;
+    } else {
+      T = Tn;
     }
-    hi *= 2;
+    f = flow(T);
   }
-  if (!found) return plan;  // infeasible (some demand has no holder)
-  double T = hi;
+  if (f < plan.required) return plan;  // infeasible (some demand has no holder)
   if (p.integer_seconds) {
-    // Bisection over integers in [1, hi] (flow.go:171-187).
-    int64_t l = 1, r = int64_t(hi), best = int64_t(hi);
-    while (l <= r) {
-      int64_t m = l + (r - l) / 2;
-      if (flow(double(m)) < plan.required) {
-        l = m + 1;
-      } else {
-        best = std::min(best, m);
-        r = m - 1;
-      }
-    }
-    T = double(best);
-  } else {
-    double lo = hi / 2;
-    if (lo < 1e-9 || flow(lo) >= plan.required) lo = 0;
-    for (int i = 0; i < 60 && (hi - lo) > hi * 1e-6; ++i) {
-      double m = 0.5 * (lo + hi);
-      if (flow(m) >= plan.required) hi = m;
-      else lo = m;
-    }
-    T = hi;
+    // the reference's integer-second search (flow.go:171-187) = the smallest whole second >= T
+    double Ti = std::max(1.0, std::ceil(T * (1 - 1e-12) - 1e-9));
+    while (flow(Ti) < plan.required) Ti += 1;
+    T = Ti;
+    f = flow(T);
   }
-  // Re-solve at T and read the per-(sender, layer, dest) flows.
-  Built b = build(p, T);
-  ++plan.solves;
-  plan.max_flow = b.d->run(b.src, b.sink);
+  plan.max_flow = f;
   plan.T = T;
-  plan.feasible = plan.max_flow >= plan.required;
-  std::map<std::pair<LayerID, NodeID>, std::vector<FlowJob>> per_demand;
-  for (auto& kv : b.job_edges) {
-    int64_t f = b.d->flow_on(kv.second);
-    if (f <= 0) continue;
-    per_demand[{std::get<1>(kv.first), std::get<2>(kv.first)}].push_back(
-        FlowJob{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), f, 0});
+  plan.feasible = true;
+  std::map<std::pair<size_t, NodeID>, std::vector<std::pair<NodeID, int64_t>>> shares;
+  for (auto& j : b.jobs) {
+    const int64_t x = d.flow_on(j.edge);
+    if (x > 0) shares[{j.cls, j.dst}].push_back({j.s, x});
   }
-  extract_jobs(per_demand, p.align, plan);
+  for (size_t ci = 0; ci < classes.size(); ++ci)
+    for (auto& dz : classes[ci].dests) split_class(classes[ci], dz.first, dz.second, shares[{ci, dz.first}], p.align, plan);
   return plan;
 }
 

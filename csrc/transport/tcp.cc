@@ -71,9 +71,25 @@ int dial(const std::string& addr, int timeout_ms = 0) {
   addrinfo hints{};
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
+  // A numeric address skips the resolver: getaddrinfo's first call loads the
+  // NSS modules (tens of ms), and the leader's first dials sit in the timed plan.
+  sockaddr_in numeric{};
+  addrinfo one_ai{};
   addrinfo* res = nullptr;
-  int rc = getaddrinfo(host.c_str(), std::to_string(hp.port).c_str(), &hints, &res);
-  if (rc != 0) throw std::runtime_error("resolve " + addr + ": " + gai_strerror(rc));
+  bool resolved = false;
+  if (inet_pton(AF_INET, host.c_str(), &numeric.sin_addr) == 1) {
+    numeric.sin_family = AF_INET;
+    numeric.sin_port = htons(uint16_t(hp.port));
+    one_ai.ai_family = AF_INET;
+    one_ai.ai_socktype = SOCK_STREAM;
+    one_ai.ai_addr = reinterpret_cast<sockaddr*>(&numeric);
+    one_ai.ai_addrlen = sizeof numeric;
+    res = &one_ai;
+  } else {
+    int rc = getaddrinfo(host.c_str(), std::to_string(hp.port).c_str(), &hints, &res);
+    if (rc != 0) throw std::runtime_error("resolve " + addr + ": " + gai_strerror(rc));
+    resolved = true;
+  }
   int fd = -1;
   for (addrinfo* ai = res; ai; ai = ai->ai_next) {
     fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC, ai->ai_protocol);
@@ -101,10 +117,15 @@ int dial(const std::string& addr, int timeout_ms = 0) {
     ::close(fd);
     fd = -1;
   }
-  freeaddrinfo(res);
+  if (resolved) freeaddrinfo(res);
   if (fd < 0) throw std::runtime_error("dial " + addr + ": " + strerror(errno));
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  // A transfer batch (tens of KiB per rank) must leave the leader in one write:
+  // with the default send buffer a write waits for the peer's reader thread,
+  // and on a loaded host that wait (up to tens of ms) lands in the timed plan.
+  int buf = 4 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
   return fd;
 }
 
@@ -175,6 +196,43 @@ class TcpTransport : public Transport {
     write_all(conn->fd, bytes.data(), bytes.size());
   }
 
+  void send_many(std::vector<std::pair<NodeID, Message>>& msgs) override {
+    struct Out {
+      std::shared_ptr<Conn> conn;
+      std::string bytes;
+      NodeID dest;
+    };
+    std::vector<Out> outs;
+    std::vector<size_t> self;
+    std::string err;
+    for (size_t i = 0; i < msgs.size(); ++i) {
+      std::string daddr;
+      if (!lookup(msgs[i].first, &daddr)) {
+        if (err.empty()) err = "addr of " + std::to_string(msgs[i].first) + " does not exist";
+        continue;
+      }
+      if (is_self(daddr)) {
+        self.push_back(i);
+        continue;
+      }
+      try {
+        outs.push_back({get_or_connect(daddr), encode_envelope(msgs[i].second), msgs[i].first});
+      } catch (const std::exception& e) {
+        if (err.empty()) err = e.what();
+      }
+    }
+    for (auto& o : outs) {
+      try {
+        std::lock_guard<std::mutex> lk(o.conn->mu);
+        write_all(o.conn->fd, o.bytes.data(), o.bytes.size());
+      } catch (const std::exception& e) {
+        if (err.empty()) err = "send to " + std::to_string(o.dest) + ": " + e.what();
+      }
+    }
+    for (size_t i : self) inbox_.push(std::make_shared<Message>(std::move(msgs[i].second)));
+    if (!err.empty()) throw std::runtime_error(err);
+  }
+
   void broadcast(const Message& m) override {
     for (auto& kv : registry()) {
       try {
@@ -203,6 +261,15 @@ class TcpTransport : public Transport {
       return true;
     } catch (const std::exception&) {
       return false;
+    }
+  }
+
+  void warm(NodeID id) override {
+    std::string daddr;
+    if (!lookup(id, &daddr) || is_self(daddr)) return;
+    try {
+      get_or_connect(daddr);
+    } catch (const std::exception&) {
     }
   }
 
@@ -302,6 +369,8 @@ class TcpTransport : public Transport {
       }
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      int rbuf = 4 << 20;  // the other end of a batch write (see dial)
+      setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rbuf, sizeof rbuf);
       std::lock_guard<std::mutex> lk(readers_mu_);
       if (closed_) {
         ::close(fd);
@@ -342,10 +411,9 @@ class TcpTransport : public Transport {
   void read_loop(int fd, uint64_t id) {
     std::string buf;
     for (;;) {
-      Json env;
       size_t used = 0;
       try {
-        used = Json::parse_prefix(buf.data(), buf.size(), env);
+        used = Json::scan_prefix(buf.data(), buf.size());  // one envelope's extent, no DOM
       } catch (const std::exception& e) {
         log::error(-1).s("error", e.what()).msg("failed to decode envelope");
         break;
@@ -354,14 +422,14 @@ class TcpTransport : public Transport {
         if (!fill(fd, buf, buf.size() + 1)) break;
         continue;
       }
-      buf.erase(0, used);
       MessagePtr m;
       try {
-        m = decode_envelope(env);
+        m = decode_envelope_text(buf.data(), used);
       } catch (const std::exception& e) {
         log::error(-1).s("error", e.what()).msg("failed to decode TransportMsg");
         break;
       }
+      buf.erase(0, used);
       if (m->type != MsgType::Layer) {
         inbox_.push(m);
         continue;

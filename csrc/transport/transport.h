@@ -12,7 +12,10 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <stdexcept>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "core/queue.h"
 #include "core/wire.h"
@@ -41,6 +44,21 @@ class Transport {
   virtual ~Transport() = default;
   // Control message or (for MsgType::Layer) header + payload.
   virtual void send(NodeID dest, const Message& m, const LayerPayload* payload = nullptr) = 0;
+  // Several control messages at once (the leader's per-rank transfer batches):
+  // TCP encodes them all before the first write, so no peer starts working
+  // (and competing for the CPU) while the rest are still being encoded.
+  // Throws on the first failed send, after trying the others.
+  virtual void send_many(std::vector<std::pair<NodeID, Message>>& msgs) {
+    std::string err;
+    for (auto& m : msgs) {
+      try {
+        send(m.first, m.second);
+      } catch (const std::exception& e) {
+        if (err.empty()) err = e.what();
+      }
+    }
+    if (!err.empty()) throw std::runtime_error(err);
+  }
   virtual void register_pipe(LayerID layer, NodeID dest) = 0;
   virtual void broadcast(const Message& m) = 0;
   virtual std::string address() const = 0;
@@ -48,6 +66,10 @@ class Transport {
   // Liveness probe used by the leader's failure detector: can `id` still be
   // reached (TCP: a fresh connect succeeds; in-process: its endpoint exists)?
   virtual bool alive(NodeID id) { return true; }
+  // Open the cached control connection to `id` ahead of the first message (the
+  // leader does this when a peer announces, so the first dispatch after "timer
+  // start" pays no connect). Best effort: errors surface on the first send.
+  virtual void warm(NodeID id) {}
 
   BlockingQueue<MessagePtr>& deliver() { return inbox_; }
   // Node-internal events (engine completions) enter the same inbox.

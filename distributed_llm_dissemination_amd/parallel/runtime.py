@@ -64,6 +64,9 @@ class SessionResult:
     bytes_planned: int = 0
     jobs: int = 0
     plan_ms: float = 0.0
+    plan_cached: bool = False
+    plan_sched_ms: float = 0.0  # leader: the scheduler's share of plan_ms (or the plan-cache lookup)
+    plan_dispatch_ms: float = 0.0  # leader: encoding + sending the transfer batches
     flow_T: float = 0.0
     error: str = ""
     nacks: int = 0  # leader: chunk re-sends after CRC mismatches
@@ -758,6 +761,9 @@ class Runtime:
             bytes_planned=st.bytes_planned,
             jobs=st.jobs_dispatched,
             plan_ms=st.plan_ms,
+            plan_cached=st.plan_cached,
+            plan_sched_ms=st.plan_sched_ms,
+            plan_dispatch_ms=st.plan_dispatch_ms,
             flow_T=st.flow_T,
             error=err if err else ("" if ok else "timeout waiting for Ready()"),
             nacks=st.nacks,
