@@ -55,7 +55,7 @@ $(BUILD)/%.o: csrc/%.cc $(wildcard csrc/*/*.h) Makefile
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-tools: bin/diskspeed bin/h2dbench bin/contention bin/cvtprobe
+tools: bin/diskspeed bin/h2dbench bin/contention bin/cvtprobe bin/walkprobe
 
 bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(BUILD)/kernels/fill.hip.o $(BUILD)/core/crc32c.o
 	@mkdir -p bin
@@ -64,6 +64,10 @@ bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(
 bin/cvtprobe: csrc/tools/cvtprobe.hip
 	@mkdir -p bin
 	$(HIPCC) -O2 -std=c++17 --offload-arch=$(ARCH) -Wno-unused-value -Wno-unused-result -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
+
+bin/walkprobe: csrc/tools/walkprobe.hip
+	@mkdir -p bin
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $< -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
 
 bin/h2dbench: csrc/tools/h2dbench.hip
 	@mkdir -p bin

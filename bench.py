@@ -77,9 +77,10 @@ def parse_args(argv=None):
     p.add_argument("--lanes", type=int, default=0,
                    help="comm lanes (RCCL communicator + stream + dedicated HW queue each); 0 = one lane per "
                         "directed link on up to 8 ranks (14 at N = 8), world-1 per-distance lanes beyond")
-    p.add_argument("--comm-init", default="parallel", choices=["parallel", "split"],
-                   help="lane communicators: one unique id each, initialized together (parallel), or split from "
-                        "the world communicator one after another (split; round 2's path)")
+    p.add_argument("--comm-init", default="split", choices=["parallel", "split"],
+                   help="lane communicators: split from the world communicator one after another (split, the "
+                        "default: 16.3-17.1 s vs 18.7-19.1 s for parallel at 8 ranks on one GPU, profiles/r3_init2), "
+                        "or one unique id each, initialized together (parallel); the JSON records both phases per lane")
     p.add_argument("--probe-mib", type=int, default=256,
                    help="N > 1: untimed pre-flight probe of every directed link with this many MiB "
                         "(all lanes at once, then each pair alone); 0 = skip")
@@ -320,8 +321,8 @@ def worker(args, world, rank, chan) -> int:
         except RuntimeError as e:
             failed(str(e))
         log(f"link probe: {probe.get('probe_ms')} ms; concurrent GB/s {probe.get('concurrent')}")
-        # the probe's concurrent rates seed the closed-loop link estimates (B/s)
-        rt.observe_links({p: g * 1e9 for p, g in probe.get("concurrent", {}).items() if g})
+        # the probe's concurrent rates floor the closed-loop link capacities (B/s)
+        rt.observe_probe({p: g * 1e9 for p, g in probe.get("concurrent", {}).items() if g})
 
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
     policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, 2 * (world - 1)),
@@ -350,10 +351,12 @@ def worker(args, world, rank, chan) -> int:
         log(f"warmup {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s)")
     links0 = rt.link_stats()
     times = []
+    plans = []  # leader (rank 0): the plan of every timed step - it runs after "timer start"
     last = None
     for i in range(args.steps):
         dt, last = step(True, i)
         times.append(dt)
+        plans.append(last)
         log(f"step {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s) ttd={last.time_to_deliver_s * 1e3:.1f} ms")
     beat("measured")
     total = sum(times)
@@ -380,6 +383,7 @@ def worker(args, world, rank, chan) -> int:
     if rank == 0:
         out = {
             "metric": BASELINE_METRIC,
+            "ranks": world,  # the metric names the 8-rank config; this line measured `ranks` of it
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
@@ -423,6 +427,17 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["store"] = args.store
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
+        if plans:
+            # the leader's plan inside the timed window (reference: node.go:1161-1165 starts the
+            # timer before the solve, :1225-1231 logs its computation time)
+            pm = [p.plan_ms for p in plans]
+            out["config"]["plan"] = {
+                "ms_mean": round(sum(pm) / len(pm), 3), "ms_max": round(max(pm), 3),
+                "sched_ms_mean": round(sum(p.plan_sched_ms for p in plans) / len(plans), 3),
+                "dispatch_ms_mean": round(sum(p.plan_dispatch_ms for p in plans) / len(plans), 3),
+                "cached_steps": sum(1 for p in plans if p.plan_cached),
+                "solver": plans[-1].plan_solver,
+            }
         out["config"]["numa_rank0"] = numa  # {} when the GPU's node is unknown or outside this cpuset
         if chan is not None:
             out["config"]["fallback"] = chan.label or None
@@ -433,6 +448,9 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["comm_init_ms_rank0"] = round(es.comm_init_ms, 1)
             out["config"]["comm_init_ms_max"] = round(max(init_ms), 1)
             out["config"]["comm_connect_ms_rank0"] = round(es.comm_connect_ms, 1)
+            # per lane, rank 0: communicator set-up and connects (settles parallel vs split on a real node)
+            out["config"]["comm_init_ms_per_lane"] = [round(x, 1) for x in es.lane_init_ms]
+            out["config"]["comm_connect_ms_per_lane"] = [round(x, 1) for x in es.lane_connect_ms]
             out["config"]["comm_init"] = args.comm_init
             if hosts:
                 out["config"]["hosts"] = len(set(hosts.values()))

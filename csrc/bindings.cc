@@ -311,6 +311,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("lanes", &PlannedStats::lanes)
       .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)
       .def_readonly("comm_connect_ms", &PlannedStats::comm_connect_ms)
+      .def_readonly("lane_init_ms", &PlannedStats::lane_init_ms)
+      .def_readonly("lane_connect_ms", &PlannedStats::lane_connect_ms)
       .def_readonly("comm_reform_ms", &PlannedStats::comm_reform_ms)
       .def_readonly("paced", &PlannedStats::paced)
       .def_readonly("disk_wait_ms", &PlannedStats::disk_wait_ms)
@@ -380,7 +382,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("p2p_rounds", &SimTiming::p2p_rounds)
       .def_readwrite("host", &SimTiming::host)
       .def_readwrite("nic_bps", &SimTiming::nic_bps)
-      .def_readwrite("wait_s", &SimTiming::wait_s);
+      .def_readwrite("wait_s", &SimTiming::wait_s)
+      .def_readwrite("recv_delay_s", &SimTiming::recv_delay_s);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
   m.def("sim_read", [](uint64_t ptr, int64_t n) {
@@ -481,6 +484,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("flow_T", &NodeStats::flow_T)
       .def_readonly("plan_ms", &NodeStats::plan_ms)
       .def_readonly("plan_cached", &NodeStats::plan_cached)
+      .def_readonly("plan_solver", &NodeStats::plan_solver)
+      .def_readonly("plan_gap_bytes", &NodeStats::plan_gap_bytes)
       .def_readonly("plan_sched_ms", &NodeStats::plan_sched_ms)
       .def_readonly("plan_dispatch_ms", &NodeStats::plan_dispatch_ms)
       .def_readonly("nacks", &NodeStats::nacks)

@@ -116,6 +116,12 @@ class Backend {
   virtual void crash() {}
   virtual double comm_init_ms() const { return 0; }     // communicator set-up, connects included
   virtual double comm_connect_ms() const { return 0; }  // the connect part
+  // Per lane: its communicator's set-up (split: that lane's ncclCommSplit, lane
+  // 0 the world init; parallel: every lane = the one concurrent group) and its
+  // share of the connects (per distance it serves; one value for all when the
+  // connects run as one group).
+  virtual std::vector<double> lane_init_ms() const { return {}; }
+  virtual std::vector<double> lane_connect_ms() const { return {}; }
 };
 
 // Lanes. Every directed pair (src -> dst) has one lane, computed identically
@@ -211,6 +217,10 @@ struct SimTiming {
   // runs of congested schedules can queue a transfer behind longer than the
   // default (the link and NIC reservations are FIFO).
   double wait_s = 30;
+  // Fault injection: a rank that posts every P2P group holding a receive this
+  // many seconds late (its peers' sends wait for it, as an RCCL send waits
+  // for the matching receive): the closed loop must not read that as slow links.
+  std::map<int, double> recv_delay_s;
 };
 
 // In-process simulated fabric: ranks of one "communicator" share `comm_key`.

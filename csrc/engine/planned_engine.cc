@@ -91,6 +91,8 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
   stats_.lane_busy_ms.assign(size_t(lanes_), 0.0);
   stats_.comm_init_ms = backend_->comm_init_ms();
   stats_.comm_connect_ms = backend_->comm_connect_ms();
+  stats_.lane_init_ms = backend_->lane_init_ms();
+  stats_.lane_connect_ms = backend_->lane_connect_ms();
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
   self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
   th_ = std::thread([this] { run(); });

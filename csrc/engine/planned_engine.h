@@ -121,7 +121,7 @@ struct PlannedConfig {
   // concurrently), then every lane connected in one group; "split" = the world
   // communicator, then ncclCommSplit per lane one after another and a grouped
   // connect per ring distance (round 2's path; the bench's last fallback).
-  std::string comm_init = "parallel";
+  std::string comm_init = "split";
 };
 
 // Comm lanes an engine of this config runs. 0 = auto: one lane per directed
@@ -152,6 +152,7 @@ struct PlannedStats {
   std::vector<double> lane_busy_ms;
   int lanes = 1;
   double comm_init_ms = 0, comm_connect_ms = 0;
+  std::vector<double> lane_init_ms, lane_connect_ms;  // per comm lane (Backend::lane_init_ms)
   double comm_reform_ms = 0;  // last elastic re-form (abort + re-init after a shrink)
   int64_t paced = 0;  // issue attempts a token bucket deferred
   double disk_wait_ms = 0;  // time disk reads waited for the node-wide read budget

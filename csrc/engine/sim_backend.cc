@@ -358,6 +358,12 @@ class SimBackend : public Backend {
         }
       }
       const auto t0 = Clock::now();
+      if (auto rd = fab->timing.recv_delay_s.find(rank); rd != fab->timing.recv_delay_s.end() && rd->second > 0)
+        for (auto& o : ops)
+          if (!o.send && !o.bcast) {
+            std::this_thread::sleep_for(std::chrono::duration<double>(rd->second));
+            break;
+          }
       std::vector<std::unique_ptr<Posted>> posted;
       // Optional RCCL round model: ops grouped by ring distance, each round
       // waits for the previous one (collectives stay in round 0).

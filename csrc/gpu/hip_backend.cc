@@ -99,24 +99,32 @@ class HipBackend : public Backend {
     const bool parallel = cfg_.parallel_init && ids.size() == n * idb;
     auto t0 = log::now_us();
     std::vector<ncclConfig_t> ncs(n, comm_config());
+    lane_init_ms_.assign(n, 0.0);
+    lane_connect_ms_.assign(n, 0.0);
     if (parallel) {
       // Every lane communicator from its own unique id, all in one group: RCCL
-      // runs the inits (bootstrap, topology, channel set-up) concurrently, so
-      // 14 lanes cost about one communicator's set-up instead of fourteen.
+      // runs the inits (bootstrap, topology, channel set-up) concurrently.
+      // Measured at 8 ranks sharing one GPU it was slower than split
+      // (profiles/r3_init2: 18.7-19.1 s vs 16.3-17.1 s), so split is the
+      // default; each lane records the group's time.
       std::vector<ncclUniqueId> uid(n);
       memcpy(uid.data(), ids.data(), n * idb);
       NCCL_OK(ncclGroupStart());
       for (size_t l = 0; l < n; ++l) NCCL_OK(ncclCommInitRankConfig(&nccl_[l], cfg_.world, uid[l], cfg_.rank, &ncs[l]));
       NCCL_OK(ncclGroupEnd());
+      std::fill(lane_init_ms_.begin(), lane_init_ms_.end(), double(log::now_us() - t0) / 1e3);
     } else {
       ncclUniqueId id;
       memcpy(&id, ids.data(), idb);
       NCCL_OK(ncclCommInitRankConfig(&nccl_[0], cfg_.world, id, cfg_.rank, &ncs[0]));
+      lane_init_ms_[0] = double(log::now_us() - t0) / 1e3;
       // Further lanes: independent communicators over the same ranks (own
       // channels and connections; collective split, same order on every rank).
       for (size_t l = 1; l < n; ++l) {
+        const auto ts = log::now_us();
         ncs[l].splitShare = 0;
         NCCL_OK(ncclCommSplit(nccl_[0], 0, cfg_.rank, &nccl_[l], &ncs[l]));
+        lane_init_ms_[l] = double(log::now_us() - ts) / 1e3;
       }
     }
     const auto t1 = log::now_us();
@@ -151,12 +159,22 @@ class HipBackend : public Backend {
       const size_t ls = size_t(lane_of_hosts(cfg_.rank, to, world, lanes, cfg_.hosts, cfg_.host_lane_classes)),
                    lr = size_t(lane_of_hosts(from, cfg_.rank, world, lanes, cfg_.hosts, cfg_.host_lane_classes));
       uint8_t* rbuf = sbuf + 4096 * size_t(std::min(d, 15));  // distinct landing per recv of the group
+      const auto tc = log::now_us();
       if (!one_group) NCCL_OK(ncclGroupStart());
       NCCL_OK(ncclSend(sbuf, 64, ncclUint8, to, nccl_[ls], comm_[ls]));
       NCCL_OK(ncclRecv(rbuf, 64, ncclUint8, from, nccl_[lr], comm_[lr]));
-      if (!one_group) NCCL_OK(ncclGroupEnd());
+      if (!one_group) {
+        NCCL_OK(ncclGroupEnd());
+        const double ms = double(log::now_us() - tc) / 1e3;  // the distance's send + recv set-up
+        if (ls < lane_connect_ms_.size()) lane_connect_ms_[ls] += ms / 2;
+        if (lr < lane_connect_ms_.size()) lane_connect_ms_[lr] += ms / 2;
+      }
     }
-    if (one_group) NCCL_OK(ncclGroupEnd());
+    if (one_group) {
+      const auto tc = log::now_us();
+      NCCL_OK(ncclGroupEnd());
+      std::fill(lane_connect_ms_.begin(), lane_connect_ms_.end(), double(log::now_us() - tc) / 1e3);
+    }
     NCCL_OK(ncclBroadcast(sbuf, sbuf, 64, ncclUint8, 0, nccl_[0], comm_[0]));
     for (hipStream_t s : comm_) HIP_OK(hipStreamSynchronize(s));
   }
@@ -165,6 +183,8 @@ class HipBackend : public Backend {
   int lanes() const override { return int(comm_.size()); }
   double comm_init_ms() const override { return init_ms_; }
   double comm_connect_ms() const override { return connect_ms_; }
+  std::vector<double> lane_init_ms() const override { return lane_init_ms_; }
+  std::vector<double> lane_connect_ms() const override { return lane_connect_ms_; }
 
   void init_thread() override { HIP_OK(hipSetDevice(cfg_.device)); }
 
@@ -493,6 +513,7 @@ class HipBackend : public Backend {
   bool flip_ = false;
   std::vector<ncclComm_t> nccl_;  // one per lane (lane 0: the world communicator, others split from it)
   double init_ms_ = 0, connect_ms_ = 0;
+  std::vector<double> lane_init_ms_, lane_connect_ms_;
   void* probe_ = nullptr;  // connect_all() scratch
   std::map<Ev, hipEvent_t> starts_;  // timed group end -> its start event
   std::vector<hipEvent_t> timed_pool_;

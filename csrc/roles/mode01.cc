@@ -35,8 +35,10 @@ void Node::schedule_mode0() {
     std::vector<NodeID> stagers;
     const int64_t cb = std::max<int64_t>(e_->chunk_bytes(), 1);
     const int64_t nchunks = (src.data_size + cb - 1) / cb;
+    // Only ranks of the leader's own host can map its shared segment.
     if (cfg_.host_share && e_->planned())
       for (auto& st : status_) {
+        if (host_of(st.first) != host_of(cfg_.id)) continue;
         auto it = st.second.find(kv.first);
         if (it != st.second.end() && it->second.location != e_->target() && it->second.location != Location::Client)
           stagers.push_back(st.first);

@@ -21,10 +21,12 @@ NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
   // A sender's rate for this job is its tier's LimitRate capped by its link to
   // the dest when the plan knows it (measured or configured): on equal links
   // this is the reference's choice.
-  // A dest that holds the layer in another tier loads it itself (as modes 1
-  // and 3 do): a transfer from a peer would land on top of its own staging
-  // of the same chunks (a race TSAN caught in the rank-death selftest).
-  if (!suspects_.count(dest)) {
+  // Planned (GPU) engines: a dest that holds the layer in another tier loads
+  // it itself (as modes 1 and 3 do): a peer's transfer into the same HBM slot
+  // would race the dest's own staging of those chunks (TSAN caught it in the
+  // rank-death selftest). Host engines keep the reference's choice below, the
+  // dest competing with its tier rate like any sender (node.go:948-978).
+  if (e_->planned() && !suspects_.count(dest)) {
     auto sd = status_.find(dest);
     if (sd != status_.end() && sd->second.count(layer) && load_.count(dest)) return dest;
   }
@@ -105,8 +107,12 @@ bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID
       if (auto s2 = status_.find(sender); s2 != status_.end())
         if (auto x = s2->second.find(l.first); x != s2->second.end()) sender_rate = x->second.limit_rate;
       int64_t node_rate = l.second.limit_rate;
+      // a slower node never steals (node.go:1037-1043 skips nodeRate < senderRate);
+      // 0 = unlimited on both sides (quirk Q1: the reference let a limited node
+      // steal from an unlimited one, whose rate reads 0)
+      auto eff = [](int64_t r) { return r == 0 ? INT64_MAX : r; };
       if (sender == node || jd.second.state != JobState::Pending || load_[sender] == 0 ||
-          (node_rate != 0 && node_rate < sender_rate))
+          eff(node_rate) < eff(sender_rate))
         continue;
       // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
       const NodeID dest = jd.first.first;

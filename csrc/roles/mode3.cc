@@ -97,14 +97,22 @@ void Node::schedule_mode3() {
   log::info(int64_t(cfg_.id)).msg("assigning a job...");
   int64_t t0 = log::now_us();
   FlowPlan plan = solve_flow(p);
+  std::string solver = plan.solver;
   if (!plan.feasible && plan.solver == "lp") {
-    // The LP did not solve (numerics on extreme measured rates, or its pivot
-    // limit): plan with the flow instead - it relaxes the budgets it cannot
+    // The LP (sched/lp.cc) solves every instance of the wide-range test set
+    // (tests/test_maxflow.py); reaching this branch is a planner defect, which
+    // is logged as an error and counted (stats plan_solver "lp->flow"). The
+    // session still runs on the flow plan: it relaxes the budgets it cannot
     // state, so its T may be optimistic, but every demand gets a sender.
-    log::warn(int64_t(cfg_.id)).s("lp_status", plan.lp_status).i("lp_pivots", plan.lp_pivots)
+    log::error(int64_t(cfg_.id)).s("lp_status", plan.lp_status).i("lp_pivots", plan.lp_pivots)
         .msg("mode 3: the LP failed, planning with the max-flow instead");
     p.solver = "flow";
     plan = solve_flow(p);
+    solver = "lp->flow";
+  }
+  {
+    std::lock_guard<std::mutex> lk(sig_mu_);
+    stats_.plan_solver = solver;
   }
   log::info(int64_t(cfg_.id)).f("computation time[ms]", double(log::now_us() - t0) / 1e3).i("solves", plan.solves)
       .s("solver", plan.solver).i("lp_pivots", plan.lp_pivots).msg("Job assignment completed");
@@ -114,10 +122,12 @@ void Node::schedule_mode3() {
     std::lock_guard<std::mutex> lk(sig_mu_);
     stats_.flow_T = plan.T;
   }
-  // Safety net: every demand's byte ranges must cover the layer, or its dest
-  // never completes it and the session hangs. A plan that leaves a gap (the
-  // LP's rounding of tiny shares onto the chunk grid can) gets the gap from
-  // the demand's largest sender, at the plan's pace.
+  // Invariant: every demand's byte ranges cover its layer exactly (the
+  // planner's split_class partitions each class by construction). A gap
+  // would leave its dest waiting forever, so it is checked here: counted
+  // (stats plan_gap_bytes, tests assert 0), logged as an error and, so that
+  // no session hangs on a planner defect, filled from the demand's largest
+  // sender at the plan's pace.
   if (plan.feasible) {
     std::map<std::pair<LayerID, NodeID>, std::vector<std::pair<int64_t, int64_t>>> cover;
     std::map<std::pair<LayerID, NodeID>, std::pair<NodeID, int64_t>> biggest;
@@ -151,8 +161,11 @@ void Node::schedule_mode3() {
         filled += g.second - g.first;
       }
     }
-    if (filled)
-      log::warn(int64_t(cfg_.id)).i("gap_bytes", filled).msg("mode 3: the plan left bytes uncovered; filled from a sender");
+    if (filled) {
+      log::error(int64_t(cfg_.id)).i("gap_bytes", filled).msg("mode 3: the plan left bytes uncovered (planner defect); filled from a sender");
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      stats_.plan_gap_bytes += filled;
+    }
   }
   for (auto& j : plan.jobs) {
     Message f;

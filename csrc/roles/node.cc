@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstring>
 #include <set>
 #include <thread>
@@ -570,11 +571,25 @@ void Node::start_distribution() {
   }
   initial_status_ = status_;
   if (cfg_.adapt_links && !measured_links_.empty()) {
-    // Closed loop: plan on the rates the senders measured (reported with their
-    // announces) instead of the estimates; links nobody measured keep theirs.
-    std::lock_guard<std::mutex> lk(sig_mu_);
+    // Closed loop: plan on the capacities the senders measured (reported with
+    // their announces) instead of the estimates; links nobody measured keep
+    // theirs. Each rank reports one level for all its normal links and its own
+    // rate only for a persistently slow one (Runtime.link_report); levels within
+    // kLevelSnap of the median report plan as that median, so the ranks' small
+    // differences never reshape a uniform plan (and an unchanged fabric gives
+    // an unchanged plan: roles/plan_cache.h).
+    constexpr double kLevelSnap = 0.15;
+    std::vector<int64_t> v;
     for (auto& kv : measured_links_)
-      if (kv.second > 0) cfg_.link_bw[kv.first] = kv.second;
+      if (kv.second > 0) v.push_back(kv.second);
+    if (!v.empty()) {
+      std::sort(v.begin(), v.end());
+      const int64_t med = v[v.size() / 2];
+      std::lock_guard<std::mutex> lk(sig_mu_);
+      for (auto& kv : measured_links_)
+        if (kv.second > 0)
+          cfg_.link_bw[kv.first] = std::abs(double(kv.second - med)) <= kLevelSnap * double(med) ? med : kv.second;
+    }
   }
   log::info(int64_t(cfg_.id)).i("mode", cfg_.mode).i("bytes_planned", planned)
       .i("measured_links", int64_t(measured_links_.size())).msg("timer start");
@@ -597,9 +612,14 @@ void Node::start_distribution() {
       std::lock_guard<std::mutex> lk(sig_mu_);
       stats_.jobs_dispatched += hit->dispatched;
       stats_.flow_T = hit->flow_T;
+      stats_.plan_solver = hit->solver;
       stats_.plan_cached = true;
     } else {
       const int64_t d0 = stats_.jobs_dispatched;
+      {
+        std::lock_guard<std::mutex> lk(sig_mu_);
+        stats_.plan_solver = cfg_.mode == 1 ? "mode1:" + cfg_.owner_policy : "mode" + std::to_string(cfg_.mode);
+      }
       switch (cfg_.mode) {
         case 0: schedule_mode0(); break;
         case 1: schedule_mode1(); break;
@@ -613,6 +633,7 @@ void Node::start_distribution() {
         std::lock_guard<std::mutex> lk(sig_mu_);
         cp.dispatched = stats_.jobs_dispatched - d0;
         cp.flow_T = stats_.flow_T;
+        cp.solver = stats_.plan_solver;
         PlanCache::instance().put(key, std::move(cp));
       }
     }

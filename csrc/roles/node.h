@@ -90,6 +90,8 @@ struct NodeStats {
   double plan_sched_ms = 0;      // leader: of which the scheduler (or the plan cache lookup)
   double plan_dispatch_ms = 0;   // leader: of which encoding + sending the transfer batches
   bool plan_cached = false;      // leader: the plan was an identical earlier session's (roles/plan_cache.h)
+  std::string plan_solver;       // leader: which scheduler / solver planned ("mode1:links", "flow", "lp", ...)
+  int64_t plan_gap_bytes = 0;    // leader, mode 3: bytes the plan left uncovered (an invariant violation; 0)
   int64_t nacks = 0;             // leader: chunk re-sends requested by receivers (CRC mismatch)
   int64_t redispatched = 0;      // leader: jobs re-sent from another owner after their deadline
   int64_t suspects = 0;          // leader: senders that missed a deadline

@@ -24,6 +24,7 @@ struct CachedPlan {
   std::vector<std::pair<XferJob, int>> jobs;  // (job, phase) as the scheduler queued them
   int64_t dispatched = 0;                     // stats: jobs_dispatched of the planning session
   double flow_T = 0;                          // mode 3: the plan's T
+  std::string solver;                         // stats: which scheduler / solver made it
 };
 
 class PlanCache {

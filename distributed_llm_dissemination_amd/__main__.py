@@ -96,9 +96,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--node-disk-gbps", type=float, default=0.0,
                    help="rccl: one NVMe shared by every rank of the node at this read rate (disk readers share it; "
                         "mode 3 plans it as one budget); 0 = per-rank disks")
-    p.add_argument("--comm-init", default="parallel", choices=["parallel", "split"],
-                   help="rccl: lane communicators from one unique id each, initialized together in one group "
-                        "(parallel), or split from the world communicator one by one (split)")
+    p.add_argument("--comm-init", default="split", choices=["parallel", "split"],
+                   help="rccl: lane communicators split from the world communicator one by one (split, the "
+                        "default: faster at 8 shared ranks, profiles/r3_init2), or one unique id each, initialized "
+                        "together in one group (parallel)")
     p.add_argument("--suspect-timeout", type=float, default=10.0,
                    help="rccl: report a P2P group stalled this long to the leader, which probes the peers and "
                         "shrinks the communicator around dead ranks (elastic recovery; 0 = only on failure)")
@@ -139,7 +140,7 @@ def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
     opts = {"reserve_cus": args.reserve_cus, "suspect_s": getattr(args, "suspect_timeout", 10.0),
             "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0)),
-            "comm_init": getattr(args, "comm_init", "parallel")}
+            "comm_init": getattr(args, "comm_init", "split")}
     if args.nccl_ctas:
         lo, _, hi = args.nccl_ctas.partition(":")
         opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)
@@ -148,7 +149,7 @@ def engine_opts(args) -> dict:
 
 def nccl_ids(core, world: int, args) -> bytes:
     """Rank 0's RCCL bootstrap ids: one per comm lane (parallel init) or one (split)."""
-    n = core.resolve_lanes(world, int(getattr(args, "lanes", 0))) if getattr(args, "comm_init", "parallel") == "parallel" else 1
+    n = core.resolve_lanes(world, int(getattr(args, "lanes", 0))) if getattr(args, "comm_init", "split") == "parallel" else 1
     return core.nccl_unique_id(n)
 
 

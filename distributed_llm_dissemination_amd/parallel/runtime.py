@@ -56,6 +56,11 @@ def hist_quantile(hist: List[int], q: float) -> int:
     return 1 << len(hist)
 
 
+def _sig(x: float, digits: int = 4) -> float:
+    """`x` to `digits` significant digits (probe rates: GB/s at any fabric scale)."""
+    return float(f"{x:.{digits}g}")
+
+
 @dataclass
 class SessionResult:
     ok: bool
@@ -65,6 +70,8 @@ class SessionResult:
     jobs: int = 0
     plan_ms: float = 0.0
     plan_cached: bool = False
+    plan_solver: str = ""  # leader: "mode1:links", "flow", "lp", ...
+    plan_gap_bytes: int = 0  # leader, mode 3: bytes the plan left uncovered (invariant: 0)
     plan_sched_ms: float = 0.0  # leader: the scheduler's share of plan_ms (or the plan-cache lookup)
     plan_dispatch_ms: float = 0.0  # leader: encoding + sending the transfer batches
     flow_T: float = 0.0
@@ -197,6 +204,9 @@ class Runtime:
         # Closed-loop link rates (planned engines): EWMA of this rank's measured
         # send rate to each peer node (B/s), reported with its announce.
         self.link_est: Dict[int, float] = {}
+        self.link_probe: Dict[int, float] = {}  # pre-flight probe's concurrent rates (B/s): the capacity floor
+        self.link_slow_streak: Dict[int, int] = {}  # consecutive observations below LINK_SLOW x the median
+        self.link_level: Optional[float] = None  # the uniform level every normal link reports (B/s)
         self._links0: Optional[Dict[str, Dict[int, float]]] = None
 
         reg = dict(registry) if registry is not None else cfg.registry()
@@ -427,14 +437,17 @@ class Runtime:
 
     def _map_shared_layers(self, layers) -> None:
         """host_share: publish this rank's segments (a ready marker), then map every
-        other rank's host-tier layers as host-tier sources of this rank."""
+        other rank's host-tier layers as host-tier sources of this rank - ranks
+        of this rank's own host only: another host's /dev/shm is not reachable
+        (and with fake host labels, DISSEM_FAKE_HOSTS, it must not be either)."""
         mine = [l for st, per in self.me.initial_layers.items() if st not in (SOURCE_DISK, SOURCE_DEVICE, SOURCE_CLIENT)
                 for l in per]
         if mine:
             self._shared.append(_core.HostBuffer.shared(self._hs_name(self.node_id, "ready"), 4096, True, False))
         pin = self.engine_kind == "rccl"
+        my_host = self.hosts.get(self.node_id, 0)
         for n in self.cfg.nodes:
-            if n.id == self.node_id:
+            if n.id == self.node_id or self.hosts.get(n.id, 0) != my_host:
                 continue
             theirs = [(l, size) for st, per in n.initial_layers.items()
                       if st not in (SOURCE_DISK, SOURCE_DEVICE, SOURCE_CLIENT) for l, size in per.items()]
@@ -762,6 +775,8 @@ class Runtime:
             jobs=st.jobs_dispatched,
             plan_ms=st.plan_ms,
             plan_cached=st.plan_cached,
+            plan_solver=st.plan_solver,
+            plan_gap_bytes=st.plan_gap_bytes,
             plan_sched_ms=st.plan_sched_ms,
             plan_dispatch_ms=st.plan_dispatch_ms,
             flow_T=st.flow_T,
@@ -801,18 +816,61 @@ class Runtime:
         return h
 
     # ------------------------------------------------- closed-loop link rates
+    # Per directed link from this rank, a CAPACITY estimate: the larger of the
+    # EWMA of earlier sessions' busy throughput (bytes / device time of the P2P
+    # groups that carried them) and the pre-flight probe's concurrent rate.
+    # Busy throughput reads low whenever a send waits for its peer's recv (the
+    # RCCL send kernel spins until the receiver posts; the simulator's groups
+    # likewise), so alone it would pace mode 3 below the fabric; the probe
+    # times both ends posted together and floors it. The report the leader
+    # plans on is uniform unless a link is really slower than the others:
+    #   * every link reports the same level U (the median capacity, moved only
+    #     when the median moves by more than LINK_LEVEL_HYST), so a uniform
+    #     mesh plans uniformly and identically session after session (the
+    #     leader's plan cache then replays the plan);
+    #   * a link whose capacity stayed below LINK_SLOW x the median in
+    #     LINK_SLOW_SESSIONS consecutive observations (the probe counts as one)
+    #     reports its own capacity, and the plans route around it.
+    # Reference analog: node.go:774-793 times jobs, :1044-1053 steers by them.
     LINK_EWMA_ALPHA = 0.5   # weight of the newest measurement
-    LINK_SNAP = 0.15        # reports within this fraction of the median are reported as the median
+    LINK_SLOW = 0.7         # a link below this fraction of the median capacity ...
+    LINK_SLOW_SESSIONS = 2  # ... in this many consecutive observations is planned at its own rate
+    LINK_LEVEL_HYST = 0.10  # the uniform level follows the median only past this relative change
     LINK_MIN_CHUNKS = 4     # a link must have carried this many grid chunks in a session to be measured
 
     def observe_links(self, rates: Dict[int, float]) -> None:
-        """Fold measured send rates (peer node -> B/s) into the per-link EWMA."""
+        """Fold one session's measured send rates (peer node -> B/s) into the per-link EWMA."""
         a = self.LINK_EWMA_ALPHA
         for p, r in rates.items():
             if r is None or r <= 0 or p == self.node_id:
                 continue
             old = self.link_est.get(p)
             self.link_est[p] = float(r) if old is None else old + a * (float(r) - old)
+        self._update_link_state()
+
+    def observe_probe(self, rates: Dict[int, float]) -> None:
+        """The pre-flight probe's concurrent send rates (peer node -> B/s): the floor
+        of every link's capacity estimate from now on."""
+        for p, r in rates.items():
+            if r and r > 0 and p != self.node_id:
+                self.link_probe[p] = float(r)
+        self._update_link_state()
+
+    def link_capacity(self) -> Dict[int, float]:
+        """Per peer node: max(session EWMA, probe) in B/s."""
+        peers = set(self.link_est) | set(self.link_probe)
+        return {p: max(self.link_est.get(p, 0.0), self.link_probe.get(p, 0.0)) for p in peers}
+
+    def _update_link_state(self) -> None:
+        cap = self.link_capacity()
+        if not cap:
+            return
+        vals = sorted(cap.values())
+        med = vals[len(vals) // 2]
+        for p, c in cap.items():
+            self.link_slow_streak[p] = self.link_slow_streak.get(p, 0) + 1 if c < self.LINK_SLOW * med else 0
+        if self.link_level is None or abs(med - self.link_level) > self.LINK_LEVEL_HYST * self.link_level:
+            self.link_level = med
 
     def _observe_session_links(self) -> None:
         """After a session: this rank's bytes to each peer over the device time of
@@ -826,17 +884,18 @@ class Runtime:
             dms = now["send_busy_ms"].get(p, 0.0) - self._links0["send_busy_ms"].get(p, 0.0)
             if db >= self.LINK_MIN_CHUNKS * self.grid and dms > 0:
                 rates[self.node_ids[p]] = db / (dms / 1e3)
-        self.observe_links(rates)
+        if rates:
+            self.observe_links(rates)
 
     def link_report(self) -> Dict[int, int]:
-        """What this rank announces: its EWMA rates, with every rate within
-        LINK_SNAP of the median replaced by the median - a uniform fabric's noise
-        must not reshape the plan from one session to the next, a slow link must."""
-        if not self.link_est:
+        """What this rank announces (B/s per peer node): the uniform level, or a
+        persistently slow link's own capacity (see above)."""
+        cap = self.link_capacity()
+        if not cap or self.link_level is None:
             return {}
-        vals = sorted(self.link_est.values())
-        med = vals[len(vals) // 2]
-        return {p: int(med if abs(r - med) <= self.LINK_SNAP * med else r) for p, r in self.link_est.items()}
+        lvl = self.link_level
+        return {p: int(c if self.link_slow_streak.get(p, 0) >= self.LINK_SLOW_SESSIONS else lvl)
+                for p, c in cap.items()}
 
     def plan_link_bw(self) -> Dict[tuple, int]:
         """Leader: the per directed link rates (B/s) its last plan used."""
@@ -915,7 +974,7 @@ class Runtime:
         conc_ms = (time.perf_counter() - t0) * 1e3
         out: Dict[str, object] = {
             "bytes": nbytes,
-            "concurrent": {self.node_ids[o["peer"]]: round(nbytes / (o["ms"] / 1e3) / 1e9, 2) if o["ms"] > 0 else None
+            "concurrent": {self.node_ids[o["peer"]]: _sig(nbytes / (o["ms"] / 1e3) / 1e9) if o["ms"] > 0 else None
                            for o in got if o["send"]},
             "concurrent_wall_ms": round(conc_ms, 3),
         }
@@ -928,7 +987,7 @@ class Runtime:
                     self._barrier()
                     if me == a:
                         o = run([(b, True, nbytes)], f"solo {self.node_ids[a]}->{self.node_ids[b]}")[0]
-                        rates[self.node_ids[b]] = round(nbytes / (o["ms"] / 1e3) / 1e9, 2) if o["ms"] > 0 else None
+                        rates[self.node_ids[b]] = _sig(nbytes / (o["ms"] / 1e3) / 1e9) if o["ms"] > 0 else None
                     elif me == b:
                         run([(a, False, nbytes)], f"solo {self.node_ids[a]}->{self.node_ids[b]}")
             self._barrier()

@@ -42,7 +42,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             slow_link=None, seeding: str = "random", policy=None, plan_links: bool = False,
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
             adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
-            nic_gbps: float = 50.0, host_lane_classes: int = 0) -> dict:
+            nic_gbps: float = 50.0, host_lane_classes: int = 0, probe_mib: int = 256, warmup: int = 1,
+            recv_delay=None) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others.
@@ -54,6 +55,16 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     (default: the simulated one) - e.g. a constant estimate the real fabric beats.
     adapt_links: every session after the first plans on the link rates the ranks
     measured in the earlier ones (closed loop, Runtime.link_report).
+    probe_mib: as bench.py, an untimed pre-flight probe of every directed link
+    (this many MiB at full size, concurrent pass only) floors the closed loop's
+    link capacities; 0 = no probe.
+    warmup: sessions run before the `steps` timed ones (bench.py --warmup).
+    recv_delay: {rank: seconds (full size)} - fault injection: that rank posts
+    every receive this late (its peers' sends wait for it).
+    A session's predicted time is its modeled transfer time (wall time minus
+    the leader's plan, divided by `slowdown`) plus the leader's plan time at
+    full weight - the plan is CPU work that does not get faster with the
+    fabric. ms_per_step is the mean over the timed sessions (min_ms: the best).
     tier="disk" (BASELINE config #4): layers are files read by each rank's disk
     readers through ONE node-wide budget of disk_gbps (the node's single NVMe,
     engine/node_pacer.h), then staged over that rank's PCIe; mode 3 plans the
@@ -70,14 +81,15 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     try:
         return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                         seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
-                        disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes)
+                        disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib, warmup,
+                        {r: v * slowdown for r, v in (recv_delay or {}).items()})
     finally:
         _core.set_log_level(level)
 
 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
              policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False,
-             hosts=1, nic_gbps=50.0, host_lane_classes=0):
+             hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1, recv_delay=None):
     import shutil
     import tempfile
 
@@ -85,7 +97,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
     try:
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
-                           storage, host_share, hosts, nic_gbps, host_lane_classes)
+                           storage, host_share, hosts, nic_gbps, host_lane_classes, probe_mib, warmup, recv_delay)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
@@ -93,7 +105,8 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
 
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
                 policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
-                host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0):
+                host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1,
+                recv_delay=None):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -105,6 +118,8 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     if slow_link is not None:
         (s, d), frac = slow_link
         t.link = {(s, d): link_gbps * 1e9 / scale * frac}
+    if recv_delay:
+        t.recv_delay_s = dict(recv_delay)
     per_host = max(1, n // max(1, hosts))
     host_of = [min(i // per_host, hosts - 1) for i in range(n)]
     if hosts > 1:
@@ -126,8 +141,10 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             (s, d), frac = slow_link
             cfg.links[s][d] = int(bw * frac)
     disk = dict(storage_path=storage, node_disk_gbps=disk_gbps / scale, node_key=key) if tier == "disk" else {}
+    bar = threading.Barrier(n)
     rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
-                   poison=False, engine_opts={"lanes": lanes, "host_lane_classes": host_lane_classes}, pack=pack, host_share=host_share, **disk)
+                   poison=False, engine_opts={"lanes": lanes, "host_lane_classes": host_lane_classes}, pack=pack,
+                   host_share=host_share, barrier=bar.wait, **disk)
            for i in range(n)]
     if host_share:
         for r in rts:
@@ -135,17 +152,36 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
         r.transport.set_registry(reg)
-    times, flow_Ts = [], []
+    times, flow_Ts, plans, cached, walls = [], [], [], [], []
     flow_T = 0.0
     plan_links_used = {}
+    probe_GBps = None
     try:
-        for _ in range(steps):
+        if n > 1 and probe_mib > 0 and adapt_links:
+            # bench.py's untimed pre-flight probe (concurrent pass): floors the link capacities
+            got = [None] * n
+
+            def pr(i):
+                got[i] = rts[i].probe_links(max(cb, (probe_mib << 20) // scale), timeout_s=600, solo=False)
+
+            ths = [threading.Thread(target=pr, args=(i,)) for i in range(n)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            for r, g in zip(rts, got):
+                r.observe_probe({p: v * 1e9 for p, v in g.get("concurrent", {}).items() if v})
+            conc = sorted(v for g in got for v in g.get("concurrent", {}).values() if v)
+            probe_GBps = round(conc[len(conc) // 2] * scale * slowdown, 1) if conc else None
+        for step in range(warmup + steps):
             for r in rts:
                 extra = {"stage_gbps": pcie_gbps / scale} if plan_links else {}
                 if plan_links and hosts > 1:
                     extra["nic_gbps"] = nic_gbps / scale
                 r.prepare(mode, **{"pull_window": max(1, n - 1), "adapt_links": adapt_links, **extra, **(policy or {})})
             res = [None] * n
+            sent0 = [r.link_stats()["sent"] for r in rts]
+            staged0 = [r.engine.stats().bytes_staged for r in rts]
 
             def go(i):
                 res[i] = rts[i].execute(600)
@@ -156,30 +192,70 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                 th.start()
             for th in ths:
                 th.join()
-            times.append(time.perf_counter() - t0)
+            wall = time.perf_counter() - t0
             if not all(x.ok for x in res):
                 raise RuntimeError([x.error for x in res if not x.ok])
+            plan_s = res[0].plan_ms / 1e3
+            walls.append(wall)
+            times.append((wall - plan_s) / slowdown + plan_s)
+            plans.append(res[0].plan_ms)
+            cached.append(res[0].plan_cached)
             flow_T = res[0].flow_T
             flow_Ts.append(flow_T)
             plan_links_used = rts[0].plan_link_bw()
+            # bytes accounting of this session (deterministic, unlike wall time):
+            # per directed link and per rank's staging, at full size
+            link_bytes = {}
+            for i, r in enumerate(rts):
+                for p, b in r.link_stats()["sent"].items():
+                    d = b - sent0[i].get(p, 0)
+                    if d:
+                        link_bytes[(i, p)] = d * scale
+            staged = [(r.engine.stats().bytes_staged - staged0[i]) * scale for i, r in enumerate(rts)]
         lanes_used = rts[0].engine.stats().lanes
+        rts_est = [dict(r.link_est) for r in rts]  # per rank: the busy-throughput EWMA per peer (B/s)
     finally:
         for r in rts:
             r.close()
-    sec = min(times) / slowdown
+    timed = times[warmup:] or times
+    sec = sum(timed) / len(timed)
     total = delivered_bytes(cfg) * scale
     return {"n": n, "link_GBps": link_gbps * slowdown, "pcie_GBps": pcie_gbps * slowdown, "mode": mode, "tier": tier,
             **({"node_disk_GBps": disk_gbps * slowdown} if tier == "disk" else {}),
             **({"pack": pack, "layers": layers, "layer_MiB": layer_bytes >> 20} if pack != "none" else {}),
             **({"hosts": hosts, "nic_GBps": nic_gbps * slowdown} if hosts > 1 else {}),
             "seeding": seeding, **({"policy": policy} if policy else {}), **({"host_share": True} if host_share else {}),
-            "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1),
-            "times_ms": [round(x / slowdown * 1e3, 1) for x in times],
+            "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1), "min_ms": round(min(timed) * 1e3, 1),
+            "warmup": warmup, "times_ms": [round(x * 1e3, 1) for x in times],
+            "plan_ms": [round(x, 2) for x in plans], "plan_cached": cached,
+            **({"probe_GBps": probe_GBps} if probe_GBps else {}),
             **({"flow_T_ms": [round(x / slowdown * 1e3, 1) for x in flow_Ts]} if any(flow_Ts) else {}),
             **({"plan_link_GBps_last": {f"{a}->{b}": round(v * scale * slowdown / 1e9, 1)
                                         for (a, b), v in sorted(plan_links_used.items())}} if plan_links_used else {}),
+            "busy_GBps": {f"{i}->{p}": round(v * scale * slowdown / 1e9, 1) for i, r in enumerate(rts_est)
+                          for p, v in sorted(r.items())},
+            "link_GiB_last": {f"{a}->{b}": round(v / 2**30, 3) for (a, b), v in sorted(link_bytes.items())},
+            "staged_GiB_last": [round(v / 2**30, 3) for v in staged],
+            "modeled_ms_last": round(modeled_ms(link_bytes, staged, n, link_gbps * slowdown, pcie_gbps * slowdown,
+                                                 slow_link) * 1e3, 1),
             "value_GBps": round(total / sec / 1e9, 1), "scale": scale,
             **({"planned_T_ms": round(flow_T * 1e3 / slowdown, 1)} if flow_T > 0 else {})}
+
+
+def modeled_ms(link_bytes, staged, n, link_gbps, pcie_gbps, slow_link=None) -> float:
+    """A load-independent lower bound of a session from its bytes accounting:
+    the busiest directed link's bytes / its rate, or the busiest rank's staged
+    bytes / PCIe, whichever is longer (seconds; the wall clock of the
+    simulated threads does not enter it)."""
+    t = 0.0
+    for (s, d), b in link_bytes.items():
+        rate = link_gbps * 1e9
+        if slow_link is not None and (s, d) == tuple(slow_link[0]):
+            rate *= slow_link[1]
+        t = max(t, b / rate)
+    for b in staged:
+        t = max(t, b / (pcie_gbps * 1e9))
+    return t
 
 
 def main() -> int:
@@ -207,14 +283,20 @@ def main() -> int:
                     help="with --hosts: every dest imports from the holders itself (no per-host import + relay)")
     ap.add_argument("--mode0", action="store_true",
                     help="BASELINE config #2 instead: mode 0 from the leader (relay vs ncclBroadcast, host vs HBM source)")
+    ap.add_argument("--steps", type=int, default=4, help="timed sessions (mean reported)")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed sessions first (bench.py --warmup)")
+    ap.add_argument("--probe-mib", type=int, default=256, help="pre-flight link probe at full size, as bench.py (0: none)")
+    ap.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
+                    help="mode 1's owner choice (bench.py's default: links)")
     args = ap.parse_args()
+    common = dict(steps=args.steps, warmup=args.warmup, probe_mib=args.probe_mib)
     _core.set_log_level(3)
     if args.mode0:
         for lg in args.link_gbps:
             for n in args.ns:
                 if args.host_share:
                     r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes,
-                                mode=0, slowdown=args.slowdown, seeding="leader", tier="host", host_share=True)
+                                mode=0, slowdown=args.slowdown, seeding="leader", tier="host", host_share=True, **common)
                     print(json.dumps(r), flush=True)
                     continue
                 for tier in ("device", "host"):
@@ -222,7 +304,7 @@ def main() -> int:
                         r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes,
                                     mode=0, slowdown=args.slowdown, seeding="leader", tier=tier,
                                     policy={"relay": relay, "collective": coll, "hierarchical": not args.flat},
-                                    hosts=args.hosts, nic_gbps=args.nic_gbps)
+                                    hosts=args.hosts, nic_gbps=args.nic_gbps, **common)
                         print(json.dumps(r), flush=True)
         return 0
     for lg in args.link_gbps:
@@ -230,7 +312,7 @@ def main() -> int:
             r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,
                         slowdown=args.slowdown, layers=args.layers, layer_bytes=args.layer_mib << 20, pack=args.pack,
                         tier=args.tier, disk_gbps=args.disk_gbps, hosts=args.hosts, nic_gbps=args.nic_gbps,
-                        policy={"owner_policy": "links", "hierarchical": not args.flat} if args.hosts > 1 else None)
+                        policy={"owner_policy": args.owner_policy, "hierarchical": not args.flat}, **common)
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
             if args.pack == "none" and args.hosts == 1:

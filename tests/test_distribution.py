@@ -339,3 +339,30 @@ def test_dead_sender_jobs_are_redispatched(core, mode):
         assert st.redispatched >= 1 and st.suspects == 1
     finally:
         c.close()
+
+
+def test_mode2_host_engine_keeps_the_fastest_source(core, tmp_path):
+    """Mode 2 on the host (TCP) engine keeps the reference's sender choice
+    (node.go:948-978, the fastest source): a dest that holds the layer only on
+    a slow disk (1 MB/s) receives it from the peer that holds it in memory
+    (unlimited) instead of loading it itself."""
+    size = 512 << 10
+    data = os.urandom(size)
+    p = tmp_path / "5.layer"
+    p.write_bytes(data)
+    c = Cluster(core, "tcp", 3)
+    try:
+        assignment = {1: [5]}
+        leader = c.node(0, 2, {}, assignment)
+        dest = c.node(1, 2, {5: core.LayerSrc.disk(str(p), size, 1_000_000)})
+        peer = c.node(2, 2, {5: core.LayerSrc.inmem(data)})
+        peer.announce()
+        wait_status(leader, 2)  # the session starts once the dest (the only Assignment key) announces
+        t0 = time.time()
+        exec_distribution(leader, [dest], assignment)
+        assert peer.wait_ready(5.0)
+        assert dest.layer(5).host_bytes() == data
+        assert time.time() - t0 < 0.4  # a disk load would take ~0.27 s + the startup
+        assert c.ts[2].bytes_sent >= size and c.ts[1].bytes_sent == 0
+    finally:
+        c.close()

@@ -21,10 +21,10 @@ MiB = 1 << 20
 _keys = itertools.count()
 
 
-def _cluster(cfg, persist, **kw):
+def _cluster(cfg, persist, chunk=MiB, **kw):
     key = f"persist{next(_keys)}"
     n = len(cfg.nodes)
-    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=MiB, sim_key=key,
+    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=chunk, sim_key=key,
                    persist_dir=str(persist), **kw) for i in range(n)]
     reg = {i: r.transport.address() for i, r in enumerate(rts)}
     for r in rts:
@@ -174,6 +174,42 @@ def test_chunk_granular_resume_moves_only_missing_chunks(tmp_path, owner_policy,
         # The holder received the two missing chunks of `target` and every byte of the others.
         got = rts[holder].link_bytes()["recv"]
         assert sum(got.values()) == (len(missing) - 1) * size + 2 * MiB
+    finally:
+        for r in rts:
+            r.close()
+
+
+def test_partial_copy_on_another_chunk_grid_is_not_resumed(tmp_path):
+    """A partial copy persisted on a 1 MiB chunk grid and a run on 512 KiB
+    chunks: its ranges would not sit on this run's grid (a chunk half from
+    disk, half over the wire, whose landing could never complete), so the
+    copy is not resumed at all - the layer moves whole - and the session
+    completes with every byte right."""
+    import json
+
+    size = 4 * MiB
+    cfg = make_workload(2, 2, size, tier="host", seeding="random", chunk_bytes=MiB)
+    rts, _ = _cluster(cfg, tmp_path)
+    try:
+        assert all(x.ok for x in _session(rts))
+        full = {l: rts[1].layer_bytes(l) for l in range(2)}
+        target = next(l for l in range(2) if l not in cfg.node(1).initial_layers.get(2, {}))
+        rts[1].persist(layers=[target])
+    finally:
+        for r in rts:
+            r.close()
+    root = os.path.join(str(tmp_path), "1")
+    man = json.load(open(os.path.join(root, "manifest.json")))
+    man["layers"][str(target)]["chunks"] = [0, 2]
+    json.dump(man, open(os.path.join(root, "manifest.json"), "w"))
+    cfg2 = make_workload(2, 2, size, tier="host", seeding="random", chunk_bytes=MiB // 2)
+    rts, _ = _cluster(cfg2, tmp_path, chunk=MiB // 2)
+    try:
+        assert rts[1].resumed == [] and rts[1].resumed_partial == []
+        res = _session(rts)
+        assert all(x.ok for x in res), [x.error for x in res]
+        for l in range(2):
+            assert rts[1].layer_bytes(l) == full[l]
     finally:
         for r in rts:
             r.close()

@@ -1,0 +1,83 @@
+"""The leader's plan sits inside the timed window (the reference starts its
+timer before the solve: node.go:1161-1165, and logs the solve's computation
+time: node.go:1225-1231). At N = 8 on the headline workload (80 x 1 GiB,
+random seeding, 560 demands) the plan must cost next to nothing: the mode-3
+flow solves over layer classes with a parametric (min-cut Newton) T search,
+deterministic plans replay from the plan cache, and the transfer batches go
+out as direct text. Measured on the simulator's 8 ranks (one process, CPU)."""
+
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from distributed_llm_dissemination_amd import _core
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+import predict_scaling  # noqa: E402
+
+
+@pytest.mark.parametrize("mode,limit_ms", [(1, 2.0), (3, 5.0)])
+def test_leader_plan_ms_at_8_ranks(mode, limit_ms):
+    """After warmup the leader's plan_ms (scheduler + dispatch of every rank's
+    batch) is <= 2 ms in mode 1 and <= 5 ms in mode 3 (median of the timed
+    sessions), the plan is replayed from the cache, and the predicted step
+    charges it at full weight (scripts/predict_scaling.py)."""
+    r = predict_scaling.predict(8, scale=1024, steps=4, warmup=1, slowdown=4, mode=mode,
+                                policy={"owner_policy": "links"}, probe_mib=4096)
+    timed = r["plan_ms"][r["warmup"]:]
+    assert statistics.median(timed) <= limit_ms, r["plan_ms"]
+    assert all(r["plan_cached"][2:]), r["plan_cached"]
+
+
+def test_mode3_flow_solve_is_fast_and_exact():
+    """The headline mode-3 instance (8 ranks, 80 x 1 GiB, one random holder
+    per layer, 560 demands, 50 GB/s links, 57.5 GB/s staging): 80 layers are 8
+    classes; the parametric search needs a handful of max-flows, not the
+    reference's doubling + bisection (flow.go:155-191); T equals the closed
+    form (each GPU stages its 10 GiB, each link carries 10 GiB)."""
+    G = 1 << 30
+    rng = np.random.default_rng(7)
+    perm = rng.permutation(80)
+    host = _core.LayerMeta(_core.Location.Inmem, 0, _core.SourceType.Mem, G)
+    hold = {s: {int(l): host for l in perm[s * 10:(s + 1) * 10]} for s in range(8)}
+    dem = [(l, d, G) for l in range(80) for d in range(8) if l not in hold[d]]
+    links = {(a, b): 50 * 10**9 for a in range(8) for b in range(8) if a != b}
+    stage = {a: 57_500_000_000 for a in range(8)}
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        p = _core.solve_flow(hold, dem, links=links, stage=stage, stage_once=True, align=64 << 20)
+        times.append(time.perf_counter() - t0)
+    assert p.solver == "flow" and p.feasible
+    assert p.solves <= 8, p.solves
+    assert p.T == pytest.approx(10 * G / 50e9, rel=1e-6)
+    assert len(p.jobs) == 560  # every layer whole from its one holder
+    assert statistics.median(times) < 0.005, times
+
+
+def test_lp_with_node_disk_group_is_fast():
+    """Config #4 at N = 8: every rank's disk tier reads one shared NVMe, a budget
+    the flow cannot state, so the LP plans it (classes keep it small): solved
+    in <= 5 ms (median of 5), T = 80 GiB / 13.3 GB/s."""
+    G = 1 << 30
+    disk = _core.LayerMeta(_core.Location.Disk, 13_300_000_000, _core.SourceType.Disk, G)
+    rng = np.random.default_rng(1)
+    hold = {s: {} for s in range(8)}
+    for l in range(80):
+        hold[int(rng.integers(8))][l] = disk
+    dem = [(l, d, G) for l in range(80) for d in range(8) if l not in hold[d]]
+    links = {(a, b): 50 * 10**9 for a in range(8) for b in range(8) if a != b}
+    stage = {a: 55 * 10**9 for a in range(8)}
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        p = _core.solve_flow(hold, dem, links=links, stage=stage, stage_once=True,
+                             disk_group={a: 0 for a in range(8)}, disk_group_bps={0: 13_300_000_000})
+        times.append(time.perf_counter() - t0)
+    assert p.solver == "lp" and p.feasible, p.lp_status
+    assert p.T == pytest.approx(80 * G / 13.3e9, rel=1e-6)
+    assert statistics.median(times) < 0.005, times

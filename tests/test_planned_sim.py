@@ -537,3 +537,19 @@ def test_mode0_host_share_layers_with_fewer_chunks_than_ranks():
     finally:
         for r in rts:
             r.close()
+
+
+def test_mode2_planned_dest_loads_its_own_lower_tier_copy():
+    """Mode 2 on the planned (GPU) engine: a dest that holds a layer in a lower
+    tier (pinned host) loads it itself rather than receiving it from a peer
+    into the HBM slot it is also staging (the race TSAN caught, round 3); the
+    peer sends nothing of it."""
+    cfg = make_workload(2, 2, 2 * MiB, tier="host", seeding="leader", chunk_bytes=MiB)
+    cfg.assignment = {0: [0, 1], 1: [0]}
+    cfg.nodes[1].initial_layers = {2: {0: 2 * MiB}}  # rank 1 holds layer 0 in host memory too
+
+    def inspect(rts):
+        assert rts[1].link_bytes()["recv"].get(0, 0) == 0  # nothing of layer 0 came from rank 0
+
+    (res,), _ = run_cluster(cfg, 2, pull_window=1, inspect=inspect)
+    assert res[1].engine_stats["bytes_staged"] == 2 * MiB
