@@ -72,6 +72,9 @@ def parse_args(argv=None):
                         "as one budget by mode 3 (default 13.3, profiles/r1_diskspeed.log; 0 = per-rank, unpaced)")
     p.add_argument("--reserve-cus", type=int, default=-1,
                    help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
+    p.add_argument("--crc-grid", type=int, default=-1,
+                   help="workgroup cap of the CRC verify kernels (-1: 32 when N > 1 - a narrow verify that keeps up "
+                        "with 7 links of landings without taking the chip's HBM bandwidth from RCCL; 0: every CU)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
     p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
     p.add_argument("--lanes", type=int, default=0,

@@ -111,6 +111,7 @@ struct PlannedConfig {
   // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
   // -1: 32 when world > 1 (one XCD's worth), 0 on one rank (no RCCL traffic).
   int reserve_cus = -1;
+  int crc_grid = -1;  // verify kernels' workgroup cap (-1: kVerifyGridPeers with peers, all CUs alone; 0: all)
   // RCCL communicator CTA (workgroup/channel) bounds via ncclCommInitRankConfig;
   // 0 keeps RCCL's own choice. More CTAs = more channels per P2P peer.
   int nccl_min_ctas = 0;

@@ -67,6 +67,7 @@ class HipBackend : public Backend {
       int cus = 0;
       HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
       crc_grid_ = cfg_.reserve_cus > 0 && cfg_.reserve_cus < cus ? cus - cfg_.reserve_cus : 0;
+      if (cfg_.crc_grid > 0) crc_grid_ = crc_grid_ > 0 ? std::min(crc_grid_, cfg_.crc_grid) : cfg_.crc_grid;
     }
     HIP_OK(hipMalloc(&ws_, std::max(kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes),
                                      kern::crc32c_batch_workspace_bytes(cfg_.max_crc_bytes, kern::kCrcBatchMax))));

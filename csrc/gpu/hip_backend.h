@@ -34,6 +34,11 @@ struct HipBackendConfig {
   // > 0: the verify and copy streams get a CU mask that leaves this many CUs
   // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
   int reserve_cus = 0;
+  // Workgroup cap of the CRC verify kernels (0: every CU the verify stream
+  // has). With peers a narrow verify runs longer but never takes the whole
+  // chip's HBM bandwidth from the comm lanes' RCCL kernels at once
+  // (bin/contention -paced, profiles/r4_contention/).
+  int crc_grid = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
   int lanes = 1;                               // comm lanes (communicator + stream each)
   int hosts = 1;                               // multi-node: hosts of world / hosts ranks (backend.h host_lanes)

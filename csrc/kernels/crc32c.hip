@@ -10,13 +10,17 @@
 //    (s ^= word; s = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3]): one table lookup per
 //    byte. Between its pieces a lane's register crosses the 4032 bytes of the
 //    other lanes as zeros: a fixed GF(2)-linear map, 8 nibble lookups;
-//  * each lane's CRC is shifted to the END OF ITS CHUNK with one GF(2)
-//    multiply by a host-computed constant (per segment and lane: the lane's
-//    distance to its segment end plus the segment's distance to the chunk
-//    end), then the lanes are XOR-reduced with cross-lane shuffles, so
-//  * a chunk's raw CRC is the plain XOR of its segments' values: a second,
-//    small kernel XOR-reduces them (one 256-thread block per chunk) and adds
-//    the init/xorout term, writing the standard CRC32C.
+//  * each lane's CRC is shifted to the END OF ITS SEGMENT with one GF(2)
+//    multiply by a per-lane constant (x^(8*64*(63-lane))), then the lanes are
+//    XOR-reduced with cross-lane shuffles: a segment's value is its raw CRC;
+//  * a second, small kernel (one workgroup per chunk) shifts every full
+//    segment to the chunk end - x^(8*16 KiB*j) from one table indexed by the
+//    segments that follow it, then x^(8*rem) for a chunk whose last segment is
+//    short - XORs them with that last segment and adds the init/xorout term,
+//    writing the standard CRC32C.
+// The constants depend on nothing but the segment geometry (chunks up to
+// 1 GiB): one upload per device, never a per-length table (a length-keyed
+// table grew with every new piece size and re-allocated mid-session).
 // The result is the exact CRC32C of each chunk for any chunk length that is a
 // multiple of 16 (the buffer's final chunk may have any length).
 //
@@ -80,8 +84,12 @@ constexpr uint32_t kStageBytes = 16 * 1024;              // fused unpack: 1 KiB 
 constexpr int kThreads = 1024;                          // one workgroup per CU, 4 waves per SIMD
 constexpr int kWaves = kThreads / 64;
 // Global constants: [T: 4 x 256 (T[k][v]: byte v then k zero bytes)]
-// [gap: 8 x 16 nibble tables of the kGapBytes shift][pow16: 1024 (x^(8*16 m))].
-constexpr int kT = 0, kGap = 1024, kPow = kGap + 128, kConstWords = kPow + 1024;
+// [gap: 8 x 16 nibble tables of the kGapBytes shift][pow16: 1024 (x^(8*16 m))]
+// [lanepow: 64 (x^(8*64*(63-l)): lane l's last piece to its segment end)]
+// [segpow: kMaxSegs (x^(8*16 KiB*j))].
+constexpr int kMaxSegs = 65536;  // segments per chunk: chunks up to 1 GiB
+constexpr int kT = 0, kGap = 1024, kPow = kGap + 128, kLanePow = kPow + 1024, kSegPow = kLanePow + 64,
+              kConstWords = kSegPow + kMaxSegs;
 
 using u32x4_t = unsigned int __attribute__((ext_vector_type(4)));
 
@@ -132,32 +140,51 @@ __device__ __forceinline__ uint32_t lds_word(const uint8_t* lds, uint32_t byte_a
   return *reinterpret_cast<const uint32_t*>(lds + byte_addr);
 }
 
-__device__ inline void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc) {
-  for (int i = threadIdx.x; i < 4 * 256 * 8; i += blockDim.x) {  // 32 replicas = 8 x 16 B
-    const int e = i >> 3, q = i & 7, t = e >> 8, b = e & 255;
-    const uint32_t v = sc[kT + e];
-    const uint32_t addr = uint32_t(t >> 1) * 65536u + uint32_t(b) * 256u + uint32_t(t & 1) * 128u;
-    reinterpret_cast<uint4*>(lds + addr)[q] = make_uint4(v, v, v, v);
+// Table replicas per entry: 32 (one per bank of a ds_read_b32 lane group:
+// conflict-free, 144 KiB with the shift tables, one workgroup per CU) or 16
+// (lanes l and l + 16 share a bank: up to 2-way conflicts, 72 KiB, two
+// workgroups per CU).
+template <int R>
+struct LdsLayout {
+  static_assert(R == 32 || R == 16, "32 or 16 table replicas");
+  static constexpr uint32_t kSh = R == 32 ? 131072u : 65536u;  // shift tables after the byte tables
+  static constexpr uint32_t kBytes = kSh + 8u * 16u * uint32_t(R) * 4u;
+  // byte table t, entry b, replica r
+  static __device__ __forceinline__ uint32_t entry(int t, int b) {
+    return R == 32 ? uint32_t(t >> 1) * 65536u + uint32_t(b) * 256u + uint32_t(t & 1) * 128u
+                   : uint32_t(b) * 256u + uint32_t(t) * 64u;
   }
-  for (int i = threadIdx.x; i < 8 * 16 * 8; i += blockDim.x) {
-    const int e = i >> 3, q = i & 7;
+};
+static_assert(LdsLayout<32>::kBytes == kLdsBytes, "144 KiB layout");
+
+template <int R = 32>
+__device__ inline void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc) {
+  constexpr int Q = R / 4;  // 16-B stores per entry
+  for (int i = threadIdx.x; i < 4 * 256 * Q; i += blockDim.x) {
+    const int e = i / Q, q = i % Q, t = e >> 8, b = e & 255;
+    const uint32_t v = sc[kT + e];
+    reinterpret_cast<uint4*>(lds + LdsLayout<R>::entry(t, b))[q] = make_uint4(v, v, v, v);
+  }
+  for (int i = threadIdx.x; i < 8 * 16 * Q; i += blockDim.x) {
+    const int e = i / Q, q = i % Q;
     const uint32_t v = sc[kGap + e];
-    reinterpret_cast<uint4*>(lds + kShLds + uint32_t(e) * 128u)[q] = make_uint4(v, v, v, v);
+    reinterpret_cast<uint4*>(lds + LdsLayout<R>::kSh + uint32_t(e) * uint32_t(R * 4))[q] = make_uint4(v, v, v, v);
   }
   __syncthreads();
 }
 
-struct Slice4 {
+template <int R>
+struct Slice4T {
   const uint8_t* lds;
-  uint32_t c3, c2, c1, c0;  // per table t: (pair << 16) | (half * 128 + replica * 4)
-  uint32_t g;               // kShLds + replica * 4
-  __device__ explicit Slice4(const uint8_t* l) : lds(l) {
-    const uint32_t r = (threadIdx.x & 31u) * 4u;
-    c0 = r;
-    c1 = 128u + r;
-    c2 = 0x10000u + r;
-    c3 = 0x10080u + r;
-    g = kShLds + r;
+  uint32_t c3, c2, c1, c0;  // per table t: its entry-0 offset + replica * 4 (bits 0-7 and 16-23)
+  uint32_t g;               // shift tables + replica * 4
+  __device__ explicit Slice4T(const uint8_t* l) : lds(l) {
+    const uint32_t r = (threadIdx.x & uint32_t(R - 1)) * 4u;
+    c0 = LdsLayout<R>::entry(0, 0) + r;
+    c1 = LdsLayout<R>::entry(1, 0) + r;
+    c2 = LdsLayout<R>::entry(2, 0) + r;
+    c3 = LdsLayout<R>::entry(3, 0) + r;
+    g = LdsLayout<R>::kSh + r;
   }
   // byte k of s at bits 8-15, the constant's bytes 0 and 2 around it (v_perm_b32:
   // selectors 0-3 pick bytes of the second operand, 4-7 of the first, 12 a zero)
@@ -178,7 +205,8 @@ struct Slice4 {
   __device__ __forceinline__ uint32_t gap(uint32_t s, uint32_t next) const {
     uint32_t r[8];
 #pragma unroll
-    for (int n = 0; n < 8; ++n) r[n] = lds_word(lds, g + uint32_t(n) * 2048u + ((s >> (4 * n)) & 15u) * 128u);
+    for (int n = 0; n < 8; ++n)
+      r[n] = lds_word(lds, g + uint32_t(n) * uint32_t(16 * R * 4) + ((s >> (4 * n)) & 15u) * uint32_t(R * 4));
     return x3(x3(x3(r[0], r[1], r[2]), r[3], r[4]), x3(r[5], r[6], r[7]), next);
   }
   // a ^ b ^ c in one v_bitop3_b32
@@ -186,6 +214,7 @@ struct Slice4 {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
 };
+using Slice4 = Slice4T<32>;
 
 // In-register 4x4 transpose across the 4 rows (16 lanes each) of a wave and 4
 // registers: afterwards register q of lane m + 16 r holds what register r of
@@ -211,7 +240,6 @@ __device__ __forceinline__ void row_transpose(u32x4_t& r0, u32x4_t& r1, u32x4_t&
 struct Seg {
   const uint8_t* p;     // first byte
   int64_t len;          // bytes (16 KiB except a chunk's last)
-  const uint32_t* row;  // 64 lane shift constants of this full segment
   int64_t chunk, chunk_start, chunk_len, seg_start;
 };
 
@@ -231,8 +259,8 @@ struct NoVisit {
 // A segment shorter than 16 KiB (only ever its chunk's last): each lane takes
 // the strided 16-B words j = lane (mod 64), CRCs each from a zero register and
 // shifts it to the segment end with a pow16 constant; lane 0 adds the byte tail.
-template <class Visit>
-__device__ uint32_t slice_partial(const Seg& sg, const uint32_t* __restrict__ sc, const Slice4& st, int lane,
+template <class Visit, class ST>
+__device__ uint32_t slice_partial(const Seg& sg, const uint32_t* __restrict__ sc, const ST& st, int lane,
                                   Visit& visit) {
   const int64_t nw = sg.len >> 4;
   const u32x4_t* words = reinterpret_cast<const u32x4_t*>(sg.p);
@@ -263,8 +291,39 @@ __device__ __forceinline__ u32x4_t seg_load(__amdgpu_buffer_rsrc_t r, int lo, in
   return __builtin_amdgcn_raw_buffer_load_b128(r, (i >> 2) * kBlockBytes + (i & 3) * 1024 + lo, 0, 2);
 }
 
+// The CRC of one full segment whose 16 words w[] (as loaded) are in
+// registers: per block, the visit sees the block's 4 words (as loaded, with
+// their byte offsets in the chunk), then the transpose hands lane l its piece
+// and the slice-by-4 chain runs; the lanes' registers are shifted to the
+// segment end (lanec = x^(8*64*(63-lane))) and XOR-reduced. `between(b)` runs
+// after block b (the persistent walk issues the next segment's block-b loads
+// there). CRC = false (diagnostic only) keeps the visits and drops the math.
+template <class Visit, bool CRC, class ST, class Between>
+__device__ __forceinline__ uint32_t seg_full(u32x4_t (&w)[4 * kBlocksPerSeg], const Seg& cur, const ST& st,
+                                             Visit& visit, const uint32_t* __restrict__ lanec, int lo,
+                                             Between between) {
+  // s holds (register ^ next word) between steps: 16 mix steps per block,
+  // the block's first word folded into the gap shift before it
+  uint32_t s = 0;
+#pragma unroll
+  for (int b = 0; b < kBlocksPerSeg; ++b) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) visit.word(w[4 * b + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo, 4 * b + j);
+    if constexpr (CRC) {
+      row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
+      s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
+#pragma unroll
+      for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    between(b);
+  }
+  if constexpr (CRC) s = wave_xor_dpp(multmodp_unrolled(lanec[threadIdx.x & 63], s));
+  return s;
+}
+
 // Every wave walks segments g = wave, wave + nwaves, ... (geo(g) -> Seg) and
-// writes seg_out[g]: the segment's raw CRC shifted to its chunk end. A wave
+// writes seg_out[g]: the segment's raw CRC (shifted to its own end). A wave
 // that owns several segments loads block b of the next one as soon as block b
 // of the current one is consumed (pinned with sched_barrier: left alone, the
 // compiler sinks those loads behind the math), so 16 KiB stay in flight per
@@ -309,9 +368,9 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
     visit.begin(cur);
     uint32_t s;
     if (cur.len == kSegBytes) {
-      const uint32_t rowc = cur.row[lane];
-      // s holds (register ^ next word) between steps: 16 mix steps per block,
-      // the block's first word folded into the gap shift before it
+      // (written out rather than through seg_full: the fused kernel sits at the
+      // 128-VGPR cap here, and the helper's form spilled 8 bytes per lane)
+      const uint32_t rowc = sc[kLanePow + lane];
       s = 0;
 #pragma unroll
       for (int b = 0; b < kBlocksPerSeg; ++b) {
@@ -351,13 +410,50 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
   }
 }
 
-// `bytes` cut into chunks of `chunk_bytes`; shift / shift_last: lane constants
-// of full chunks / of a shorter final chunk.
+// One segment per wave (no walk): the wave issues its segment's loads (and
+// the scales) BEFORE the workgroup fills the LDS tables, then runs the
+// segment and exits. On gfx9 one in-order counter (vmcnt) covers loads and
+// stores, so a walking wave's next loads, issued behind its stores, cannot be
+// waited for without those stores completing: a persistent read->write walk
+// moved 512 MiB of bf16 in 160 us where one-segment waves took 139 and a
+// plain one-shot grid 131 (bin/walkprobe, profiles/r4_walk*/). Here a CU
+// streams many short-lived waves instead, and the table fill is paid per
+// workgroup of kWaves segments.
+template <class Geo, class Visit, bool CRC = true, int R = 32, int WAVES = kWaves>
+__device__ __forceinline__ void slice_once(const Geo& geo, int64_t total_segs, const uint32_t* __restrict__ sc,
+                                           uint8_t* lds, Visit& visit, uint32_t* __restrict__ seg_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = int64_t(blockIdx.x) * WAVES + (threadIdx.x >> 6);
+  const bool have = g < total_segs;
+  const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
+  Seg cur = have ? geo(g) : geo(0);
+  const bool full = have && cur.len == kSegBytes;
+  u32x4_t w[4 * kBlocksPerSeg];
+  {
+    const auto r = seg_rsrc(cur.p, full);
+    visit.prefetch(cur, full);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
+      w[i] = seg_load(r, lo, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    visit.advance();
+  }
+  load_lds<R>(lds, sc);  // every wave joins the fill and its barrier
+  if (!have) return;
+  const Slice4T<R> st(lds);
+  visit.begin(cur);
+  uint32_t s;
+  if (full) s = seg_full<Visit, CRC>(w, cur, st, visit, sc + kLanePow, lo, [](int) {});
+  else s = slice_partial(cur, sc, st, lane, visit);
+  if (lane == 0) seg_out[g] = s;
+}
+
+// `bytes` cut into chunks of `chunk_bytes`.
 struct ChunkGeo {
   const uint8_t* src;
   int64_t bytes, chunk_bytes, spc;
-  const uint32_t* shift;
-  const uint32_t* shift_last;
   __device__ Seg operator()(int64_t g) const {
     const int64_t c = g / spc, k = g - c * spc;
     Seg s;
@@ -367,7 +463,6 @@ struct ChunkGeo {
     s.seg_start = k * kSegBytes;
     s.p = src + s.chunk_start + s.seg_start;
     s.len = min(int64_t(kSegBytes), s.chunk_len - s.seg_start);
-    s.row = (s.chunk_len == chunk_bytes ? shift : shift_last) + k * 64;
     return s;
   }
 };
@@ -516,6 +611,45 @@ verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t ou
   slice_walk<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC>(geo, total_segs, sc, st, v, seg_out);
 }
 
+// store = 5: one segment per wave (slice_once), the grid as large as the work.
+template <int BLOCK, bool CRC = true>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+verify_unpack_once_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
+                          const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
+                          uint16_t* __restrict__ out) {
+  __shared__ uint4 lds_raw[(kLdsBytes + kStageBytes) / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  UnpackVisit<BLOCK, true> v{out_chunk_elems, out, geo.src};
+  v.slot = lds + kLdsBytes + (threadIdx.x >> 6) * 1024;
+  slice_once<ChunkGeo, UnpackVisit<BLOCK, true>, CRC>(geo, total_segs, sc, lds, v, seg_out);
+}
+
+// store = 7: one segment per wave, 512-thread workgroups with 16 table
+// replicas (72 KiB + 8 KiB of staging): two workgroups per CU, so one fills
+// its tables and waits for its first loads while the other computes.
+constexpr int kWaves16 = 8;
+template <int BLOCK, bool CRC = true, bool STAGE = true>
+__global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
+verify_unpack_once16_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
+                            const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
+                            uint16_t* __restrict__ out) {
+  __shared__ uint4 lds_raw[(LdsLayout<16>::kBytes + (STAGE ? kWaves16 * 1024 : 0)) / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  UnpackVisit<BLOCK, STAGE> v{out_chunk_elems, out, geo.src};
+  v.slot = lds + LdsLayout<16>::kBytes + (threadIdx.x >> 6) * 1024;
+  slice_once<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(geo, total_segs, sc, lds, v, seg_out);
+}
+
+// CRC only, one segment per wave.
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+crc32c_segments_once_kernel(const ChunkGeo geo, int64_t total_segs, const uint32_t* __restrict__ sc,
+                            uint32_t* __restrict__ seg_out) {
+  __shared__ uint4 lds_raw[kLdsBytes / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  NoVisit v;
+  slice_once<ChunkGeo, NoVisit, true>(geo, total_segs, sc, lds, v, seg_out);
+}
+
 // store = 2: the same CRC walk on half of the waves (0-7) while the other half
 // (8-15) stream the same segments' q bytes through the plain unpack (8 B of
 // fp8 in, 16 B of bf16 out per lane: every load and store instruction fully
@@ -578,23 +712,49 @@ verify_unpack_split_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_c
   }
 }
 
-// One 256-thread block per chunk: XOR of the chunk's (pre-shifted) segment
-// values plus the init/xorout term. init[0]: full chunks, init[1]: short last chunk.
-__global__ void __launch_bounds__(256) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
-                                                          int64_t chunk_bytes, int64_t spc,
-                                                          const uint32_t* __restrict__ init,
-                                                          uint32_t* __restrict__ out) {
-  __shared__ uint32_t part[4];
-  const int64_t c = blockIdx.x;
-  const int64_t chunk_len = min(chunk_bytes, bytes - c * chunk_bytes);
-  const int64_t n = (chunk_len + kSegBytes - 1) / kSegBytes;
-  const uint32_t* seg = seg_out + c * spc;
+// A chunk's raw CRC from its segments' values (each at its own segment end):
+// full segment k is shifted over the nfull-1-k full segments behind it
+// (segpow), the sum over the chunk's short last segment (x^(8*rem)), and that
+// segment's own value added. Called by every thread of a 1024-thread block;
+// returns the raw CRC on thread 0.
+__device__ uint32_t fold_chunk(const uint32_t* __restrict__ seg, int64_t len, uint32_t xrem,
+                               const uint32_t* __restrict__ sc) {
+  __shared__ uint32_t part[16];
+  const int64_t nfull = len / kSegBytes;
+  const bool tail = len % kSegBytes != 0;
   uint32_t r = 0;
-  for (int64_t k = threadIdx.x; k < n; k += 256) r ^= seg[k];
+  for (int64_t k = threadIdx.x; k < nfull; k += blockDim.x) r ^= multmodp_unrolled(sc[kSegPow + (nfull - 1 - k)], seg[k]);
   r = wave_xor(r);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
   __syncthreads();
-  if (threadIdx.x == 0) out[c] = part[0] ^ part[1] ^ part[2] ^ part[3] ^ init[chunk_len == chunk_bytes ? 0 : 1];
+  if (threadIdx.x != 0) return 0;
+  r = 0;
+  for (int i = 0; i < int(blockDim.x >> 6); ++i) r ^= part[i];
+  if (tail) r = multmodp(xrem, r) ^ seg[nfull];
+  return r;
+}
+
+// Per chunk: (x^(8*rem), init/xorout term) of full chunks [0..1] and of the short last chunk [2..3].
+struct FoldTail {
+  uint32_t xrem_full, init_full, xrem_last, init_last;
+};
+
+// One 1024-thread block per chunk.
+__global__ void __launch_bounds__(1024) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
+                                                           int64_t chunk_bytes, int64_t spc,
+                                                           const uint32_t* __restrict__ sc, FoldTail t,
+                                                           uint32_t* __restrict__ out) {
+  const int64_t c = blockIdx.x;
+  const int64_t chunk_len = min(chunk_bytes, bytes - c * chunk_bytes);
+  const bool full = chunk_len == chunk_bytes;
+  const uint32_t r = fold_chunk(seg_out + c * spc, chunk_len, full ? t.xrem_full : t.xrem_last, sc);
+  if (threadIdx.x == 0) out[c] = r ^ (full ? t.init_full : t.init_last);
+}
+
+FoldTail fold_tail(int64_t chunk_bytes, int64_t last_len) {
+  auto xrem = [](int64_t len) { return crc32c_xpow8n(uint64_t(len % kSegBytes)); };
+  return FoldTail{xrem(chunk_bytes), crc32c_init_term(uint64_t(chunk_bytes)), xrem(last_len),
+                  crc32c_init_term(uint64_t(last_len))};
 }
 
 // ---- batched: up to kCrcBatchMax independent buffers (the chunks one P2P
@@ -604,7 +764,7 @@ struct BatchArgs {
   int64_t seg_base[kCrcBatchMax + 1];  // prefix sums of the items' segment counts
   const uint8_t* src[kCrcBatchMax];
   int64_t bytes[kCrcBatchMax];
-  const uint32_t* shift[kCrcBatchMax];  // lane shift table of a `bytes`-byte chunk
+  uint32_t xrem[kCrcBatchMax];  // x^(8 * (bytes mod 16 KiB))
   uint32_t init[kCrcBatchMax];
   uint32_t* out[kCrcBatchMax];
 };
@@ -626,34 +786,28 @@ crc32c_batch_segments_kernel(const BatchArgs a, const uint32_t* __restrict__ sc,
     s.seg_start = k * kSegBytes;
     s.p = a.src[j] + s.seg_start;
     s.len = min(int64_t(kSegBytes), a.bytes[j] - s.seg_start);
-    s.row = a.shift[j] + k * 64;
     return s;
   };
   NoVisit v;
   slice_walk(geo, a.seg_base[a.n], sc, st, v, seg_out);
 }
 
-__global__ void __launch_bounds__(256) crc32c_batch_fold_kernel(const BatchArgs a,
-                                                                const uint32_t* __restrict__ seg_out) {
-  __shared__ uint32_t part[4];
+__global__ void __launch_bounds__(1024) crc32c_batch_fold_kernel(const BatchArgs a, const uint32_t* __restrict__ seg_out,
+                                                                 const uint32_t* __restrict__ sc) {
   const int j = blockIdx.x;
-  uint32_t r = 0;
-  for (int64_t g = a.seg_base[j] + threadIdx.x; g < a.seg_base[j + 1]; g += 256) r ^= seg_out[g];
-  r = wave_xor(r);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
-  __syncthreads();
-  if (threadIdx.x == 0) *a.out[j] = part[0] ^ part[1] ^ part[2] ^ part[3] ^ a.init[j];
+  const uint32_t r = fold_chunk(seg_out + a.seg_base[j], a.bytes[j], a.xrem[j], sc);
+  if (threadIdx.x == 0) *a.out[j] = r ^ a.init[j];
 }
 
-// Per-device constant tables and per-(chunk, last chunk) fold tables.
+// Per-device constant tables (one upload per device, before any RCCL traffic:
+// crc32c_warm at engine set-up).
 //
-// Built on first use and uploaded WITHOUT a host-synchronous copy: a
-// hipMemcpy here ran on the null stream in the middle of a session (the first
-// CRC of a rank that starts by receiving), waited for the comm lanes' RCCL
-// kernels, and hung a rank whose peers waited for it (profiles/r3_multihost/).
-// Tables go into pinned host and device arenas (bump-allocated, never reused
-// or freed) and are copied with hipMemcpyAsync on the caller's stream; an
-// event recorded behind the copy orders any later user on another stream.
+// Uploaded WITHOUT a host-synchronous copy: a hipMemcpy here ran on the null
+// stream in the middle of a session (the first CRC of a rank that starts by
+// receiving), waited for the comm lanes' RCCL kernels, and hung a rank whose
+// peers waited for it (profiles/r3_multihost/). The tables go to pinned host
+// memory and are copied with hipMemcpyAsync on the caller's stream; an event
+// recorded behind the copy orders any later user on another stream.
 struct ConstEntry {
   uint32_t* d = nullptr;
   hipEvent_t ready = nullptr;
@@ -661,36 +815,18 @@ struct ConstEntry {
 struct DeviceConsts {
   std::mutex mu;
   std::map<int, ConstEntry> by_device;
-  // (device, chunk_bytes, last_len) -> [shift: spc x 64][shift_last: spc x 64][init: 2]
-  std::map<std::tuple<int, int64_t, int64_t>, ConstEntry> fold;
-  struct Arena {
-    uint8_t* dev = nullptr;
-    uint8_t* host = nullptr;
-    size_t cap = 0, used = 0;
-  };
-  std::map<int, Arena> arena;  // per device
 };
 DeviceConsts g_consts;
 
-// Caller holds g_consts.mu. A new arena (the rare case: first use, or one
-// more after 64 MiB of tables) is the only allocation on this path.
-ConstEntry upload_consts(int dev, const std::vector<uint32_t>& h, hipStream_t s) {
-  const size_t n = (h.size() * 4 + 255) & ~size_t(255);
-  auto& a = g_consts.arena[dev];
-  if (!a.dev || a.used + n > a.cap) {
-    const size_t cap = std::max(n, size_t(64) << 20);
-    void *d = nullptr, *hp = nullptr;
-    if (hipMalloc(&d, cap) != hipSuccess) return {};
-    if (hipHostMalloc(&hp, cap, hipHostMallocDefault) != hipSuccess) return {};
-    a = DeviceConsts::Arena{static_cast<uint8_t*>(d), static_cast<uint8_t*>(hp), cap, 0};
-  }
-  uint8_t* hd = a.host + a.used;
-  uint8_t* dd = a.dev + a.used;
-  a.used += n;
-  memcpy(hd, h.data(), h.size() * 4);
+ConstEntry upload_consts(const std::vector<uint32_t>& h, hipStream_t s) {
+  void *d = nullptr, *hp = nullptr;
+  const size_t n = h.size() * 4;
+  if (hipMalloc(&d, n) != hipSuccess) return {};
+  if (hipHostMalloc(&hp, n, hipHostMallocDefault) != hipSuccess) return {};  // kept: the copy may still read it
+  memcpy(hp, h.data(), n);
   ConstEntry e;
-  e.d = reinterpret_cast<uint32_t*>(dd);
-  if (hipMemcpyAsync(dd, hd, h.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess) return {};
+  e.d = static_cast<uint32_t*>(d);
+  if (hipMemcpyAsync(d, hp, n, hipMemcpyHostToDevice, s) != hipSuccess) return {};
   if (hipEventCreateWithFlags(&e.ready, hipEventDisableTiming) != hipSuccess) return {};
   if (hipEventRecord(e.ready, s) != hipSuccess) return {};
   return e;
@@ -700,41 +836,6 @@ ConstEntry upload_consts(int dev, const std::vector<uint32_t>& h, hipStream_t s)
 uint32_t* use_on(const ConstEntry& e, hipStream_t s) {
   if (!e.d) return nullptr;
   if (hipStreamWaitEvent(s, e.ready, 0) != hipSuccess) return nullptr;
-  return e.d;
-}
-
-// Per full segment k of a `len`-byte chunk and lane l: x^(8 * (bytes from the
-// end of lane l's last piece to the chunk end)) = x^(8*64*(63 - l)) * x^(8 * (len - end of k)).
-void lane_shifts(int64_t len, int64_t spc, uint32_t* out) {
-  const int64_t nfull = len / kSegBytes;
-  std::fill(out, out + spc * 64, 0u);  // partial / absent segments: unused
-  if (nfull == 0) return;
-  uint32_t lanepow[64];
-  for (int m = 0; m < 64; ++m) lanepow[m] = crc32c_xpow8n(uint64_t(kPieceBytes) * uint64_t(m));
-  const uint32_t xs = crc32c_xpow8n(kSegBytes);
-  uint32_t seg = crc32c_xpow8n(uint64_t(len - nfull * kSegBytes));  // last full segment
-  for (int64_t k = nfull - 1; k >= 0; --k) {
-    for (int l = 0; l < 64; ++l) out[k * 64 + l] = crc32c_multmodp(lanepow[63 - l], seg);
-    seg = crc32c_multmodp(xs, seg);
-  }
-}
-
-uint32_t* fold_consts(int64_t chunk_bytes, int64_t last_len, hipStream_t s) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(g_consts.mu);
-  auto key = std::make_tuple(dev, chunk_bytes, last_len);
-  auto it = g_consts.fold.find(key);
-  if (it != g_consts.fold.end()) return use_on(it->second, s);
-  const int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
-  std::vector<uint32_t> h(size_t(2 * spc * 64 + 2));
-  lane_shifts(chunk_bytes, spc, h.data());
-  lane_shifts(last_len, spc, h.data() + spc * 64);
-  h[size_t(2 * spc * 64)] = crc32c_init_term(uint64_t(chunk_bytes));
-  h[size_t(2 * spc * 64 + 1)] = crc32c_init_term(uint64_t(last_len));
-  const ConstEntry e = upload_consts(dev, h, s);
-  if (!e.d) return nullptr;
-  g_consts.fold[key] = e;
   return e.d;
 }
 
@@ -751,7 +852,11 @@ uint32_t* device_consts(hipStream_t s) {
   for (int n = 0; n < 8; ++n)
     for (uint32_t v = 0; v < 16; ++v) h[size_t(kGap + n * 16 + int(v))] = crc32c_multmodp(xg, v << (4 * n));
   for (int m = 0; m < 1024; ++m) h[size_t(kPow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
-  const ConstEntry e = upload_consts(dev, h, s);
+  for (int l = 0; l < 64; ++l) h[size_t(kLanePow + l)] = crc32c_xpow8n(uint64_t(kPieceBytes) * uint64_t(63 - l));
+  const uint32_t xs = crc32c_xpow8n(kSegBytes);
+  h[size_t(kSegPow)] = 0x80000000u;  // x^0
+  for (int j = 1; j < kMaxSegs; ++j) h[size_t(kSegPow + j)] = crc32c_multmodp(xs, h[size_t(kSegPow + j - 1)]);
+  const ConstEntry e = upload_consts(h, s);
   if (!e.d) return nullptr;
   g_consts.by_device[dev] = e;
   return e.d;
@@ -777,25 +882,26 @@ dim3 seg_grid(int64_t total_segs, int max_blocks) {
 
 struct Plan {
   int64_t spc, nchunks, total_segs;
-  uint32_t *consts, *fold;
+  uint32_t* consts;
+  FoldTail tail;
 };
 
 hipError_t plan(int64_t bytes, int64_t chunk_bytes, Plan* p, hipStream_t s) {
   p->spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
+  if (p->spc > kMaxSegs) return hipErrorInvalidValue;  // chunks up to 1 GiB (segpow table)
   p->nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
   const int64_t last_len = bytes - (p->nchunks - 1) * chunk_bytes;
   p->total_segs = (p->nchunks - 1) * p->spc + (last_len + kSegBytes - 1) / kSegBytes;
   p->consts = device_consts(s);
-  p->fold = fold_consts(chunk_bytes, last_len, s);
-  return p->consts && p->fold ? hipSuccess : hipErrorOutOfMemory;
+  p->tail = fold_tail(chunk_bytes, last_len);
+  return p->consts ? hipSuccess : hipErrorOutOfMemory;
 }
 
 }  // namespace
 
 hipError_t crc32c_warm(int64_t chunk_bytes, hipStream_t s) {
-  if (!device_consts(s)) return hipErrorOutOfMemory;
-  if (chunk_bytes > 0 && !fold_consts(chunk_bytes, chunk_bytes, s)) return hipErrorOutOfMemory;
-  return hipSuccess;
+  if ((chunk_bytes + kSegBytes - 1) / kSegBytes > kMaxSegs) return hipErrorInvalidValue;
+  return device_consts(s) ? hipSuccess : hipErrorOutOfMemory;
 }
 
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes) {
@@ -822,11 +928,11 @@ hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_by
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p, s); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.fold, p.fold + p.spc * 64};
+  const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc};
   crc32c_segments_kernel<<<seg_grid(p.total_segs, max_blocks), dim3(kThreads), 0, s>>>(geo, p.total_segs, p.consts,
                                                                                         seg);
-  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, chunk_bytes, p.spc,
-                                                                     p.fold + 2 * p.spc * 64, out);
+  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(1024), 0, s>>>(seg, bytes, chunk_bytes, p.spc, p.consts,
+                                                                      p.tail, out);
   return hipGetLastError();
 }
 
@@ -847,13 +953,12 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
     const CrcItem& it = items[i];
     if (it.bytes <= 0) continue;
     if (reinterpret_cast<uintptr_t>(it.src) & 15) return hipErrorInvalidValue;  // any length
-    uint32_t* fold = fold_consts(it.bytes, it.bytes, s);
-    if (!fold) return hipErrorOutOfMemory;
     const int64_t spc = (it.bytes + kSegBytes - 1) / kSegBytes;
+    if (spc > kMaxSegs) return hipErrorInvalidValue;
     const int j = a.n++;
     a.src[j] = static_cast<const uint8_t*>(it.src);
     a.bytes[j] = it.bytes;
-    a.shift[j] = fold;
+    a.xrem[j] = crc32c_xpow8n(uint64_t(it.bytes % kSegBytes));
     a.init[j] = crc32c_init_term(uint64_t(it.bytes));
     a.out[j] = it.out;
     a.seg_base[j + 1] = a.seg_base[j] + spc;
@@ -861,7 +966,7 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
   if (a.n == 0) return hipSuccess;
   auto* seg = static_cast<uint32_t*>(workspace);
   crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n], max_blocks), dim3(kThreads), 0, s>>>(a, consts, seg);
-  crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(256), 0, s>>>(a, seg);
+  crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(1024), 0, s>>>(a, seg, consts);
   return hipGetLastError();
 }
 
@@ -877,22 +982,32 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   Plan p;
   if (hipError_t e = plan(bytes, pchunk, &p, s); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.fold, p.fold + p.spc * 64};
+  const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc};
   const int64_t oc = src_chunk / 2;
   const dim3 grid = seg_grid(p.total_segs, max_blocks), tpb{kThreads};
   if (store < 0) store = kFusedStoreDefault;
   // the split kernel's CRC half walks 8 segments per workgroup at a time
   const dim3 grid2(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + 7) / 8, max_blocks > 0 ? max_blocks : 256))));
+  const dim3 grid5(unsigned((p.total_segs + kWaves - 1) / kWaves));  // store 5: one segment per wave
+  const dim3 grid7(unsigned((p.total_segs + kWaves16 - 1) / kWaves16)), tpb7(kWaves16 * 64);
 #define DLD_VU(B)                                                                                           \
-  (store == 2   ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
+  (store == 9   ? (verify_unpack_once16_kernel<B, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
+   : store == 7 ? (verify_unpack_once16_kernel<B><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))  \
+   : store == 5 ? (verify_unpack_once_kernel<B><<<grid5, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))      \
+   : store == 2 ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
    : store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
                 : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
-  if (store == 3 || store == 4) {  // diagnostic: the same walk without the CRC math (CRCs are garbage)
+  if (store == 8) {  // diagnostic: store 7 without the CRC math
+    if (block != 128) return hipErrorInvalidValue;
+    verify_unpack_once16_kernel<128, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
+  } else if (store == 3 || store == 4 || store == 6) {  // diagnostic: the same walk without the CRC math (CRCs are garbage)
     if (block != 128) return hipErrorInvalidValue;
     if (store == 3)
       verify_unpack_segments_kernel<128, true, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
-    else
+    else if (store == 4)
       verify_unpack_segments_kernel<128, false, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
+    else
+      verify_unpack_once_kernel<128, false><<<grid5, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
   } else {
     switch (block) {
       case 32: DLD_VU(32); break;
@@ -904,8 +1019,8 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
     }
   }
 #undef DLD_VU
-  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(256), 0, s>>>(seg, bytes, pchunk, p.spc,
-                                                                     p.fold + 2 * p.spc * 64, crc_out);
+  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(1024), 0, s>>>(seg, bytes, pchunk, p.spc, p.consts, p.tail,
+                                                                      crc_out);
   return hipGetLastError();
 }
 

@@ -19,6 +19,17 @@
 // back to back on the verify stream (unmasked / masked with R CUs free). The
 // copy's GB/s (bytes copied per second) says whether the CU reservation leaves
 // a lane its bandwidth: 7 lanes at >= 60 GB/s each need >= 420 GB/s.
+//
+// Continuous verification at the landing rate (-paced): at N = 8 a GPU lands
+// 7 links x ~64 GB/s = ~450 GB/s, every byte CRC-checked. For 10 s a host
+// thread enqueues one batched CRC of 7 x 64 MiB chunks every 7 x 64 MiB /
+// 450 GB/s (~1 ms) on the verify stream with the grid capped at C workgroups,
+// while a 64-workgroup copy runs back to back on a comm-lane-like queue. Per
+// cap: the copy's GB/s against its alone rate, and whether the verify kept up
+// (the batches still pending at the end and the time to drain them).
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -67,13 +78,32 @@ static hipStream_t make_stream(int reserve, bool dedicated = false) {
   return s;
 }
 
+int paced(double secs, double land_gbps, const std::vector<int>& caps);
+
+// A stream on the CUs whose mask bit `pick(cu)` says (every CU's bit set or not).
+template <class Pick>
+static hipStream_t make_masked(Pick pick) {
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0u);
+  for (int cu = 0; cu < cus; ++cu)
+    if (pick(cu, cus)) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+  hipStream_t s = nullptr;
+  CHECK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  return s;
+}
+
 int main(int argc, char** argv) {
   int trials = 40, reserve = 32;
+  double paced_s = 0, land_gbps = 450;
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string a = argv[i];
     if (a == "-trials") trials = atoi(argv[i + 1]);
     else if (a == "-reserve") reserve = atoi(argv[i + 1]);
+    else if (a == "-paced") paced_s = atof(argv[i + 1]);
+    else if (a == "-gbps") land_gbps = atof(argv[i + 1]);
   }
+  if (paced_s > 0) return paced(paced_s, land_gbps, {0, 64, 32, 24, 16});
   CHECK(hipSetDevice(0));
   const int64_t chunk = 64ll << 20, nchunks = 7;
   uint8_t* buf = nullptr;
@@ -175,6 +205,176 @@ int main(int argc, char** argv) {
              wgs, r < 0 ? "false" : "true", r < 0 ? 0 : r, cap, pct(gbps, 0.5), pct(gbps, 0.1), pct(gbps, 0.0));
       if (verify) CHECK(hipStreamDestroy(verify));
     }
+  }
+  return 0;
+}
+
+// ---- continuous verification at the landing rate beside a copy (see the top)
+int paced(double secs, double land_gbps, const std::vector<int>& caps) {
+  CHECK(hipSetDevice(0));
+  const int64_t chunk = 64ll << 20, nchunks = 7;
+  uint8_t* buf = nullptr;
+  CHECK(hipMalloc(&buf, size_t(chunk * nchunks)));
+  CHECK(dissem::kern::fill_random(buf, chunk * nchunks, 42, nullptr));
+  const int kRing = 64;  // batches in flight at most (workspace + CRC slots per batch)
+  const size_t wsb = dissem::kern::crc32c_batch_workspace_bytes(chunk, int(nchunks));
+  uint8_t* ws = nullptr;
+  CHECK(hipMalloc(&ws, wsb * kRing));
+  uint32_t* crc = nullptr;
+  CHECK(hipMalloc(&crc, size_t(kRing) * nchunks * sizeof(uint32_t)));
+  const int64_t copy_bytes = 256ll << 20;
+  uint8_t *csrc = nullptr, *cdst = nullptr;
+  CHECK(hipMalloc(&csrc, size_t(copy_bytes)));
+  CHECK(hipMalloc(&cdst, size_t(copy_bytes)));
+  CHECK(hipMemset(csrc, 1, size_t(copy_bytes)));
+  hipStream_t lane = make_stream(0, true);
+  hipStream_t verify;
+  CHECK(hipStreamCreateWithFlags(&verify, hipStreamNonBlocking));
+  const double period_s = double(chunk * nchunks) / (land_gbps * 1e9);
+  auto copy_run = [&](double dur, std::vector<float>& gbps) {
+    const int n = 64;
+    std::vector<hipEvent_t> ev(size_t(n) + 1);
+    for (auto& e : ev) CHECK(hipEventCreate(&e));
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(dur);
+    while (std::chrono::steady_clock::now() < t_end) {
+      CHECK(hipEventRecord(ev[0], lane));
+      for (int k = 0; k < n; ++k) {
+        copy_kernel<<<64, 256, 0, lane>>>(reinterpret_cast<const uint4*>(csrc), reinterpret_cast<uint4*>(cdst),
+                                          copy_bytes / 16);
+        CHECK(hipEventRecord(ev[size_t(k) + 1], lane));
+      }
+      CHECK(hipStreamSynchronize(lane));
+      for (int k = 0; k < n; ++k) {
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, ev[size_t(k)], ev[size_t(k) + 1]));
+        gbps.push_back(float(double(copy_bytes) / (double(ms) * 1e-3) / 1e9));
+      }
+    }
+    for (auto& e : ev) CHECK(hipEventDestroy(e));
+  };
+  auto pct = [](std::vector<float> v, double q) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.f : v[size_t(q * double(v.size() - 1))];
+  };
+  std::vector<float> alone;
+  copy_run(std::min(secs, 3.0), alone);
+  printf("{\"case\": \"paced_copy_alone\", \"copy_workgroups\": 64, \"copy_GBps_p50\": %.1f, \"copy_GBps_p10\": %.1f}\n",
+         pct(alone, 0.5), pct(alone, 0.1));
+  fflush(stdout);
+  // warm the CRC tables
+  {
+    dissem::kern::CrcItem it[nchunks];
+    for (int64_t c = 0; c < nchunks; ++c) it[c] = dissem::kern::CrcItem{buf + c * chunk, chunk, crc + c};
+    CHECK(dissem::kern::crc32c_batch(it, int(nchunks), ws, verify, 0));
+    CHECK(hipStreamSynchronize(verify));
+  }
+  for (int cap : caps) {
+    std::atomic<bool> stop{false};
+    std::atomic<int64_t> issued{0};
+    std::vector<hipEvent_t> done(kRing);
+    for (auto& e : done) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int64_t stalls = 0;  // ring full: the verify fell a whole ring behind
+    std::thread th([&] {
+      auto next = std::chrono::steady_clock::now();
+      for (int64_t b = 0; !stop.load(); ++b) {
+        std::this_thread::sleep_until(next);
+        next += std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(period_s));
+        const int slot = int(b % kRing);
+        if (b >= kRing && hipEventQuery(done[size_t(slot)]) == hipErrorNotReady) {
+          ++stalls;
+          CHECK(hipEventSynchronize(done[size_t(slot)]));
+        }
+        dissem::kern::CrcItem it[nchunks];
+        for (int64_t c = 0; c < nchunks; ++c)
+          it[c] = dissem::kern::CrcItem{buf + c * chunk, chunk, crc + slot * nchunks + c};
+        CHECK(dissem::kern::crc32c_batch(it, int(nchunks), ws + size_t(slot) * wsb, verify, cap));
+        CHECK(hipEventRecord(done[size_t(slot)], verify));
+        issued.store(b + 1);
+      }
+    });
+    std::vector<float> beside;
+    copy_run(secs, beside);
+    stop.store(true);
+    th.join();
+    // still pending at the end, and the time the verify stream needs to drain
+    int pending = 0;
+    for (auto& e : done)
+      if (hipEventQuery(e) == hipErrorNotReady) ++pending;
+    const auto d0 = std::chrono::steady_clock::now();
+    CHECK(hipStreamSynchronize(verify));
+    const double drain_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
+    const double verified_gbps = double(issued.load()) * double(chunk * nchunks) / secs / 1e9;
+    printf("{\"case\": \"paced_copy_beside_verify\", \"land_GBps\": %.0f, \"crc_grid_cap\": %d, \"copy_workgroups\": 64, "
+           "\"copy_GBps_p50\": %.1f, \"copy_GBps_p10\": %.1f, \"copy_vs_alone\": %.3f, \"verified_GBps\": %.1f, "
+           "\"batches\": %lld, \"ring_stalls\": %lld, \"pending_at_end\": %d, \"drain_ms\": %.2f}\n",
+           land_gbps, cap, pct(beside, 0.5), pct(beside, 0.1), pct(beside, 0.5) / pct(alone, 0.5), verified_gbps,
+           (long long)issued.load(), (long long)stalls, pending, drain_ms);
+    fflush(stdout);
+    for (auto& e : done) CHECK(hipEventDestroy(e));
+  }
+  // CU partitions: the verify stream on a set of CUs (grid = that many
+  // workgroups, one per CU), the copy lane on the rest - no workgroup of one
+  // ever shares a CU with the other. Sets: the last 32 mask bits
+  // (contiguous), every 8th bit (32 CUs spread over the mask), every 4th (64).
+  struct Part {
+    const char* name;
+    int every, phase, n;  // every < 0: contiguous last n
+  };
+  const Part parts[] = {{"last32", -1, 0, 32}, {"every8th", 8, 7, 32}, {"every4th", 4, 3, 64}};
+  for (const Part& pt : parts) {
+    auto is_verify = [pt](int cu, int cus) { return pt.every < 0 ? cu >= cus - pt.n : cu % pt.every == pt.phase; };
+    hipStream_t vs = make_masked([&](int cu, int cus) { return is_verify(cu, cus); });
+    hipStream_t ls = make_masked([&](int cu, int cus) { return !is_verify(cu, cus); });
+    std::swap(verify, vs);
+    std::swap(lane, ls);
+    std::vector<float> alone_p;
+    copy_run(std::min(secs, 3.0), alone_p);
+    std::atomic<bool> stop{false};
+    std::atomic<int64_t> issued{0};
+    std::vector<hipEvent_t> done(kRing);
+    for (auto& e : done) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int64_t stalls = 0;
+    std::thread th([&] {
+      auto next = std::chrono::steady_clock::now();
+      for (int64_t b = 0; !stop.load(); ++b) {
+        std::this_thread::sleep_until(next);
+        next += std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(period_s));
+        const int slot = int(b % kRing);
+        if (b >= kRing && hipEventQuery(done[size_t(slot)]) == hipErrorNotReady) {
+          ++stalls;
+          CHECK(hipEventSynchronize(done[size_t(slot)]));
+        }
+        dissem::kern::CrcItem it[nchunks];
+        for (int64_t c = 0; c < nchunks; ++c)
+          it[c] = dissem::kern::CrcItem{buf + c * chunk, chunk, crc + slot * nchunks + c};
+        CHECK(dissem::kern::crc32c_batch(it, int(nchunks), ws + size_t(slot) * wsb, verify, pt.n));
+        CHECK(hipEventRecord(done[size_t(slot)], verify));
+        issued.store(b + 1);
+      }
+    });
+    std::vector<float> beside;
+    copy_run(secs, beside);
+    stop.store(true);
+    th.join();
+    int pending = 0;
+    for (auto& e : done)
+      if (hipEventQuery(e) == hipErrorNotReady) ++pending;
+    const auto d0 = std::chrono::steady_clock::now();
+    CHECK(hipStreamSynchronize(verify));
+    const double drain_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
+    printf("{\"case\": \"paced_partitioned\", \"land_GBps\": %.0f, \"verify_cus\": \"%s\", \"crc_grid_cap\": %d, "
+           "\"copy_GBps_alone_p50\": %.1f, \"copy_GBps_p50\": %.1f, \"copy_GBps_p10\": %.1f, \"copy_vs_alone\": %.3f, "
+           "\"copy_vs_all_cu_alone\": %.3f, \"verified_GBps\": %.1f, \"ring_stalls\": %lld, \"pending_at_end\": %d, "
+           "\"drain_ms\": %.2f}\n",
+           land_gbps, pt.name, pt.n, pct(alone_p, 0.5), pct(beside, 0.5), pct(beside, 0.1),
+           pct(beside, 0.5) / pct(alone_p, 0.5), pct(beside, 0.5) / pct(alone, 0.5),
+           double(issued.load()) * double(chunk * nchunks) / secs / 1e9, (long long)stalls, pending, drain_ms);
+    fflush(stdout);
+    for (auto& e : done) CHECK(hipEventDestroy(e));
+    std::swap(verify, vs);
+    std::swap(lane, ls);
+    CHECK(hipStreamDestroy(vs));
+    CHECK(hipStreamDestroy(ls));
   }
   return 0;
 }

@@ -14,6 +14,8 @@
 #   init       parallel vs split lane-communicator set-up at 8 shared ranks; rank-death re-form
 #   r3rehearse host-share (config #2), disk tier + node NVMe budget (config #4) at 8 shared ranks; N = 1 A/Bs
 #   r3kernels  fused verify+unpack store A/B + counters, copy bandwidth beside CRC, NUMA A/B
+#   r4kernels  walk access patterns, kernel numerics, fused store A/B (walk vs one segment per wave) + counters
+#   r4contention  continuous CRC verification at 450 GB/s beside a 64-workgroup copy, per CRC grid cap
 #   multihost  8 shared ranks rehearsed as 2 hosts x 4 GPUs: host-aware lanes, hierarchical vs flat modes 1/0, modes 2/3
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
 #   queues     per-rank rocprofv3 kernel traces of a shared-GPU bench (HW queue ids; QRANKS=8 for 8 ranks)
@@ -143,6 +145,35 @@ case "$RECIPE" in
     DISSEM_SHARED_GPU=1 timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 --layer-mib 128 \
       --chunk-mib 16 --mode 0 --seeding leader --host-share --probe-mib 16 > $OUT/b8_m0_hostshare.json \
       2> $OUT/b8_m0_hostshare.log
+    ;;
+  r4kernels)
+    # round 4: walk access patterns (bin/walkprobe), CRC/fused numerics with the new fold constants,
+    # fused store A/B (persistent walk vs one segment per wave) at 512 MiB and 4 GiB, counters of both
+    timeout -k 10 120 bin/walkprobe 512 20 > $OUT/walk512.jsonl 2>&1 &&
+    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py > $OUT/pytest_kernels.log 2>&1 &&
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log &&
+    timeout -k 10 200 python scripts/fused_ab.py --src-mib 4096 --reps 5 --store 1 5 7 9 > $OUT/fused_ab_4g.json \
+      2> $OUT/fused_ab_4g.log || exit 1
+    for st in ${PMC_STORES:-1 7}; do
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VALU --output-format csv -d $OUT/pmc_sq_$st -o sq -- \
+        python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_sq_$st.log 2>&1 || exit 1
+      timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE TA_BUSY_avr TD_BUSY_avr --output-format csv -d $OUT/pmc_mem_$st \
+        -o mem -- python3 scripts/fused_ab.py --store $st --reps 5 > $OUT/pmc_mem_$st.log 2>&1 || exit 1
+    done
+    ;;
+  r4contention)
+    # continuous verification at the landing rate of 7 links (450 GB/s) beside a 64-workgroup copy, per CRC grid cap
+    timeout -k 10 300 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1
+    ;;
+  r4sweep)
+    # fused store 7/8/9 against the source size (tail of the one-segment-per-wave grid), then the
+    # paced contention run with CU-partitioned verify
+    for mib in 448 480 496 504 512 520 528 544 576; do
+      timeout -k 10 60 python scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 9 > $OUT/sweep_$mib.json \
+        2> $OUT/sweep_$mib.log || exit 1
+    done
+    timeout -k 10 400 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1
     ;;
   r3mx)
     # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters

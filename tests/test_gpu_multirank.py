@@ -87,6 +87,12 @@ def test_bench_modes(n, mode, extra, request):
     assert out["n_gpus"] == n and out["value"] > 0
     st = out["config"]["engine_stats_rank0"]
     assert st["verify_failures"] == 0 and st["unverified_pieces"] == 0
+    if _ngpus() >= n and not any(a.startswith("slow-link") for a in extra):
+        # real GPUs: RCCL's P2P over xGMI on every directed link, not a fallback (tests/benchcheck.py)
+        from distributed_llm_dissemination_amd import _core
+        from benchcheck import real_multi_gpu_problems
+
+        assert real_multi_gpu_problems(out, n, _core.resolve_lanes(n, 0)) == [], out["config"]
 
 
 @pytest.mark.parametrize("mode,extra", [(1, []), (0, ["--seeding", "leader"])])
