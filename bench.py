@@ -71,10 +71,14 @@ def parse_args(argv=None):
                    help="--tier disk: the node's one NVMe read rate shared by every rank's disk readers and planned "
                         "as one budget by mode 3 (default 13.3, profiles/r1_diskspeed.log; 0 = per-rank, unpaced)")
     p.add_argument("--reserve-cus", type=int, default=-1,
-                   help="CUs the verify/copy kernels leave free for RCCL (-1: 32 when N > 1)")
+                   help="CUs the verify/copy kernels leave free for RCCL when --verify-cus is 0 (-1: 32 when N > 1)")
+    p.add_argument("--verify-cus", type=int, default=-1,
+                   help="the verify stream runs on the last N CUs only, RCCL lanes and copies on the others (-1: 32, "
+                        "one XCD's worth, when N > 1 - 128 with --store bf16 - and 0 alone; 0: all shared). "
+                        "bin/contention: a 64-workgroup copy keeps 99.6 %% of its rate beside 450 GB/s of verify "
+                        "on the last 32 CUs (profiles/r4_contention)")
     p.add_argument("--crc-grid", type=int, default=-1,
-                   help="workgroup cap of the CRC verify kernels (-1: 32 when N > 1 - a narrow verify that keeps up "
-                        "with 7 links of landings without taking the chip's HBM bandwidth from RCCL; 0: every CU)")
+                   help="workgroup cap of the CRC verify kernels (-1/0: every CU of the verify stream)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
     p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
     p.add_argument("--lanes", type=int, default=0,
@@ -455,6 +459,9 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["comm_init_ms_per_lane"] = [round(x, 1) for x in es.lane_init_ms]
             out["config"]["comm_connect_ms_per_lane"] = [round(x, 1) for x in es.lane_connect_ms]
             out["config"]["comm_init"] = args.comm_init
+            # the verify stream's CUs (the last ones of the mask; RCCL and copies on the rest)
+            out["config"]["verify_cus"] = (args.verify_cus if args.verify_cus >= 0
+                                           else 128 if args.store == "bf16" else 32)
             if hosts:
                 out["config"]["hosts"] = len(set(hosts.values()))
         if world > 1:

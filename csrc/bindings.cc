@@ -262,6 +262,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s)
       .def_readwrite("reserve_cus", &PlannedConfig::reserve_cus)
       .def_readwrite("crc_grid", &PlannedConfig::crc_grid)
+      .def_readwrite("verify_cus", &PlannedConfig::verify_cus)
       .def_readwrite("suspect_s", &PlannedConfig::suspect_s)
       .def_readwrite("inject_die_after_groups", &PlannedConfig::inject_die_after_groups)
       .def_readwrite("nccl_min_ctas", &PlannedConfig::nccl_min_ctas)

@@ -111,7 +111,11 @@ struct PlannedConfig {
   // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
   // -1: 32 when world > 1 (one XCD's worth), 0 on one rank (no RCCL traffic).
   int reserve_cus = -1;
-  int crc_grid = -1;  // verify kernels' workgroup cap (-1: kVerifyGridPeers with peers, all CUs alone; 0: all)
+  int crc_grid = -1;  // verify kernels' workgroup cap (-1: the verify stream's CUs; 0: all)
+  // CUs of the verify stream, the last ones of the mask; RCCL and copies get the
+  // rest (HipBackendConfig::verify_cus). -1: 32 (one XCD's worth) with peers,
+  // 128 when every landing is also unpacked (unpack_store), 0 (all CUs shared) alone.
+  int verify_cus = -1;
   // RCCL communicator CTA (workgroup/channel) bounds via ncclCommInitRankConfig;
   // 0 keeps RCCL's own choice. More CTAs = more channels per P2P peer.
   int nccl_min_ctas = 0;

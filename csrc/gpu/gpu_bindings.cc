@@ -444,11 +444,10 @@ void register_gpu_bindings(PyObject* module) {
     hc.nccl_uid = std::string(uid);
     hc.max_crc_bytes = cfg.chunk_bytes;
     hc.reserve_cus = cfg.reserve_cus >= 0 ? cfg.reserve_cus : (cfg.world > 1 ? 32 : 0);
-    // with peers, the verify kernels run narrow (bin/contention -paced: the
-    // landing rate of 7 links needs ~20 workgroups of CRC; a 64-workgroup
-    // RCCL-like copy keeps its rate beside a 32-workgroup verify)
-    constexpr int kVerifyGridPeers = 32;
-    hc.crc_grid = cfg.crc_grid >= 0 ? cfg.crc_grid : (cfg.world > 1 ? kVerifyGridPeers : 0);
+    // with peers the verify owns the last 32 CUs (128 with the fused unpack) and
+    // RCCL the rest (hip_backend.h verify_cus)
+    hc.verify_cus = cfg.verify_cus >= 0 ? cfg.verify_cus : (cfg.world > 1 ? (cfg.unpack_store ? 128 : 32) : 0);
+    hc.crc_grid = std::max(0, cfg.crc_grid);
     hc.nccl_min_ctas = cfg.nccl_min_ctas;
     hc.nccl_max_ctas = cfg.nccl_max_ctas;
     hc.nccl_register = cfg.nccl_register;

@@ -41,32 +41,35 @@ class HipBackend : public Backend {
     // back the other lane's kernel that peer may itself be waiting for. A
     // CU-masked stream gets a dedicated queue, so extra lanes are created with
     // a mask of every CU (profiles/: Queue_Id per lane).
+    const int part = std::max(0, cfg_.verify_cus);  // CUs kept for the verify stream alone
     for (int l = 0; l < lanes; ++l) {
       hipStream_t s = nullptr;
-      if (lanes > 1) {
-        s = create_stream_reserving(cfg_.device, 0, /*dedicated=*/true);
+      if (lanes > 1 || part > 0) {
+        s = create_stream_reserving(cfg_.device, part, /*dedicated=*/true);
       } else {
         HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
       }
       comm_.push_back(s);
     }
     nccl_.assign(size_t(lanes), nullptr);
-    copy_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
+    const int keep_free = part > 0 ? part : cfg_.reserve_cus;  // CUs the copy streams stay off
+    copy_ = create_stream_reserving(cfg_.device, keep_free);
     // Two SDMA copy queues in alternation keep the PCIe link busier across copy
     // boundaries (h2dbench: 56.8 -> 57.4 GB/s; bench 56.0 -> 56.9 GB/s). With
     // RCCL in the process only when the copy queues are CU-masked: a masked
     // stream gets a hardware queue of its own, so no copy can end up queued
     // behind a comm-stream kernel that waits for a peer.
-    if ((cfg_.world == 1 && !cfg_.self_comm) || cfg_.reserve_cus > 0)
-      copy2_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
-    verify_ = create_stream_reserving(cfg_.device, cfg_.reserve_cus);
+    if ((cfg_.world == 1 && !cfg_.self_comm) || keep_free > 0)
+      copy2_ = create_stream_reserving(cfg_.device, keep_free);
+    verify_ = part > 0 ? create_stream_on_last(cfg_.device, part) : create_stream_reserving(cfg_.device, cfg_.reserve_cus);
     // The CRC kernels run one workgroup per CU (144 KiB of LDS tables each): on
     // the masked verify stream a 256-workgroup grid would leave the last
     // reserve_cus workgroups for a second wave, so cap it at the stream's CUs.
     {
       int cus = 0;
       HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-      crc_grid_ = cfg_.reserve_cus > 0 && cfg_.reserve_cus < cus ? cus - cfg_.reserve_cus : 0;
+      crc_grid_ = part > 0 ? std::min(part, cus)
+                  : cfg_.reserve_cus > 0 && cfg_.reserve_cus < cus ? cus - cfg_.reserve_cus : 0;
       if (cfg_.crc_grid > 0) crc_grid_ = crc_grid_ > 0 ? std::min(crc_grid_, cfg_.crc_grid) : cfg_.crc_grid;
     }
     HIP_OK(hipMalloc(&ws_, std::max(kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes),
@@ -546,6 +549,18 @@ hipStream_t create_stream_reserving(int device, int reserve, bool dedicated) {
   }
   std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0u);
   for (int cu = 0; cu < cus - reserve; ++cu) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+  HIP_OK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  return s;
+}
+
+hipStream_t create_stream_on_last(int device, int n) {
+  HIP_OK(hipSetDevice(device));
+  int cus = 0;
+  HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  n = std::max(1, std::min(n, cus));
+  std::vector<uint32_t> mask(size_t((cus + 31) / 32), 0u);
+  for (int cu = cus - n; cu < cus; ++cu) mask[size_t(cu / 32)] |= 1u << (cu % 32);
+  hipStream_t s = nullptr;
   HIP_OK(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
   return s;
 }

@@ -39,6 +39,16 @@ struct HipBackendConfig {
   // chip's HBM bandwidth from the comm lanes' RCCL kernels at once
   // (bin/contention -paced, profiles/r4_contention/).
   int crc_grid = 0;
+  // > 0: the verify stream runs on the LAST verify_cus CU-mask bits only and
+  // every comm lane and copy stream on the others, so no CRC workgroup shares a
+  // CU - or, at 32, an XCD and its L2 - with an RCCL kernel. bin/contention
+  // -paced (profiles/r4_contention/paced_partitioned.jsonl): a 64-workgroup
+  // copy keeps 99.6 % of its alone rate beside 450 GB/s of continuous
+  // verification on the last 32 CUs, against 93.8 % beside an unmasked
+  // full-grid verify and 85.6 % beside a 32-workgroup one; the same 32 CUs
+  // taken as every 8th bit (spread over the XCDs) keep only 86 %. Overrides
+  // reserve_cus; the CRC grid is capped at verify_cus.
+  int verify_cus = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
   int lanes = 1;                               // comm lanes (communicator + stream each)
   int hosts = 1;                               // multi-node: hosts of world / hosts ranks (backend.h host_lanes)
@@ -51,6 +61,8 @@ struct HipBackendConfig {
 // (reserve <= 0: a plain non-blocking stream, or with `dedicated` a stream
 // masked to every CU, which gets a hardware queue of its own).
 hipStream_t create_stream_reserving(int device, int reserve, bool dedicated = false);
+// A stream whose kernels run on the last `cus` CU-mask bits only.
+hipStream_t create_stream_on_last(int device, int cus);
 
 std::unique_ptr<Backend> make_hip_backend(const HipBackendConfig& cfg);
 std::shared_ptr<HostBuffer> alloc_pinned(int64_t size);

@@ -13,11 +13,11 @@
 //  * each lane's CRC is shifted to the END OF ITS SEGMENT with one GF(2)
 //    multiply by a per-lane constant (x^(8*64*(63-lane))), then the lanes are
 //    XOR-reduced with cross-lane shuffles: a segment's value is its raw CRC;
-//  * a second, small kernel (one workgroup per chunk) shifts every full
-//    segment to the chunk end - x^(8*16 KiB*j) from one table indexed by the
-//    segments that follow it, then x^(8*rem) for a chunk whose last segment is
-//    short - XORs them with that last segment and adds the init/xorout term,
-//    writing the standard CRC32C.
+//  * the wave then shifts that value to the END OF ITS CHUNK - x^(8*16 KiB*j)
+//    from one table indexed by the segments that follow it, then x^(8*rem)
+//    for a chunk whose last segment is short (wave-uniform products);
+//  * a second, small kernel (one workgroup per chunk) XORs a chunk's segment
+//    values and adds the init/xorout term, writing the standard CRC32C.
 // The constants depend on nothing but the segment geometry (chunks up to
 // 1 GiB): one upload per device, never a per-length table (a length-keyed
 // table grew with every new piece size and re-allocated mid-session).
@@ -241,7 +241,24 @@ struct Seg {
   const uint8_t* p;     // first byte
   int64_t len;          // bytes (16 KiB except a chunk's last)
   int64_t chunk, chunk_start, chunk_len, seg_start;
+  uint32_t xrem;        // x^(8 * (chunk_len mod 16 KiB))
 };
+
+// A segment's raw CRC (at its own end) shifted to its chunk's end: what the
+// segment adds to the chunk's raw CRC, so the fold is a plain XOR over the
+// chunk's segments. Full segment k of a chunk with nfull full ones and a short
+// tail of rem bytes moves over (nfull - 1 - k) segments (segpow) and rem bytes
+// (xrem, skipped when rem = 0); the short tail segment already ends there.
+// Every operand is wave-uniform: one or two 32-step products per segment, off
+// the loads' critical path (the separate shift-and-fold launch took 7.4 us
+// per 512 MiB, profiles/r4_kernels).
+__device__ __forceinline__ uint32_t to_chunk_end(const Seg& sg, uint32_t s, const uint32_t* __restrict__ sc) {
+  if (sg.len != kSegBytes) return s;
+  const int64_t nfull = sg.chunk_len / kSegBytes, k = sg.seg_start / kSegBytes;
+  uint32_t m = sc[kSegPow + (nfull - 1 - k)];
+  if (sg.chunk_len % kSegBytes) m = multmodp_unrolled(m, sg.xrem);
+  return multmodp_unrolled(m, s);
+}
 
 // Visit hooks: begin(seg) at a segment's start; operator()(w, e) per word of a
 // partial segment; word(w, e, i) per word i (0-15, load order) of a full one;
@@ -323,7 +340,7 @@ __device__ __forceinline__ uint32_t seg_full(u32x4_t (&w)[4 * kBlocksPerSeg], co
 }
 
 // Every wave walks segments g = wave, wave + nwaves, ... (geo(g) -> Seg) and
-// writes seg_out[g]: the segment's raw CRC (shifted to its own end). A wave
+// writes seg_out[g]: the segment's raw CRC shifted to its chunk's end. A wave
 // that owns several segments loads block b of the next one as soon as block b
 // of the current one is consumed (pinned with sched_barrier: left alone, the
 // compiler sinks those loads behind the math), so 16 KiB stay in flight per
@@ -395,7 +412,7 @@ __device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, c
     } else {
       s = slice_partial(cur, sc, st, lane, visit);
     }
-    if (lane == 0) seg_out[g] = s;
+    if (lane == 0) seg_out[g] = to_chunk_end(cur, s, sc);
     if (cur.len != kSegBytes) {  // (rare) w did not take the next segment's words yet
       visit.prefetch(nxt, nfull);
       __builtin_amdgcn_sched_barrier(0);
@@ -447,13 +464,98 @@ __device__ __forceinline__ void slice_once(const Geo& geo, int64_t total_segs, c
   uint32_t s;
   if (full) s = seg_full<Visit, CRC>(w, cur, st, visit, sc + kLanePow, lo, [](int) {});
   else s = slice_partial(cur, sc, st, lane, visit);
-  if (lane == 0) seg_out[g] = s;
+  if (lane == 0) seg_out[g] = to_chunk_end(cur, s, sc);
+}
+
+// Half a segment per wave, for the grid's last, partial round (see
+// once_split): waves 2 m and 2 m + 1 of the workgroup take blocks 0-1 and 2-3
+// of its segment m. Each half is a chain over its lanes' two pieces, shifted to
+// the half's end like a segment (the per-lane constants are the same: a
+// lane's last piece sits 64 * (63 - lane) bytes before its block's end); the
+// first half moves over the second (x^(8 * 8 KiB) = pow16[512]) and the second
+// hands its value over through LDS. A short segment is done whole by the
+// first wave of the pair.
+// (H is a template parameter so that every word index, and with it the scale
+// register a word reads, is a compile-time constant: with a run-time half the
+// scale array was indexed dynamically and moved to LDS, 36 KiB per workgroup.)
+template <int H, class Visit>
+__device__ __forceinline__ void half_load(const Seg& cur, bool full, Visit& visit, u32x4_t (&w)[8]) {
+  const int lane = threadIdx.x & 63;
+  const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
+  const auto r = seg_rsrc(cur.p, full);
+  visit.prefetch(cur, full);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    w[i] = seg_load(r, lo, 8 * H + i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  visit.advance();
+}
+
+template <int H, class Visit, bool CRC, int R>
+__device__ __forceinline__ uint32_t half_seg(const Seg& cur, bool have, bool full, const uint32_t* __restrict__ sc,
+                                             const uint8_t* lds, Visit& visit, u32x4_t (&w)[8]) {
+  const int lane = threadIdx.x & 63;
+  const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
+  const Slice4T<R> st(lds);
+  uint32_t v = 0;
+  if (have) {
+    visit.begin(cur);
+    if (full) {
+      uint32_t s = 0;
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        const int b = 2 * H + bb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) visit.word(w[4 * bb + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo, 4 * b + j);
+        if constexpr (CRC) {
+          row_transpose(w[4 * bb], w[4 * bb + 1], w[4 * bb + 2], w[4 * bb + 3]);
+          s = bb ? st.gap(s, w[4 * bb][0]) : w[4 * bb][0];
+#pragma unroll
+          for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * bb + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
+        }
+      }
+      if constexpr (CRC) {
+        s = wave_xor_dpp(multmodp_unrolled(sc[kLanePow + lane], s));
+        if constexpr (H == 0) s = multmodp_unrolled(sc[kPow + (kSegBytes / 2) / 16], s);
+      }
+      v = s;
+    } else if constexpr (H == 0) {
+      v = slice_partial(cur, sc, st, lane, visit);
+    }
+  }
+  return v;
+}
+
+// The second half's value goes through LDS word xch[stride * pair]: the
+// second wave's own staging slot when there is one (two 80 KiB workgroups
+// fill the CU's 160 KiB: not one more word to spare).
+template <class Geo, class Visit, bool CRC = true, int R = 32, int WAVES = kWaves>
+__device__ __forceinline__ void slice_half(const Geo& geo, int64_t total_segs, int64_t g0,
+                                           const uint32_t* __restrict__ sc, uint8_t* lds, Visit& visit,
+                                           uint32_t* __restrict__ seg_out, uint32_t* xch, int stride) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = wave & 1;
+  const int64_t g = g0 + (wave >> 1);
+  const bool have = g < total_segs;
+  const Seg cur = have ? geo(g) : geo(0);
+  const bool full = have && cur.len == kSegBytes;
+  u32x4_t w[8];
+  if (h) half_load<1>(cur, full, visit, w);
+  else half_load<0>(cur, full, visit, w);
+  load_lds<R>(lds, sc);  // every wave joins the fill and its barrier
+  const uint32_t v = h ? half_seg<1, Visit, CRC, R>(cur, have, full, sc, lds, visit, w)
+                       : half_seg<0, Visit, CRC, R>(cur, have, full, sc, lds, visit, w);
+  if (h == 1 && lane == 0) xch[stride * (wave >> 1)] = v;
+  __syncthreads();
+  if (h == 0 && have && lane == 0) seg_out[g] = to_chunk_end(cur, v ^ xch[stride * (wave >> 1)], sc);
 }
 
 // `bytes` cut into chunks of `chunk_bytes`.
 struct ChunkGeo {
   const uint8_t* src;
   int64_t bytes, chunk_bytes, spc;
+  uint32_t xrem_full, xrem_last;  // x^(8 * (len mod 16 KiB)) of a full chunk / the last chunk
   __device__ Seg operator()(int64_t g) const {
     const int64_t c = g / spc, k = g - c * spc;
     Seg s;
@@ -463,6 +565,7 @@ struct ChunkGeo {
     s.seg_start = k * kSegBytes;
     s.p = src + s.chunk_start + s.seg_start;
     s.len = min(int64_t(kSegBytes), s.chunk_len - s.seg_start);
+    s.xrem = s.chunk_len == chunk_bytes ? xrem_full : xrem_last;
     return s;
   }
 };
@@ -630,14 +733,26 @@ verify_unpack_once_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_ch
 constexpr int kWaves16 = 8;
 template <int BLOCK, bool CRC = true, bool STAGE = true>
 __global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
-verify_unpack_once16_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
+verify_unpack_once16_kernel(const ChunkGeo geo, int64_t total_segs, int64_t split_block, int64_t out_chunk_elems,
                             const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
                             uint16_t* __restrict__ out) {
   __shared__ uint4 lds_raw[(LdsLayout<16>::kBytes + (STAGE ? kWaves16 * 1024 : 0)) / 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
   UnpackVisit<BLOCK, STAGE> v{out_chunk_elems, out, geo.src};
   v.slot = lds + LdsLayout<16>::kBytes + (threadIdx.x >> 6) * 1024;
-  slice_once<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(geo, total_segs, sc, lds, v, seg_out);
+  if (int64_t(blockIdx.x) < split_block) {
+    slice_once<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(geo, total_segs, sc, lds, v, seg_out);
+  } else {
+    const int64_t g0 = split_block * kWaves16 + (int64_t(blockIdx.x) - split_block) * (kWaves16 / 2);
+    if constexpr (STAGE) {  // pair m hands over in word 0 of wave 2 m + 1's slot
+      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(
+          geo, total_segs, g0, sc, lds, v, seg_out, reinterpret_cast<uint32_t*>(lds + LdsLayout<16>::kBytes + 1024), 512);
+    } else {
+      __shared__ uint32_t xch[kWaves16 / 2];
+      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(geo, total_segs, g0, sc, lds, v, seg_out, xch,
+                                                                         1);
+    }
+  }
 }
 
 // CRC only, one segment per wave.
@@ -712,25 +827,21 @@ verify_unpack_split_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_c
   }
 }
 
-// A chunk's raw CRC from its segments' values (each at its own segment end):
-// full segment k is shifted over the nfull-1-k full segments behind it
-// (segpow), the sum over the chunk's short last segment (x^(8*rem)), and that
-// segment's own value added. Called by every thread of a 1024-thread block;
-// returns the raw CRC on thread 0.
-__device__ uint32_t fold_chunk(const uint32_t* __restrict__ seg, int64_t len, uint32_t xrem,
-                               const uint32_t* __restrict__ sc) {
-  __shared__ uint32_t part[16];
-  const int64_t nfull = len / kSegBytes;
-  const bool tail = len % kSegBytes != 0;
+// A chunk's raw CRC: the XOR of its segments' values (each already shifted
+// to the chunk end). Called by every thread of a kFoldThreads block; returns
+// the raw CRC on thread 0.
+constexpr int kFoldThreads = 256;
+__device__ uint32_t xor_chunk(const uint32_t* __restrict__ seg, int64_t nseg) {
+  __shared__ uint32_t part[kFoldThreads / 64];
   uint32_t r = 0;
-  for (int64_t k = threadIdx.x; k < nfull; k += blockDim.x) r ^= multmodp_unrolled(sc[kSegPow + (nfull - 1 - k)], seg[k]);
-  r = wave_xor(r);
+  for (int64_t k = threadIdx.x; k < nseg; k += kFoldThreads) r ^= seg[k];
+  r = wave_xor_dpp(r);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
   __syncthreads();
   if (threadIdx.x != 0) return 0;
   r = 0;
-  for (int i = 0; i < int(blockDim.x >> 6); ++i) r ^= part[i];
-  if (tail) r = multmodp(xrem, r) ^ seg[nfull];
+#pragma unroll
+  for (int i = 0; i < kFoldThreads / 64; ++i) r ^= part[i];
   return r;
 }
 
@@ -739,15 +850,14 @@ struct FoldTail {
   uint32_t xrem_full, init_full, xrem_last, init_last;
 };
 
-// One 1024-thread block per chunk.
-__global__ void __launch_bounds__(1024) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
-                                                           int64_t chunk_bytes, int64_t spc,
-                                                           const uint32_t* __restrict__ sc, FoldTail t,
-                                                           uint32_t* __restrict__ out) {
+// One block per chunk.
+__global__ void __launch_bounds__(kFoldThreads) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
+                                                                   int64_t chunk_bytes, int64_t spc, FoldTail t,
+                                                                   uint32_t* __restrict__ out) {
   const int64_t c = blockIdx.x;
   const int64_t chunk_len = min(chunk_bytes, bytes - c * chunk_bytes);
   const bool full = chunk_len == chunk_bytes;
-  const uint32_t r = fold_chunk(seg_out + c * spc, chunk_len, full ? t.xrem_full : t.xrem_last, sc);
+  const uint32_t r = xor_chunk(seg_out + c * spc, (chunk_len + kSegBytes - 1) / kSegBytes);
   if (threadIdx.x == 0) out[c] = r ^ (full ? t.init_full : t.init_last);
 }
 
@@ -786,16 +896,17 @@ crc32c_batch_segments_kernel(const BatchArgs a, const uint32_t* __restrict__ sc,
     s.seg_start = k * kSegBytes;
     s.p = a.src[j] + s.seg_start;
     s.len = min(int64_t(kSegBytes), a.bytes[j] - s.seg_start);
+    s.xrem = a.xrem[j];
     return s;
   };
   NoVisit v;
   slice_walk(geo, a.seg_base[a.n], sc, st, v, seg_out);
 }
 
-__global__ void __launch_bounds__(1024) crc32c_batch_fold_kernel(const BatchArgs a, const uint32_t* __restrict__ seg_out,
-                                                                 const uint32_t* __restrict__ sc) {
+__global__ void __launch_bounds__(kFoldThreads) crc32c_batch_fold_kernel(const BatchArgs a,
+                                                                         const uint32_t* __restrict__ seg_out) {
   const int j = blockIdx.x;
-  const uint32_t r = fold_chunk(seg_out + a.seg_base[j], a.bytes[j], a.xrem[j], sc);
+  const uint32_t r = xor_chunk(seg_out + a.seg_base[j], a.seg_base[j + 1] - a.seg_base[j]);
   if (threadIdx.x == 0) *a.out[j] = r ^ a.init[j];
 }
 
@@ -880,6 +991,45 @@ dim3 seg_grid(int64_t total_segs, int max_blocks) {
   return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>(blocks, cap))));
 }
 
+// Resident once16 workgroups on the device (per CU x CUs), cached per device.
+int once16_slots() {
+  static std::mutex mu;
+  static std::map<int, int> by_device;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  if (auto it = by_device.find(dev); it != by_device.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, verify_unpack_once16_kernel<128>, kWaves16 * 64, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 512;
+  return by_device[dev] = std::max(1, per_cu) * std::max(1, cus);
+}
+
+// Grid of the one-segment-per-wave kernel with its last, partial round of
+// workgroups done in half segments (slice_half). Every workgroup lasts about
+// as long, so with W workgroups on S slots the kernel takes ceil(W / S)
+// rounds even when the last holds only a few: 16896 segments (512 MiB of bf16
+// packed) are 2112 workgroups on 512 slots, 4.125 rounds. Cutting the last
+// round's segments in halves gives twice the workgroups at half the length,
+// so a last round up to half full ends in half the time. W <= S / 2: every
+// segment in halves (twice the parallelism); otherwise no split.
+struct OnceGrid {
+  int64_t split_block;  // workgroups [0, split_block) take whole segments
+  unsigned blocks;
+};
+OnceGrid once_split(int64_t total_segs, bool split) {
+  const int64_t W = (total_segs + kWaves16 - 1) / kWaves16, S = once16_slots();
+  int64_t full = W;
+  if (split) {
+    if (W <= S) full = 2 * W <= S ? 0 : W;
+    else if (const int64_t tail = W % S; tail && 2 * tail <= S) full = W - tail;
+  }
+  const int64_t half_segs = std::max<int64_t>(0, total_segs - full * kWaves16);
+  return OnceGrid{full, unsigned(full + (half_segs + kWaves16 / 2 - 1) / (kWaves16 / 2))};
+}
+
 struct Plan {
   int64_t spc, nchunks, total_segs;
   uint32_t* consts;
@@ -928,11 +1078,11 @@ hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_by
   Plan p;
   if (hipError_t e = plan(bytes, chunk_bytes, &p, s); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc};
+  const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.tail.xrem_full, p.tail.xrem_last};
   crc32c_segments_kernel<<<seg_grid(p.total_segs, max_blocks), dim3(kThreads), 0, s>>>(geo, p.total_segs, p.consts,
                                                                                         seg);
-  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(1024), 0, s>>>(seg, bytes, chunk_bytes, p.spc, p.consts,
-                                                                      p.tail, out);
+  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(kFoldThreads), 0, s>>>(seg, bytes, chunk_bytes, p.spc, p.tail,
+                                                                              out);
   return hipGetLastError();
 }
 
@@ -966,7 +1116,7 @@ hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_
   if (a.n == 0) return hipSuccess;
   auto* seg = static_cast<uint32_t*>(workspace);
   crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n], max_blocks), dim3(kThreads), 0, s>>>(a, consts, seg);
-  crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(1024), 0, s>>>(a, seg, consts);
+  crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(kFoldThreads), 0, s>>>(a, seg);
   return hipGetLastError();
 }
 
@@ -982,24 +1132,26 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   Plan p;
   if (hipError_t e = plan(bytes, pchunk, &p, s); e != hipSuccess) return e;
   auto* seg = static_cast<uint32_t*>(workspace);
-  const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc};
+  const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.tail.xrem_full, p.tail.xrem_last};
   const int64_t oc = src_chunk / 2;
   const dim3 grid = seg_grid(p.total_segs, max_blocks), tpb{kThreads};
   if (store < 0) store = kFusedStoreDefault;
   // the split kernel's CRC half walks 8 segments per workgroup at a time
   const dim3 grid2(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + 7) / 8, max_blocks > 0 ? max_blocks : 256))));
   const dim3 grid5(unsigned((p.total_segs + kWaves - 1) / kWaves));  // store 5: one segment per wave
-  const dim3 grid7(unsigned((p.total_segs + kWaves16 - 1) / kWaves16)), tpb7(kWaves16 * 64);
+  const OnceGrid og = once_split(p.total_segs, store != 10);
+  const dim3 grid7(og.blocks), tpb7(kWaves16 * 64);
+  const int64_t sb = og.split_block;
 #define DLD_VU(B)                                                                                           \
-  (store == 9   ? (verify_unpack_once16_kernel<B, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
-   : store == 7 ? (verify_unpack_once16_kernel<B><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))  \
+  (store == 9   ? (verify_unpack_once16_kernel<B, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
+   : store == 7 || store == 10 ? (verify_unpack_once16_kernel<B><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out))  \
    : store == 5 ? (verify_unpack_once_kernel<B><<<grid5, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))      \
    : store == 2 ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
    : store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
                 : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
   if (store == 8) {  // diagnostic: store 7 without the CRC math
     if (block != 128) return hipErrorInvalidValue;
-    verify_unpack_once16_kernel<128, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
+    verify_unpack_once16_kernel<128, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out);
   } else if (store == 3 || store == 4 || store == 6) {  // diagnostic: the same walk without the CRC math (CRCs are garbage)
     if (block != 128) return hipErrorInvalidValue;
     if (store == 3)
@@ -1019,8 +1171,8 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
     }
   }
 #undef DLD_VU
-  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(1024), 0, s>>>(seg, bytes, pchunk, p.spc, p.consts, p.tail,
-                                                                      crc_out);
+  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(kFoldThreads), 0, s>>>(seg, bytes, pchunk, p.spc, p.tail,
+                                                                              crc_out);
   return hipGetLastError();
 }
 

@@ -81,7 +81,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--streams-per-peer", type=int, default=1,
                    help="P2P ops per peer and direction in one RCCL group")
     p.add_argument("--reserve-cus", type=int, default=-1,
-                   help="rccl: CUs the verify/copy kernels leave free for RCCL (-1: 32 with peers, else 0)")
+                   help="rccl: CUs the verify/copy kernels leave free for RCCL when --verify-cus is 0 (-1: 32 "
+                        "with peers, else 0)")
+    p.add_argument("--verify-cus", type=int, default=-1,
+                   help="rccl: the verify stream runs on the last N CUs only, RCCL lanes and copies on the others "
+                        "(-1: 32 - one XCD's worth - with peers, 128 with --store bf16, 0 alone; 0: shared)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX",
                    help="rccl: communicator CTA bounds (ncclConfig minCTAs/maxCTAs; channels per P2P peer)")
     p.add_argument("--nccl-register", action="store_true",
@@ -97,7 +101,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="rccl: one NVMe shared by every rank of the node at this read rate (disk readers share it; "
                         "mode 3 plans it as one budget); 0 = per-rank disks")
     p.add_argument("--crc-grid", type=int, default=-1,
-                   help="rccl: workgroup cap of the CRC verify kernels (-1: 32 with peers, every CU alone)")
+                   help="rccl: workgroup cap of the CRC verify kernels (-1/0: every CU of the verify stream)")
     p.add_argument("--comm-init", default="split", choices=["parallel", "split"],
                    help="rccl: lane communicators split from the world communicator one by one (split, the "
                         "default: faster at 8 shared ranks, profiles/r3_init2), or one unique id each, initialized "
@@ -141,6 +145,7 @@ def build_parser() -> argparse.ArgumentParser:
 def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
     opts = {"reserve_cus": args.reserve_cus, "crc_grid": int(getattr(args, "crc_grid", -1)),
+            "verify_cus": int(getattr(args, "verify_cus", -1)),
             "suspect_s": getattr(args, "suspect_timeout", 10.0),
             "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0)),
             "comm_init": getattr(args, "comm_init", "split")}

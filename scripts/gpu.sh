@@ -169,11 +169,19 @@ case "$RECIPE" in
   r4sweep)
     # fused store 7/8/9 against the source size (tail of the one-segment-per-wave grid), then the
     # paced contention run with CU-partitioned verify
+    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest_kernels.log 2>&1 || exit 1
     for mib in 448 480 496 504 512 520 528 544 576; do
-      timeout -k 10 60 python scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 9 > $OUT/sweep_$mib.json \
+      timeout -k 10 60 python scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 9 10 > $OUT/sweep_$mib.json \
         2> $OUT/sweep_$mib.log || exit 1
     done
     timeout -k 10 400 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1
+    ;;
+  r4trace)
+    # fused store 7 against size under a kernel trace: main kernel vs fold durations (fixed per-call cost)
+    for mib in 64 128 256 512 1024 2048; do
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$mib -o kt -- \
+        python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 10 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
+    done
     ;;
   r3mx)
     # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters
