@@ -5,11 +5,11 @@
 //
 // Hardware queues: HIP maps ordinary streams onto a pool of GPU_MAX_HW_QUEUES
 // (4) queues, so streams can share one; a CU-masked stream always gets a queue
-// of its own. The copy and verify streams are CU-masked whenever RCCL runs
-// (reserve_cus > 0, the default with peers) and extra comm lanes are created
-// with a mask of every CU, so no RCCL kernel waiting for a peer can hold back
-// a copy, a check or another lane (queue ids: profiles/r2_queues/ at 3 ranks,
-// profiles/r2_queues8/ at 8 ranks with 14 lanes each).
+// of its own. With peers the verify stream is masked to the last verify_cus
+// CUs and every comm lane and copy stream to the others (verify_cus below), so
+// no RCCL kernel waiting for a peer can hold back a copy, a check or another
+// lane (queue ids: profiles/r2_queues/ at 3 ranks, profiles/r2_queues8/ at 8
+// ranks with 14 lanes each) and no CRC workgroup shares a CU with RCCL.
 #pragma once
 
 #include <hip/hip_runtime_api.h>

@@ -54,7 +54,12 @@
 // the chunk end (the divergent multiply loop cost 212 us per GiB).
 // Two recurrences per lane (blocks 0-1 and 2-3, joined by an 8 KiB shift
 // table in the last 16 KiB of LDS) measured 229 us: the chain latency is not
-// what bounds it.
+// what bounds it. Round 4 (fused kernel, profiles/r4_chains): four chains per
+// lane, one per block, joined by 4096-byte shifts, measured the same as one
+// chain (160.4 vs 157.9 us main kernel at 512 MiB, 29.6 vs 30.3 at 64 MiB):
+// the ~9 us a launch pays over the same kernel without CRC math is the first
+// and last waves' ~600 VALU + 256 LDS lookups per lane per segment with
+// nothing to hide behind, not the length of the dependency chain.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

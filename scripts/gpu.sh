@@ -183,6 +183,18 @@ case "$RECIPE" in
         python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 10 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
     done
     ;;
+  r4chains)
+    # four independent chains per lane: numerics, fused A/B at 512 MiB and 4 GiB, CRC-only bulk, kernel trace vs size
+    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest_kernels.log 2>&1 &&
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log &&
+    timeout -k 10 200 python scripts/fused_ab.py --src-mib 4096 --reps 5 --store 1 7 9 > $OUT/fused_ab_4g.json \
+      2> $OUT/fused_ab_4g.log &&
+    timeout -k 10 300 python scripts/kernel_bench.py > $OUT/kernel_bench.json 2> $OUT/kernel_bench.log || exit 1
+    for mib in 64 512 2048; do
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$mib -o kt -- \
+        python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
+    done
+    ;;
   r3mx)
     # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters
     timeout -k 10 400 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py tests/test_gpu_engine.py -k "fp8 or fused" \
