@@ -195,6 +195,17 @@ case "$RECIPE" in
         python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
     done
     ;;
+  r4vcus)
+    # A/B of the verify CU partition at 8 shared ranks, same box, interleaved
+    rc=0
+    for spec in "1 0" "1 32" "2 0" "2 32" "1 0" "1 32" "2 0" "2 32"; do
+      set -- $spec
+      DISSEM_SHARED_GPU=1 timeout -k 10 150 python bench.py --gpus 8 --steps 2 --warmup 1 --layers 16 \
+        --layer-mib 64 --chunk-mib 16 --mode $1 --verify-cus $2 > $OUT/b_m$1_v$2_$RANDOM.json 2> $OUT/b_m$1_v$2.log \
+        || { rc=$?; break; }
+    done
+    [ $rc -eq 0 ]
+    ;;
   r3mx)
     # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters
     timeout -k 10 400 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py tests/test_gpu_engine.py -k "fp8 or fused" \

@@ -154,3 +154,26 @@ def test_layer_weights_zero_copy_in_hbm(gpu, pack):
             assert float((y - y0).norm() / y0.norm()) < 2e-2
     finally:
         rt.close()
+
+
+@pytest.mark.parametrize("verify_cus,store", [(32, "packed"), (128, "bf16")])
+def test_verify_on_its_own_cus(gpu, verify_cus, store):
+    """The verify stream on the last `verify_cus` CUs, copies (and RCCL lanes) on the
+    others (hip_backend.h verify_cus: the default with peers): every chunk still
+    verified; with the fused fp8 unpack the check and the unpack share those CUs."""
+    size = 6 * MiB + 4096
+    kw = {"pack": "fp8", "store": "bf16"} if store == "bf16" else {}
+    cfg = make_workload(1, 6, size, tier="host", chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="rccl", chunk_bytes=MiB, registry={0: "127.0.0.1:0"},
+                 engine_opts={"verify_cus": verify_cus}, **kw)
+    try:
+        res = rt.run(1, timeout=60)
+        assert res.ok, res.error
+        assert res.engine_stats["verify_failures"] == 0
+        for l in range(6):
+            if store == "packed":
+                assert rt.layer_bytes(l) == gpu.fill_random_host(size, layer_seed(0, l))
+            else:  # the fused check + unpack on the verify CUs restored the bf16 layer
+                assert rt.unpacked_layer_bytes(l) == gpu.fp8_unpack_layer_host(rt.layer_bytes(l), size, MiB, 128)
+    finally:
+        rt.close()
