@@ -206,6 +206,16 @@ case "$RECIPE" in
     done
     [ $rc -eq 0 ]
     ;;
+  r4halves)
+    # store 7 vs 11 (every segment in halves) vs 12 (half a round of halves first), numerics + sizes + trace
+    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 || exit 1
+    for mib in 64 512 4096; do
+      timeout -k 10 200 python scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 10 11 12 7 > $OUT/ab_$mib.json \
+        2> $OUT/ab_$mib.log || exit 1
+    done
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_512 -o kt -- \
+      python3 scripts/fused_ab.py --src-mib 512 --reps 10 --store 7 11 12 > $OUT/kt_512.json 2> $OUT/kt_512.log
+    ;;
   r3mx)
     # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters
     timeout -k 10 400 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py tests/test_gpu_engine.py -k "fp8 or fused" \
