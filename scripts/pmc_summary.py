@@ -16,7 +16,7 @@ def load(d):
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                k = r["Kernel_Name"].split("(")[0]
+                k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
                 rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 meta[k] = (r["Grid_Size"], r["Workgroup_Size"], r["LDS_Block_Size"],
                            r["Scratch_Size"], r["VGPR_Count"])
