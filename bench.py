@@ -74,7 +74,7 @@ def parse_args(argv=None):
                    help="CUs the verify/copy kernels leave free for RCCL when --verify-cus is 0 (-1: 32 when N > 1)")
     p.add_argument("--verify-cus", type=int, default=-1,
                    help="the verify stream runs on the last N CUs only, RCCL lanes and copies on the others (-1: 32, "
-                        "one XCD's worth, when N > 1 - 128 with --store bf16 - and 0 alone; 0: all shared). "
+                        "4 CUs on each XCD, when N > 1 - 128 with --store bf16 - and 0 alone; 0: all shared). "
                         "bin/contention: a 64-workgroup copy keeps 99.6 %% of its rate beside 450 GB/s of verify "
                         "on the last 32 CUs (profiles/r4_contention)")
     p.add_argument("--crc-grid", type=int, default=-1,

@@ -109,11 +109,11 @@ struct PlannedConfig {
   // CUs the verify/copy-stream kernels (CRC, fp8 pack) may never occupy, so an
   // RCCL group kernel always finds free CUs to launch on instead of queueing
   // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
-  // -1: 32 when world > 1 (one XCD's worth), 0 on one rank (no RCCL traffic).
+  // -1: 32 when world > 1, 0 on one rank (no RCCL traffic). Ignored when verify_cus > 0.
   int reserve_cus = -1;
   int crc_grid = -1;  // verify kernels' workgroup cap (-1: the verify stream's CUs; 0: all)
   // CUs of the verify stream, the last ones of the mask; RCCL and copies get the
-  // rest (HipBackendConfig::verify_cus). -1: 32 (one XCD's worth) with peers,
+  // rest (HipBackendConfig::verify_cus). -1: 32 (4 CUs on each XCD) with peers,
   // 128 when every landing is also unpacked (unpack_store), 0 (all CUs shared) alone.
   int verify_cus = -1;
   // RCCL communicator CTA (workgroup/channel) bounds via ncclCommInitRankConfig;

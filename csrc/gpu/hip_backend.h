@@ -35,18 +35,18 @@ struct HipBackendConfig {
   // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
   int reserve_cus = 0;
   // Workgroup cap of the CRC verify kernels (0: every CU the verify stream
-  // has). With peers a narrow verify runs longer but never takes the whole
-  // chip's HBM bandwidth from the comm lanes' RCCL kernels at once
-  // (bin/contention -paced, profiles/r4_contention/).
+  // has). A narrow verify sharing CUs with RCCL hurts it more than a short
+  // full-chip one (bin/contention -paced, profiles/r4_contention/).
   int crc_grid = 0;
   // > 0: the verify stream runs on the LAST verify_cus CU-mask bits only and
   // every comm lane and copy stream on the others, so no CRC workgroup shares a
-  // CU - or, at 32, an XCD and its L2 - with an RCCL kernel. bin/contention
-  // -paced (profiles/r4_contention/paced_partitioned.jsonl): a 64-workgroup
-  // copy keeps 99.6 % of its alone rate beside 450 GB/s of continuous
-  // verification on the last 32 CUs, against 93.8 % beside an unmasked
-  // full-grid verify and 85.6 % beside a 32-workgroup one; the same 32 CUs
-  // taken as every 8th bit (spread over the XCDs) keep only 86 %. Overrides
+  // CU with an RCCL kernel. Mask bit i is CU i / 8 of XCD i mod 8 (bin/contention
+  // -cumap), so the last 32 bits are 4 CUs on each of the 8 XCDs: keep
+  // verify_cus a multiple of 8 (an XCD left with no CU ignores its mask).
+  // bin/contention -paced (profiles/r4_contention/paced_partitioned.jsonl): a
+  // 64-workgroup copy keeps 99.6 % of its alone rate beside 450 GB/s of
+  // continuous verification on the last 32 bits, against 93.8 % beside an
+  // unmasked full-grid verify and 85.6 % beside a 32-workgroup one. Overrides
   // reserve_cus; the CRC grid is capped at verify_cus.
   int verify_cus = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default

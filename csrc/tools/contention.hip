@@ -36,6 +36,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <map>
+#include <set>
 #include <vector>
 
 #include "kernels/kernels.h"
@@ -93,9 +95,80 @@ static hipStream_t make_masked(Pick pick) {
   return s;
 }
 
+// Which XCD (HW_REG_XCC_ID) and which CU inside it (HW_REG_HW_ID) each
+// workgroup of a long kernel ran on: the map from CU-mask bits to the
+// hardware that the verify partition relies on. Measured (profiles/r4_contention/
+// cumap.jsonl): bit i is CU i / 8 of XCD i mod 8, workgroups go to the XCDs
+// round-robin whatever the mask, and an XCD left without a CU runs its share on
+// all of its CUs.
+__global__ void __launch_bounds__(64) where_kernel(uint32_t* __restrict__ out, int64_t spin) {
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID[15:0]
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+  int64_t t0 = clock64();
+  while (clock64() - t0 < spin) {
+  }
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = xcc;
+    out[2 * blockIdx.x + 1] = hw;
+  }
+}
+
+static int cumap() {
+  CHECK(hipSetDevice(0));
+  const int blocks = 2048;
+  uint32_t* out = nullptr;
+  CHECK(hipMalloc(&out, size_t(blocks) * 2 * sizeof(uint32_t)));
+  std::vector<uint32_t> h(size_t(blocks) * 2);
+  struct Mask {
+    const char* name;
+    int every, phase, n;  // every < 0: contiguous last n; every == 0: contiguous first n
+  };
+  const Mask masks[] = {{"all", 1, 0, 0}, {"last32", -1, 0, 32}, {"first32", 0, 0, 32}, {"every8th", 8, 7, 32},
+                        {"bits_224_255_complement", -2, 0, 32}};
+  for (const Mask& m : masks) {
+    hipStream_t st = make_masked([m](int cu, int cus) {
+      if (m.every == 1) return true;
+      if (m.every == -1) return cu >= cus - m.n;
+      if (m.every == -2) return cu < cus - m.n;
+      if (m.every == 0) return cu < m.n;
+      return cu % m.every == m.phase;
+    });
+    CHECK(hipMemsetAsync(out, 0xff, size_t(blocks) * 2 * sizeof(uint32_t), st));
+    where_kernel<<<blocks, 64, 0, st>>>(out, 200000);
+    CHECK(hipStreamSynchronize(st));
+    CHECK(hipMemcpy(h.data(), out, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::map<uint32_t, int> per_xcc;
+    std::map<uint32_t, std::set<uint32_t>> cus_of_xcc;
+    for (int b = 0; b < blocks; ++b) {
+      const uint32_t x = h[size_t(2 * b)] & 0xf, hw = h[size_t(2 * b + 1)];
+      ++per_xcc[x];
+      // gfx9 HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]
+      cus_of_xcc[x].insert(((hw >> 13) & 7) * 32 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15));
+    }
+    printf("{\"case\": \"cumap\", \"mask\": \"%s\", \"workgroups_per_xcd\": {", m.name);
+    bool first = true;
+    for (auto& [x, c] : per_xcc) {
+      printf("%s\"%u\": %d", first ? "" : ", ", x, c);
+      first = false;
+    }
+    printf("}, \"distinct_cus_per_xcd\": {");
+    first = true;
+    for (auto& [x, c] : cus_of_xcc) {
+      printf("%s\"%u\": %zu", first ? "" : ", ", x, c.size());
+      first = false;
+    }
+    printf("}}\n");
+    fflush(stdout);
+    CHECK(hipStreamDestroy(st));
+  }
+  CHECK(hipFree(out));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   int trials = 40, reserve = 32;
   double paced_s = 0, land_gbps = 450;
+  if (argc > 1 && std::string(argv[1]) == "-cumap") return cumap();
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string a = argv[i];
     if (a == "-trials") trials = atoi(argv[i + 1]);

@@ -85,7 +85,7 @@ def build_parser() -> argparse.ArgumentParser:
                         "with peers, else 0)")
     p.add_argument("--verify-cus", type=int, default=-1,
                    help="rccl: the verify stream runs on the last N CUs only, RCCL lanes and copies on the others "
-                        "(-1: 32 - one XCD's worth - with peers, 128 with --store bf16, 0 alone; 0: shared)")
+                        "(-1: 32 - CUs 28-31 of each XCD - with peers, 128 with --store bf16, 0 alone; 0: shared)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX",
                    help="rccl: communicator CTA bounds (ncclConfig minCTAs/maxCTAs; channels per P2P peer)")
     p.add_argument("--nccl-register", action="store_true",
