@@ -594,11 +594,17 @@ __device__ inline void unpack16_regs(const u32x4_t& w, float s, uint32_t (&o)[8]
     o[2 * i + 1] = fp8x2_to_bf16x2<true>(w[i], s);
   }
 }
+template <bool NT = false>
 __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ dst) {
   uint32_t o[8];
   unpack16_regs(w, s, o);
-  dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-  dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  if constexpr (NT) {
+    __builtin_nontemporal_store(u32x4_t{o[0], o[1], o[2], o[3]}, reinterpret_cast<u32x4_t*>(dst));
+    __builtin_nontemporal_store(u32x4_t{o[4], o[5], o[6], o[7]}, reinterpret_cast<u32x4_t*>(dst) + 1);
+  } else {
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  }
 }
 
 // A wave's 2 KiB of bf16 from one loaded word (lane m + 16 r holds output bytes
@@ -613,6 +619,7 @@ __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ d
 // distinct bank quads instead of 2 (4-way conflicts: 29 M conflict cycles per
 // 512 MiB, profiles/r3_kernels), and the readers (granule = lane) stay distinct.
 __device__ __forceinline__ uint32_t swz(uint32_t g) { return g ^ ((g >> 3) & 6u); }
+template <bool NT = false>
 __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* slot, uint4* __restrict__ region) {
   const int lane = threadIdx.x & 63, m = lane & 15, r = lane >> 4;
   uint4* g = reinterpret_cast<uint4*>(slot);  // granules
@@ -625,7 +632,10 @@ __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* sl
       g[w1] = make_uint4(o[4], o[5], o[6], o[7]);
     }
     __builtin_amdgcn_wave_barrier();
-    region[64 * h + lane] = *rd;
+    if constexpr (NT)
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(rd), reinterpret_cast<u32x4_t*>(region) + 64 * h + lane);
+    else
+      region[64 * h + lane] = *rd;
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -643,8 +653,13 @@ __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* sl
 // straddle 64). Loading each word's scale where it is used made every use wait
 // for all older loads - the next segment's prefetch included (vmcnt counts in
 // order): 3.93 -> 4.12 TB/s (profiles/r2_fused_ahead). Nontemporal bf16 stores
-// measured slower (3.61 TB/s, profiles/r2_fused_nt).
-template <int BLOCK, bool STAGE = false>
+// (NT) measured slower in the round-2 walk, whose lanes stored half-dense 16-B
+// pieces (3.61 TB/s, profiles/r2_fused_nt), and still lose there (store 14:
+// 3.6); the staged, whole-KiB stores of the one-segment-per-wave kernel gain
+// from them: 5.04 -> 5.39-5.43 TB/s at 512 MiB, 5.37-5.67 -> 5.92-6.13 at
+// 4 GiB (profiles/r4_nt): the output is written once and never read back, so
+// it has no business in L2 or the Infinity Cache.
+template <int BLOCK, bool STAGE = false, bool NT = false>
 struct UnpackVisit {
   static constexpr int kR = kSegBytes / BLOCK >= 64 ? kSegBytes / BLOCK / 64 : 1;  // scale registers
   // BLOCK 32 would hold 16 scale registers and spill: it keeps the per-word load
@@ -663,7 +678,7 @@ struct UnpackVisit {
     obase = out + sg.chunk * out_chunk_elems;
   }
   __device__ void operator()(const u32x4_t& w, int64_t e) {  // e: byte offset in chunk = element index in q
-    if (e < n_q) unpack16(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
+    if (e < n_q) unpack16<NT>(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
   }
   __device__ void prefetch(const Seg& sg, bool full) {
     if constexpr (!kAhead) return;
@@ -697,11 +712,11 @@ struct UnpackVisit {
       if (kib + 1024 <= n_q) {
         uint32_t o[8];
         unpack16_regs(w, s, o);
-        store_staged(o, slot, reinterpret_cast<uint4*>(obase + kib));
+        store_staged<NT>(o, slot, reinterpret_cast<uint4*>(obase + kib));
         return;
       }
     }
-    if (e < n_q) unpack16(w, s, reinterpret_cast<uint4*>(obase + e));
+    if (e < n_q) unpack16<NT>(w, s, reinterpret_cast<uint4*>(obase + e));
   }
 };
 
@@ -736,25 +751,25 @@ verify_unpack_once_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_ch
 // replicas (72 KiB + 8 KiB of staging): two workgroups per CU, so one fills
 // its tables and waits for its first loads while the other computes.
 constexpr int kWaves16 = 8;
-template <int BLOCK, bool CRC = true, bool STAGE = true>
+template <int BLOCK, bool CRC = true, bool STAGE = true, bool NT = false>
 __global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
 verify_unpack_once16_kernel(const ChunkGeo geo, int64_t total_segs, int64_t split_block, int64_t out_chunk_elems,
                             const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
                             uint16_t* __restrict__ out) {
   __shared__ uint4 lds_raw[(LdsLayout<16>::kBytes + (STAGE ? kWaves16 * 1024 : 0)) / 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  UnpackVisit<BLOCK, STAGE> v{out_chunk_elems, out, geo.src};
+  UnpackVisit<BLOCK, STAGE, NT> v{out_chunk_elems, out, geo.src};
   v.slot = lds + LdsLayout<16>::kBytes + (threadIdx.x >> 6) * 1024;
   if (int64_t(blockIdx.x) < split_block) {
-    slice_once<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(geo, total_segs, sc, lds, v, seg_out);
+    slice_once<ChunkGeo, UnpackVisit<BLOCK, STAGE, NT>, CRC, 16, kWaves16>(geo, total_segs, sc, lds, v, seg_out);
   } else {
     const int64_t g0 = split_block * kWaves16 + (int64_t(blockIdx.x) - split_block) * (kWaves16 / 2);
     if constexpr (STAGE) {  // pair m hands over in word 0 of wave 2 m + 1's slot
-      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(
+      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE, NT>, CRC, 16, kWaves16>(
           geo, total_segs, g0, sc, lds, v, seg_out, reinterpret_cast<uint32_t*>(lds + LdsLayout<16>::kBytes + 1024), 512);
     } else {
       __shared__ uint32_t xch[kWaves16 / 2];
-      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC, 16, kWaves16>(geo, total_segs, g0, sc, lds, v, seg_out, xch,
+      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE, NT>, CRC, 16, kWaves16>(geo, total_segs, g0, sc, lds, v, seg_out, xch,
                                                                          1);
     }
   }
@@ -835,12 +850,26 @@ verify_unpack_split_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_c
 // A chunk's raw CRC: the XOR of its segments' values (each already shifted
 // to the chunk end). Called by every thread of a kFoldThreads block; returns
 // the raw CRC on thread 0.
-constexpr int kFoldThreads = 256;
+// The loads go out four at a time (independent accumulators): a plain strided
+// loop waits for each before the next (~9 round trips per 2112-segment chunk
+// on 256 threads). A fold launch costs ~4.5 us whatever its work
+// (profiles/r4_nt): folding in the fused kernel's last workgroup instead
+// (generation-tagged slots that one workgroup polls) measured slower at
+// 512 MiB, 159.8 vs 148.3 + 4.5 us, since one workgroup reads the slots at a
+// fraction of the chip's rate (profiles/r4_fold_in_kernel).
+constexpr int kFoldThreads = 1024;
 __device__ uint32_t xor_chunk(const uint32_t* __restrict__ seg, int64_t nseg) {
   __shared__ uint32_t part[kFoldThreads / 64];
-  uint32_t r = 0;
-  for (int64_t k = threadIdx.x; k < nseg; k += kFoldThreads) r ^= seg[k];
-  r = wave_xor_dpp(r);
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  int64_t k = threadIdx.x;
+  for (; k + 3 * kFoldThreads < nseg; k += 4 * kFoldThreads) {
+    r0 ^= seg[k];
+    r1 ^= seg[k + kFoldThreads];
+    r2 ^= seg[k + 2 * kFoldThreads];
+    r3 ^= seg[k + 3 * kFoldThreads];
+  }
+  for (; k < nseg; k += kFoldThreads) r0 ^= seg[k];
+  uint32_t r = wave_xor_dpp(r0 ^ r1 ^ r2 ^ r3);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
   __syncthreads();
   if (threadIdx.x != 0) return 0;
@@ -1149,14 +1178,16 @@ hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_
   const int64_t sb = og.split_block;
 #define DLD_VU(B)                                                                                           \
   (store == 9   ? (verify_unpack_once16_kernel<B, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
-   : store == 7 || store == 10 ? (verify_unpack_once16_kernel<B><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out))  \
+   : store == 14 ? (verify_unpack_once16_kernel<B, true, false, true><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
+   : store == 13 ? (verify_unpack_once16_kernel<B, true, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
+   : store == 7 || store == 10 ? (verify_unpack_once16_kernel<B, true, true, true><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out))  \
    : store == 5 ? (verify_unpack_once_kernel<B><<<grid5, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))      \
    : store == 2 ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
    : store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
                 : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
   if (store == 8) {  // diagnostic: store 7 without the CRC math
     if (block != 128) return hipErrorInvalidValue;
-    verify_unpack_once16_kernel<128, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out);
+    verify_unpack_once16_kernel<128, false, true, true><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out);
   } else if (store == 3 || store == 4 || store == 6) {  // diagnostic: the same walk without the CRC math (CRCs are garbage)
     if (block != 128) return hipErrorInvalidValue;
     if (store == 3)

@@ -98,7 +98,9 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__
   int hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[4], y[5], 0, false);
   hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], hi, true);
   if (!active) return;
-  out[t] = make_uint2(uint32_t(lo), uint32_t(hi));
+  // written once, read by a later pass or another GPU: nontemporal (profiles/r4_nt)
+  __builtin_nontemporal_store(uint32_t(lo), &out[t].x);
+  __builtin_nontemporal_store(uint32_t(hi), &out[t].y);
   if ((threadIdx.x % LANES) == 0) scales[t / LANES] = __uint_as_float(uint32_t(127 + e) << 23);
 }
 
@@ -110,8 +112,10 @@ __global__ void __launch_bounds__(256) fp8_unpack_kernel(const uint2* __restrict
   if (t >= nthreads) return;
   const uint2 q = in[t];
   const float s = scales[t / LANES];
-  out[t] = make_uint4(fp8x2_to_bf16x2<false>(q.x, s), fp8x2_to_bf16x2<true>(q.x, s),
-                      fp8x2_to_bf16x2<false>(q.y, s), fp8x2_to_bf16x2<true>(q.y, s));
+  using v4 = unsigned int __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4{fp8x2_to_bf16x2<false>(q.x, s), fp8x2_to_bf16x2<true>(q.x, s),
+                                 fp8x2_to_bf16x2<false>(q.y, s), fp8x2_to_bf16x2<true>(q.y, s)},
+                              reinterpret_cast<v4*>(out) + t);
 }
 
 }  // namespace

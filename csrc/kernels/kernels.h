@@ -83,12 +83,13 @@ hipError_t fp8_pack_chunks(const void* src, int64_t src_bytes, int64_t src_chunk
 // wave as fully coalesced 1 KiB stores, 2 = split roles: half of each
 // workgroup's waves CRC the segments while the other half unpack them;
 // 5 = one segment per wave (1024-thread workgroups, 32 table replicas), 7 = the
-// same with 512-thread workgroups and 16 replicas (two per CU) and the grid's
-// last partial round in half segments, 9 = 7 with direct stores, 10 = 7
-// without the half-segment round; 3, 4, 6, 8 are no-CRC diagnostics (their
-// CRCs are garbage); -1 = kFusedStoreDefault.
-// 7: 4.98 TB/s at 512 MiB and 5.42 main-kernel at 2 GiB vs store 1's 4.60 / 5.10
-// (profiles/r4_kernels, profiles/r4_sweep, profiles/r4_trace)
+// same with 512-thread workgroups and 16 replicas (two per CU), the grid's
+// last partial round in half segments and nontemporal staged stores, 9 = 7
+// with direct stores (temporal), 10 = 7 without the half-segment round, 13 = 7
+// with temporal stores, 14 = 9 with nontemporal ones; 3, 4, 6, 8 are no-CRC
+// diagnostics (their CRCs are garbage); -1 = kFusedStoreDefault.
+// 7: 5.3-5.4 TB/s at 512 MiB, 5.9-6.2 at 4 GiB vs store 1's 4.66 / 4.89
+// (profiles/r4_nt, profiles/r4_kernels_final)
 constexpr int kFusedStoreDefault = 7;
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
                              uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks = 0, int store = -1);

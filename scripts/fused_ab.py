@@ -6,7 +6,7 @@ issues two fully coalesced 1 KiB stores, store=2 splits each workgroup's waves
 into CRC walkers and unpack streamers over the same segments; store=5 runs one segment per wave
 (no walk: a grid as large as the work, the LDS tables filled per workgroup), store=7 the same in 512-thread
 workgroups with 16 table replicas (two workgroups per CU) and the grid's last partial round in half segments,
-store=9 store=7 with unstaged stores, store=10 store=7 without the half-segment round; store=3/4/6/8 are
+store=9 store=7 with unstaged stores, store=10 store=7 without the half-segment round, store=13 store=7 with temporal stores, store=14 store=9 with nontemporal ones (store 7 stores its staged KiBs nontemporally); store=3/4/6/8 are
 store=1/0/5/7 with the CRC
 math removed (diagnostic: what the walk, loads and stores cost alone). Same input, same CRCs and bf16 bytes
 (checked), timed with HIP events on 512 MiB of bf16 (264 MiB packed), plus the
@@ -39,7 +39,7 @@ def timed(fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--store", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+    ap.add_argument("--store", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 14])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--src-mib", type=int, default=512)
     ap.add_argument("--max-blocks", type=int, default=0, help="cap on the fused kernel's workgroups (0: one per CU)")

@@ -216,6 +216,31 @@ case "$RECIPE" in
     timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_512 -o kt -- \
       python3 scripts/fused_ab.py --src-mib 512 --reps 10 --store 7 11 12 > $OUT/kt_512.json 2> $OUT/kt_512.log
     ;;
+  r4nt)
+    # nontemporal stores: store 7 (staged NT) vs 13 (temporal) vs 9, plain pack/unpack NT; numerics, sizes, trace
+    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest_kernels.log 2>&1 &&
+    timeout -k 10 300 python scripts/kernel_bench.py > $OUT/kernel_bench.json 2> $OUT/kernel_bench.log || exit 1
+    for mib in 64 512 4096; do
+      timeout -k 10 200 python scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 13 9 7 13 > $OUT/ab_$mib.json \
+        2> $OUT/ab_$mib.log || exit 1
+    done
+    for mib in 64 512 2048; do
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$mib -o kt -- \
+        python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
+    done
+    ;;
+  r4ffold)
+    # the once16 kernels fold in their last workgroup (tagged slots): numerics, engine fp8 paths, sizes, trace
+    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest_kernels.log 2>&1 &&
+    timeout -k 10 600 $PYTEST tests/test_gpu_engine.py > $OUT/pytest_engine.log 2>&1 || exit 1
+    for mib in 64 512 4096; do
+      timeout -k 10 200 python scripts/fused_ab.py --src-mib $mib --reps 20 --store 7 13 7 > $OUT/ab_$mib.json \
+        2> $OUT/ab_$mib.log || exit 1
+    done
+    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log &&
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_512 -o kt -- \
+      python3 scripts/fused_ab.py --src-mib 512 --reps 10 --store 7 > $OUT/kt_512.json 2> $OUT/kt_512.log
+    ;;
   r3mx)
     # power-of-two (E8M0-valued) fp8 scales: unpack via v_cvt_scalef32_pk_bf16_fp8; numerics + fused A/B + counters
     timeout -k 10 400 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py tests/test_gpu_engine.py -k "fp8 or fused" \

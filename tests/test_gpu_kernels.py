@@ -238,7 +238,7 @@ def test_fp8_pack_chunks_matches_host_layout(gpu, size, chunk, block):
     # partial segments between full ones)
     (48 << 20, 16 << 20, 128, 3), ((24 << 20) + 4096, 1 << 20, 256, 7), (16 << 20, (1 << 20) + 4096, 64, 1),
     (8 << 20, 4 << 20, 32, 2), ((8 << 20) + 1024, 64 << 10, 512, 5)])
-@pytest.mark.parametrize("store", [0, 1, 2, 5, 7, 9, 10])
+@pytest.mark.parametrize("store", [0, 1, 2, 5, 7, 9, 10, 13, 14])
 def test_fp8_fused_verify_unpack(gpu, size, chunk, block, max_blocks, store):
     """One pass: CRC32C of every packed chunk + bf16 dequantization; compared with
     the CRC kernel, the host CRC and the standalone unpack kernel (same math).
