@@ -23,11 +23,12 @@ __global__ void __launch_bounds__(256) fill_random_kernel(ulonglong2* __restrict
                                                           uint64_t seed) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    ulonglong2 v;
-    v.x = mix64(seed, uint64_t(2 * i));
-    v.y = mix64(seed, uint64_t(2 * i + 1));
-    __builtin_nontemporal_store(v.x, &dst[i].x);
-    __builtin_nontemporal_store(v.y, &dst[i].y);
+    // one 16-B nontemporal store per lane: whole lines per instruction (two 8-B
+    // stores leave each instruction's lines half written, which NT stores pay
+    // for: profiles/r4_nt, store 14)
+    using v2u64 = unsigned long long __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(v2u64{mix64(seed, uint64_t(2 * i)), mix64(seed, uint64_t(2 * i + 1))},
+                                reinterpret_cast<v2u64*>(dst) + i);
   }
 }
 

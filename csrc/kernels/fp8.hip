@@ -99,8 +99,8 @@ __global__ void __launch_bounds__(256) fp8_pack_kernel(const uint4* __restrict__
   hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], hi, true);
   if (!active) return;
   // written once, read by a later pass or another GPU: nontemporal (profiles/r4_nt)
-  __builtin_nontemporal_store(uint32_t(lo), &out[t].x);
-  __builtin_nontemporal_store(uint32_t(hi), &out[t].y);
+  using v2 = unsigned int __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(v2{uint32_t(lo), uint32_t(hi)}, reinterpret_cast<v2*>(out) + t);
   if ((threadIdx.x % LANES) == 0) scales[t / LANES] = __uint_as_float(uint32_t(127 + e) << 23);
 }
 
