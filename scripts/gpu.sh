@@ -164,7 +164,8 @@ case "$RECIPE" in
     ;;
   r4contention)
     # continuous verification at the landing rate of 7 links (450 GB/s) beside a 64-workgroup copy, per CRC grid cap
-    timeout -k 10 300 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1
+    timeout -k 10 120 bin/contention -cumap > $OUT/cumap.jsonl 2>&1 &&
+    timeout -k 10 400 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1
     ;;
   r4sweep)
     # fused store 7/8/9 against the source size (tail of the one-segment-per-wave grid), then the
@@ -183,18 +184,6 @@ case "$RECIPE" in
         python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 10 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
     done
     ;;
-  r4chains)
-    # four independent chains per lane: numerics, fused A/B at 512 MiB and 4 GiB, CRC-only bulk, kernel trace vs size
-    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest_kernels.log 2>&1 &&
-    timeout -k 10 120 python scripts/fused_ab.py > $OUT/fused_ab.json 2> $OUT/fused_ab.log &&
-    timeout -k 10 200 python scripts/fused_ab.py --src-mib 4096 --reps 5 --store 1 7 9 > $OUT/fused_ab_4g.json \
-      2> $OUT/fused_ab_4g.log &&
-    timeout -k 10 300 python scripts/kernel_bench.py > $OUT/kernel_bench.json 2> $OUT/kernel_bench.log || exit 1
-    for mib in 64 512 2048; do
-      timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$mib -o kt -- \
-        python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
-    done
-    ;;
   r4vcus)
     # A/B of the verify CU partition at 8 shared ranks, same box, interleaved
     rc=0
@@ -205,16 +194,6 @@ case "$RECIPE" in
         || { rc=$?; break; }
     done
     [ $rc -eq 0 ]
-    ;;
-  r4halves)
-    # store 7 vs 11 (every segment in halves) vs 12 (half a round of halves first), numerics + sizes + trace
-    timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py -k fused > $OUT/pytest_fused.log 2>&1 || exit 1
-    for mib in 64 512 4096; do
-      timeout -k 10 200 python scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 10 11 12 7 > $OUT/ab_$mib.json \
-        2> $OUT/ab_$mib.log || exit 1
-    done
-    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_512 -o kt -- \
-      python3 scripts/fused_ab.py --src-mib 512 --reps 10 --store 7 11 12 > $OUT/kt_512.json 2> $OUT/kt_512.log
     ;;
   r4nt)
     # nontemporal stores: store 7 (staged NT) vs 13 (temporal) vs 9, plain pack/unpack NT; numerics, sizes, trace
@@ -229,8 +208,8 @@ case "$RECIPE" in
         python3 scripts/fused_ab.py --src-mib $mib --reps 10 --store 7 8 > $OUT/kt_$mib.json 2> $OUT/kt_$mib.log || exit 1
     done
     ;;
-  r4ffold)
-    # the once16 kernels fold in their last workgroup (tagged slots): numerics, engine fp8 paths, sizes, trace
+  r4validate)
+    # fused kernel numerics (kernel + ops + engine GPU tests), A/B at 64 / 512 / 4096 MiB, all stores, trace at 512 MiB
     timeout -k 10 600 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest_kernels.log 2>&1 &&
     timeout -k 10 600 $PYTEST tests/test_gpu_engine.py > $OUT/pytest_engine.log 2>&1 || exit 1
     for mib in 64 512 4096; do
