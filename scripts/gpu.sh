@@ -330,7 +330,9 @@ case "$RECIPE" in
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench -o bench -- \
       python3 bench.py --steps 2 --warmup 1 > $OUT/bench.log 2>&1 &&
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fp8 -o fp8 -- \
-      python3 bench.py --pack fp8 --layers 20 --layer-mib 3072 --steps 2 --warmup 1 > $OUT/fp8.log 2>&1
+      python3 bench.py --pack fp8 --layers 20 --layer-mib 3072 --steps 2 --warmup 1 > $OUT/fp8.log 2>&1 &&
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fp8_bf16 -o fp8b -- \
+      python3 bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --steps 2 --warmup 1 > $OUT/fp8_bf16.log 2>&1
     ;;
   disk)
     mkdir -p /tmp/dl_disk &&
