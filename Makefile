@@ -59,7 +59,8 @@ tools: bin/diskspeed bin/h2dbench bin/contention bin/cvtprobe bin/walkprobe
 
 bin/contention: $(BUILD)/tools/contention.hip.o $(BUILD)/kernels/crc32c.hip.o $(BUILD)/kernels/fill.hip.o $(BUILD)/core/crc32c.o
 	@mkdir -p bin
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib
 
 bin/cvtprobe: csrc/tools/cvtprobe.hip
 	@mkdir -p bin

@@ -40,6 +40,8 @@
 #include <set>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "kernels/kernels.h"
 
 #define CHECK(x)                                                       \
@@ -165,10 +167,154 @@ static int cumap() {
   return 0;
 }
 
+// ---- RCCL's own P2P kernel beside continuous verification (-rccl SECS): a
+// one-rank communicator sends 256 MiB to itself and receives it (one group
+// per transfer, back to back on the lane stream), timed per group, alone and
+// beside verification paced at the landing rate: unmasked full grid, grid
+// capped at 32, and partitioned (verify on the last 32 CU-mask bits, the lane
+// on the rest - the engine's layout with peers).
+#define NCHECK(x)                                                                       \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    if (r_ != ncclSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, ncclGetErrorString(r_)); \
+      exit(1);                                                                          \
+    }                                                                                   \
+  } while (0)
+
+static int rccl_paced(double secs, double land_gbps) {
+  CHECK(hipSetDevice(0));
+  ncclUniqueId id;
+  NCHECK(ncclGetUniqueId(&id));
+  ncclComm_t comm;
+  NCHECK(ncclCommInitRank(&comm, 1, id, 0));
+  const int64_t chunk = 64ll << 20, nchunks = 7, xfer = 256ll << 20;
+  uint8_t *buf = nullptr, *sbuf = nullptr, *rbuf = nullptr;
+  CHECK(hipMalloc(&buf, size_t(chunk * nchunks)));
+  CHECK(dissem::kern::fill_random(buf, chunk * nchunks, 42, nullptr));
+  CHECK(hipMalloc(&sbuf, size_t(xfer)));
+  CHECK(hipMalloc(&rbuf, size_t(xfer)));
+  CHECK(hipMemset(sbuf, 3, size_t(xfer)));
+  const int kRing = 64;
+  const size_t wsb = dissem::kern::crc32c_batch_workspace_bytes(chunk, int(nchunks));
+  uint8_t* ws = nullptr;
+  CHECK(hipMalloc(&ws, wsb * kRing));
+  uint32_t* crc = nullptr;
+  CHECK(hipMalloc(&crc, size_t(kRing) * nchunks * sizeof(uint32_t)));
+  const double period_s = double(chunk * nchunks) / (land_gbps * 1e9);
+  auto pct = [](std::vector<float> v, double q) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.f : v[size_t(q * double(v.size() - 1))];
+  };
+  auto rccl_run = [&](hipStream_t lane, double dur, std::vector<float>& gbps) {
+    const int n = 16;
+    std::vector<hipEvent_t> ev(size_t(n) + 1);
+    for (auto& e : ev) CHECK(hipEventCreate(&e));
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::duration<double>(dur);
+    while (std::chrono::steady_clock::now() < t_end) {
+      CHECK(hipEventRecord(ev[0], lane));
+      for (int k = 0; k < n; ++k) {
+        NCHECK(ncclGroupStart());
+        NCHECK(ncclSend(sbuf, size_t(xfer), ncclChar, 0, comm, lane));
+        NCHECK(ncclRecv(rbuf, size_t(xfer), ncclChar, 0, comm, lane));
+        NCHECK(ncclGroupEnd());
+        CHECK(hipEventRecord(ev[size_t(k) + 1], lane));
+      }
+      CHECK(hipStreamSynchronize(lane));
+      for (int k = 0; k < n; ++k) {
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, ev[size_t(k)], ev[size_t(k) + 1]));
+        gbps.push_back(float(double(xfer) / (double(ms) * 1e-3) / 1e9));
+      }
+    }
+    for (auto& e : ev) CHECK(hipEventDestroy(e));
+  };
+  // warm: RCCL connections, CRC tables
+  hipStream_t lane_all = make_stream(0, true);
+  {
+    std::vector<float> w;
+    rccl_run(lane_all, 0.2, w);
+    hipStream_t v0;
+    CHECK(hipStreamCreateWithFlags(&v0, hipStreamNonBlocking));
+    dissem::kern::CrcItem it[nchunks];
+    for (int64_t c = 0; c < nchunks; ++c) it[c] = dissem::kern::CrcItem{buf + c * chunk, chunk, crc + c};
+    CHECK(dissem::kern::crc32c_batch(it, int(nchunks), ws, v0, 0));
+    CHECK(hipStreamSynchronize(v0));
+    CHECK(hipStreamDestroy(v0));
+  }
+  std::vector<float> alone;
+  rccl_run(lane_all, std::min(secs, 3.0), alone);
+  printf("{\"case\": \"rccl_self_p2p_alone\", \"xfer_MiB\": %lld, \"GBps_p50\": %.1f, \"GBps_p10\": %.1f}\n",
+         (long long)(xfer >> 20), pct(alone, 0.5), pct(alone, 0.1));
+  fflush(stdout);
+  struct Case {
+    const char* name;
+    int cap;
+    bool partition;
+  };
+  const Case cases[] = {{"unmasked_full_grid", 0, false}, {"unmasked_cap32", 32, false}, {"partitioned_last32", 32, true}};
+  for (const Case& cs : cases) {
+    hipStream_t verify, lane;
+    if (cs.partition) {
+      verify = make_masked([](int cu, int cus) { return cu >= cus - 32; });
+      lane = make_masked([](int cu, int cus) { return cu < cus - 32; });
+    } else {
+      CHECK(hipStreamCreateWithFlags(&verify, hipStreamNonBlocking));
+      lane = make_stream(0, true);
+    }
+    std::vector<float> alone_here;
+    rccl_run(lane, std::min(secs, 3.0), alone_here);
+    std::atomic<bool> stop{false};
+    std::atomic<int64_t> issued{0};
+    std::vector<hipEvent_t> done(kRing);
+    for (auto& e : done) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int64_t stalls = 0;
+    std::thread th([&] {
+      auto next = std::chrono::steady_clock::now();
+      for (int64_t b = 0; !stop.load(); ++b) {
+        std::this_thread::sleep_until(next);
+        next += std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(period_s));
+        const int slot = int(b % kRing);
+        if (b >= kRing && hipEventQuery(done[size_t(slot)]) == hipErrorNotReady) {
+          ++stalls;
+          CHECK(hipEventSynchronize(done[size_t(slot)]));
+        }
+        dissem::kern::CrcItem it[nchunks];
+        for (int64_t c = 0; c < nchunks; ++c)
+          it[c] = dissem::kern::CrcItem{buf + c * chunk, chunk, crc + slot * nchunks + c};
+        CHECK(dissem::kern::crc32c_batch(it, int(nchunks), ws + size_t(slot) * wsb, verify, cs.cap));
+        CHECK(hipEventRecord(done[size_t(slot)], verify));
+        issued.store(b + 1);
+      }
+    });
+    std::vector<float> beside;
+    rccl_run(lane, secs, beside);
+    stop.store(true);
+    th.join();
+    int pending = 0;
+    for (auto& e : done)
+      if (hipEventQuery(e) == hipErrorNotReady) ++pending;
+    CHECK(hipStreamSynchronize(verify));
+    printf("{\"case\": \"rccl_self_p2p_beside_verify\", \"layout\": \"%s\", \"land_GBps\": %.0f, \"crc_grid_cap\": %d, "
+           "\"GBps_alone_here_p50\": %.1f, \"GBps_p50\": %.1f, \"GBps_p10\": %.1f, \"vs_alone\": %.3f, "
+           "\"verified_GBps\": %.1f, \"ring_stalls\": %lld, \"pending_at_end\": %d}\n",
+           cs.name, land_gbps, cs.cap, pct(alone_here, 0.5), pct(beside, 0.5), pct(beside, 0.1),
+           pct(beside, 0.5) / pct(alone_here, 0.5), double(issued.load()) * double(chunk * nchunks) / secs / 1e9,
+           (long long)stalls, pending);
+    fflush(stdout);
+    for (auto& e : done) CHECK(hipEventDestroy(e));
+    CHECK(hipStreamDestroy(verify));
+    CHECK(hipStreamDestroy(lane));
+  }
+  NCHECK(ncclCommDestroy(comm));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   int trials = 40, reserve = 32;
   double paced_s = 0, land_gbps = 450;
   if (argc > 1 && std::string(argv[1]) == "-cumap") return cumap();
+  if (argc > 2 && std::string(argv[1]) == "-rccl") return rccl_paced(atof(argv[2]), argc > 4 ? atof(argv[4]) : 450);
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string a = argv[i];
     if (a == "-trials") trials = atoi(argv[i + 1]);

@@ -165,7 +165,8 @@ case "$RECIPE" in
   r4contention)
     # continuous verification at the landing rate of 7 links (450 GB/s) beside a 64-workgroup copy, per CRC grid cap
     timeout -k 10 120 bin/contention -cumap > $OUT/cumap.jsonl 2>&1 &&
-    timeout -k 10 400 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1
+    timeout -k 10 400 bin/contention -paced 10 -gbps 450 > $OUT/paced.jsonl 2>&1 &&
+    timeout -k 10 240 bin/contention -rccl 8 -gbps 450 > $OUT/rccl_paced.jsonl 2> $OUT/rccl_paced.log
     ;;
   r4sweep)
     # fused store 7/8/9 against the source size (tail of the one-segment-per-wave grid), then the
