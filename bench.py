@@ -434,6 +434,9 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["store"] = args.store
         if last is not None and last.engine_stats:
             out["config"]["engine_stats_rank0"] = last.engine_stats
+            vb = last.engine_stats.get("verify_busy_ms")
+            if vb is not None and last.seconds > 0:  # occupancy of the verify CUs in the last session
+                out["config"]["verify_busy_frac_rank0"] = round(vb / (last.seconds * 1e3), 3)
         if plans:
             # the leader's plan inside the timed window (reference: node.go:1161-1165 starts the
             # timer before the solve, :1225-1231 logs its computation time)

@@ -300,6 +300,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("nacks", &PlannedStats::nacks)
       .def_readonly("injected", &PlannedStats::injected)
       .def_readonly("issue_ms", &PlannedStats::issue_ms)
+      .def_readonly("verify_busy_ms", &PlannedStats::verify_busy_ms)
       .def_readonly("peer_sent", &PlannedStats::peer_sent)
       .def_readonly("peer_recv", &PlannedStats::peer_recv)
       .def_readonly("group_us_hist", &PlannedStats::group_us_hist)

@@ -1406,8 +1406,10 @@ void PlannedEngine::poll() {
       }
     }
     {
+      const double vms = backend_->group_ms(it->ev);
       std::lock_guard<std::mutex> lk(stats_mu_);
       stats_.land_us_hist[log2_bucket(it->t0)] += int64_t(it->pieces.size());
+      if (vms > 0) stats_.verify_busy_ms += vms;
     }
     backend_->release(it->ev);
     it = verifies_.erase(it);

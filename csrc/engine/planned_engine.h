@@ -162,6 +162,9 @@ struct PlannedStats {
   int64_t paced = 0;  // issue attempts a token bucket deferred
   double disk_wait_ms = 0;  // time disk reads waited for the node-wide read budget
   int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
+  // device time the verify stream spent on checks (landing met -> check done):
+  // against the session's wall time, the occupancy of the verify CUs
+  double verify_busy_ms = 0;
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
   std::vector<int64_t> group_us_hist = std::vector<int64_t>(32, 0);  // P2P group issue -> complete
   std::vector<int64_t> land_us_hist = std::vector<int64_t>(32, 0);   // chunk issue -> landed + verified

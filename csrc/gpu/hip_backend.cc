@@ -311,19 +311,26 @@ class HipBackend : public Backend {
     return hipEventElapsedTime(&ms, it->second, ev(e)) == hipSuccess ? double(ms) : -1;
   }
 
+  // Verify work is timed like a group (group_ms): from where the verify
+  // stream reaches it (its landing met) to its end - the engine sums that into
+  // verify_busy_ms, the verify CUs' occupancy.
   Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
     if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
+    hipEvent_t start = timed();
+    HIP_OK(hipEventRecord(start, verify_));
     if (n > 0) {
       if (n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
       HIP_OK(kern::crc32c_chunks_capped(p, n, n, crc_dev_ + slot, ws_, verify_, crc_grid_));
     }
-    return record(verify_);
+    return timed_end(verify_, start);
   }
 
   Ev crc_batch(const std::vector<CrcReq>& reqs, Ev after) override {
     // One segments + one fold launch per kCrcBatchMax landed chunks (instead of
     // two launches per chunk): fewer LDS table fills and partially empty grids.
     if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
+    hipEvent_t start = timed();
+    HIP_OK(hipEventRecord(start, verify_));
     std::vector<kern::CrcItem> items;
     for (size_t i = 0; i <= reqs.size(); ++i) {
       if (i == reqs.size() || items.size() == size_t(kern::kCrcBatchMax)) {
@@ -335,16 +342,18 @@ class HipBackend : public Backend {
       if (r.n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
       if (r.n > 0) items.push_back(kern::CrcItem{r.p, r.n, crc_dev_ + r.slot});
     }
-    return record(verify_);
+    return timed_end(verify_, start);
   }
 
   Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out, uint32_t slot,
                    Ev after) override {
     if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
     if (src_len > cfg_.max_crc_bytes) throw std::runtime_error("verify_unpack chunk larger than the verify workspace");
+    hipEvent_t start = timed();
+    HIP_OK(hipEventRecord(start, verify_));
     HIP_OK(kern::fp8_verify_unpack(packed, src_len, src_chunk, block, reinterpret_cast<uint16_t*>(out), crc_dev_ + slot,
                                    ws_, verify_, crc_grid_));
-    return record(verify_);
+    return timed_end(verify_, start);
   }
 
   int query(Ev e) override {
@@ -497,6 +506,13 @@ class HipBackend : public Backend {
     }
     HIP_OK(hipEventRecord(e, s));
     return reinterpret_cast<Ev>(e);
+  }
+  Ev timed_end(hipStream_t s, hipEvent_t start) {
+    hipEvent_t end = timed();
+    HIP_OK(hipEventRecord(end, s));
+    const Ev e = reinterpret_cast<Ev>(end);
+    starts_[e] = start;
+    return e;
   }
   hipEvent_t timed() {
     hipEvent_t e;
