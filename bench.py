@@ -437,6 +437,9 @@ def worker(args, world, rank, chan) -> int:
             vb = last.engine_stats.get("verify_busy_ms")
             if vb is not None and last.seconds > 0:  # occupancy of the verify CUs in the last session
                 out["config"]["verify_busy_frac_rank0"] = round(vb / (last.seconds * 1e3), 3)
+            st = last.engine_stats.get("bytes_staged")
+            if st and last.seconds > 0:  # this rank's host -> HBM rate over the session (PCIe bound: ~57 GB/s)
+                out["config"]["stage_GBps_rank0"] = round(st / last.seconds / 1e9, 2)
         if plans:
             # the leader's plan inside the timed window (reference: node.go:1161-1165 starts the
             # timer before the solve, :1225-1231 logs its computation time)
