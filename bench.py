@@ -53,8 +53,10 @@ def parse_args(argv=None):
     p.add_argument("--timeout", type=float, default=120.0,
                    help="seconds one session (step) may take before the rank gives up (also the P2P group timeout)")
     p.add_argument("--pull-window", type=int, default=0,
-                   help="mode 2 jobs in flight per sender (0 = 2 x peers: the next layers stage over PCIe while "
-                        "the current ones cross the links; sim sweep at N=8: 7 -> 264 ms, 14 -> 241, 21 -> 273)")
+                   help="mode 2 jobs in flight per sender (0 = one per peer; round-4 sim at N=8, 50 GB/s links, "
+                        "closed loop on: 7 -> 265 ms, 10 -> 294, 14 -> 388 - with more jobs than links the "
+                        "concurrent transfers share each link and the busy-time estimate reads it low; round 2, "
+                        "before the closed loop: 14 -> 241, profiles/r4_predict_mode2.jsonl)")
     p.add_argument("--storage", default="", help="disk tier directory")
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0: scatter+relay P2P, ncclBroadcast, or leader fan-out")
@@ -332,7 +334,7 @@ def worker(args, world, rank, chan) -> int:
         rt.observe_probe({p: g * 1e9 for p, g in probe.get("concurrent", {}).items() if g})
 
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
-    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, 2 * (world - 1)),
+    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1),
                   owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective",
                   adapt_links=not args.no_adapt_links, hierarchical=not args.no_hierarchical)

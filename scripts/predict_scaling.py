@@ -288,6 +288,8 @@ def main() -> int:
     ap.add_argument("--probe-mib", type=int, default=256, help="pre-flight link probe at full size, as bench.py (0: none)")
     ap.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
                     help="mode 1's owner choice (bench.py's default: links)")
+    ap.add_argument("--pull-window", type=int, default=0,
+                    help="mode 2: jobs in flight per sender (0: N - 1; bench.py's default is 2 (N - 1))")
     args = ap.parse_args()
     common = dict(steps=args.steps, warmup=args.warmup, probe_mib=args.probe_mib)
     _core.set_log_level(3)
@@ -312,7 +314,8 @@ def main() -> int:
             r = predict(n, link_gbps=lg, pcie_gbps=args.pcie_gbps, scale=args.scale, lanes=args.lanes, mode=args.mode,
                         slowdown=args.slowdown, layers=args.layers, layer_bytes=args.layer_mib << 20, pack=args.pack,
                         tier=args.tier, disk_gbps=args.disk_gbps, hosts=args.hosts, nic_gbps=args.nic_gbps,
-                        policy={"owner_policy": args.owner_policy, "hierarchical": not args.flat}, **common)
+                        policy={"owner_policy": args.owner_policy, "hierarchical": not args.flat,
+                                **({"pull_window": args.pull_window} if args.pull_window else {})}, **common)
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
             if args.pack == "none" and args.hosts == 1:
