@@ -79,8 +79,6 @@ def parse_args(argv=None):
                         "4 CUs on each XCD, when N > 1 - 128 with --store bf16 - and 0 alone; 0: all shared). "
                         "bin/contention: a 64-workgroup copy keeps 99.6 %% of its rate beside 450 GB/s of verify "
                         "on the last 32 CUs (profiles/r4_contention)")
-    p.add_argument("--crc-grid", type=int, default=-1,
-                   help="workgroup cap of the CRC verify kernels (-1/0: every CU of the verify stream)")
     p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
     p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
     p.add_argument("--lanes", type=int, default=0,
@@ -331,7 +329,8 @@ def worker(args, world, rank, chan) -> int:
             failed(str(e))
         log(f"link probe: {probe.get('probe_ms')} ms; concurrent GB/s {probe.get('concurrent')}")
         # the probe's concurrent rates floor the closed-loop link capacities (B/s)
-        rt.observe_probe({p: g * 1e9 for p, g in probe.get("concurrent", {}).items() if g})
+        rt.observe_probe({p: g * 1e9 for p, g in probe.get("concurrent", {}).items() if g},
+                         {p: g * 1e9 for p, g in probe.get("concurrent_in", {}).items() if g})
 
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
     policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1),

@@ -261,7 +261,6 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("inject_seed", &PlannedConfig::inject_seed)
       .def_readwrite("group_timeout_s", &PlannedConfig::group_timeout_s)
       .def_readwrite("reserve_cus", &PlannedConfig::reserve_cus)
-      .def_readwrite("crc_grid", &PlannedConfig::crc_grid)
       .def_readwrite("verify_cus", &PlannedConfig::verify_cus)
       .def_readwrite("suspect_s", &PlannedConfig::suspect_s)
       .def_readwrite("inject_die_after_groups", &PlannedConfig::inject_die_after_groups)
@@ -310,6 +309,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("aborted_pieces", &PlannedStats::aborted_pieces)
       .def_readonly("peer_busy_ms", &PlannedStats::peer_busy_ms)
       .def_readonly("peer_send_busy_ms", &PlannedStats::peer_send_busy_ms)
+      .def_readonly("peer_recv_busy_ms", &PlannedStats::peer_recv_busy_ms)
       .def_readonly("lane_busy_ms", &PlannedStats::lane_busy_ms)
       .def_readonly("lanes", &PlannedStats::lanes)
       .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)
@@ -472,6 +472,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("job_min_rate", &NodeConfig::job_min_rate)
       .def_readwrite("max_redispatch", &NodeConfig::max_redispatch)
       .def_readwrite("link_report", &NodeConfig::link_report)
+      .def_readwrite("link_report_in", &NodeConfig::link_report_in)
       .def_readwrite("adapt_links", &NodeConfig::adapt_links)
       .def_readwrite("disk_group", &NodeConfig::disk_group)
       .def_readwrite("disk_group_bw", &NodeConfig::disk_group_bw)

@@ -193,6 +193,11 @@ Json encode_payload(const Message& m) {
         for (auto& kv : m.link_rates) lr[std::to_string(kv.first)] = Json(kv.second);
         p["LinkRates"] = lr;
       }
+      if (!m.link_rates_in.empty()) {  // inbound links timed at the receiving end
+        Json lr = Json::object();
+        for (auto& kv : m.link_rates_in) lr[std::to_string(kv.first)] = Json(kv.second);
+        p["LinkRatesIn"] = lr;
+      }
       if (!m.partial_layers.empty()) {
         Json part = Json::object();
         for (auto& kv : m.partial_layers) {
@@ -602,6 +607,9 @@ MessagePtr decode_envelope(const Json& env) {
       }
       if (auto* lr = p.find("LinkRates"); lr && lr->is_object())
         for (auto& kv : lr->as_object()) m->link_rates[NodeID(strtoull(kv.first.c_str(), nullptr, 10))] = kv.second.as_i64();
+      if (auto* lr = p.find("LinkRatesIn"); lr && lr->is_object())
+        for (auto& kv : lr->as_object())
+          m->link_rates_in[NodeID(strtoull(kv.first.c_str(), nullptr, 10))] = kv.second.as_i64();
       break;
     case MsgType::XferBatch:
       m->batch = p.get_u64("Batch");

@@ -93,6 +93,7 @@ struct Message {
   std::map<LayerID, CrcManifest> manifest;
   PartialLayers partial_layers;  // Announce extension: layers held only in these byte ranges
   std::map<NodeID, int64_t> link_rates;  // Announce extension: sender's measured rate to each peer (B/s)
+  std::map<NodeID, int64_t> link_rates_in;  // ... and each peer's link INTO the sender, timed at this end (B/s)
   // Simple
   std::string src_addr, payload_str;
 

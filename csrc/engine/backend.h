@@ -70,29 +70,21 @@ class Backend {
   // comm lane (fault injection): overwrite 4 bytes at p behind everything
   // queued so far on the lane, e.g. a chunk a group just received
   virtual Ev corrupt(uint8_t* p, int lane = 0) = 0;
-  // verify queue: after `after`, CRC32C of [p, p+n) into result slot `slot`
-  // (n == 0: just an ordering marker on the verify queue)
-  virtual Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) = 0;
-  // verify queue: after `after`, CRC32C of several independent buffers (the
-  // chunks one P2P group landed) into their result slots; one event for all.
-  struct CrcReq {
+  // verify queue: wait for `waits`, then check every request - all of them in
+  // one event (one launch per kCrcBatchMax requests on GPUs, the fold inside
+  // it): the CRC32C of [p, p+n) into result slot `slot`. A request with `out`
+  // is an fp8-packed chunk (core/fp8.h layout of `n` bf16 SOURCE bytes with
+  // `block`-element scales): its packed bytes are checked and dequantized to
+  // `out` in the same pass (the fused kernel). No requests: an ordering
+  // marker on the verify queue.
+  struct CheckReq {
     const uint8_t* p;
     int64_t n;
     uint32_t slot;
+    uint8_t* out = nullptr;
+    int block = 0;
   };
-  virtual Ev crc_batch(const std::vector<CrcReq>& reqs, Ev after) {
-    Ev last = 0;
-    for (auto& r : reqs) {
-      if (last) release(last);
-      last = crc(r.p, r.n, r.slot, after);
-    }
-    return last ? last : crc(nullptr, 0, 0, after);
-  }
-  // verify queue: after `after`, the fused check + dequantization of one packed
-  // chunk (core/fp8.h layout of `src_len` bf16 source bytes on a `src_chunk`
-  // grid): CRC32C of the packed bytes into `slot`, bf16 values to `out`.
-  virtual Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out,
-                           uint32_t slot, Ev after) = 0;
+  virtual Ev verify(const std::vector<CheckReq>& reqs, const std::vector<Ev>& waits) = 0;
   virtual int query(Ev e) = 0;  // 1 done, 0 pending, -1 failed
   virtual void release(Ev e) = 0;
   virtual uint32_t crc_result(uint32_t slot) = 0;

@@ -516,12 +516,11 @@ bool PlannedEngine::stage_paced(Layer& L, LayerID id, int64_t c) {
   return false;
 }
 
-Ev PlannedEngine::unpack_chunk(Layer& L, int64_t c, uint32_t slot, Ev after) {
+Backend::CheckReq PlannedEngine::unpack_req(Layer& L, int64_t c, uint32_t slot) {
   const int64_t src_total = fp8::source_size(L.size, cfg_.chunk_bytes, cfg_.pack_block);
   if (!L.out) L.out = backend_->alloc(src_total);
   const int64_t slen = std::min(cfg_.chunk_bytes, src_total - c * cfg_.chunk_bytes);
-  return backend_->verify_unpack(L.dev + c * grid_, slen, cfg_.chunk_bytes, cfg_.pack_block,
-                                 L.out + c * cfg_.chunk_bytes, slot, after);
+  return Backend::CheckReq{L.dev + c * grid_, slen, slot, L.out + c * cfg_.chunk_bytes, cfg_.pack_block};
 }
 
 void PlannedEngine::partial_landed(Layer& L, const Piece& p, std::vector<Verify>& out) {
@@ -542,16 +541,16 @@ void PlannedEngine::partial_landed(Layer& L, const Piece& p, std::vector<Verify>
   L.part.erase(p.chunk);
   Verify v;
   uint32_t slot = ~0u;
+  std::vector<Backend::CheckReq> reqs;
   if (cfg_.unpack_store) {
     const uint32_t s = crc_slot();
-    v.ev = unpack_chunk(L, f.chunk, s, 0);
+    reqs.push_back(unpack_req(L, f.chunk, s));
     if (f.has_crc) slot = s;
   } else if (f.has_crc) {
     slot = crc_slot();
-    v.ev = backend_->crc(L.dev + a, b - a, slot, 0);
-  } else {
-    v.ev = backend_->crc(nullptr, 0, 0, 0);
+    reqs.push_back(Backend::CheckReq{L.dev + a, b - a, slot});
   }
+  v.ev = backend_->verify(reqs, {});
   v.pieces.push_back(f);
   v.slots.push_back(slot);
   out.push_back(std::move(v));
@@ -741,7 +740,6 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   set_chunk_ev(L, c, e);
   Piece p{Kind::Local, 0, 0, cfg_.rank, id, off, len, L.size, c, true};
   p.src_node = self_node_;
-  Verify v;
   // The chunk's expected CRC: this rank's manifest of the layer, or - for a
   // layer it stages from a node-shared host copy it did not generate - the
   // CRC the leader put in the job.
@@ -754,6 +752,11 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
     want = jc->second;
     known = true;
   }
+  // The check joins the staging batch (flush_stage_checks): one verify launch
+  // per kVerifyBatch staged chunks instead of one per chunk.
+  StageCheck sc;
+  sc.ev = e;
+  ev_hold(e);
   if (cfg_.unpack_store) {
     // fused: check the packed chunk and write its bf16 image (one pass)
     const bool check = cfg_.verify && known;
@@ -761,21 +764,20 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
       p.has_crc = true;
       p.crc = want;
     }
-    uint32_t slot = crc_slot();
-    v.ev = unpack_chunk(L, c, slot, e);
-    v.slots.push_back(check ? slot : ~0u);
+    const uint32_t slot = crc_slot();
+    sc.req = unpack_req(L, c, slot);
+    sc.has_req = true;
+    sc.slot = check ? slot : ~0u;
   } else if (cfg_.verify && known) {
     p.has_crc = true;
     p.crc = want;
-    uint32_t slot = crc_slot();
-    v.ev = backend_->crc(L.dev + off, len, slot, e);
-    v.slots.push_back(slot);
-  } else {
-    v.ev = backend_->crc(nullptr, 0, 0, e);
-    v.slots.push_back(~0u);
+    sc.slot = crc_slot();
+    sc.req = Backend::CheckReq{L.dev + off, len, sc.slot};
+    sc.has_req = true;
   }
-  v.pieces.push_back(p);
-  verifies_.push_back(std::move(v));
+  sc.piece = p;
+  stage_checks_.push_back(sc);
+  if (stage_checks_.size() >= size_t(kVerifyBatch)) flush_stage_checks();
   if (bounce) {
     // The bounce buffer is free again once its H2D copy has landed - not after
     // the chunk's CRC check: the verify queue is in order, and a check queued
@@ -786,6 +788,24 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   }
   std::lock_guard<std::mutex> lk(stats_mu_);
   stats_.bytes_staged += slen;
+}
+
+void PlannedEngine::flush_stage_checks() {
+  if (stage_checks_.empty()) return;
+  Verify v;
+  v.t0 = stage_checks_.front().t0;
+  std::vector<Backend::CheckReq> reqs;
+  std::vector<Ev> waits;
+  for (auto& sc : stage_checks_) {
+    if (sc.has_req) reqs.push_back(sc.req);
+    if (std::find(waits.begin(), waits.end(), sc.ev) == waits.end()) waits.push_back(sc.ev);
+    v.pieces.push_back(sc.piece);
+    v.slots.push_back(sc.slot);
+  }
+  v.ev = backend_->verify(reqs, waits);
+  for (auto& sc : stage_checks_) ev_drop(sc.ev);
+  stage_checks_.clear();
+  verifies_.push_back(std::move(v));
 }
 
 int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed) {
@@ -1088,6 +1108,9 @@ bool PlannedEngine::issue_lane(int lane) {
       if (p.kind == Kind::Send && !p.bcast &&
           std::find(inf.send_peers.begin(), inf.send_peers.end(), p.peer) == inf.send_peers.end())
         inf.send_peers.push_back(p.peer);
+      if (p.kind == Kind::Recv && !p.bcast &&
+          std::find(inf.recv_peers.begin(), inf.recv_peers.end(), p.peer) == inf.recv_peers.end())
+        inf.recv_peers.push_back(p.peer);
     }
     infl.push_back(std::move(inf));
     // Fault injection: damage some received chunks behind the group, before their check.
@@ -1107,8 +1130,8 @@ bool PlannedEngine::issue_lane(int lane) {
     // verify queue. With one lane a later send of the chunk is ordered behind
     // `g` on the same queue; with several, it waits for a mark on this lane.
     Verify v;
-    Ev last = 0, mark = 0;
-    std::vector<Backend::CrcReq> checks;
+    Ev mark = 0;
+    std::vector<Backend::CheckReq> checks;
     for (auto& p : group) {
       if (p.kind != Kind::Recv) continue;
       Layer& L = layers_[p.layer];
@@ -1125,31 +1148,24 @@ bool PlannedEngine::issue_lane(int lane) {
       }
       uint32_t slot = ~0u;
       if (cfg_.unpack_store && p.full) {
-        // fused check + dequantization of the landed packed chunk, per chunk
+        // fused check + dequantization of the landed packed chunk
         const uint32_t s = crc_slot();
-        if (last) backend_->release(last);
-        last = unpack_chunk(L, p.chunk, s, landed_ev);
+        checks.push_back(unpack_req(L, p.chunk, s));
         if (cfg_.verify && p.has_crc) slot = s;
       } else if (cfg_.verify && p.has_crc && p.full) {
         slot = crc_slot();
-        checks.push_back(Backend::CrcReq{L.dev + p.off, p.len, slot});
+        checks.push_back(Backend::CheckReq{L.dev + p.off, p.len, slot});
       }
       v.pieces.push_back(p);
       v.slots.push_back(slot);
     }
-    // Every chunk this group landed is checked by one batched launch (behind
-    // any fused unpacks, which share the verify queue).
-    if (!v.pieces.empty() && (!checks.empty() || !last)) {
-      if (last) backend_->release(last);
-      last = backend_->crc_batch(checks, landed_ev);
+    // Every chunk this group landed is checked by one batched verify (one
+    // launch per kVerifyBatch chunks, the fold inside it).
+    if (!v.pieces.empty()) {
+      v.ev = backend_->verify(checks, {landed_ev});
+      verifies_.push_back(std::move(v));
     }
     if (landed_ev != g) backend_->release(landed_ev);
-    if (!v.pieces.empty()) {
-      v.ev = last;
-      verifies_.push_back(std::move(v));
-    } else if (last) {
-      backend_->release(last);
-    }
     {
       std::lock_guard<std::mutex> lk(stats_mu_);
       stats_.groups++;
@@ -1261,6 +1277,11 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
     backend_->release(v.ev);
   }
   verifies_.clear();
+  for (auto& sc : stage_checks_) {
+    aborted++;
+    ev_drop(sc.ev);
+  }
+  stage_checks_.clear();
   for (auto& b : bounce_busy_) {  // every queue drained in the backend's shrink: the copies are done
     ev_drop(b.first);
     bounce_free_.push_back(b.second);
@@ -1310,6 +1331,7 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
 }
 
 void PlannedEngine::poll() {
+  flush_stage_checks();  // what this pass staged: one batched check
   const auto now = std::chrono::steady_clock::now();
   for (int lane = 0; lane < lanes_; ++lane) {
     auto& infl = inflight_[size_t(lane)];
@@ -1352,6 +1374,7 @@ void PlannedEngine::poll() {
           stats_.lane_busy_ms[size_t(lane)] += ms;
           for (int p : head.peers) stats_.peer_busy_ms[p] += ms;
           for (int p : head.send_peers) stats_.peer_send_busy_ms[p] += ms;
+          for (int p : head.recv_peers) stats_.peer_recv_busy_ms[p] += ms;
         }
       }
       backend_->release(head.ev);
@@ -1520,6 +1543,8 @@ void PlannedEngine::run() {
         for (auto& q : ops_) q.clear();
         for (auto& q : inflight_) q.clear();
         verifies_.clear();
+        for (auto& sc : stage_checks_) ev_drop(sc.ev);
+        stage_checks_.clear();
         local_wait_.clear();
         std::lock_guard<std::mutex> lk(req_mu_);
         busy_ = false;

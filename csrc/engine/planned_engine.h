@@ -111,7 +111,6 @@ struct PlannedConfig {
   // behind a burst of CRC launches that fills every CU's LDS (tools/contention).
   // -1: 32 when world > 1, 0 on one rank (no RCCL traffic). Ignored when verify_cus > 0.
   int reserve_cus = -1;
-  int crc_grid = -1;  // verify kernels' workgroup cap (-1: the verify stream's CUs; 0: all)
   // CUs of the verify stream, the last ones of the mask; RCCL and copies get the
   // rest (HipBackendConfig::verify_cus). -1: 32 (4 CUs on each XCD) with peers,
   // 128 when every landing is also unpacked (unpack_store), 0 (all CUs shared) alone.
@@ -154,6 +153,11 @@ struct PlannedStats {
   // device time of completed groups involving each peer / on each lane (ms)
   std::map<int, double> peer_busy_ms;
   std::map<int, double> peer_send_busy_ms;  // groups that sent to the peer (the directed link's own time)
+  // groups that received from the peer: the same link timed at its other end.
+  // A send's time includes waiting for its receive to be posted and a receive's
+  // waiting for its send, so the closed loop takes the faster of the two ends
+  // per link (Runtime.link_capacity): the later poster times the transfer alone.
+  std::map<int, double> peer_recv_busy_ms;
   std::vector<double> lane_busy_ms;
   int lanes = 1;
   double comm_init_ms = 0, comm_connect_ms = 0;
@@ -285,6 +289,14 @@ class PlannedEngine : public DataEngine {
     std::vector<Piece> pieces;
     std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
   };
+  struct StageCheck {  // a staged chunk whose check waits for the staging batch
+    Piece piece;
+    Ev ev = 0;                  // its staging copy (held)
+    uint32_t slot = ~0u;        // result slot, ~0u = not verified
+    bool has_req = false;
+    Backend::CheckReq req{};
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  };
   struct DiskRead {  // chunk of a disk-tier layer: pread into a bounce buffer, then H2D
     LayerID layer;
     int64_t chunk, file_off, len;
@@ -314,6 +326,7 @@ class PlannedEngine : public DataEngine {
     std::chrono::steady_clock::time_point t0;
     std::vector<int> peers;  // partner ranks
     std::vector<int> send_peers;  // ranks it sends to (point-to-point)
+    std::vector<int> recv_peers;  // ranks it receives from (point-to-point)
   };
   struct Pace {  // token bucket, non-blocking (burst: one chunk; mode-3 jobs two, see pace_ready)
     double rate = 0, tokens = 0, burst = 0;
@@ -331,7 +344,7 @@ class PlannedEngine : public DataEngine {
       if (!q.empty()) return false;
     for (auto& q : inflight_)
       if (!q.empty()) return false;
-    return verifies_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty() &&
+    return verifies_.empty() && stage_checks_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty() &&
            bounce_busy_.empty();
   }
   int lane_for(int peer, bool send) const {
@@ -370,8 +383,10 @@ class PlannedEngine : public DataEngine {
   void partial_landed(Layer& L, const Piece& p, std::vector<Verify>& out);
   void nack(const Piece& p, Layer& L, uint32_t got);
   uint32_t crc_slot();
-  // unpack_store: the fused check of chunk c (packed at L.dev) into its bf16 slot, after `after`.
-  Ev unpack_chunk(Layer& L, int64_t c, uint32_t slot, Ev after);
+  // unpack_store: the fused check of chunk c (packed at L.dev) into its bf16 slot.
+  Backend::CheckReq unpack_req(Layer& L, int64_t c, uint32_t slot);
+  // Launch the checks of the chunks staged since the last flush as one verify.
+  void flush_stage_checks();
   void fail(const std::string& what);
   int64_t src_len(const Layer& L, int64_t c) const;  // source bytes of chunk c
   int64_t src_grid(const Layer& L) const { return cfg_.pack == 1 && !L.src_packed ? cfg_.chunk_bytes : grid_; }
@@ -396,6 +411,7 @@ class PlannedEngine : public DataEngine {
   std::vector<std::deque<Piece>> ops_;          // per lane, key order
   std::vector<std::deque<Inflight>> inflight_;  // per lane
   std::deque<Verify> verifies_;
+  std::vector<StageCheck> stage_checks_;  // staged chunks whose checks are not launched yet
   std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
   std::deque<std::pair<LayerID, int64_t>> local_wait_;  // local promotions deferred by tier pacing
   // keys of the queued (not yet posted) sends of each chunk: relay cuts, and
@@ -458,5 +474,9 @@ class PlannedEngine : public DataEngine {
 };
 
 constexpr uint32_t kCrcSlots = 1u << 16;
+// Chunks per verify launch (kern::kCrcBatchMax): at 64 MiB source chunks a
+// batch of 16 is 1 GiB of bf16 per launch, where the fused kernel runs at
+// its streaming rate; one chunk alone fills less than a round of the chip.
+constexpr int kVerifyBatch = 16;
 
 }  // namespace dissem

@@ -50,6 +50,9 @@ struct Posted {
   bool done = false;
   bool bad = false;
   Clock::time_point done_at{};  // timing model: when the link finishes this transfer
+  Clock::time_point posted = Clock::now();
+  double injected_s = 0;  // fault injection: this post came that late (SimTiming::recv_delay_s)
+  double model_s = 0;     // modeled device time of the op (see Fabric::post)
 };
 
 struct Fabric {
@@ -102,7 +105,9 @@ struct Fabric {
           // NIC ingress as two queues of their own (a packet network keeps both
           // ends busy; a transfer waiting on one end never idles the other).
           // The transfer is done when its last queue is.
-          const auto now = Clock::now();
+          // both ends posted: the transfer may start (timed from the posts
+          // themselves, not from when this thread got the fabric's lock)
+          const auto now = std::max(s->posted, r->posted);
           const auto dur = std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(s->len) / bps));
           auto& free_at = link_free[{src, dst}];
           free_at = std::max(now, free_at) + dur;
@@ -115,6 +120,16 @@ struct Fabric {
             done = std::max({done, o, i});
           }
           s->done_at = r->done_at = done;
+          // Modeled device time of each op: from the later of the two posts
+          // (the transfer cannot start before both ends are there) to the end
+          // on its link - queueing behind the link's earlier transfers
+          // included - plus, for a send, any wait the fault injection put on
+          // its receive. How late the simulator's own threads got to either
+          // post never enters it, so rates derived from it (the closed loop's
+          // busy throughput) are the same on an idle or a loaded host.
+          const double span = std::chrono::duration<double>(done - std::max(s->posted, r->posted)).count();
+          s->model_s = span + r->injected_s;
+          r->model_s = span;
         }
       }
       s->done = r->done = true;
@@ -357,13 +372,19 @@ class SimBackend : public Backend {
           return;
         }
       }
-      const auto t0 = Clock::now();
+      double injected = 0;
       if (auto rd = fab->timing.recv_delay_s.find(rank); rd != fab->timing.recv_delay_s.end() && rd->second > 0)
         for (auto& o : ops)
           if (!o.send && !o.bcast) {
             std::this_thread::sleep_for(std::chrono::duration<double>(rd->second));
+            injected = rd->second;
             break;
           }
+      auto mk = [&](const XOp& o) {
+        auto p = std::make_unique<Posted>(Posted{o.ptr, o.len});
+        if (!o.send) p->injected_s = injected;
+        return p;
+      };
       std::vector<std::unique_ptr<Posted>> posted;
       // Optional RCCL round model: ops grouped by ring distance, each round
       // waits for the previous one (collectives stay in round 0).
@@ -388,11 +409,11 @@ class SimBackend : public Backend {
           if (o.peer == rank) {
             for (int r = 0; r < world_; ++r)
               if (r != rank) {
-                posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
+                posted.push_back(mk(o));
                 fab->post(lane, rank, r, true, posted.back().get());
               }
           } else {
-            posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
+            posted.push_back(mk(o));
             fab->post(lane, o.peer, rank, false, posted.back().get());
           }
           continue;
@@ -402,7 +423,7 @@ class SimBackend : public Backend {
           ev->state = -1;
           return;
         }
-        posted.push_back(std::make_unique<Posted>(Posted{o.ptr, o.len}));
+        posted.push_back(mk(o));
         if (o.send) fab->post(lane, rank, o.peer, true, posted.back().get());
         else fab->post(lane, o.peer, rank, false, posted.back().get());
       }
@@ -421,7 +442,11 @@ class SimBackend : public Backend {
         ev->state = -1;
         return;
       }
-      ev->ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+      // The group's device time: its longest op in the model (ops of one group
+      // run concurrently; with the timing model off, transfers take no time).
+      double ms = 0;
+      for (auto& p : posted) ms = std::max(ms, p->model_s * 1e3);
+      ev->ms = ms;
       ev->state = 1;
     });
     return id;
@@ -432,35 +457,29 @@ class SimBackend : public Backend {
     return ev && ev->state.load() > 0 ? ev->ms : -1;
   }
 
-  Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
+  Ev verify(const std::vector<CheckReq>& reqs, const std::vector<Ev>& waits) override {
     auto [id, ev] = make_event();
-    auto dep = lookup(after);
-    verify_.push([=] {
-      if (dep && !wait_event(dep, fab_->timing.wait_s)) {
-        ev->state = -1;
-        return;
-      }
-      if (n > 0) results_[slot] = crc32c(p, size_t(n));
-      ev->state = 1;
-    });
-    return id;
-  }
-
-  Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out, uint32_t slot,
-                   Ev after) override {
-    auto [id, ev] = make_event();
-    auto dep = lookup(after);
+    std::vector<std::shared_ptr<SimEvent>> deps;
+    for (Ev w : waits)
+      if (w) deps.push_back(lookup(w));
     const bool copy = fab_->timing.copy_bytes;
     verify_.push([=] {
-      if (dep && !wait_event(dep, fab_->timing.wait_s)) {
-        ev->state = -1;
-        return;
+      for (auto& d : deps)
+        if (!d || !wait_event(d, fab_->timing.wait_s)) {
+          ev->state = -1;
+          return;
+        }
+      for (const CheckReq& r : reqs) {
+        if (r.n <= 0) continue;
+        if (!r.out) {
+          results_[r.slot] = crc32c(r.p, size_t(r.n));
+          continue;
+        }
+        const int64_t n = r.n / 2;  // fp8 values of the chunk
+        results_[r.slot] = crc32c(r.p, size_t(fp8::packed_len(r.n, r.block)));
+        if (copy)
+          fp8::unpack_host(r.p, reinterpret_cast<const float*>(r.p + n), n, reinterpret_cast<uint16_t*>(r.out), r.block);
       }
-      (void)src_chunk;
-      const int64_t n = src_len / 2;
-      const int64_t plen = fp8::packed_len(src_len, block);
-      results_[slot] = crc32c(packed, size_t(plen));
-      if (copy) fp8::unpack_host(packed, reinterpret_cast<const float*>(packed + n), n, reinterpret_cast<uint16_t*>(out), block);
       ev->state = 1;
     });
     return id;

@@ -52,6 +52,7 @@ std::vector<uint32_t> crc_chunks_sync(uint64_t ptr, int64_t bytes, int64_t chunk
   if (s.ws_bytes < need) {
     if (s.ws) check(hipFree(s.ws), "hipFree");
     check(hipMalloc(&s.ws, need), "hipMalloc");
+    check(hipMemset(s.ws, 0, need), "hipMemset");  // fold words: zeroed once (kernels.h)
     s.ws_bytes = need;
   }
   size_t n = size_t(bytes > 0 ? (bytes + chunk - 1) / chunk : 0);
@@ -151,6 +152,8 @@ void register_gpu_bindings(PyObject* module) {
     check(hipStreamSynchronize(work), "sync");
     void* ws = nullptr;
     check(hipMalloc(&ws, kern::crc32c_workspace_bytes(bytes, bytes)), "hipMalloc");
+    check(hipMemsetAsync(ws, 0, kern::crc32c_workspace_bytes(bytes, bytes), work), "hipMemsetAsync");
+    check(hipStreamSynchronize(work), "sync");
     check(kern::spin_until(flag_dev, max_iters, iters, blocked), "spin");
     const auto t0 = std::chrono::steady_clock::now();
     check(kern::crc32c_chunks(data, bytes, bytes, out, ws, work), "crc32c_chunks");
@@ -291,50 +294,51 @@ void register_gpu_bindings(PyObject* module) {
     py::gil_scoped_release nogil;
     return crc_chunks_sync(ptr, n, chunk, stream);
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("stream") = 0);
-  // max_blocks caps the segment kernel's grid (0: one workgroup per CU)
+  // Asynchronous forms take a caller-owned workspace of the size the
+  // *_workspace_bytes helper names, zeroed once before its first use (every
+  // launch leaves it zeroed). `cus`: CUs the stream may use (0: all).
   m.def("crc32c_chunks_async", [](uint64_t ptr, int64_t n, int64_t chunk, uint64_t out_dev, uint64_t ws,
-                                  uint64_t stream, int max_blocks) {
-    check(kern::crc32c_chunks_capped(reinterpret_cast<const void*>(ptr), n, chunk,
-                                     reinterpret_cast<uint32_t*>(out_dev), reinterpret_cast<void*>(ws),
-                                     as_stream(stream), max_blocks),
+                                  uint64_t stream, int cus) {
+    check(kern::crc32c_chunks(reinterpret_cast<const void*>(ptr), n, chunk, reinterpret_cast<uint32_t*>(out_dev),
+                              reinterpret_cast<void*>(ws), as_stream(stream), cus),
           "crc32c_chunks");
   }, py::arg("ptr"), py::arg("nbytes"), py::arg("chunk_bytes"), py::arg("out"), py::arg("workspace"),
-     py::arg("stream") = 0, py::arg("max_blocks") = 0);
+     py::arg("stream") = 0, py::arg("cus") = 0);
   m.def("crc32c_workspace_bytes", &kern::crc32c_workspace_bytes);
+  m.def("crc32c_batch_workspace_bytes", [] { return kern::crc32c_batch_workspace_bytes(); });
+  m.def("crc32c_batch_max", [] { return kern::kCrcBatchMax; });
   // Batched CRC of independent device buffers [(ptr, nbytes), ...] (synchronous).
-  // max_blocks: cap on the segment kernel's grid (0 = one workgroup per CU)
-  m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream, int max_blocks) {
+  m.def("crc32c_batch", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t stream, int cus) {
     py::gil_scoped_release nogil;
     if (bufs.size() > size_t(kern::kCrcBatchMax)) throw std::invalid_argument("too many buffers for one batch");
-    int64_t mx = 0;
-    for (auto& b : bufs) mx = std::max(mx, b.second);
     void* ws = nullptr;
     uint32_t *host = nullptr, *dev = nullptr;
-    check(hipMalloc(&ws, kern::crc32c_batch_workspace_bytes(mx, int(bufs.size()))), "hipMalloc");
+    check(hipMalloc(&ws, kern::crc32c_batch_workspace_bytes()), "hipMalloc");
+    check(hipMemset(ws, 0, kern::crc32c_batch_workspace_bytes()), "hipMemset");
     check(hipHostMalloc(reinterpret_cast<void**>(&host), std::max<size_t>(bufs.size(), 1) * 4, hipHostMallocMapped),
           "hipHostMalloc");
     check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
     std::vector<kern::CrcItem> items;
     for (size_t i = 0; i < bufs.size(); ++i)
       items.push_back(kern::CrcItem{reinterpret_cast<const void*>(bufs[i].first), bufs[i].second, dev + i});
-    hipError_t e = kern::crc32c_batch(items.data(), int(items.size()), ws, as_stream(stream), max_blocks);
+    hipError_t e = kern::crc32c_batch(items.data(), int(items.size()), ws, as_stream(stream), cus);
     if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
     std::vector<uint32_t> out(host, host + bufs.size());
     (void)hipFree(ws);
     (void)hipHostFree(host);
     check(e, "crc32c_batch");
     return out;
-  }, py::arg("buffers"), py::arg("stream") = 0, py::arg("max_blocks") = 0);
+  }, py::arg("buffers"), py::arg("stream") = 0, py::arg("cus") = 0);
   m.def("crc32c_batch_async", [](const std::vector<std::pair<uint64_t, int64_t>>& bufs, uint64_t out_dev, uint64_t ws,
-                                 uint64_t stream) {
+                                 uint64_t stream, int cus) {
+    if (bufs.size() > size_t(kern::kCrcBatchMax)) throw std::invalid_argument("too many buffers for one batch");
     std::vector<kern::CrcItem> items;
     for (size_t i = 0; i < bufs.size(); ++i)
       items.push_back(kern::CrcItem{reinterpret_cast<const void*>(bufs[i].first), bufs[i].second,
                                     reinterpret_cast<uint32_t*>(out_dev) + i});
-    check(kern::crc32c_batch(items.data(), int(items.size()), reinterpret_cast<void*>(ws), as_stream(stream)),
+    check(kern::crc32c_batch(items.data(), int(items.size()), reinterpret_cast<void*>(ws), as_stream(stream), cus),
           "crc32c_batch");
-  });
-  m.def("crc32c_batch_workspace_bytes", &kern::crc32c_batch_workspace_bytes);
+  }, py::arg("buffers"), py::arg("out"), py::arg("workspace"), py::arg("stream") = 0, py::arg("cus") = 0);
   m.def("fp8_pack", [](uint64_t bf16, int64_t n, uint64_t fp8, uint64_t scales, int block, uint64_t stream) {
     check(kern::fp8_pack(reinterpret_cast<const uint16_t*>(bf16), n, reinterpret_cast<uint8_t*>(fp8),
                          reinterpret_cast<float*>(scales), block, as_stream(stream)),
@@ -353,31 +357,31 @@ void register_gpu_bindings(PyObject* module) {
   }, py::arg("src"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("dst"),
         py::arg("stream") = 0);
   m.def("fp8_verify_unpack_async", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block,
-                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream, int store,
-                                      int max_blocks) {
+                                      uint64_t out, uint64_t crc_out_dev, uint64_t ws, uint64_t stream, int cus) {
     check(kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
                                   reinterpret_cast<uint16_t*>(out), reinterpret_cast<uint32_t*>(crc_out_dev),
-                                  reinterpret_cast<void*>(ws), as_stream(stream), max_blocks, store),
+                                  reinterpret_cast<void*>(ws), as_stream(stream), cus),
           "fp8_verify_unpack");
   }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
-     py::arg("crc_out"), py::arg("ws"), py::arg("stream") = 0, py::arg("store") = -1, py::arg("max_blocks") = 0);
+     py::arg("crc_out"), py::arg("ws"), py::arg("stream") = 0, py::arg("cus") = 0);
   // Fused verify + unpack (synchronous): writes the bf16 layer to `out`, returns
   // the CRC32C of every packed chunk.
   m.def("fp8_verify_unpack", [](uint64_t packed, int64_t src_bytes, int64_t src_chunk, int block, uint64_t out,
-                                uint64_t stream, int max_blocks, int store) {
+                                uint64_t stream, int cus) {
     py::gil_scoped_release nogil;
     const int64_t pbytes = fp8::packed_size(src_bytes, src_chunk, block);
     const int64_t pchunk = fp8::packed_chunk(src_chunk, block);
     const size_t n = size_t((pbytes + pchunk - 1) / pchunk);
     void* ws = nullptr;
     uint32_t *host = nullptr, *dev = nullptr;
-    check(hipMalloc(&ws, kern::crc32c_workspace_bytes(pbytes, pchunk)), "hipMalloc");
+    const size_t wsb = kern::crc32c_workspace_bytes(pbytes, pchunk);
+    check(hipMalloc(&ws, wsb), "hipMalloc");
+    check(hipMemset(ws, 0, wsb), "hipMemset");
     check(hipHostMalloc(reinterpret_cast<void**>(&host), std::max<size_t>(n, 1) * 4, hipHostMallocMapped),
           "hipHostMalloc");
     check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
     hipError_t e = kern::fp8_verify_unpack(reinterpret_cast<const void*>(packed), src_bytes, src_chunk, block,
-                                           reinterpret_cast<uint16_t*>(out), dev, ws, as_stream(stream), max_blocks,
-                                           store);
+                                           reinterpret_cast<uint16_t*>(out), dev, ws, as_stream(stream), cus);
     if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
     std::vector<uint32_t> crc(host, host + n);
     (void)hipFree(ws);
@@ -385,7 +389,52 @@ void register_gpu_bindings(PyObject* module) {
     check(e, "fp8_verify_unpack");
     return crc;
   }, py::arg("packed"), py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block"), py::arg("out"),
-        py::arg("stream") = 0, py::arg("max_blocks") = 0, py::arg("store") = -1);
+        py::arg("stream") = 0, py::arg("cus") = 0);
+  // Batched fused verify + unpack of independent packed chunks
+  // [(packed_ptr, src_len, out_ptr), ...]: the engine's launch for the chunks
+  // one P2P group or staging batch landed. _async writes CRCs to crc_out[i].
+  auto fused_items = [](const std::vector<std::tuple<uint64_t, int64_t, uint64_t>>& items, uint32_t* crc) {
+    if (items.size() > size_t(kern::kCrcBatchMax)) throw std::invalid_argument("too many chunks for one batch");
+    std::vector<kern::FusedItem> v;
+    for (size_t i = 0; i < items.size(); ++i)
+      v.push_back(kern::FusedItem{reinterpret_cast<const void*>(std::get<0>(items[i])), std::get<1>(items[i]),
+                                  reinterpret_cast<uint16_t*>(std::get<2>(items[i])), crc + i});
+    return v;
+  };
+  m.def("fp8_verify_unpack_batch_async", [fused_items](const std::vector<std::tuple<uint64_t, int64_t, uint64_t>>& items,
+                                                       int block, uint64_t crc_out_dev, uint64_t ws, uint64_t stream,
+                                                       int cus) {
+    auto v = fused_items(items, reinterpret_cast<uint32_t*>(crc_out_dev));
+    check(kern::fp8_verify_unpack_batch(v.data(), int(v.size()), block, reinterpret_cast<void*>(ws), as_stream(stream),
+                                        cus),
+          "fp8_verify_unpack_batch");
+  }, py::arg("items"), py::arg("block"), py::arg("crc_out"), py::arg("ws"), py::arg("stream") = 0, py::arg("cus") = 0);
+  m.def("fp8_verify_unpack_batch", [fused_items](const std::vector<std::tuple<uint64_t, int64_t, uint64_t>>& items,
+                                                 int block, uint64_t stream, int cus) {
+    py::gil_scoped_release nogil;
+    void* ws = nullptr;
+    uint32_t *host = nullptr, *dev = nullptr;
+    check(hipMalloc(&ws, kern::crc32c_batch_workspace_bytes()), "hipMalloc");
+    check(hipMemset(ws, 0, kern::crc32c_batch_workspace_bytes()), "hipMemset");
+    check(hipHostMalloc(reinterpret_cast<void**>(&host), std::max<size_t>(items.size(), 1) * 4, hipHostMallocMapped),
+          "hipHostMalloc");
+    check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
+    hipError_t e = hipSuccess;
+    try {
+      auto v = fused_items(items, dev);
+      e = kern::fp8_verify_unpack_batch(v.data(), int(v.size()), block, ws, as_stream(stream), cus);
+    } catch (...) {
+      (void)hipFree(ws);
+      (void)hipHostFree(host);
+      throw;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(as_stream(stream));
+    std::vector<uint32_t> crc(host, host + items.size());
+    (void)hipFree(ws);
+    (void)hipHostFree(host);
+    check(e, "fp8_verify_unpack_batch");
+    return crc;
+  }, py::arg("items"), py::arg("block") = 128, py::arg("stream") = 0, py::arg("cus") = 0);
 
   // ---- RCCL path on one GPU: a one-rank communicator driven through the same
   // Backend::group / crc calls the planned engine issues. `rounds` groups of
@@ -396,7 +445,7 @@ void register_gpu_bindings(PyObject* module) {
     if (bytes <= 0 || chunk <= 0 || chunk % 16) throw std::invalid_argument("bytes > 0, chunk % 16 == 0");
     HipBackendConfig hc;
     hc.device = device;
-    hc.max_crc_bytes = bytes;
+    hc.max_chunk_bytes = bytes;
     hc.self_comm = true;
     auto be = make_hip_backend(hc);
     be->init_thread();
@@ -442,12 +491,11 @@ void register_gpu_bindings(PyObject* module) {
     hc.rank = cfg.rank;
     hc.world = cfg.world;
     hc.nccl_uid = std::string(uid);
-    hc.max_crc_bytes = cfg.chunk_bytes;
+    hc.max_chunk_bytes = cfg.chunk_bytes;
     hc.reserve_cus = cfg.reserve_cus >= 0 ? cfg.reserve_cus : (cfg.world > 1 ? 32 : 0);
     // with peers the verify owns the last 32 CUs (128 with the fused unpack) and
     // RCCL the rest (hip_backend.h verify_cus)
     hc.verify_cus = cfg.verify_cus >= 0 ? cfg.verify_cus : (cfg.world > 1 ? (cfg.unpack_store ? 128 : 32) : 0);
-    hc.crc_grid = std::max(0, cfg.crc_grid);
     hc.nccl_min_ctas = cfg.nccl_min_ctas;
     hc.nccl_max_ctas = cfg.nccl_max_ctas;
     hc.nccl_register = cfg.nccl_register;

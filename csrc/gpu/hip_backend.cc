@@ -62,24 +62,23 @@ class HipBackend : public Backend {
     if ((cfg_.world == 1 && !cfg_.self_comm) || keep_free > 0)
       copy2_ = create_stream_reserving(cfg_.device, keep_free);
     verify_ = part > 0 ? create_stream_on_last(cfg_.device, part) : create_stream_reserving(cfg_.device, cfg_.reserve_cus);
-    // The CRC kernels run one workgroup per CU (144 KiB of LDS tables each): on
-    // the masked verify stream a 256-workgroup grid would leave the last
-    // reserve_cus workgroups for a second wave, so cap it at the stream's CUs.
+    // The verify kernels size the last round of their grid for the CUs the
+    // verify stream may use (kernels.h `cus`).
     {
       int cus = 0;
       HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-      crc_grid_ = part > 0 ? std::min(part, cus)
-                  : cfg_.reserve_cus > 0 && cfg_.reserve_cus < cus ? cus - cfg_.reserve_cus : 0;
-      if (cfg_.crc_grid > 0) crc_grid_ = crc_grid_ > 0 ? std::min(crc_grid_, cfg_.crc_grid) : cfg_.crc_grid;
+      verify_cus_ = part > 0 ? std::min(part, cus)
+                    : cfg_.reserve_cus > 0 && cfg_.reserve_cus < cus ? cus - cfg_.reserve_cus : 0;
     }
-    HIP_OK(hipMalloc(&ws_, std::max(kern::crc32c_workspace_bytes(cfg_.max_crc_bytes, cfg_.max_crc_bytes),
-                                     kern::crc32c_batch_workspace_bytes(cfg_.max_crc_bytes, kern::kCrcBatchMax))));
+    // The fold words of one verify launch ({acc, count} per item): zeroed once,
+    // every launch leaves them zeroed (kernels.h).
+    HIP_OK(hipMalloc(&ws_, kern::crc32c_batch_workspace_bytes()));
+    HIP_OK(hipMemsetAsync(ws_, 0, kern::crc32c_batch_workspace_bytes(), verify_));
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&crc_host_), kCrcSlots * sizeof(uint32_t),
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&crc_dev_), crc_host_, 0));
-    // CRC tables and the full-chunk fold tables before any RCCL traffic (the
-    // packed grid too when fp8 chunks may be checked)
-    HIP_OK(kern::crc32c_warm(cfg_.max_crc_bytes, verify_));
+    // CRC tables before any RCCL traffic
+    HIP_OK(kern::crc32c_warm(verify_));
     HIP_OK(hipStreamSynchronize(verify_));
     if (cfg_.world > 1 || cfg_.self_comm) {
       std::string ids = cfg_.nccl_uid;
@@ -260,7 +259,7 @@ class HipBackend : public Backend {
       HIP_OK(hipStreamSynchronize(s));
       if (scratch_[q]) HIP_OK(hipFree(scratch_[q]));
       scratch_[q] = nullptr;
-      const int64_t want = std::max(n_src, cfg_.max_crc_bytes);
+      const int64_t want = std::max(n_src, cfg_.max_chunk_bytes);
       HIP_OK(hipMalloc(&scratch_[q], size_t(want)));
       scratch_bytes_[q] = want;
     }
@@ -312,47 +311,41 @@ class HipBackend : public Backend {
   }
 
   // Verify work is timed like a group (group_ms): from where the verify
-  // stream reaches it (its landing met) to its end - the engine sums that into
-  // verify_busy_ms, the verify CUs' occupancy.
-  Ev crc(const uint8_t* p, int64_t n, uint32_t slot, Ev after) override {
-    if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
+  // stream reaches it (its landings met) to its end - the engine sums that into
+  // verify_busy_ms, the verify CUs' occupancy. Plain checks and fused
+  // check+unpacks go out as batched launches of up to kCrcBatchMax chunks
+  // each (a 64 MiB chunk alone fills less than one round of the chip).
+  Ev verify(const std::vector<CheckReq>& reqs, const std::vector<Ev>& waits) override {
+    for (Ev w : waits)
+      if (w) HIP_OK(hipStreamWaitEvent(verify_, ev(w), 0));
     hipEvent_t start = timed();
     HIP_OK(hipEventRecord(start, verify_));
-    if (n > 0) {
-      if (n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
-      HIP_OK(kern::crc32c_chunks_capped(p, n, n, crc_dev_ + slot, ws_, verify_, crc_grid_));
-    }
-    return timed_end(verify_, start);
-  }
-
-  Ev crc_batch(const std::vector<CrcReq>& reqs, Ev after) override {
-    // One segments + one fold launch per kCrcBatchMax landed chunks (instead of
-    // two launches per chunk): fewer LDS table fills and partially empty grids.
-    if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
-    hipEvent_t start = timed();
-    HIP_OK(hipEventRecord(start, verify_));
-    std::vector<kern::CrcItem> items;
-    for (size_t i = 0; i <= reqs.size(); ++i) {
-      if (i == reqs.size() || items.size() == size_t(kern::kCrcBatchMax)) {
-        if (!items.empty()) HIP_OK(kern::crc32c_batch(items.data(), int(items.size()), ws_, verify_, crc_grid_));
-        items.clear();
-        if (i == reqs.size()) break;
+    std::vector<kern::CrcItem> plain;
+    std::vector<kern::FusedItem> fused;
+    int block = 0;
+    auto flush_plain = [&] {
+      if (!plain.empty()) HIP_OK(kern::crc32c_batch(plain.data(), int(plain.size()), ws_, verify_, verify_cus_));
+      plain.clear();
+    };
+    auto flush_fused = [&] {
+      if (!fused.empty())
+        HIP_OK(kern::fp8_verify_unpack_batch(fused.data(), int(fused.size()), block, ws_, verify_, verify_cus_));
+      fused.clear();
+    };
+    for (const CheckReq& r : reqs) {
+      if (r.n <= 0) continue;
+      if (r.out) {
+        if (block && r.block != block) flush_fused();
+        block = r.block;
+        fused.push_back(kern::FusedItem{r.p, r.n, reinterpret_cast<uint16_t*>(r.out), crc_dev_ + r.slot});
+        if (fused.size() == size_t(kern::kCrcBatchMax)) flush_fused();
+      } else {
+        plain.push_back(kern::CrcItem{r.p, r.n, crc_dev_ + r.slot});
+        if (plain.size() == size_t(kern::kCrcBatchMax)) flush_plain();
       }
-      const CrcReq& r = reqs[i];
-      if (r.n > cfg_.max_crc_bytes) throw std::runtime_error("crc span larger than the verify workspace");
-      if (r.n > 0) items.push_back(kern::CrcItem{r.p, r.n, crc_dev_ + r.slot});
     }
-    return timed_end(verify_, start);
-  }
-
-  Ev verify_unpack(const uint8_t* packed, int64_t src_len, int64_t src_chunk, int block, uint8_t* out, uint32_t slot,
-                   Ev after) override {
-    if (after) HIP_OK(hipStreamWaitEvent(verify_, ev(after), 0));
-    if (src_len > cfg_.max_crc_bytes) throw std::runtime_error("verify_unpack chunk larger than the verify workspace");
-    hipEvent_t start = timed();
-    HIP_OK(hipEventRecord(start, verify_));
-    HIP_OK(kern::fp8_verify_unpack(packed, src_len, src_chunk, block, reinterpret_cast<uint16_t*>(out), crc_dev_ + slot,
-                                   ws_, verify_, crc_grid_));
+    flush_fused();
+    flush_plain();
     return timed_end(verify_, start);
   }
 
@@ -537,8 +530,8 @@ class HipBackend : public Backend {
   void* probe_ = nullptr;  // connect_all() scratch
   std::map<Ev, hipEvent_t> starts_;  // timed group end -> its start event
   std::vector<hipEvent_t> timed_pool_;
-  void* ws_ = nullptr;
-  int crc_grid_ = 0;  // CRC segment-kernel grid cap: the verify stream's CUs (0 = all)
+  void* ws_ = nullptr;  // fold words of the verify launches
+  int verify_cus_ = 0;  // CUs of the verify stream (0 = all): kernels.h `cus`
   void* scratch_[2] = {nullptr, nullptr};  // bf16 landing chunk for stage_pack, per copy queue
   int64_t scratch_bytes_[2] = {0, 0};
   uint32_t* crc_host_ = nullptr;

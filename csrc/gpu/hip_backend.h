@@ -27,17 +27,13 @@ struct HipBackendConfig {
   int rank = 0;
   int world = 1;
   std::string nccl_uid;  // ncclUniqueId bytes (world > 1): one id, or one per lane (parallel init)
-  int64_t max_crc_bytes = 64ll << 20;  // largest chunk the verify workspace must hold
+  int64_t max_chunk_bytes = 64ll << 20;  // largest source chunk staged (sizes the fp8 packing scratch)
   // world == 1: still build a one-rank communicator, so P2P groups to self
   // exercise the RCCL path on a single-GPU box (rccl_selftest)
   bool self_comm = false;
   // > 0: the verify and copy streams get a CU mask that leaves this many CUs
   // free for the comm stream's RCCL kernels (hipExtStreamCreateWithCUMask).
   int reserve_cus = 0;
-  // Workgroup cap of the CRC verify kernels (0: every CU the verify stream
-  // has). A narrow verify sharing CUs with RCCL hurts it more than a short
-  // full-chip one (bin/contention -paced, profiles/r4_contention/).
-  int crc_grid = 0;
   // > 0: the verify stream runs on the LAST verify_cus CU-mask bits only and
   // every comm lane and copy stream on the others, so no CRC workgroup shares a
   // CU with an RCCL kernel. Mask bit i is CU i / 8 of XCD i mod 8 (bin/contention
@@ -47,7 +43,7 @@ struct HipBackendConfig {
   // 64-workgroup copy keeps 99.6 % of its alone rate beside 450 GB/s of
   // continuous verification on the last 32 bits, against 93.8 % beside an
   // unmasked full-grid verify and 85.6 % beside a 32-workgroup one. Overrides
-  // reserve_cus; the CRC grid is capped at verify_cus.
+  // reserve_cus; the verify kernels size their grid's last round for verify_cus.
   int verify_cus = 0;
   int nccl_min_ctas = 0, nccl_max_ctas = 0;  // 0: RCCL default
   int lanes = 1;                               // comm lanes (communicator + stream each)

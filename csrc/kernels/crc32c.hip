@@ -67,6 +67,7 @@
 #include <cstring>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "core/crc32c.h"
@@ -85,16 +86,16 @@ constexpr int kBlocksPerSeg = kSegBytes / kBlockBytes;  // 4
 constexpr int kGapBytes = kBlockBytes - kPieceBytes;    // between a lane's pieces
 constexpr uint32_t kShLds = 131072;                     // shift tables after the byte tables
 constexpr uint32_t kLdsBytes = kShLds + 8 * 16 * 128;   // 144 KiB
-constexpr uint32_t kStageBytes = 16 * 1024;              // fused unpack: 1 KiB output staging per wave
-constexpr int kThreads = 1024;                          // one workgroup per CU, 4 waves per SIMD
-constexpr int kWaves = kThreads / 64;
 // Global constants: [T: 4 x 256 (T[k][v]: byte v then k zero bytes)]
 // [gap: 8 x 16 nibble tables of the kGapBytes shift][pow16: 1024 (x^(8*16 m))]
 // [lanepow: 64 (x^(8*64*(63-l)): lane l's last piece to its segment end)]
-// [segpow: kMaxSegs (x^(8*16 KiB*j))].
-constexpr int kMaxSegs = 65536;  // segments per chunk: chunks up to 1 GiB
+// [segpow: 3 levels x 1024 (x^(8*16 KiB*i*1024^L)): x^(8*16 KiB*j) for any j
+// below 2^30 is the product of at most three entries - chunks up to 16 TiB
+// (one 1 GiB-chunk table capped a single CRC at 1 GiB in round 4)].
+constexpr int kSegLevels = 3, kSegLevel = 1024;
+constexpr int64_t kMaxSegs = int64_t(1) << (10 * kSegLevels);
 constexpr int kT = 0, kGap = 1024, kPow = kGap + 128, kLanePow = kPow + 1024, kSegPow = kLanePow + 64,
-              kConstWords = kSegPow + kMaxSegs;
+              kConstWords = kSegPow + kSegLevels * kSegLevel;
 
 using u32x4_t = unsigned int __attribute__((ext_vector_type(4)));
 
@@ -219,7 +220,6 @@ struct Slice4T {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
 };
-using Slice4 = Slice4T<32>;
 
 // In-register 4x4 transpose across the 4 rows (16 lanes each) of a wave and 4
 // registers: afterwards register q of lane m + 16 r holds what register r of
@@ -247,20 +247,22 @@ struct Seg {
   int64_t len;          // bytes (16 KiB except a chunk's last)
   int64_t chunk, chunk_start, chunk_len, seg_start;
   uint32_t xrem;        // x^(8 * (chunk_len mod 16 KiB))
+  uint16_t* out;        // the chunk's bf16 output (fused unpack), else nullptr
 };
 
 // A segment's raw CRC (at its own end) shifted to its chunk's end: what the
 // segment adds to the chunk's raw CRC, so the fold is a plain XOR over the
 // chunk's segments. Full segment k of a chunk with nfull full ones and a short
-// tail of rem bytes moves over (nfull - 1 - k) segments (segpow) and rem bytes
-// (xrem, skipped when rem = 0); the short tail segment already ends there.
-// Every operand is wave-uniform: one or two 32-step products per segment, off
-// the loads' critical path (the separate shift-and-fold launch took 7.4 us
-// per 512 MiB, profiles/r4_kernels).
+// tail of rem bytes moves over j = nfull - 1 - k segments (segpow, one entry
+// per 10 bits of j) and rem bytes (xrem, skipped when rem = 0); the short tail
+// segment already ends there. Every operand is wave-uniform (scalar ALU work,
+// off the loads' critical path).
 __device__ __forceinline__ uint32_t to_chunk_end(const Seg& sg, uint32_t s, const uint32_t* __restrict__ sc) {
   if (sg.len != kSegBytes) return s;
-  const int64_t nfull = sg.chunk_len / kSegBytes, k = sg.seg_start / kSegBytes;
-  uint32_t m = sc[kSegPow + (nfull - 1 - k)];
+  const int64_t nfull = sg.chunk_len / kSegBytes, k = sg.seg_start / kSegBytes, j = nfull - 1 - k;
+  uint32_t m = sc[kSegPow + (j & (kSegLevel - 1))];
+  if (j >> 10) m = multmodp_unrolled(m, sc[kSegPow + kSegLevel + ((j >> 10) & (kSegLevel - 1))]);
+  if (j >> 20) m = multmodp_unrolled(m, sc[kSegPow + 2 * kSegLevel + (j >> 20)]);
   if (sg.chunk_len % kSegBytes) m = multmodp_unrolled(m, sg.xrem);
   return multmodp_unrolled(m, s);
 }
@@ -344,109 +346,20 @@ __device__ __forceinline__ uint32_t seg_full(u32x4_t (&w)[4 * kBlocksPerSeg], co
   return s;
 }
 
-// Every wave walks segments g = wave, wave + nwaves, ... (geo(g) -> Seg) and
-// writes seg_out[g]: the segment's raw CRC shifted to its chunk's end. A wave
-// that owns several segments loads block b of the next one as soon as block b
-// of the current one is consumed (pinned with sched_barrier: left alone, the
-// compiler sinks those loads behind the math), so 16 KiB stay in flight per
-// wave. Visit sees every 16-B word (as loaded, before the transpose) with its
-// byte offset in the chunk.
-// CRC = false (diagnostic A/B only: its segment values are garbage) keeps the
-// walk, the loads and the visits and drops the CRC math.
-template <class Geo, class Visit, bool CRC = true>
-__device__ __forceinline__ void slice_walk(const Geo& geo, int64_t total_segs, const uint32_t* __restrict__ sc,
-                                           const Slice4& st, Visit& visit, uint32_t* __restrict__ seg_out,
-                                           int waves_per_wg = kWaves) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave =
-      __builtin_amdgcn_readfirstlane(int(blockIdx.x * waves_per_wg + ((threadIdx.x >> 6) % waves_per_wg)));
-  const int64_t nwaves = int64_t(gridDim.x) * waves_per_wg;
-  const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
-  int64_t g = wave;
-  if (g >= total_segs) return;
-  Seg cur = geo(g);
-  // invariant at the loop top: w holds cur's words if cur is a full segment
-  u32x4_t w[4 * kBlocksPerSeg];
-  {
-    const auto r = seg_rsrc(cur.p, cur.len == kSegBytes);
-    visit.prefetch(cur, cur.len == kSegBytes);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {  // in order: every path issues w[0..15] oldest first
-      w[i] = seg_load(r, lo, i);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    visit.advance();
-  }
-  for (; g < total_segs; g += nwaves) {
-    const int64_t gn = g + nwaves;
-    Seg nxt = cur;  // no next segment: loads against an empty resource
-    bool nfull = false;
-    if (gn < total_segs) {
-      nxt = geo(gn);
-      nfull = nxt.len == kSegBytes;
-    }
-    const auto rn = seg_rsrc(nxt.p, nfull);
-    visit.begin(cur);
-    uint32_t s;
-    if (cur.len == kSegBytes) {
-      // (written out rather than through seg_full: the fused kernel sits at the
-      // 128-VGPR cap here, and the helper's form spilled 8 bytes per lane)
-      const uint32_t rowc = sc[kLanePow + lane];
-      s = 0;
-#pragma unroll
-      for (int b = 0; b < kBlocksPerSeg; ++b) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) visit.word(w[4 * b + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo, 4 * b + j);
-        if constexpr (CRC) {
-          row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
-          s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
-#pragma unroll
-          for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (b == 0) {  // the next segment's scales go out ahead of its data
-          visit.prefetch(nxt, nfull);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[4 * b + j] = seg_load(rn, lo, 4 * b + j);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (CRC) s = wave_xor_dpp(multmodp_unrolled(rowc, s));
-    } else {
-      s = slice_partial(cur, sc, st, lane, visit);
-    }
-    if (lane == 0) seg_out[g] = to_chunk_end(cur, s, sc);
-    if (cur.len != kSegBytes) {  // (rare) w did not take the next segment's words yet
-      visit.prefetch(nxt, nfull);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
-        w[i] = seg_load(rn, lo, i);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    visit.advance();
-    cur = nxt;
-  }
-}
 
-// One segment per wave (no walk): the wave issues its segment's loads (and
-// the scales) BEFORE the workgroup fills the LDS tables, then runs the
-// segment and exits. On gfx9 one in-order counter (vmcnt) covers loads and
-// stores, so a walking wave's next loads, issued behind its stores, cannot be
-// waited for without those stores completing: a persistent read->write walk
-// moved 512 MiB of bf16 in 160 us where one-segment waves took 139 and a
-// plain one-shot grid 131 (bin/walkprobe, profiles/r4_walk*/). Here a CU
-// streams many short-lived waves instead, and the table fill is paid per
-// workgroup of kWaves segments.
-template <class Geo, class Visit, bool CRC = true, int R = 32, int WAVES = kWaves>
-__device__ __forceinline__ void slice_once(const Geo& geo, int64_t total_segs, const uint32_t* __restrict__ sc,
-                                           uint8_t* lds, Visit& visit, uint32_t* __restrict__ seg_out) {
+// One segment per wave: the wave issues its segment's loads (and the scales)
+// BEFORE the workgroup fills the LDS tables, then runs the segment and exits.
+// On gfx9 one in-order counter (vmcnt) covers loads and stores, so a walking
+// wave's next loads, issued behind its stores, cannot be waited for without
+// those stores completing: a persistent read->write walk moved 512 MiB of bf16
+// in 160 us where one-segment waves took 139 and a plain one-shot grid 131
+// (bin/walkprobe, profiles/r4_walk*/). A CU streams many short-lived waves
+// instead, and the table fill is paid per workgroup of WAVES segments.
+// Returns the segment's value at its chunk's end (to_chunk_end).
+template <class Geo, class Visit, int R, int WAVES>
+__device__ __forceinline__ uint32_t slice_once(const Geo& geo, int64_t g, bool have, const uint32_t* __restrict__ sc,
+                                               uint8_t* lds, Visit& visit) {
   const int lane = threadIdx.x & 63;
-  const int64_t g = int64_t(blockIdx.x) * WAVES + (threadIdx.x >> 6);
-  const bool have = g < total_segs;
   const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
   Seg cur = have ? geo(g) : geo(0);
   const bool full = have && cur.len == kSegBytes;
@@ -463,13 +376,13 @@ __device__ __forceinline__ void slice_once(const Geo& geo, int64_t total_segs, c
     visit.advance();
   }
   load_lds<R>(lds, sc);  // every wave joins the fill and its barrier
-  if (!have) return;
+  if (!have) return 0;
   const Slice4T<R> st(lds);
   visit.begin(cur);
   uint32_t s;
-  if (full) s = seg_full<Visit, CRC>(w, cur, st, visit, sc + kLanePow, lo, [](int) {});
+  if (full) s = seg_full<Visit, true>(w, cur, st, visit, sc + kLanePow, lo, [](int) {});
   else s = slice_partial(cur, sc, st, lane, visit);
-  if (lane == 0) seg_out[g] = to_chunk_end(cur, s, sc);
+  return to_chunk_end(cur, s, sc);
 }
 
 // Half a segment per wave, for the grid's last, partial round (see
@@ -498,7 +411,7 @@ __device__ __forceinline__ void half_load(const Seg& cur, bool full, Visit& visi
   visit.advance();
 }
 
-template <int H, class Visit, bool CRC, int R>
+template <int H, class Visit, int R>
 __device__ __forceinline__ uint32_t half_seg(const Seg& cur, bool have, bool full, const uint32_t* __restrict__ sc,
                                              const uint8_t* lds, Visit& visit, u32x4_t (&w)[8]) {
   const int lane = threadIdx.x & 63;
@@ -514,17 +427,13 @@ __device__ __forceinline__ uint32_t half_seg(const Seg& cur, bool have, bool ful
         const int b = 2 * H + bb;
 #pragma unroll
         for (int j = 0; j < 4; ++j) visit.word(w[4 * bb + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo, 4 * b + j);
-        if constexpr (CRC) {
-          row_transpose(w[4 * bb], w[4 * bb + 1], w[4 * bb + 2], w[4 * bb + 3]);
-          s = bb ? st.gap(s, w[4 * bb][0]) : w[4 * bb][0];
+        row_transpose(w[4 * bb], w[4 * bb + 1], w[4 * bb + 2], w[4 * bb + 3]);
+        s = bb ? st.gap(s, w[4 * bb][0]) : w[4 * bb][0];
 #pragma unroll
-          for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * bb + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
-        }
+        for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * bb + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
       }
-      if constexpr (CRC) {
-        s = wave_xor_dpp(multmodp_unrolled(sc[kLanePow + lane], s));
-        if constexpr (H == 0) s = multmodp_unrolled(sc[kPow + (kSegBytes / 2) / 16], s);
-      }
+      s = wave_xor_dpp(multmodp_unrolled(sc[kLanePow + lane], s));
+      if constexpr (H == 0) s = multmodp_unrolled(sc[kPow + (kSegBytes / 2) / 16], s);
       v = s;
     } else if constexpr (H == 0) {
       v = slice_partial(cur, sc, st, lane, visit);
@@ -535,55 +444,23 @@ __device__ __forceinline__ uint32_t half_seg(const Seg& cur, bool have, bool ful
 
 // The second half's value goes through LDS word xch[stride * pair]: the
 // second wave's own staging slot when there is one (two 80 KiB workgroups
-// fill the CU's 160 KiB: not one more word to spare).
-template <class Geo, class Visit, bool CRC = true, int R = 32, int WAVES = kWaves>
-__device__ __forceinline__ void slice_half(const Geo& geo, int64_t total_segs, int64_t g0,
-                                           const uint32_t* __restrict__ sc, uint8_t* lds, Visit& visit,
-                                           uint32_t* __restrict__ seg_out, uint32_t* xch, int stride) {
+// fill the CU's 160 KiB: not one more word to spare). Returns the pair's
+// segment value (at its chunk's end) on the first wave, 0 on the second.
+template <class Geo, class Visit, int R>
+__device__ __forceinline__ uint32_t slice_half(const Geo& geo, int64_t g, bool have, const uint32_t* __restrict__ sc,
+                                               uint8_t* lds, Visit& visit, uint32_t* xch, int stride) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = wave & 1;
-  const int64_t g = g0 + (wave >> 1);
-  const bool have = g < total_segs;
   const Seg cur = have ? geo(g) : geo(0);
   const bool full = have && cur.len == kSegBytes;
   u32x4_t w[8];
   if (h) half_load<1>(cur, full, visit, w);
   else half_load<0>(cur, full, visit, w);
   load_lds<R>(lds, sc);  // every wave joins the fill and its barrier
-  const uint32_t v = h ? half_seg<1, Visit, CRC, R>(cur, have, full, sc, lds, visit, w)
-                       : half_seg<0, Visit, CRC, R>(cur, have, full, sc, lds, visit, w);
+  const uint32_t v = h ? half_seg<1, Visit, R>(cur, have, full, sc, lds, visit, w)
+                       : half_seg<0, Visit, R>(cur, have, full, sc, lds, visit, w);
   if (h == 1 && lane == 0) xch[stride * (wave >> 1)] = v;
   __syncthreads();
-  if (h == 0 && have && lane == 0) seg_out[g] = to_chunk_end(cur, v ^ xch[stride * (wave >> 1)], sc);
-}
-
-// `bytes` cut into chunks of `chunk_bytes`.
-struct ChunkGeo {
-  const uint8_t* src;
-  int64_t bytes, chunk_bytes, spc;
-  uint32_t xrem_full, xrem_last;  // x^(8 * (len mod 16 KiB)) of a full chunk / the last chunk
-  __device__ Seg operator()(int64_t g) const {
-    const int64_t c = g / spc, k = g - c * spc;
-    Seg s;
-    s.chunk = c;
-    s.chunk_start = c * chunk_bytes;
-    s.chunk_len = min(chunk_bytes, bytes - s.chunk_start);
-    s.seg_start = k * kSegBytes;
-    s.p = src + s.chunk_start + s.seg_start;
-    s.len = min(int64_t(kSegBytes), s.chunk_len - s.seg_start);
-    s.xrem = s.chunk_len == chunk_bytes ? xrem_full : xrem_last;
-    return s;
-  }
-};
-
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_segments_kernel(const ChunkGeo geo, int64_t total_segs, const uint32_t* __restrict__ sc,
-                       uint32_t* __restrict__ seg_out) {
-  __shared__ uint4 lds_raw[kLdsBytes / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  load_lds(lds, sc);
-  const Slice4 st(lds);
-  NoVisit v;
-  slice_walk(geo, total_segs, sc, st, v, seg_out);
+  return h == 0 && have ? to_chunk_end(cur, v ^ xch[stride * (wave >> 1)], sc) : 0;
 }
 
 // 16 e4m3fn values (one 16-B word) times their power-of-two block scale -> 16 bf16 (32 B in o).
@@ -594,17 +471,11 @@ __device__ inline void unpack16_regs(const u32x4_t& w, float s, uint32_t (&o)[8]
     o[2 * i + 1] = fp8x2_to_bf16x2<true>(w[i], s);
   }
 }
-template <bool NT = false>
-__device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ dst) {
+__device__ inline void unpack16_nt(const u32x4_t& w, float s, uint4* __restrict__ dst) {
   uint32_t o[8];
   unpack16_regs(w, s, o);
-  if constexpr (NT) {
-    __builtin_nontemporal_store(u32x4_t{o[0], o[1], o[2], o[3]}, reinterpret_cast<u32x4_t*>(dst));
-    __builtin_nontemporal_store(u32x4_t{o[4], o[5], o[6], o[7]}, reinterpret_cast<u32x4_t*>(dst) + 1);
-  } else {
-    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
-  }
+  __builtin_nontemporal_store(u32x4_t{o[0], o[1], o[2], o[3]}, reinterpret_cast<u32x4_t*>(dst));
+  __builtin_nontemporal_store(u32x4_t{o[4], o[5], o[6], o[7]}, reinterpret_cast<u32x4_t*>(dst) + 1);
 }
 
 // A wave's 2 KiB of bf16 from one loaded word (lane m + 16 r holds output bytes
@@ -618,8 +489,10 @@ __device__ inline void unpack16(const u32x4_t& w, float s, uint4* __restrict__ d
 // writers of one 16-lane group (granules 8 m + 2 r, m = 0..7) then hit 8
 // distinct bank quads instead of 2 (4-way conflicts: 29 M conflict cycles per
 // 512 MiB, profiles/r3_kernels), and the readers (granule = lane) stay distinct.
+// The stores are nontemporal: the output is written once and never read back,
+// so it has no business in L2 or the Infinity Cache (5.04 -> 5.39-5.43 TB/s at
+// 512 MiB, profiles/r4_nt).
 __device__ __forceinline__ uint32_t swz(uint32_t g) { return g ^ ((g >> 3) & 6u); }
-template <bool NT = false>
 __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* slot, uint4* __restrict__ region) {
   const int lane = threadIdx.x & 63, m = lane & 15, r = lane >> 4;
   uint4* g = reinterpret_cast<uint4*>(slot);  // granules
@@ -632,10 +505,7 @@ __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* sl
       g[w1] = make_uint4(o[4], o[5], o[6], o[7]);
     }
     __builtin_amdgcn_wave_barrier();
-    if constexpr (NT)
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(rd), reinterpret_cast<u32x4_t*>(region) + 64 * h + lane);
-    else
-      region[64 * h + lane] = *rd;
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(rd), reinterpret_cast<u32x4_t*>(region) + 64 * h + lane);
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -646,39 +516,30 @@ __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* sl
 // words as loaded: each wave store instruction writes 2 whole KiB). Every
 // packed byte is read once from HBM.
 //
-// Scales: a full segment's 16 KiB / BLOCK scales are loaded one segment ahead
-// (lane l, register r: scale l + 64 r of the segment), issued before that
-// segment's data loads, and each word takes its scale from the owning lane with
+// Scales: a full segment's 16 KiB / BLOCK scales are loaded with the
+// segment's data, issued before it (lane l, register r: scale l + 64 r of the
+// segment), and each word takes its scale from the owning lane with
 // ds_bpermute (the register index is uniform per word: a word's scales never
 // straddle 64). Loading each word's scale where it is used made every use wait
-// for all older loads - the next segment's prefetch included (vmcnt counts in
-// order): 3.93 -> 4.12 TB/s (profiles/r2_fused_ahead). Nontemporal bf16 stores
-// (NT) measured slower in the round-2 walk, whose lanes stored half-dense 16-B
-// pieces (3.61 TB/s, profiles/r2_fused_nt), and still lose there (store 14:
-// 3.6); the staged, whole-KiB stores of the one-segment-per-wave kernel gain
-// from them: 5.04 -> 5.39-5.43 TB/s at 512 MiB, 5.37-5.67 -> 5.92-6.13 at
-// 4 GiB (profiles/r4_nt): the output is written once and never read back, so
-// it has no business in L2 or the Infinity Cache.
-template <int BLOCK, bool STAGE = false, bool NT = false>
+// for all older loads (vmcnt counts in order): 3.93 -> 4.12 TB/s in the round-2
+// walk (profiles/r2_fused_ahead).
+template <int BLOCK>
 struct UnpackVisit {
   static constexpr int kR = kSegBytes / BLOCK >= 64 ? kSegBytes / BLOCK / 64 : 1;  // scale registers
   // BLOCK 32 would hold 16 scale registers and spill: it keeps the per-word load
   static constexpr bool kAhead = kR <= 4;
-  int64_t out_chunk_elems;
-  uint16_t* out;
-  const uint8_t* src;
   int64_t n_q = 0;
   const float* scales = nullptr;
   uint16_t* obase = nullptr;
-  uint8_t* slot = nullptr;  // STAGE: this wave's 1 KiB of LDS
+  uint8_t* slot = nullptr;  // this wave's 1 KiB of LDS
   float cs[kAhead ? kR : 1] = {}, ns[kAhead ? kR : 1] = {};  // scales of the current / next full segment
   __device__ void begin(const Seg& sg) {
     n_q = sg.chunk_len / (BLOCK + 4) * BLOCK;  // q bytes (= elements) of this chunk
-    scales = reinterpret_cast<const float*>(src + sg.chunk_start + n_q);
-    obase = out + sg.chunk * out_chunk_elems;
+    scales = reinterpret_cast<const float*>(sg.p - sg.seg_start + n_q);
+    obase = sg.out;
   }
   __device__ void operator()(const u32x4_t& w, int64_t e) {  // e: byte offset in chunk = element index in q
-    if (e < n_q) unpack16<NT>(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
+    if (e < n_q) unpack16_nt(w, scales[e / BLOCK], reinterpret_cast<uint4*>(obase + e));
   }
   __device__ void prefetch(const Seg& sg, bool full) {
     if constexpr (!kAhead) return;
@@ -706,242 +567,188 @@ struct UnpackVisit {
     const int from = (base & 63) + (64 * (lane & 15) + 16 * (lane >> 4)) / BLOCK;
     const float s = __builtin_bit_cast(
         float, __builtin_amdgcn_ds_bpermute(from * 4, __builtin_bit_cast(int, cs[kAhead ? (base >> 6) : 0])));
-    if constexpr (STAGE) {
-      // the KiB this word covers: wave-uniform (lane offsets 0..1008 inside it)
-      const int64_t kib = e - (64 * (lane & 15) + 16 * (lane >> 4));
-      if (kib + 1024 <= n_q) {
-        uint32_t o[8];
-        unpack16_regs(w, s, o);
-        store_staged<NT>(o, slot, reinterpret_cast<uint4*>(obase + kib));
-        return;
-      }
+    // the KiB this word covers: wave-uniform (lane offsets 0..1008 inside it)
+    const int64_t kib = e - (64 * (lane & 15) + 16 * (lane >> 4));
+    if (kib + 1024 <= n_q) {
+      uint32_t o[8];
+      unpack16_regs(w, s, o);
+      store_staged(o, slot, reinterpret_cast<uint4*>(obase + kib));
+      return;
     }
-    if (e < n_q) unpack16<NT>(w, s, reinterpret_cast<uint4*>(obase + e));
+    if (e < n_q) unpack16_nt(w, s, reinterpret_cast<uint4*>(obase + e));
   }
 };
 
-template <int BLOCK, bool STAGE, bool CRC = true>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-verify_unpack_segments_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
-                              const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
-                              uint16_t* __restrict__ out) {
-  __shared__ uint4 lds_raw[(kLdsBytes + (STAGE ? kStageBytes : 0)) / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  load_lds(lds, sc);
-  const Slice4 st(lds);
-  UnpackVisit<BLOCK, STAGE> v{out_chunk_elems, out, geo.src};
-  v.slot = lds + kLdsBytes + (threadIdx.x >> 6) * 1024;
-  slice_walk<ChunkGeo, UnpackVisit<BLOCK, STAGE>, CRC>(geo, total_segs, sc, st, v, seg_out);
-}
+// ---- geometry of a launch: which bytes each segment covers, and per item
+// (a chunk whose CRC32C is one result) its segment count, init/xorout term and
+// result word.
 
-// store = 5: one segment per wave (slice_once), the grid as large as the work.
-template <int BLOCK, bool CRC = true>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-verify_unpack_once_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
-                          const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
-                          uint16_t* __restrict__ out) {
-  __shared__ uint4 lds_raw[(kLdsBytes + kStageBytes) / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  UnpackVisit<BLOCK, true> v{out_chunk_elems, out, geo.src};
-  v.slot = lds + kLdsBytes + (threadIdx.x >> 6) * 1024;
-  slice_once<ChunkGeo, UnpackVisit<BLOCK, true>, CRC>(geo, total_segs, sc, lds, v, seg_out);
-}
-
-// store = 7: one segment per wave, 512-thread workgroups with 16 table
-// replicas (72 KiB + 8 KiB of staging): two workgroups per CU, so one fills
-// its tables and waits for its first loads while the other computes.
-constexpr int kWaves16 = 8;
-template <int BLOCK, bool CRC = true, bool STAGE = true, bool NT = false>
-__global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
-verify_unpack_once16_kernel(const ChunkGeo geo, int64_t total_segs, int64_t split_block, int64_t out_chunk_elems,
-                            const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
-                            uint16_t* __restrict__ out) {
-  __shared__ uint4 lds_raw[(LdsLayout<16>::kBytes + (STAGE ? kWaves16 * 1024 : 0)) / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  UnpackVisit<BLOCK, STAGE, NT> v{out_chunk_elems, out, geo.src};
-  v.slot = lds + LdsLayout<16>::kBytes + (threadIdx.x >> 6) * 1024;
-  if (int64_t(blockIdx.x) < split_block) {
-    slice_once<ChunkGeo, UnpackVisit<BLOCK, STAGE, NT>, CRC, 16, kWaves16>(geo, total_segs, sc, lds, v, seg_out);
-  } else {
-    const int64_t g0 = split_block * kWaves16 + (int64_t(blockIdx.x) - split_block) * (kWaves16 / 2);
-    if constexpr (STAGE) {  // pair m hands over in word 0 of wave 2 m + 1's slot
-      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE, NT>, CRC, 16, kWaves16>(
-          geo, total_segs, g0, sc, lds, v, seg_out, reinterpret_cast<uint32_t*>(lds + LdsLayout<16>::kBytes + 1024), 512);
-    } else {
-      __shared__ uint32_t xch[kWaves16 / 2];
-      slice_half<ChunkGeo, UnpackVisit<BLOCK, STAGE, NT>, CRC, 16, kWaves16>(geo, total_segs, g0, sc, lds, v, seg_out, xch,
-                                                                         1);
-    }
+// `bytes` cut into chunks of `chunk_bytes` (one item per chunk); with an
+// unpack, chunk c's bf16 goes to out + c * out_chunk_elems.
+struct ChunkGeo {
+  const uint8_t* src;
+  int64_t bytes, chunk_bytes, spc;
+  uint32_t xrem_full, xrem_last;  // x^(8 * (len mod 16 KiB)) of a full chunk / the last chunk
+  uint32_t init_full, init_last;  // init/xorout terms of a full chunk / the last chunk
+  uint32_t* crc_out;              // crc_out[c]: chunk c's CRC32C
+  uint16_t* out;                  // bf16 output (fused), else nullptr
+  int64_t out_chunk_elems;
+  __device__ Seg operator()(int64_t g) const {
+    const int64_t c = g / spc, k = g - c * spc;
+    Seg s;
+    s.chunk = c;
+    s.chunk_start = c * chunk_bytes;
+    s.chunk_len = min(chunk_bytes, bytes - s.chunk_start);
+    s.seg_start = k * kSegBytes;
+    s.p = src + s.chunk_start + s.seg_start;
+    s.len = min(int64_t(kSegBytes), s.chunk_len - s.seg_start);
+    s.xrem = s.chunk_len == chunk_bytes ? xrem_full : xrem_last;
+    s.out = out ? out + c * out_chunk_elems : nullptr;
+    return s;
   }
-}
-
-// CRC only, one segment per wave.
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_segments_once_kernel(const ChunkGeo geo, int64_t total_segs, const uint32_t* __restrict__ sc,
-                            uint32_t* __restrict__ seg_out) {
-  __shared__ uint4 lds_raw[kLdsBytes / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  NoVisit v;
-  slice_once<ChunkGeo, NoVisit, true>(geo, total_segs, sc, lds, v, seg_out);
-}
-
-// store = 2: the same CRC walk on half of the waves (0-7) while the other half
-// (8-15) stream the same segments' q bytes through the plain unpack (8 B of
-// fp8 in, 16 B of bf16 out per lane: every load and store instruction fully
-// coalesced), one segment behind or ahead, so the packed bytes come twice from
-// L2 / the Infinity Cache instead of twice from HBM. In the fused walk every
-// wave does both jobs in sequence: its CRC (LDS lookups, VALU) and its stores
-// do not overlap, and the kernel takes about the sum of a CRC pass and an
-// unpack pass (profiles/r3_kernels).
-template <int BLOCK>
-__device__ __forceinline__ void unpack_walk(const ChunkGeo& geo, int64_t total_segs, int64_t out_chunk_elems,
-                                            uint16_t* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = __builtin_amdgcn_readfirstlane(int(blockIdx.x * 8 + ((threadIdx.x >> 6) & 7)));
-  const int64_t nwaves = int64_t(gridDim.x) * 8;
-  for (int64_t g = wave; g < total_segs; g += nwaves) {
-    const Seg sg = geo(g);
-    const int64_t n_q = sg.chunk_len / (BLOCK + 4) * BLOCK;
-    if (sg.seg_start >= n_q) continue;  // the chunk's scales: nothing to unpack
-    const float* scales = reinterpret_cast<const float*>(geo.src + sg.chunk_start + n_q);
-    uint16_t* obase = out + sg.chunk * out_chunk_elems;
-    const int64_t end = min(sg.seg_start + sg.len, n_q);
-    const uint2* q = reinterpret_cast<const uint2*>(sg.p);
-    constexpr int kU = 8;  // 8 x 512 B of loads in flight per wave
-    for (int64_t base = 0; sg.seg_start + base < end; base += kU * 512) {
-      uint2 v[kU];
-      float sc[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int64_t e = sg.seg_start + base + u * 512 + 8 * lane;
-        v[u] = e < end ? q[(base + u * 512) / 8 + lane] : make_uint2(0, 0);
-        sc[u] = e < end ? scales[e / BLOCK] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int64_t e = sg.seg_start + base + u * 512 + 8 * lane;
-        if (e >= end) continue;
-        const float s = sc[u];
-        *reinterpret_cast<uint4*>(obase + e) =
-            make_uint4(fp8x2_to_bf16x2<false>(v[u].x, s), fp8x2_to_bf16x2<true>(v[u].x, s),
-                       fp8x2_to_bf16x2<false>(v[u].y, s), fp8x2_to_bf16x2<true>(v[u].y, s));
-      }
-    }
+  __device__ int64_t item_segs(int64_t c) const {
+    return (min(chunk_bytes, bytes - c * chunk_bytes) + kSegBytes - 1) / kSegBytes;
   }
-}
-
-template <int BLOCK>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-verify_unpack_split_kernel(const ChunkGeo geo, int64_t total_segs, int64_t out_chunk_elems,
-                           const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out,
-                           uint16_t* __restrict__ out) {
-  __shared__ uint4 lds_raw[kLdsBytes / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  load_lds(lds, sc);
-  if ((threadIdx.x >> 6) < 8) {
-    const Slice4 st(lds);
-    NoVisit v;
-    slice_walk(geo, total_segs, sc, st, v, seg_out, 8);
-  } else {
-    unpack_walk<BLOCK>(geo, total_segs, out_chunk_elems, out);
-  }
-}
-
-// A chunk's raw CRC: the XOR of its segments' values (each already shifted
-// to the chunk end). Called by every thread of a kFoldThreads block; returns
-// the raw CRC on thread 0.
-// The loads go out four at a time (independent accumulators): a plain strided
-// loop waits for each before the next (~9 round trips per 2112-segment chunk
-// on 256 threads). A fold launch costs ~4.5 us whatever its work
-// (profiles/r4_nt): folding in the fused kernel's last workgroup instead
-// (generation-tagged slots that one workgroup polls) measured slower at
-// 512 MiB, 159.8 vs 148.3 + 4.5 us, since one workgroup reads the slots at a
-// fraction of the chip's rate (profiles/r4_fold_in_kernel).
-constexpr int kFoldThreads = 1024;
-__device__ uint32_t xor_chunk(const uint32_t* __restrict__ seg, int64_t nseg) {
-  __shared__ uint32_t part[kFoldThreads / 64];
-  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-  int64_t k = threadIdx.x;
-  for (; k + 3 * kFoldThreads < nseg; k += 4 * kFoldThreads) {
-    r0 ^= seg[k];
-    r1 ^= seg[k + kFoldThreads];
-    r2 ^= seg[k + 2 * kFoldThreads];
-    r3 ^= seg[k + 3 * kFoldThreads];
-  }
-  for (; k < nseg; k += kFoldThreads) r0 ^= seg[k];
-  uint32_t r = wave_xor_dpp(r0 ^ r1 ^ r2 ^ r3);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = r;
-  __syncthreads();
-  if (threadIdx.x != 0) return 0;
-  r = 0;
-#pragma unroll
-  for (int i = 0; i < kFoldThreads / 64; ++i) r ^= part[i];
-  return r;
-}
-
-// Per chunk: (x^(8*rem), init/xorout term) of full chunks [0..1] and of the short last chunk [2..3].
-struct FoldTail {
-  uint32_t xrem_full, init_full, xrem_last, init_last;
+  __device__ uint32_t item_init(int64_t c) const { return (c + 1) * chunk_bytes <= bytes ? init_full : init_last; }
+  __device__ uint32_t* item_out(int64_t c) const { return crc_out + c; }
 };
 
-// One block per chunk.
-__global__ void __launch_bounds__(kFoldThreads) crc32c_fold_kernel(const uint32_t* __restrict__ seg_out, int64_t bytes,
-                                                                   int64_t chunk_bytes, int64_t spc, FoldTail t,
-                                                                   uint32_t* __restrict__ out) {
-  const int64_t c = blockIdx.x;
-  const int64_t chunk_len = min(chunk_bytes, bytes - c * chunk_bytes);
-  const bool full = chunk_len == chunk_bytes;
-  const uint32_t r = xor_chunk(seg_out + c * spc, (chunk_len + kSegBytes - 1) / kSegBytes);
-  if (threadIdx.x == 0) out[c] = r ^ (full ? t.init_full : t.init_last);
-}
-
-FoldTail fold_tail(int64_t chunk_bytes, int64_t last_len) {
-  auto xrem = [](int64_t len) { return crc32c_xpow8n(uint64_t(len % kSegBytes)); };
-  return FoldTail{xrem(chunk_bytes), crc32c_init_term(uint64_t(chunk_bytes)), xrem(last_len),
-                  crc32c_init_term(uint64_t(last_len))};
-}
-
-// ---- batched: up to kCrcBatchMax independent buffers (the chunks one P2P
-// group landed) in one segments launch + one fold launch.
-struct BatchArgs {
+// Up to kCrcBatchMax independent items (the chunks one P2P group or one
+// staging batch landed), each 16-B aligned, any length.
+struct BatchGeo {
   int n;
   int64_t seg_base[kCrcBatchMax + 1];  // prefix sums of the items' segment counts
   const uint8_t* src[kCrcBatchMax];
   int64_t bytes[kCrcBatchMax];
   uint32_t xrem[kCrcBatchMax];  // x^(8 * (bytes mod 16 KiB))
   uint32_t init[kCrcBatchMax];
-  uint32_t* out[kCrcBatchMax];
-};
-
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
-crc32c_batch_segments_kernel(const BatchArgs a, const uint32_t* __restrict__ sc, uint32_t* __restrict__ seg_out) {
-  __shared__ uint4 lds_raw[kLdsBytes / 16];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  load_lds(lds, sc);
-  const Slice4 st(lds);
-  auto geo = [&](int64_t g) {
+  uint32_t* crc_out[kCrcBatchMax];
+  uint16_t* out[kCrcBatchMax];  // bf16 output of each item (fused)
+  __device__ Seg operator()(int64_t g) const {
     int j = 0;
-    while (g >= a.seg_base[j + 1]) ++j;
-    const int64_t k = g - a.seg_base[j];
+    while (g >= seg_base[j + 1]) ++j;  // wave-uniform, at most kCrcBatchMax steps
+    const int64_t k = g - seg_base[j];
     Seg s;
     s.chunk = j;
     s.chunk_start = 0;
-    s.chunk_len = a.bytes[j];
+    s.chunk_len = bytes[j];
     s.seg_start = k * kSegBytes;
-    s.p = a.src[j] + s.seg_start;
-    s.len = min(int64_t(kSegBytes), a.bytes[j] - s.seg_start);
-    s.xrem = a.xrem[j];
+    s.p = src[j] + s.seg_start;
+    s.len = min(int64_t(kSegBytes), bytes[j] - s.seg_start);
+    s.xrem = xrem[j];
+    s.out = out[j];
     return s;
-  };
-  NoVisit v;
-  slice_walk(geo, a.seg_base[a.n], sc, st, v, seg_out);
+  }
+  __device__ int64_t item_segs(int64_t j) const { return seg_base[j + 1] - seg_base[j]; }
+  __device__ uint32_t item_init(int64_t j) const { return init[j]; }
+  __device__ uint32_t* item_out(int64_t j) const { return crc_out[j]; }
+};
+
+// ---- the fold, inside the kernel (no second launch). A chunk's raw CRC is
+// the XOR of its segments' values (each already shifted to the chunk end).
+// Per item the workspace holds {acc, count}: every workgroup XORs the values
+// of its segments of the item into acc (one device-scope atomic per run of
+// its waves that share an item), waits for that atomic to return, then adds
+// its segment count to count; the workgroup whose add completes the item's
+// count takes acc (exchanging in 0), resets count and writes raw ^ init.
+// Both words are back at 0 when the launch ends, so a workspace zeroed once
+// serves every later launch on its stream. Every access to them is a vector
+// atomic, performed where the device's XCDs see one copy of the word.
+// The separate fold launch this replaces cost 8.4-9.6 us per 64 MiB chunk in
+// the round-4 engine traces (profiles/r4_profile), a quarter of the verify.
+template <class Geo>
+__device__ __forceinline__ void fold_add(const Geo& geo, int64_t item, uint32_t x, uint32_t n, uint32_t* acc) {
+  uint32_t* a = acc + 2 * item;
+  const uint32_t prev = __hip_atomic_fetch_xor(a, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("" ::"v"(prev) : "memory");  // the XOR has returned (is performed) before the count moves
+  const uint32_t got = __hip_atomic_fetch_add(a + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + n;
+  if (int64_t(got) == geo.item_segs(item)) {
+    const uint32_t raw = __hip_atomic_exchange(a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *geo.item_out(item) = raw ^ geo.item_init(item);
+  }
 }
 
-__global__ void __launch_bounds__(kFoldThreads) crc32c_batch_fold_kernel(const BatchArgs a,
-                                                                         const uint32_t* __restrict__ seg_out) {
-  const int j = blockIdx.x;
-  const uint32_t r = xor_chunk(seg_out + a.seg_base[j], a.seg_base[j + 1] - a.seg_base[j]);
-  if (threadIdx.x == 0) *a.out[j] = r ^ a.init[j];
+// Thread 0 of a workgroup: its waves' values (item < 0: none) in runs of equal item.
+template <class Geo, int WAVES>
+__device__ __forceinline__ void fold_workgroup(const Geo& geo, const uint32_t* v, const int64_t* item, uint32_t* acc) {
+  int64_t cur = -1;
+  uint32_t x = 0, n = 0;
+  for (int w = 0; w < WAVES; ++w) {
+    if (item[w] < 0) continue;
+    if (item[w] != cur) {
+      if (cur >= 0) fold_add(geo, cur, x, n, acc);
+      cur = item[w];
+      x = 0;
+      n = 0;
+    }
+    x ^= v[w];
+    ++n;
+  }
+  if (cur >= 0) fold_add(geo, cur, x, n, acc);
+}
+
+// The verify kernel: one 16 KiB segment per wave (slice_once), 512-thread
+// workgroups with 16 table replicas (72 KiB of LDS, + 8 KiB of bf16 staging
+// with an unpack): two workgroups per CU, so one fills its tables and waits
+// for its first loads while the other computes. Workgroups [split_block, ..)
+// take half segments (once_split). BLOCK = 0: CRC only; else the fused fp8
+// unpack with that scale block.
+// Round 4 measured this shape against the alternatives for the fused path
+// (profiles/r4_nt, r4_kernels_final: 5.3-5.5 TB/s at 512 MiB vs 4.66 for the
+// persistent walk with staged stores, 3.6-4.1 for the walk's other store
+// forms, 4.3 for split CRC/unpack waves); those variants were removed from
+// the library. Batching several landed chunks into one launch is what makes
+// it fast at the engine's chunk size: one 64 MiB chunk alone is 264
+// workgroups, less than one per CU slot, and ran at 3.0 TB/s (profiles/r4_sizes).
+constexpr int kWaves16 = 8;
+template <class Geo, int BLOCK>
+__global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
+verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, const uint32_t* __restrict__ sc,
+                     uint32_t* __restrict__ acc) {
+  constexpr bool kUnpack = BLOCK > 0;
+  using Visit = std::conditional_t<kUnpack, UnpackVisit<kUnpack ? BLOCK : 128>, NoVisit>;
+  // Per wave after the tables: its 1 KiB bf16 staging slot (fused) or 32 B.
+  // Bytes 16-31 of a wave's slot carry its fold value and item to thread 0
+  // (its staging is done by then; word 0 may hold a half-pair hand-over).
+  // Two 80 KiB workgroups fill the CU's 160 KiB: not one more byte to spare.
+  constexpr uint32_t kSlot = kUnpack ? 1024 : 32;
+  __shared__ uint4 lds_raw[(LdsLayout<16>::kBytes + kWaves16 * kSlot) / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  uint8_t* slots = lds + LdsLayout<16>::kBytes;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  Visit v{};
+  if constexpr (kUnpack) v.slot = slots + wave * kSlot;
+  uint32_t val;
+  int64_t item = -1;
+  if (int64_t(blockIdx.x) < split_block) {
+    const int64_t g = int64_t(blockIdx.x) * kWaves16 + wave;
+    const bool have = g < total_segs;
+    val = slice_once<Geo, Visit, 16, kWaves16>(geo, g, have, sc, lds, v);
+    if (have) item = geo(g).chunk;
+  } else {
+    const int64_t g = split_block * kWaves16 + (int64_t(blockIdx.x) - split_block) * (kWaves16 / 2) + (wave >> 1);
+    const bool have = g < total_segs;
+    // pair m hands over in word 0 of wave 2 m + 1's slot
+    val = slice_half<Geo, Visit, 16>(geo, g, have, sc, lds, v, reinterpret_cast<uint32_t*>(slots + kSlot),
+                                     int(2 * kSlot / 4));
+    if (have && (wave & 1) == 0) item = geo(g).chunk;
+  }
+  if (lane == 0) {
+    *reinterpret_cast<uint32_t*>(slots + wave * kSlot + 16) = val;
+    *reinterpret_cast<int64_t*>(slots + wave * kSlot + 24) = item;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t vs[kWaves16];
+    int64_t its[kWaves16];
+#pragma unroll
+    for (int w = 0; w < kWaves16; ++w) {
+      vs[w] = *reinterpret_cast<const uint32_t*>(slots + w * kSlot + 16);
+      its[w] = *reinterpret_cast<const int64_t*>(slots + w * kSlot + 24);
+    }
+    fold_workgroup<Geo, kWaves16>(geo, vs, its, acc);
+  }
 }
 
 // Per-device constant tables (one upload per device, before any RCCL traffic:
@@ -998,218 +805,200 @@ uint32_t* device_consts(hipStream_t s) {
     for (uint32_t v = 0; v < 16; ++v) h[size_t(kGap + n * 16 + int(v))] = crc32c_multmodp(xg, v << (4 * n));
   for (int m = 0; m < 1024; ++m) h[size_t(kPow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
   for (int l = 0; l < 64; ++l) h[size_t(kLanePow + l)] = crc32c_xpow8n(uint64_t(kPieceBytes) * uint64_t(63 - l));
-  const uint32_t xs = crc32c_xpow8n(kSegBytes);
-  h[size_t(kSegPow)] = 0x80000000u;  // x^0
-  for (int j = 1; j < kMaxSegs; ++j) h[size_t(kSegPow + j)] = crc32c_multmodp(xs, h[size_t(kSegPow + j - 1)]);
+  // segpow level L, entry i: x^(8 * 16 KiB * i * 1024^L)
+  for (int L = 0; L < kSegLevels; ++L) {
+    const uint64_t step = uint64_t(kSegBytes) << (10 * L);
+    const uint32_t xs = crc32c_xpow8n(step);
+    h[size_t(kSegPow + L * kSegLevel)] = 0x80000000u;  // x^0
+    for (int i = 1; i < kSegLevel; ++i)
+      h[size_t(kSegPow + L * kSegLevel + i)] = crc32c_multmodp(xs, h[size_t(kSegPow + L * kSegLevel + i - 1)]);
+  }
   const ConstEntry e = upload_consts(h, s);
   if (!e.d) return nullptr;
   g_consts.by_device[dev] = e;
   return e.d;
 }
 
-// One workgroup per CU (LDS-bound), 16 segments per workgroup at a time,
-// grid-stride beyond that. Kernel trace on 1 GiB (profiles/r2_crc_slice):
-// 186.5 us with 256 workgroups, 185.0 with 512, 187.8 with 1024.
-// Workgroups for a segment walk: as few rounds of kWaves segments per
-// workgroup as `cap` allows, then as few workgroups as still need only that
-// many rounds. A wave takes segments g, g + nwaves, ..., so a last round that
-// only some waves reach costs a whole round: 16896 segments (512 MiB of
-// bf16 packed) on 256 x 16 waves are 4.125 rounds, 5 for the kernel; 212
-// workgroups do the same 5 rounds with every wave busy, and the freed CUs'
-// share of HBM goes to the rest: fused verify+unpack 4.30 -> 4.61 TB/s
-// (profiles/r3_tail).
-dim3 seg_grid(int64_t total_segs, int max_blocks) {
-  const int64_t cap = max_blocks > 0 ? max_blocks : 256;
-  const int64_t rounds = std::max<int64_t>(1, (total_segs + cap * kWaves - 1) / (cap * kWaves));
-  const int64_t blocks = (total_segs + kWaves * rounds - 1) / (kWaves * rounds);
-  return dim3(unsigned(std::max<int64_t>(1, std::min<int64_t>(blocks, cap))));
-}
-
-// Resident once16 workgroups on the device (per CU x CUs), cached per device.
-int once16_slots() {
+// Resident verify workgroups per CU, cached per device.
+int once16_per_cu() {
   static std::mutex mu;
   static std::map<int, int> by_device;
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(mu);
   if (auto it = by_device.find(dev); it != by_device.end()) return it->second;
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, verify_unpack_once16_kernel<128>, kWaves16 * 64, 0) !=
-          hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 512;
-  return by_device[dev] = std::max(1, per_cu) * std::max(1, cus);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, verify_once16_kernel<ChunkGeo, 128>, kWaves16 * 64, 0) !=
+      hipSuccess)
+    per_cu = 2;
+  return by_device[dev] = std::max(1, per_cu);
 }
 
-// Grid of the one-segment-per-wave kernel with its last, partial round of
-// workgroups done in half segments (slice_half). Every workgroup lasts about
-// as long, so with W workgroups on S slots the kernel takes ceil(W / S)
-// rounds even when the last holds only a few: 16896 segments (512 MiB of bf16
-// packed) are 2112 workgroups on 512 slots, 4.125 rounds. Cutting the last
-// round's segments in halves gives twice the workgroups at half the length,
-// so a last round up to half full ends in half the time. W <= S / 2: every
-// segment in halves (twice the parallelism); otherwise no split.
+int device_cus() {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  return cus;
+}
+
+// Grid with its last, partial round of workgroups done in half segments
+// (slice_half). Every workgroup lasts about as long, so with W workgroups on
+// S slots the kernel takes ceil(W / S) rounds even when the last holds only a
+// few: 16896 segments (512 MiB of bf16 packed) are 2112 workgroups on 512
+// slots, 4.125 rounds. Cutting the last round's segments in halves gives
+// twice the workgroups at half the length, so a last round up to half full
+// ends in half the time. W <= S / 2: every segment in halves (twice the
+// parallelism); otherwise no split. S counts the slots of the CUs the stream
+// may use (`cus`: a CU-masked verify stream passes its CU count; 0 = all).
 struct OnceGrid {
   int64_t split_block;  // workgroups [0, split_block) take whole segments
   unsigned blocks;
 };
-OnceGrid once_split(int64_t total_segs, bool split) {
-  const int64_t W = (total_segs + kWaves16 - 1) / kWaves16, S = once16_slots();
+OnceGrid once_split(int64_t total_segs, int cus) {
+  const int dc = device_cus();
+  const int64_t W = (total_segs + kWaves16 - 1) / kWaves16;
+  const int64_t S = int64_t(once16_per_cu()) * (cus > 0 ? std::min(cus, dc) : dc);
   int64_t full = W;
-  if (split) {
-    if (W <= S) full = 2 * W <= S ? 0 : W;
-    else if (const int64_t tail = W % S; tail && 2 * tail <= S) full = W - tail;
-  }
+  if (W <= S) full = 2 * W <= S ? 0 : W;
+  else if (const int64_t tail = W % S; tail && 2 * tail <= S) full = W - tail;
   const int64_t half_segs = std::max<int64_t>(0, total_segs - full * kWaves16);
   return OnceGrid{full, unsigned(full + (half_segs + kWaves16 / 2 - 1) / (kWaves16 / 2))};
 }
 
-struct Plan {
-  int64_t spc, nchunks, total_segs;
-  uint32_t* consts;
-  FoldTail tail;
-};
-
-hipError_t plan(int64_t bytes, int64_t chunk_bytes, Plan* p, hipStream_t s) {
-  p->spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
-  if (p->spc > kMaxSegs) return hipErrorInvalidValue;  // chunks up to 1 GiB (segpow table)
-  p->nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
-  const int64_t last_len = bytes - (p->nchunks - 1) * chunk_bytes;
-  p->total_segs = (p->nchunks - 1) * p->spc + (last_len + kSegBytes - 1) / kSegBytes;
-  p->consts = device_consts(s);
-  p->tail = fold_tail(chunk_bytes, last_len);
-  return p->consts ? hipSuccess : hipErrorOutOfMemory;
+template <class Geo>
+hipError_t launch(const Geo& geo, int64_t total_segs, int block, const uint32_t* consts, void* ws, hipStream_t s,
+                  int cus) {
+  if (total_segs <= 0) return hipSuccess;
+  const OnceGrid og = once_split(total_segs, cus);
+  const dim3 grid(og.blocks), tpb(kWaves16 * 64);
+  auto* acc = static_cast<uint32_t*>(ws);
+  switch (block) {
+    case 0: verify_once16_kernel<Geo, 0><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
+    case 32: verify_once16_kernel<Geo, 32><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
+    case 64: verify_once16_kernel<Geo, 64><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
+    case 128: verify_once16_kernel<Geo, 128><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
+    case 256: verify_once16_kernel<Geo, 256><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
+    case 512: verify_once16_kernel<Geo, 512><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
+
+int64_t segs_of(int64_t n) { return (n + kSegBytes - 1) / kSegBytes; }
+
+// A ChunkGeo over `bytes` in `chunk_bytes` chunks (the caller checked alignment).
+hipError_t chunk_geo(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* crc_out, ChunkGeo* g,
+                     int64_t* total_segs) {
+  const int64_t spc = segs_of(chunk_bytes);
+  if (spc > kMaxSegs) return hipErrorInvalidValue;
+  const int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
+  const int64_t last_len = bytes - (nchunks - 1) * chunk_bytes;
+  auto xrem = [](int64_t len) { return crc32c_xpow8n(uint64_t(len % kSegBytes)); };
+  *g = ChunkGeo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, spc, xrem(chunk_bytes), xrem(last_len),
+                crc32c_init_term(uint64_t(chunk_bytes)), crc32c_init_term(uint64_t(last_len)), crc_out, nullptr, 0};
+  *total_segs = (nchunks - 1) * spc + segs_of(last_len);
+  return hipSuccess;
+}
+
+// Appends item (src, bytes) to a BatchGeo.
+hipError_t batch_add(BatchGeo& a, const void* src, int64_t bytes, uint32_t* crc_out, uint16_t* out) {
+  if (reinterpret_cast<uintptr_t>(src) & 15) return hipErrorInvalidValue;
+  const int64_t spc = segs_of(bytes);
+  if (spc > kMaxSegs || a.n >= kCrcBatchMax) return hipErrorInvalidValue;
+  const int j = a.n++;
+  a.src[j] = static_cast<const uint8_t*>(src);
+  a.bytes[j] = bytes;
+  a.xrem[j] = crc32c_xpow8n(uint64_t(bytes % kSegBytes));
+  a.init[j] = crc32c_init_term(uint64_t(bytes));
+  a.crc_out[j] = crc_out;
+  a.out[j] = out;
+  a.seg_base[j + 1] = a.seg_base[j] + spc;
+  return hipSuccess;
+}
+
+// Packed bytes of `src_len` bf16 source bytes (one chunk's worth) with `block` scales.
+int64_t packed_of(int64_t src_len, int block) { return src_len / 2 + src_len / 2 / block * 4; }
+
+bool valid_block(int block) { return block == 32 || block == 64 || block == 128 || block == 256 || block == 512; }
 
 }  // namespace
 
-hipError_t crc32c_warm(int64_t chunk_bytes, hipStream_t s) {
-  if ((chunk_bytes + kSegBytes - 1) / kSegBytes > kMaxSegs) return hipErrorInvalidValue;
-  return device_consts(s) ? hipSuccess : hipErrorOutOfMemory;
-}
+hipError_t crc32c_warm(hipStream_t s) { return device_consts(s) ? hipSuccess : hipErrorOutOfMemory; }
 
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes) {
   if (bytes <= 0 || chunk_bytes <= 0) return 16;
-  int64_t spc = (chunk_bytes + kSegBytes - 1) / kSegBytes;
-  int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
-  return size_t(nchunks * spc * 4 + 16);
+  const int64_t nchunks = (bytes + chunk_bytes - 1) / chunk_bytes;
+  return size_t((nchunks * 8 + 15) / 16 * 16);
 }
+
+size_t crc32c_batch_workspace_bytes() { return size_t(kCrcBatchMax) * 8; }
 
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
-                         hipStream_t s) {
-  return crc32c_chunks_capped(src, bytes, chunk_bytes, out, workspace, s, 0);
-}
-
-hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
-                                hipStream_t s, int max_blocks) {
+                         hipStream_t s, int cus) {
   if (bytes <= 0) return hipSuccess;
   if (chunk_bytes <= 0 || (reinterpret_cast<uintptr_t>(src) & 15)) return hipErrorInvalidValue;
-  // One chunk (the engine's per-chunk checks) may have any length: only a
-  // chunk's last segment is partial, and it takes a byte tail. Several chunks
-  // need a 16-B multiple so that every chunk starts 16-B aligned.
+  // One chunk may have any length: only a chunk's last segment is partial, and
+  // it takes a byte tail. Several chunks need a 16-B multiple so that every
+  // chunk starts 16-B aligned.
   if (bytes <= chunk_bytes) chunk_bytes = bytes;
   else if (chunk_bytes % 16) return hipErrorInvalidValue;
-  Plan p;
-  if (hipError_t e = plan(bytes, chunk_bytes, &p, s); e != hipSuccess) return e;
-  auto* seg = static_cast<uint32_t*>(workspace);
-  const ChunkGeo geo{static_cast<const uint8_t*>(src), bytes, chunk_bytes, p.spc, p.tail.xrem_full, p.tail.xrem_last};
-  crc32c_segments_kernel<<<seg_grid(p.total_segs, max_blocks), dim3(kThreads), 0, s>>>(geo, p.total_segs, p.consts,
-                                                                                        seg);
-  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(kFoldThreads), 0, s>>>(seg, bytes, chunk_bytes, p.spc, p.tail,
-                                                                              out);
-  return hipGetLastError();
+  const uint32_t* consts = device_consts(s);
+  if (!consts) return hipErrorOutOfMemory;
+  ChunkGeo geo;
+  int64_t total = 0;
+  if (hipError_t e = chunk_geo(src, bytes, chunk_bytes, out, &geo, &total); e != hipSuccess) return e;
+  return launch(geo, total, 0, consts, workspace, s, cus);
 }
 
-size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n) {
-  const int64_t spc = (std::max<int64_t>(max_item_bytes, 1) + kSegBytes - 1) / kSegBytes;
-  return size_t(int64_t(std::max(n, 1)) * spc * 4 + 16);
-}
-
-hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int max_blocks) {
+hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int cus) {
   if (n <= 0) return hipSuccess;
   if (n > kCrcBatchMax) return hipErrorInvalidValue;
-  BatchArgs a{};
-  a.n = 0;
-  a.seg_base[0] = 0;
-  uint32_t* consts = device_consts(s);
+  const uint32_t* consts = device_consts(s);
   if (!consts) return hipErrorOutOfMemory;
-  for (int i = 0; i < n; ++i) {
-    const CrcItem& it = items[i];
-    if (it.bytes <= 0) continue;
-    if (reinterpret_cast<uintptr_t>(it.src) & 15) return hipErrorInvalidValue;  // any length
-    const int64_t spc = (it.bytes + kSegBytes - 1) / kSegBytes;
-    if (spc > kMaxSegs) return hipErrorInvalidValue;
-    const int j = a.n++;
-    a.src[j] = static_cast<const uint8_t*>(it.src);
-    a.bytes[j] = it.bytes;
-    a.xrem[j] = crc32c_xpow8n(uint64_t(it.bytes % kSegBytes));
-    a.init[j] = crc32c_init_term(uint64_t(it.bytes));
-    a.out[j] = it.out;
-    a.seg_base[j + 1] = a.seg_base[j] + spc;
-  }
+  BatchGeo a{};
+  for (int i = 0; i < n; ++i)
+    if (items[i].bytes > 0)
+      if (hipError_t e = batch_add(a, items[i].src, items[i].bytes, items[i].out, nullptr); e != hipSuccess) return e;
   if (a.n == 0) return hipSuccess;
-  auto* seg = static_cast<uint32_t*>(workspace);
-  crc32c_batch_segments_kernel<<<seg_grid(a.seg_base[a.n], max_blocks), dim3(kThreads), 0, s>>>(a, consts, seg);
-  crc32c_batch_fold_kernel<<<dim3(unsigned(a.n)), dim3(kFoldThreads), 0, s>>>(a, seg);
-  return hipGetLastError();
+  for (int j = a.n; j < kCrcBatchMax; ++j) a.seg_base[j + 1] = a.seg_base[a.n];
+  return launch(a, a.seg_base[a.n], 0, consts, workspace, s, cus);
 }
 
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
-                             uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks, int store) {
+                             uint32_t* crc_out, void* workspace, hipStream_t s, int cus) {
   if (src_bytes <= 0) return hipSuccess;
-  if (src_chunk <= 0 || src_chunk % 4096 || src_bytes % (2 * block) || (reinterpret_cast<uintptr_t>(packed) & 15) ||
-      (reinterpret_cast<uintptr_t>(out) & 15))
+  if (src_chunk <= 0 || src_chunk % 4096 || !valid_block(block) || src_bytes % (2 * block) ||
+      (reinterpret_cast<uintptr_t>(packed) & 15) || (reinterpret_cast<uintptr_t>(out) & 15))
     return hipErrorInvalidValue;
-  const int64_t pchunk = src_chunk / 2 + src_chunk / 2 / block * 4;
+  const int64_t pchunk = packed_of(src_chunk, block);
   const int64_t full = src_bytes / src_chunk, tail = src_bytes % src_chunk;
-  const int64_t bytes = full * pchunk + (tail ? tail / 2 + tail / 2 / block * 4 : 0);
-  Plan p;
-  if (hipError_t e = plan(bytes, pchunk, &p, s); e != hipSuccess) return e;
-  auto* seg = static_cast<uint32_t*>(workspace);
-  const ChunkGeo geo{static_cast<const uint8_t*>(packed), bytes, pchunk, p.spc, p.tail.xrem_full, p.tail.xrem_last};
-  const int64_t oc = src_chunk / 2;
-  const dim3 grid = seg_grid(p.total_segs, max_blocks), tpb{kThreads};
-  if (store < 0) store = kFusedStoreDefault;
-  // the split kernel's CRC half walks 8 segments per workgroup at a time
-  const dim3 grid2(unsigned(std::max<int64_t>(1, std::min<int64_t>((p.total_segs + 7) / 8, max_blocks > 0 ? max_blocks : 256))));
-  const dim3 grid5(unsigned((p.total_segs + kWaves - 1) / kWaves));  // store 5: one segment per wave
-  const OnceGrid og = once_split(p.total_segs, store != 10);
-  const dim3 grid7(og.blocks), tpb7(kWaves16 * 64);
-  const int64_t sb = og.split_block;
-#define DLD_VU(B)                                                                                           \
-  (store == 9   ? (verify_unpack_once16_kernel<B, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
-   : store == 14 ? (verify_unpack_once16_kernel<B, true, false, true><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
-   : store == 13 ? (verify_unpack_once16_kernel<B, true, true, false><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out)) \
-   : store == 7 || store == 10 ? (verify_unpack_once16_kernel<B, true, true, true><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out))  \
-   : store == 5 ? (verify_unpack_once_kernel<B><<<grid5, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))      \
-   : store == 2 ? (verify_unpack_split_kernel<B><<<grid2, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out))     \
-   : store == 1 ? (verify_unpack_segments_kernel<B, true><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)) \
-                : (verify_unpack_segments_kernel<B, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out)))
-  if (store == 8) {  // diagnostic: store 7 without the CRC math
-    if (block != 128) return hipErrorInvalidValue;
-    verify_unpack_once16_kernel<128, false, true, true><<<grid7, tpb7, 0, s>>>(geo, p.total_segs, sb, oc, p.consts, seg, out);
-  } else if (store == 3 || store == 4 || store == 6) {  // diagnostic: the same walk without the CRC math (CRCs are garbage)
-    if (block != 128) return hipErrorInvalidValue;
-    if (store == 3)
-      verify_unpack_segments_kernel<128, true, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
-    else if (store == 4)
-      verify_unpack_segments_kernel<128, false, false><<<grid, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
-    else
-      verify_unpack_once_kernel<128, false><<<grid5, tpb, 0, s>>>(geo, p.total_segs, oc, p.consts, seg, out);
-  } else {
-    switch (block) {
-      case 32: DLD_VU(32); break;
-      case 64: DLD_VU(64); break;
-      case 128: DLD_VU(128); break;
-      case 256: DLD_VU(256); break;
-      case 512: DLD_VU(512); break;
-      default: return hipErrorInvalidValue;
-    }
+  const int64_t bytes = full * pchunk + (tail ? packed_of(tail, block) : 0);
+  const uint32_t* consts = device_consts(s);
+  if (!consts) return hipErrorOutOfMemory;
+  ChunkGeo geo;
+  int64_t total = 0;
+  if (hipError_t e = chunk_geo(packed, bytes, pchunk, crc_out, &geo, &total); e != hipSuccess) return e;
+  geo.out = out;
+  geo.out_chunk_elems = src_chunk / 2;
+  return launch(geo, total, block, consts, workspace, s, cus);
+}
+
+hipError_t fp8_verify_unpack_batch(const FusedItem* items, int n, int block, void* workspace, hipStream_t s, int cus) {
+  if (n <= 0) return hipSuccess;
+  if (n > kCrcBatchMax || !valid_block(block)) return hipErrorInvalidValue;
+  const uint32_t* consts = device_consts(s);
+  if (!consts) return hipErrorOutOfMemory;
+  BatchGeo a{};
+  for (int i = 0; i < n; ++i) {
+    const FusedItem& it = items[i];
+    if (it.src_len <= 0) continue;
+    if (it.src_len % (2 * block) || (reinterpret_cast<uintptr_t>(it.out) & 15)) return hipErrorInvalidValue;
+    if (hipError_t e = batch_add(a, it.packed, packed_of(it.src_len, block), it.crc_out, it.out); e != hipSuccess)
+      return e;
   }
-#undef DLD_VU
-  crc32c_fold_kernel<<<dim3(unsigned(p.nchunks)), dim3(kFoldThreads), 0, s>>>(seg, bytes, pchunk, p.spc, p.tail,
-                                                                              crc_out);
-  return hipGetLastError();
+  if (a.n == 0) return hipSuccess;
+  for (int j = a.n; j < kCrcBatchMax; ++j) a.seg_base[j + 1] = a.seg_base[a.n];
+  return launch(a, a.seg_base[a.n], block, consts, workspace, s, cus);
 }
 
 }  // namespace kern

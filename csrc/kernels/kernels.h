@@ -34,38 +34,36 @@ hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, i
 // out: blocks * 1024 dwords; bytes % 16384 == 0.
 hipError_t read_seg(const void* src, int64_t bytes, uint32_t* out, int blocks, int layout, bool roll, hipStream_t s);
 
-// ---- crc32c.hip: CRC32C of every `chunk_bytes` chunk of [src, src+bytes).
-// out[c] (device or host-mapped memory) receives the standard CRC32C of chunk c.
-// `workspace` must hold crc32c_workspace_bytes(bytes, chunk_bytes) bytes of
-// device memory. src 16-B aligned; chunk_bytes a multiple of 16 unless the span
-// is one chunk (bytes <= chunk_bytes: any length, e.g. a layer's last chunk).
+// ---- crc32c.hip: CRC32C verification (and the fused fp8 unpack) on gfx950.
+// One kernel shape serves every entry point: one 16 KiB segment per wave,
+// 512-thread workgroups, two per CU, and the fold of a chunk's segments done
+// inside the same launch (device-scope atomics on a {acc, count} pair per
+// item in `workspace`; crc32c.hip). A workspace must be zeroed ONCE (e.g.
+// hipMemsetAsync) before its first use; every launch leaves it zeroed again.
+// Launches that share a workspace must be ordered (one stream).
+// `cus`: the CUs the launch's stream may use (a CU-masked verify stream); the
+// grid's last partial round is sized for them. 0 = the whole device.
+//
+// out[c] (device or host-mapped memory) receives the standard CRC32C of chunk
+// c of [src, src+bytes). src 16-B aligned; chunk_bytes a multiple of 16
+// unless the span is one chunk (bytes <= chunk_bytes: any length).
 size_t crc32c_workspace_bytes(int64_t bytes, int64_t chunk_bytes);
-// Build and upload (stream-ordered on s) the CRC tables and the fold tables of
-// `chunk_bytes` chunks ahead of time; later launches then never allocate. Any
-// table first needed later is uploaded the same way, never with a host sync.
-hipError_t crc32c_warm(int64_t chunk_bytes, hipStream_t s);
+// Upload the CRC tables (stream-ordered on s) ahead of time; later launches
+// then never allocate or copy. Never a host-synchronous copy.
+hipError_t crc32c_warm(hipStream_t s);
 hipError_t crc32c_chunks(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
-                         hipStream_t s);
+                         hipStream_t s, int cus = 0);
 // Batched: the standard CRC32C of each of up to kCrcBatchMax independent
-// buffers (any length, 16-B aligned) in one launch pair - the chunks a P2P
-// group landed. `workspace`: crc32c_batch_workspace_bytes(max bytes, n).
+// buffers (any length, 16-B aligned) in one launch - the chunks one P2P group
+// or one staging batch landed. `workspace`: crc32c_batch_workspace_bytes().
 constexpr int kCrcBatchMax = 16;
 struct CrcItem {
   const void* src;
   int64_t bytes;
   uint32_t* out;
 };
-size_t crc32c_batch_workspace_bytes(int64_t max_item_bytes, int n);
-// crc32c_chunks with the segment kernel's grid capped at max_blocks workgroups
-// (0 = one per CU); capped grids put many segments on every wave (tests, A/B).
-// The segment kernel (slice-by-4 byte tables on lane-contiguous 64-B pieces of
-// coalesced loads) and the variants it replaced: crc32c.hip, profiles/r2_crc_ab.
-hipError_t crc32c_chunks_capped(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* out, void* workspace,
-                                hipStream_t s, int max_blocks);
-// max_blocks (here and in fp8_verify_unpack): cap on the segment kernel's grid,
-// one workgroup per CU (0 = all 256); a CU-masked stream passes its CU count so
-// no workgroup waits for a second wave.
-hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int max_blocks = 0);
+size_t crc32c_batch_workspace_bytes();
+hipError_t crc32c_batch(const CrcItem* items, int n, void* workspace, hipStream_t s, int cus = 0);
 
 // ---- fp8.hip: bf16 -> OCP fp8 e4m3fn with one f32 scale per `block` elements
 // (power-of-two scale 2^E, core/fp8.h; +-inf saturate, NaN stays NaN), and back.
@@ -77,22 +75,20 @@ hipError_t fp8_pack_chunks(const void* src, int64_t src_bytes, int64_t src_chunk
 
 // ---- crc32c.hip: fused verify + unpack of a packed layer: crc_out[c] = CRC32C of
 // packed chunk c, out = the bf16 layer (src_bytes). One pass over the packed bytes.
-// `workspace`: crc32c_workspace_bytes(packed bytes, packed chunk) bytes.
-// store: how the bf16 output leaves the CU - 0 = each lane's 32 B straight from
-// registers (two half-dense 2 KiB stores per word), 1 = through 1 KiB of LDS per
-// wave as fully coalesced 1 KiB stores, 2 = split roles: half of each
-// workgroup's waves CRC the segments while the other half unpack them;
-// 5 = one segment per wave (1024-thread workgroups, 32 table replicas), 7 = the
-// same with 512-thread workgroups and 16 replicas (two per CU), the grid's
-// last partial round in half segments and nontemporal staged stores, 9 = 7
-// with direct stores (temporal), 10 = 7 without the half-segment round, 13 = 7
-// with temporal stores, 14 = 9 with nontemporal ones; 3, 4, 6, 8 are no-CRC
-// diagnostics (their CRCs are garbage); -1 = kFusedStoreDefault.
-// 7: 5.3-5.4 TB/s at 512 MiB, 5.9-6.2 at 4 GiB vs store 1's 4.66 / 4.89
-// (profiles/r4_nt, profiles/r4_kernels_final)
-constexpr int kFusedStoreDefault = 7;
+// `workspace`: crc32c_workspace_bytes(packed bytes, packed chunk) bytes, zeroed once.
 hipError_t fp8_verify_unpack(const void* packed, int64_t src_bytes, int64_t src_chunk, int block, uint16_t* out,
-                             uint32_t* crc_out, void* workspace, hipStream_t s, int max_blocks = 0, int store = -1);
+                             uint32_t* crc_out, void* workspace, hipStream_t s, int cus = 0);
+// Batched: up to kCrcBatchMax independent packed chunks (each the core/fp8.h
+// image of `src_len` bf16 source bytes) in one launch: CRC32C of each packed
+// chunk to *crc_out, its bf16 values to out. `workspace`: crc32c_batch_workspace_bytes().
+struct FusedItem {
+  const void* packed;
+  int64_t src_len;
+  uint16_t* out;
+  uint32_t* crc_out;
+};
+hipError_t fp8_verify_unpack_batch(const FusedItem* items, int n, int block, void* workspace, hipStream_t s,
+                                   int cus = 0);
 
 }  // namespace kern
 }  // namespace dissem

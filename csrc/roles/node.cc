@@ -30,7 +30,7 @@ Node::Node(NodeConfig cfg, std::shared_ptr<Transport> t, std::shared_ptr<DataEng
   if (is_leader_) {
     status_[cfg_.id] = store_.inventory();  // node.go:252-257
     partial_[cfg_.id] = store_.partial();
-    for (auto& kv : cfg_.link_report) measured_links_[{cfg_.id, kv.first}] = kv.second;
+    merge_link_rates(cfg_.id, cfg_.link_report, cfg_.link_report_in);
   }
   e_->bind(this);
   if (is_leader_ && e_->planned()) {
@@ -173,6 +173,7 @@ void Node::announce() {
   m.layers = store_.inventory();
   m.partial_layers = store_.partial();
   m.link_rates = cfg_.link_report;
+  m.link_rates_in = cfg_.link_report_in;
   if (e_->planned()) {
     // Whole copies' manifests, and a resumed partial copy's too: the leader
     // takes from the latter only the chunks inside its announced ranges.
@@ -444,6 +445,21 @@ int64_t Node::layer_size(LayerID l) {
   return sz;
 }
 
+// A directed link s -> d is timed at both ends: s reports it with its send
+// rates, d with its receive rates. Each end's P2P time includes waiting for the
+// other end to post, so the faster reading is the link's (the later poster
+// timed the transfer alone); the announces arrive in any order.
+void Node::merge_link_rates(NodeID src, const std::map<NodeID, int64_t>& out, const std::map<NodeID, int64_t>& in) {
+  for (auto& kv : out) {
+    int64_t& v = measured_links_[{src, kv.first}];
+    v = std::max(v, kv.second);
+  }
+  for (auto& kv : in) {
+    int64_t& v = measured_links_[{kv.first, src}];
+    v = std::max(v, kv.second);
+  }
+}
+
 void Node::on_announce(const MessagePtr& m) {
   // node.go:295-324
   if (!status_.count(m->src)) {
@@ -451,7 +467,7 @@ void Node::on_announce(const MessagePtr& m) {
     status_[m->src] = m->layers;
     partial_[m->src] = m->partial_layers;
     add_node(m->src);
-    for (auto& kv : m->link_rates) measured_links_[{m->src, kv.first}] = kv.second;
+    merge_link_rates(m->src, m->link_rates, m->link_rates_in);
   }
   if (!started_) t_->warm(m->src);  // the first dispatch after "timer start" pays no connect
   for (auto& kv : m->manifest) {

@@ -57,7 +57,8 @@ struct NodeConfig {
   // plans on every node's reported rates instead of link_bw's estimates:
   // mode-1 "links" owners and relays, mode-3 capacities and T, mode-2 sender
   // choice (reference: node.go:774-793 measures job times, :1044-1053 uses them).
-  std::map<NodeID, int64_t> link_report;
+  std::map<NodeID, int64_t> link_report;     // closed loop: this node's measured rate to each peer (B/s)
+  std::map<NodeID, int64_t> link_report_in;  // ... and each peer's link into this node, timed here
   bool adapt_links = true;
   // Nodes whose disk tiers read one shared device (all ranks of one MI355X
   // node share its NVMe): node -> group, group -> read rate (B/s). Mode 3 plans
@@ -155,6 +156,7 @@ class Node {
   void fetch_from_client(LayerID layer, NodeID dest);
   // leader-side
   void on_announce(const MessagePtr& m);
+  void merge_link_rates(NodeID src, const std::map<NodeID, int64_t>& out, const std::map<NodeID, int64_t>& in);
   void on_ack(const MessagePtr& m);
   bool assignment_satisfied();
   void send_startup();

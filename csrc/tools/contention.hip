@@ -196,9 +196,10 @@ static int rccl_paced(double secs, double land_gbps) {
   CHECK(hipMalloc(&rbuf, size_t(xfer)));
   CHECK(hipMemset(sbuf, 3, size_t(xfer)));
   const int kRing = 64;
-  const size_t wsb = dissem::kern::crc32c_batch_workspace_bytes(chunk, int(nchunks));
+  const size_t wsb = dissem::kern::crc32c_batch_workspace_bytes();
   uint8_t* ws = nullptr;
   CHECK(hipMalloc(&ws, wsb * kRing));
+  CHECK(hipMemset(ws, 0, wsb * kRing));  // fold words: zeroed once (kernels.h)
   uint32_t* crc = nullptr;
   CHECK(hipMalloc(&crc, size_t(kRing) * nchunks * sizeof(uint32_t)));
   const double period_s = double(chunk * nchunks) / (land_gbps * 1e9);
@@ -329,7 +330,8 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&buf, size_t(chunk * nchunks)));
   CHECK(dissem::kern::fill_random(buf, chunk * nchunks, 42, nullptr));
   void* ws = nullptr;
-  CHECK(hipMalloc(&ws, dissem::kern::crc32c_batch_workspace_bytes(chunk, int(nchunks))));
+  CHECK(hipMalloc(&ws, dissem::kern::crc32c_batch_workspace_bytes()));
+  CHECK(hipMemset(ws, 0, dissem::kern::crc32c_batch_workspace_bytes()));
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   uint32_t *crc = nullptr, *probe_out = nullptr;
@@ -436,9 +438,10 @@ int paced(double secs, double land_gbps, const std::vector<int>& caps) {
   CHECK(hipMalloc(&buf, size_t(chunk * nchunks)));
   CHECK(dissem::kern::fill_random(buf, chunk * nchunks, 42, nullptr));
   const int kRing = 64;  // batches in flight at most (workspace + CRC slots per batch)
-  const size_t wsb = dissem::kern::crc32c_batch_workspace_bytes(chunk, int(nchunks));
+  const size_t wsb = dissem::kern::crc32c_batch_workspace_bytes();
   uint8_t* ws = nullptr;
   CHECK(hipMalloc(&ws, wsb * kRing));
+  CHECK(hipMemset(ws, 0, wsb * kRing));  // fold words: zeroed once (kernels.h)
   uint32_t* crc = nullptr;
   CHECK(hipMalloc(&crc, size_t(kRing) * nchunks * sizeof(uint32_t)));
   const int64_t copy_bytes = 256ll << 20;

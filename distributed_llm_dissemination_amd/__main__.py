@@ -100,8 +100,6 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--node-disk-gbps", type=float, default=0.0,
                    help="rccl: one NVMe shared by every rank of the node at this read rate (disk readers share it; "
                         "mode 3 plans it as one budget); 0 = per-rank disks")
-    p.add_argument("--crc-grid", type=int, default=-1,
-                   help="rccl: workgroup cap of the CRC verify kernels (-1/0: every CU of the verify stream)")
     p.add_argument("--comm-init", default="split", choices=["parallel", "split"],
                    help="rccl: lane communicators split from the world communicator one by one (split, the "
                         "default: faster at 8 shared ranks, profiles/r3_init2), or one unique id each, initialized "
@@ -144,7 +142,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
-    opts = {"reserve_cus": args.reserve_cus, "crc_grid": int(getattr(args, "crc_grid", -1)),
+    opts = {"reserve_cus": args.reserve_cus,
             "verify_cus": int(getattr(args, "verify_cus", -1)),
             "suspect_s": getattr(args, "suspect_timeout", 10.0),
             "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0)),

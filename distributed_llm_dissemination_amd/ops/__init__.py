@@ -9,6 +9,7 @@ from .kernels import (  # noqa: F401
     fp8_packed_size,
     fp8_unpack,
     fp8_verify_unpack,
+    fp8_verify_unpack_chunks,
 )
 
 __all__ = [
@@ -20,4 +21,5 @@ __all__ = [
     "fp8_packed_size",
     "fp8_unpack",
     "fp8_verify_unpack",
+    "fp8_verify_unpack_chunks",
 ]

@@ -33,6 +33,7 @@ __all__ = [
     "fp8_unpack",
     "fp8_pack_layer",
     "fp8_verify_unpack",
+    "fp8_verify_unpack_chunks",
     "fp8_packed_size",
 ]
 
@@ -78,7 +79,8 @@ def crc32c(t: torch.Tensor, chunk_bytes: int = 0) -> torch.Tensor:
         raise ValueError("chunk_bytes must be a multiple of 16")
     nchunks = (n + chunk - 1) // chunk
     out = torch.empty(nchunks, dtype=torch.int32, device=t.device)
-    ws = torch.empty(_core.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device=t.device)
+    # the fold words of the launch: zeroed (kernels.h: the kernel leaves them zeroed)
+    ws = torch.zeros(_core.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device=t.device)
     _core.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), _stream())
     return out
 
@@ -152,7 +154,34 @@ def fp8_verify_unpack(packed: torch.Tensor, src_bytes: int, chunk_bytes: int,
     nchunks = (pbytes + pchunk - 1) // pchunk
     out = torch.empty(src_bytes // 2, dtype=torch.bfloat16, device=packed.device)
     crcs = torch.empty(nchunks, dtype=torch.int32, device=packed.device)
-    ws = torch.empty(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device=packed.device)
+    ws = torch.zeros(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device=packed.device)
     _core.fp8_verify_unpack_async(packed.data_ptr(), src_bytes, chunk_bytes, block, out.data_ptr(), crcs.data_ptr(),
                                   ws.data_ptr(), _stream())
     return out, crcs
+
+
+def fp8_verify_unpack_chunks(chunks: List[Tuple[torch.Tensor, int]], block: int = 128
+                             ) -> Tuple[List[torch.Tensor], torch.Tensor]:
+    """The engine's batched form: independent packed chunks [(packed uint8, src_len), ...]
+    (each the core/fp8.h image of `src_len` bf16 bytes, up to `_core.crc32c_batch_max()`
+    of them) checked and dequantized in ONE launch. Returns ([bf16 per chunk], crcs int32)."""
+    if not chunks or len(chunks) > _core.crc32c_batch_max():
+        raise ValueError(f"1 to {_core.crc32c_batch_max()} chunks per launch")
+    if block not in _FP8_BLOCKS:
+        raise ValueError(f"block must be one of {_FP8_BLOCKS}")
+    outs, items = [], []
+    dev = chunks[0][0].device
+    for packed, src_len in chunks:
+        _check_dev(packed, "packed", torch.uint8)
+        if src_len <= 0 or src_len % (2 * block):
+            raise ValueError("src_len must be a positive multiple of 2 * block")
+        need = src_len // 2 + src_len // 2 // block * 4
+        if packed.numel() < need:
+            raise ValueError(f"packed chunk holds {packed.numel()} bytes, its layout needs {need}")
+        y = torch.empty(src_len // 2, dtype=torch.bfloat16, device=dev)
+        outs.append(y)
+        items.append((packed.data_ptr(), src_len, y.data_ptr()))
+    crcs = torch.empty(len(chunks), dtype=torch.int32, device=dev)
+    ws = torch.zeros(_core.crc32c_batch_workspace_bytes(), dtype=torch.uint8, device=dev)
+    _core.fp8_verify_unpack_batch_async(items, block, crcs.data_ptr(), ws.data_ptr(), _stream())
+    return outs, crcs

@@ -56,6 +56,35 @@ def hist_quantile(hist: List[int], q: float) -> int:
     return 1 << len(hist)
 
 
+def mode3_plan(cfg: Config, integer_seconds: bool = True, storage: bool = False) -> "_core.FlowPlan":
+    """The mode-3 leader's plan for `cfg` on the TCP data plane, without moving a
+    byte: the flow problem Node::schedule_mode3 builds from the announces -
+    every node's initial layers as holdings at its Sources rate of their tier
+    (disk tier on disk, the others in memory unless `storage`, as `-s` does),
+    a demand for every assigned layer its node does not hold (a node that holds
+    it in some tier loads it itself: a self-job, node.go:1205-1217), each
+    node's NetworkBW as its egress and ingress budget, the config's Links -
+    solved by sched/maxflow (reference: flow.go:146-219; with integer_seconds
+    T is bisected over whole seconds as the reference does, flow.go:155-187)."""
+    holdings: Dict[int, Dict[int, object]] = {}
+    size: Dict[int, int] = {}
+    for n in cfg.nodes:
+        held = holdings.setdefault(n.id, {})
+        for st, per in n.initial_layers.items():
+            rate = n.sources.get(st, 0)
+            on_disk = st == SOURCE_DISK or (storage and st not in (SOURCE_CLIENT, SOURCE_DEVICE))
+            loc = (_core.Location.Client if st == SOURCE_CLIENT else _core.Location.Disk if on_disk
+                   else _core.Location.Device if st == SOURCE_DEVICE else _core.Location.Inmem)
+            for l, sz in per.items():
+                held[l] = _core.LayerMeta(loc, rate, _core.SourceType(st), sz)
+                size[l] = max(size.get(l, 0), sz)
+    demands = [(l, d, size.get(l, cfg.layer_size)) for d, ls in sorted(cfg.assignment.items()) for l in ls
+               if l not in holdings.get(d, {})]
+    bw = {n.id: n.network_bw for n in cfg.nodes if n.network_bw > 0}
+    links = {(s, d): b for s, per in cfg.links.items() for d, b in per.items()}
+    return _core.solve_flow(holdings, demands, bw, bw, links=links, integer_seconds=integer_seconds)
+
+
 def _sig(x: float, digits: int = 4) -> float:
     """`x` to `digits` significant digits (probe rates: GB/s at any fabric scale)."""
     return float(f"{x:.{digits}g}")
@@ -201,12 +230,16 @@ class Runtime:
         self._closed = False
         self.device: Optional[int] = None
         self.keep: List[object] = []  # buffers that must outlive sessions
-        # Closed-loop link rates (planned engines): EWMA of this rank's measured
-        # send rate to each peer node (B/s), reported with its announce.
-        self.link_est: Dict[int, float] = {}
-        self.link_probe: Dict[int, float] = {}  # pre-flight probe's concurrent rates (B/s): the capacity floor
-        self.link_slow_streak: Dict[int, int] = {}  # consecutive observations below LINK_SLOW x the median
-        self.link_level: Optional[float] = None  # the uniform level every normal link reports (B/s)
+        # Closed-loop link rates (planned engines): per peer node, the EWMA of
+        # this rank's measured busy throughput on the link to it (sends) and on
+        # the link from it (receives), reported with its announce.
+        self.link_est: Dict[int, float] = {}      # out: this rank -> peer (B/s)
+        self.link_est_in: Dict[int, float] = {}   # in: peer -> this rank (B/s)
+        self.link_obs: Dict[tuple, int] = {}      # (dir, peer): sessions that measured the link
+        self.link_probe: Dict[int, float] = {}  # pre-flight probe's concurrent send rates (B/s)
+        self.link_probe_in: Dict[int, float] = {}  # ... and receive rates (the links into this rank)
+        self.link_slow_streak: Dict[tuple, int] = {}  # (dir, peer): observations below LINK_SLOW x the median
+        self.link_level: Dict[str, float] = {}  # dir -> the uniform level every normal link reports (B/s)
         self._links0: Optional[Dict[str, Dict[int, float]]] = None
 
         reg = dict(registry) if registry is not None else cfg.registry()
@@ -729,6 +762,7 @@ class Runtime:
         nc.adapt_links = adapt_links
         if adapt_links:
             nc.link_report = self.link_report()
+            nc.link_report_in = self.link_report_in()
         nc.integer_seconds = integer_seconds
         nc.job_timeout_s = job_timeout_s
         nc.job_min_rate = job_min_rate
@@ -816,18 +850,24 @@ class Runtime:
         return h
 
     # ------------------------------------------------- closed-loop link rates
-    # Per directed link from this rank, a CAPACITY estimate: the larger of the
-    # EWMA of earlier sessions' busy throughput (bytes / device time of the P2P
-    # groups that carried them) and the pre-flight probe's concurrent rate.
-    # Busy throughput reads low whenever a send waits for its peer's recv (the
-    # RCCL send kernel spins until the receiver posts; the simulator's groups
-    # likewise), so alone it would pace mode 3 below the fabric; the probe
-    # times both ends posted together and floors it. The report the leader
-    # plans on is uniform unless a link is really slower than the others:
-    #   * every link reports the same level U (the median capacity, moved only
-    #     when the median moves by more than LINK_LEVEL_HYST), so a uniform
-    #     mesh plans uniformly and identically session after session (the
-    #     leader's plan cache then replays the plan);
+    # Per directed link touching this rank, a CAPACITY estimate from earlier
+    # sessions: bytes over the device time of the P2P groups that carried them,
+    # timed at this end - sends for the links out of this rank, receives for
+    # the links into it (EWMA over sessions). Either end's time includes
+    # waiting for the other end to post (an RCCL send kernel spins until its
+    # receive is posted, and a receive until its send is), so the leader plans
+    # each link on the FASTER of its two ends' reports (Node::merge_link_rates):
+    # the later poster timed the transfer alone. A receiver that posts late
+    # slows the send-side reading of the links into it, never the plan.
+    # The pre-flight probe (both ends posted together) floors a send-side
+    # estimate until LINK_PROBE_SESSIONS sessions have measured the link;
+    # from then on the sessions alone decide, so a link that degrades after
+    # the probe is seen. The report the leader plans on is uniform unless a
+    # link is really slower than the others:
+    #   * every normal link reports the same level U (the median capacity of
+    #     its direction, moved only when the median moves by more than
+    #     LINK_LEVEL_HYST), so a uniform mesh plans uniformly and identically
+    #     session after session (the leader's plan cache then replays it);
     #   * a link whose capacity stayed below LINK_SLOW x the median in
     #     LINK_SLOW_SESSIONS consecutive observations (the probe counts as one)
     #     reports its own capacity, and the plans route around it.
@@ -837,65 +877,99 @@ class Runtime:
     LINK_SLOW_SESSIONS = 2  # ... in this many consecutive observations is planned at its own rate
     LINK_LEVEL_HYST = 0.10  # the uniform level follows the median only past this relative change
     LINK_MIN_CHUNKS = 4     # a link must have carried this many grid chunks in a session to be measured
+    LINK_PROBE_SESSIONS = 2  # sessions after which the probe no longer floors a link
 
-    def observe_links(self, rates: Dict[int, float]) -> None:
-        """Fold one session's measured send rates (peer node -> B/s) into the per-link EWMA."""
+    def _est(self, d: str) -> Dict[int, float]:
+        return self.link_est if d == "out" else self.link_est_in
+
+    def observe_links(self, rates: Dict[int, float], rates_in: Optional[Dict[int, float]] = None) -> None:
+        """Fold one session's measured rates (peer node -> B/s; send side, and
+        optionally receive side) into the per-link EWMAs."""
         a = self.LINK_EWMA_ALPHA
-        for p, r in rates.items():
-            if r is None or r <= 0 or p == self.node_id:
-                continue
-            old = self.link_est.get(p)
-            self.link_est[p] = float(r) if old is None else old + a * (float(r) - old)
-        self._update_link_state()
+        for d, rs in (("out", rates), ("in", rates_in or {})):
+            est = self._est(d)
+            for p, r in rs.items():
+                if r is None or r <= 0 or p == self.node_id:
+                    continue
+                old = est.get(p)
+                est[p] = float(r) if old is None else old + a * (float(r) - old)
+                self.link_obs[(d, p)] = self.link_obs.get((d, p), 0) + 1
+            if rs:
+                self._update_link_state(d)
 
-    def observe_probe(self, rates: Dict[int, float]) -> None:
-        """The pre-flight probe's concurrent send rates (peer node -> B/s): the floor
-        of every link's capacity estimate from now on."""
-        for p, r in rates.items():
-            if r and r > 0 and p != self.node_id:
-                self.link_probe[p] = float(r)
-        self._update_link_state()
+    def observe_probe(self, rates: Dict[int, float], rates_in: Optional[Dict[int, float]] = None) -> None:
+        """The pre-flight probe's concurrent rates (peer node -> B/s) at this
+        rank's sending end and, optionally, its receiving end: the floor of
+        every link's capacity until sessions measured it."""
+        for d, rs in (("out", rates), ("in", rates_in or {})):
+            probe = self.link_probe if d == "out" else self.link_probe_in
+            for p, r in rs.items():
+                if r and r > 0 and p != self.node_id:
+                    probe[p] = float(r)
+            if rs:
+                self._update_link_state(d)
 
-    def link_capacity(self) -> Dict[int, float]:
-        """Per peer node: max(session EWMA, probe) in B/s."""
-        peers = set(self.link_est) | set(self.link_probe)
-        return {p: max(self.link_est.get(p, 0.0), self.link_probe.get(p, 0.0)) for p in peers}
+    def link_capacity(self, d: str = "out") -> Dict[int, float]:
+        """Per peer node (B/s): the session EWMA of direction `d`, floored by the
+        probe while fewer than LINK_PROBE_SESSIONS sessions measured the link
+        (the probe alone before any)."""
+        est = self._est(d)
+        probe = self.link_probe if d == "out" else self.link_probe_in
+        out = {}
+        for p in set(est) | set(probe):
+            e = est.get(p, 0.0)
+            if p in probe and self.link_obs.get((d, p), 0) < self.LINK_PROBE_SESSIONS:
+                e = max(e, probe[p])
+            out[p] = e
+        return out
 
-    def _update_link_state(self) -> None:
-        cap = self.link_capacity()
+    def _update_link_state(self, d: str) -> None:
+        cap = self.link_capacity(d)
         if not cap:
             return
         vals = sorted(cap.values())
         med = vals[len(vals) // 2]
         for p, c in cap.items():
-            self.link_slow_streak[p] = self.link_slow_streak.get(p, 0) + 1 if c < self.LINK_SLOW * med else 0
-        if self.link_level is None or abs(med - self.link_level) > self.LINK_LEVEL_HYST * self.link_level:
-            self.link_level = med
+            k = (d, p)
+            self.link_slow_streak[k] = self.link_slow_streak.get(k, 0) + 1 if c < self.LINK_SLOW * med else 0
+        lvl = self.link_level.get(d)
+        if lvl is None or abs(med - lvl) > self.LINK_LEVEL_HYST * lvl:
+            self.link_level[d] = med
 
     def _observe_session_links(self) -> None:
-        """After a session: this rank's bytes to each peer over the device time of
-        the P2P groups that carried them (per directed link busy throughput)."""
+        """After a session: this rank's bytes to / from each peer over the device
+        time of the P2P groups that carried them (per directed link busy throughput)."""
         if self._links0 is None:
             return
         now = self.link_stats()
-        rates = {}
-        for p, b in now["sent"].items():
-            db = b - self._links0["sent"].get(p, 0)
-            dms = now["send_busy_ms"].get(p, 0.0) - self._links0["send_busy_ms"].get(p, 0.0)
-            if db >= self.LINK_MIN_CHUNKS * self.grid and dms > 0:
-                rates[self.node_ids[p]] = db / (dms / 1e3)
-        if rates:
-            self.observe_links(rates)
+        got = {}
+        for d, bytes_k, ms_k in (("out", "sent", "send_busy_ms"), ("in", "recv", "recv_busy_ms")):
+            rates = {}
+            for p, b in now[bytes_k].items():
+                db = b - self._links0[bytes_k].get(p, 0)
+                dms = now[ms_k].get(p, 0.0) - self._links0[ms_k].get(p, 0.0)
+                if db >= self.LINK_MIN_CHUNKS * self.grid and dms > 0:
+                    rates[self.node_ids[p]] = db / (dms / 1e3)
+            got[d] = rates
+        if got["out"] or got["in"]:
+            self.observe_links(got["out"], got["in"])
+
+    def _report(self, d: str) -> Dict[int, int]:
+        cap = self.link_capacity(d)
+        lvl = self.link_level.get(d)
+        if not cap or lvl is None:
+            return {}
+        return {p: int(c if self.link_slow_streak.get((d, p), 0) >= self.LINK_SLOW_SESSIONS else lvl)
+                for p, c in cap.items()}
 
     def link_report(self) -> Dict[int, int]:
-        """What this rank announces (B/s per peer node): the uniform level, or a
-        persistently slow link's own capacity (see above)."""
-        cap = self.link_capacity()
-        if not cap or self.link_level is None:
-            return {}
-        lvl = self.link_level
-        return {p: int(c if self.link_slow_streak.get(p, 0) >= self.LINK_SLOW_SESSIONS else lvl)
-                for p, c in cap.items()}
+        """What this rank announces for its links out (B/s per peer node): the
+        uniform level, or a persistently slow link's own capacity (see above)."""
+        return self._report("out")
+
+    def link_report_in(self) -> Dict[int, int]:
+        """The same for the links into this rank, timed at the receiving end."""
+        return self._report("in")
 
     def plan_link_bw(self) -> Dict[tuple, int]:
         """Leader: the per directed link rates (B/s) its last plan used."""
@@ -951,7 +1025,8 @@ class Runtime:
         pair once more on its own (barrier between pairs; ranks not in the pair
         idle), which separates a slow link from a congested one. Every rank
         calls this at the same time. Rates are this rank's sends (GB/s of device
-        time, keyed by peer node). A lane that does not complete within
+        time, keyed by peer node); ``concurrent_in`` its receives (the links
+        into it, keyed by the sending node). A lane that does not complete within
         ``timeout_s`` raises RuntimeError naming the lane and the pair."""
         if self.engine is None or self.world < 2:
             return {}
@@ -976,6 +1051,9 @@ class Runtime:
             "bytes": nbytes,
             "concurrent": {self.node_ids[o["peer"]]: _sig(nbytes / (o["ms"] / 1e3) / 1e9) if o["ms"] > 0 else None
                            for o in got if o["send"]},
+            # the same pass timed at the receiving end: the links into this rank
+            "concurrent_in": {self.node_ids[o["peer"]]: _sig(nbytes / (o["ms"] / 1e3) / 1e9) if o["ms"] > 0 else None
+                              for o in got if not o["send"]},
             "concurrent_wall_ms": round(conc_ms, 3),
         }
         if solo:
@@ -1005,7 +1083,7 @@ class Runtime:
         of the P2P groups that involved the peer; per-lane device time."""
         es = self.engine.stats()
         return {"sent": dict(es.peer_sent), "recv": dict(es.peer_recv), "busy_ms": dict(es.peer_busy_ms),
-                "send_busy_ms": dict(es.peer_send_busy_ms),
+                "send_busy_ms": dict(es.peer_send_busy_ms), "recv_busy_ms": dict(es.peer_recv_busy_ms),
                 "lane_busy_ms": list(es.lane_busy_ms)}
 
     def layer_bytes(self, layer: int) -> bytes:

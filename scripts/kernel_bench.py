@@ -36,27 +36,12 @@ def main():
     out["fill_random_GBps"] = n / t / 1e9
     chunk = 64 << 20
     nch = n // chunk
-    ws = torch.empty(_core.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    # fold words of the verify launches: zeroed once (the kernels leave them zeroed)
+    ws = torch.zeros(_core.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
     res = torch.empty(nch, dtype=torch.int32, device="cuda")
     t = timed(lambda: _core.crc32c_chunks_async(buf.data_ptr(), n, chunk, res.data_ptr(), ws.data_ptr(), 0))
     out["crc32c_GBps"] = n / t / 1e9
-    # one 64 MiB chunk alone (the per-landing verify in the data engine)
-    ws1 = torch.empty(_core.crc32c_workspace_bytes(chunk, chunk), dtype=torch.uint8, device="cuda")
-    t = timed(lambda: _core.crc32c_chunks_async(buf.data_ptr(), chunk, chunk, res.data_ptr(), ws1.data_ptr(), 0), 50)
-    out["crc32c_one_64MiB_chunk_us"] = t * 1e6
-    # what a P2P group of 7 peers lands: 7 chunks, checked one by one or in one batch
-    outs7 = torch.empty(16, dtype=torch.int32, device="cuda")
-    bufs7 = [(buf.data_ptr() + i * chunk, chunk) for i in range(7)]
-
-    def seven_separate():
-        for i in range(7):
-            _core.crc32c_chunks_async(buf.data_ptr() + i * chunk, chunk, chunk, outs7.data_ptr() + 4 * i,
-                                      ws1.data_ptr(), 0)
-
-    wsb = torch.empty(_core.crc32c_batch_workspace_bytes(chunk, 7), dtype=torch.uint8, device="cuda")
-    out["crc32c_7x64MiB_separate_us"] = timed(seven_separate, 20) * 1e6
-    out["crc32c_7x64MiB_batched_us"] = timed(
-        lambda: _core.crc32c_batch_async(bufs7, outs7.data_ptr(), wsb.data_ptr(), 0), 20) * 1e6
+    # the per-landing check sizes: scripts/verify_bench.py
     ne = n // 2
     x = buf.view(torch.bfloat16)[:ne]
     q = torch.empty(ne, dtype=torch.uint8, device="cuda")
@@ -75,7 +60,7 @@ def main():
     t = timed(lambda: _core.fp8_pack_chunks(buf.data_ptr(), src, chunk, 128, packed.data_ptr()))
     out["fp8_pack_chunks_GBps"] = (src + pbytes) / t / 1e9
     pchunk = chunk // 2 + chunk // 2 // 128 * 4
-    ws2 = torch.empty(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device="cuda")
+    ws2 = torch.zeros(_core.crc32c_workspace_bytes(pbytes, pchunk), dtype=torch.uint8, device="cuda")
     t = timed(lambda: _core.fp8_verify_unpack_async(packed.data_ptr(), src, chunk, 128, unpacked.data_ptr(),
                                                     res.data_ptr(), ws2.data_ptr(), 0))
     out["fp8_verify_unpack_GBps"] = (pbytes + src) / t / 1e9

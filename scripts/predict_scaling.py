@@ -43,10 +43,11 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
             adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
             nic_gbps: float = 50.0, host_lane_classes: int = 0, probe_mib: int = 256, warmup: int = 1,
-            recv_delay=None) -> dict:
+            recv_delay=None, slow_after_probe: bool = False) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
-    slow_link=((s, d), frac): that directed link runs at frac of the others.
+    slow_link=((s, d), frac): that directed link runs at frac of the others
+    (slow_after_probe: only from the first session on - the probe saw it at full speed).
     plan_links: the leader's plan knows every link's capacity (config Links)
     and every GPU's staging rate, at the simulated (scaled) rates: mode 1 with
     owner_policy "links" can relay around a slow link, and mode 3 plans - and
@@ -82,14 +83,15 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
         return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                         seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
                         disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib, warmup,
-                        {r: v * slowdown for r, v in (recv_delay or {}).items()})
+                        {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe)
     finally:
         _core.set_log_level(level)
 
 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
              policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False,
-             hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1, recv_delay=None):
+             hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1, recv_delay=None,
+             slow_after_probe=False):
     import shutil
     import tempfile
 
@@ -97,7 +99,8 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
     try:
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
-                           storage, host_share, hosts, nic_gbps, host_lane_classes, probe_mib, warmup, recv_delay)
+                           storage, host_share, hosts, nic_gbps, host_lane_classes, probe_mib, warmup, recv_delay,
+                           slow_after_probe)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
@@ -106,7 +109,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
                 policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
                 host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1,
-                recv_delay=None):
+                recv_delay=None, slow_after_probe=False):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -115,9 +118,12 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     t.wait_s = 600.0  # congested schedules queue transfers behind their links and NICs for long
     t.stage_bps = pcie_gbps * 1e9 / scale
     t.link_bps = link_gbps * 1e9 / scale
+    slow = {}
     if slow_link is not None:
         (s, d), frac = slow_link
-        t.link = {(s, d): link_gbps * 1e9 / scale * frac}
+        slow = {(s, d): link_gbps * 1e9 / scale * frac}
+        if not slow_after_probe:
+            t.link = slow
     if recv_delay:
         t.recv_delay_s = dict(recv_delay)
     per_host = max(1, n // max(1, hosts))
@@ -170,9 +176,13 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             for th in ths:
                 th.join()
             for r, g in zip(rts, got):
-                r.observe_probe({p: v * 1e9 for p, v in g.get("concurrent", {}).items() if v})
+                r.observe_probe({p: v * 1e9 for p, v in g.get("concurrent", {}).items() if v},
+                                {p: v * 1e9 for p, v in g.get("concurrent_in", {}).items() if v})
             conc = sorted(v for g in got for v in g.get("concurrent", {}).values() if v)
             probe_GBps = round(conc[len(conc) // 2] * scale * slowdown, 1) if conc else None
+        if slow and slow_after_probe:  # the link degrades after the probe
+            t.link = slow
+            _core.sim_set_timing(key, t)
         for step in range(warmup + steps):
             for r in rts:
                 extra = {"stage_gbps": pcie_gbps / scale} if plan_links else {}
@@ -213,7 +223,8 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                         link_bytes[(i, p)] = d * scale
             staged = [(r.engine.stats().bytes_staged - staged0[i]) * scale for i, r in enumerate(rts)]
         lanes_used = rts[0].engine.stats().lanes
-        rts_est = [dict(r.link_est) for r in rts]  # per rank: the busy-throughput EWMA per peer (B/s)
+        rts_est = [dict(r.link_est) for r in rts]  # per rank: the send-side busy-throughput EWMA per peer (B/s)
+        rts_est_in = [dict(r.link_est_in) for r in rts]  # ... and the receive-side one per peer
     finally:
         for r in rts:
             r.close()
@@ -234,6 +245,8 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                                         for (a, b), v in sorted(plan_links_used.items())}} if plan_links_used else {}),
             "busy_GBps": {f"{i}->{p}": round(v * scale * slowdown / 1e9, 1) for i, r in enumerate(rts_est)
                           for p, v in sorted(r.items())},
+            "busy_in_GBps": {f"{p}->{i}": round(v * scale * slowdown / 1e9, 1) for i, r in enumerate(rts_est_in)
+                             for p, v in sorted(r.items())},
             "link_GiB_last": {f"{a}->{b}": round(v / 2**30, 3) for (a, b), v in sorted(link_bytes.items())},
             "staged_GiB_last": [round(v / 2**30, 3) for v in staged],
             "modeled_ms_last": round(modeled_ms(link_bytes, staged, n, link_gbps * slowdown, pcie_gbps * slowdown,

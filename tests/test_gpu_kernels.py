@@ -48,23 +48,27 @@ def test_crc32c_chunks_match_host(gpu, n, chunk):
         ((3 << 20) + 5, 1 << 20),  # byte tail
         (5 << 20, (1 << 20) + 4096),  # partial segment at every chunk end
         (96 << 20, 64 << 20),  # short last chunk of whole segments
+        ((520 << 20) + 4096, 64 << 20),  # several rounds of workgroups, last round in half segments
     ],
 )
-@pytest.mark.parametrize("max_blocks", [0, 3, 64])
-def test_crc32c_capped_grid_matches_host(gpu, n, chunk, max_blocks):
-    """Capped grids put many segments (full and partial, across chunk boundaries)
-    on every wave, so the rolling prefetch of each wave's next segment runs."""
+@pytest.mark.parametrize("cus", [0, 8, 32])
+def test_crc32c_cus_and_workspace_reuse(gpu, n, chunk, cus):
+    """The grid's last round is sized for the CUs the stream may use (a CU-masked
+    verify stream passes its count), and the fold words in the workspace are
+    left zeroed by every launch: the same workspace serves three launches."""
     t = _dev_bytes(n)
     gpu.fill_random(t.data_ptr(), n, 5 + n)
     torch.cuda.synchronize()
     host = t.cpu().numpy().tobytes()
     want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
     nch = len(want)
-    out = torch.zeros(nch, dtype=torch.int32, device="cuda")
-    ws = torch.empty(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
-    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, max_blocks)
-    torch.cuda.synchronize()
-    assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
+    ws = torch.zeros(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    for rep in range(3):
+        out = torch.zeros(nch, dtype=torch.int32, device="cuda")
+        gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, cus)
+        torch.cuda.synchronize()
+        assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want, rep
+        assert int(ws.count_nonzero()) == 0  # the launch left its fold words zeroed
 
 
 def test_crc32c_batch_matches_host(gpu):
@@ -78,23 +82,43 @@ def test_crc32c_batch_matches_host(gpu):
     torch.cuda.synchronize()
     got = gpu.crc32c_batch([(t.data_ptr(), t.numel()) for t in bufs])
     assert got == [gpu.crc32c(t.cpu().numpy().tobytes()) for t in bufs]
-    # the batched and per-buffer kernels agree
+    # the batched and per-buffer launches agree
     assert got == [gpu.crc32c_chunks(t.data_ptr(), t.numel(), t.numel())[0] for t in bufs]
 
 
-@pytest.mark.parametrize("max_blocks", [1, 7, 224])
-def test_crc32c_batch_capped_grid_matches_host(gpu, max_blocks):
-    """The engine caps the batched verify at its CU-masked stream's CUs (224 with
-    32 reserved); small caps put many segments of several buffers on one wave."""
-    sizes = [64 << 20, 3 * (16 << 10) + 32, 16, (5 << 20) + 4096, 48 << 10]
+@pytest.mark.parametrize("cus", [1, 7, 224])
+def test_crc32c_batch_full_and_cus(gpu, cus):
+    """A full batch (crc32c_batch_max items, the engine's staging batch) of mixed
+    sizes, with the grid sized for few CUs (the masked verify stream) and the
+    async form reusing one workspace."""
+    nmax = gpu.crc32c_batch_max()
+    sizes = [[64 << 20, 3 * (16 << 10) + 32, 16, (5 << 20) + 4096, 48 << 10][i % 5] for i in range(nmax)]
     bufs = []
     for i, n in enumerate(sizes):
         t = _dev_bytes(n)
         gpu.fill_random(t.data_ptr(), n, 2000 + i)
         bufs.append(t)
     torch.cuda.synchronize()
-    got = gpu.crc32c_batch([(t.data_ptr(), t.numel()) for t in bufs], 0, max_blocks)
-    assert got == [gpu.crc32c(t.cpu().numpy().tobytes()) for t in bufs]
+    want = [gpu.crc32c(t.cpu().numpy().tobytes()) for t in bufs]
+    assert gpu.crc32c_batch([(t.data_ptr(), t.numel()) for t in bufs], 0, cus) == want
+    ws = torch.zeros(gpu.crc32c_batch_workspace_bytes(), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        out = torch.zeros(nmax, dtype=torch.int32, device="cuda")
+        gpu.crc32c_batch_async([(t.data_ptr(), t.numel()) for t in bufs], out.data_ptr(), ws.data_ptr(), 0, cus)
+        torch.cuda.synchronize()
+        assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
+
+
+def test_crc32c_single_chunk_over_1gib(gpu):
+    """One chunk larger than 1 GiB (a whole-tensor ops.crc32c of a big layer):
+    its segments' shifts to the chunk end combine two segpow levels."""
+    n = (1 << 30) + (3 << 20) + 4096 + 7
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 4242)
+    torch.cuda.synchronize()
+    want = gpu.crc32c(t.cpu().numpy().tobytes())
+    assert gpu.crc32c_chunks(t.data_ptr(), n, n) == [want]
+    assert gpu.crc32c_batch([(t.data_ptr(), n)]) == [want]
 
 
 @pytest.mark.parametrize("n", [5, 16 + 7, (16 << 10) + 9, 59055800, (64 << 20) - 8])
@@ -228,29 +252,59 @@ def test_fp8_pack_chunks_matches_host_layout(gpu, size, chunk, block):
     _host_fp8_codes_close(out.cpu().numpy().tobytes(), want, n_q, pchunk)
 
 
-@pytest.mark.parametrize("size,chunk,block,max_blocks", [
+def _torch_unpack(packed: torch.Tensor, src_len: int, block: int) -> torch.Tensor:
+    """fp32 PyTorch reference of one packed chunk's dequantization: e4m3fn -> f32,
+    times its block's f32 scale, rounded to bf16 (core/fp8.h layout [q][scales])."""
+    n = src_len // 2
+    q = packed[:n].view(torch.float8_e4m3fn).float()
+    sc = packed[n : n + n // block * 4].view(torch.float32)
+    return (q.view(-1, block) * sc[:, None]).view(-1).to(torch.bfloat16)
+
+
+def _assert_bf16_bits_equal(got: torch.Tensor, want: torch.Tensor):
+    """Bit for bit, except that any NaN matches any NaN (payloads may differ)."""
+    g, w = got.view(torch.bfloat16), want.view(torch.bfloat16)
+    gn, wn = torch.isnan(g), torch.isnan(w)
+    assert torch.equal(gn, wn)
+    assert torch.equal(g.view(torch.int16)[~gn], w.view(torch.int16)[~wn])
+
+
+@pytest.mark.parametrize("block", [32, 128, 512])
+def test_fp8_unpack_matches_torch_fp32(gpu, block):
+    """The standalone unpack kernel against the fp32 torch reference, on random
+    bit patterns packed by the kernel (NaN codes and every scale exponent)."""
+    size, chunk = 4 << 20, 4 << 20
+    raw = _dev_bytes(size)
+    gpu.fill_random(raw.data_ptr(), size, 31 + block)
+    packed = _dev_bytes(gpu.fp8_packed_size(size, chunk, block))
+    gpu.fp8_pack_chunks(raw.data_ptr(), size, chunk, block, packed.data_ptr())
+    n = size // 2
+    y = _dev_bytes(size)
+    gpu.fp8_unpack(packed.data_ptr(), packed.data_ptr() + n, n, y.data_ptr(), block)
+    torch.cuda.synchronize()
+    _assert_bf16_bits_equal(y.view(torch.bfloat16), _torch_unpack(packed, size, block))
+
+
+@pytest.mark.parametrize("size,chunk,block,cus", [
     (3 * (1 << 20) + 4096, 1 << 20, 128, 0), (2 << 20, 1 << 20, 64, 0), ((1 << 20) + 1024, 64 << 10, 512, 0),
     (64 << 20, 64 << 20, 128, 0), (2 << 20, 1 << 20, 256, 0), (2 << 20, 1 << 20, 32, 0),
-    # store 7/9: more workgroups than slots with a short last round -> that round in half
+    # more workgroups than slots with a short last round -> that round in half
     # segments (short segments inside it); the small sizes above run every segment in halves
-    (160 << 20, (5 << 20) + 4096, 128, 0),
-    # capped grids: every wave walks many segments (scales prefetched one segment ahead,
-    # partial segments between full ones)
+    (160 << 20, (5 << 20) + 4096, 128, 0), (512 << 20, 64 << 20, 128, 0),
+    # grids sized for few CUs (a masked verify stream): other split points
     (48 << 20, 16 << 20, 128, 3), ((24 << 20) + 4096, 1 << 20, 256, 7), (16 << 20, (1 << 20) + 4096, 64, 1),
-    (8 << 20, 4 << 20, 32, 2), ((8 << 20) + 1024, 64 << 10, 512, 5)])
-@pytest.mark.parametrize("store", [0, 1, 2, 5, 7, 9, 10, 13, 14])
-def test_fp8_fused_verify_unpack(gpu, size, chunk, block, max_blocks, store):
+    (8 << 20, 4 << 20, 32, 2), ((8 << 20) + 1024, 64 << 10, 512, 5), (136 << 20, 64 << 20, 128, 128)])
+def test_fp8_fused_verify_unpack(gpu, size, chunk, block, cus):
     """One pass: CRC32C of every packed chunk + bf16 dequantization; compared with
-    the CRC kernel, the host CRC and the standalone unpack kernel (same math).
-    store 1: the bf16 leaves through the per-wave LDS staging slot (coalesced 1 KiB stores)."""
+    the CRC kernel, the host CRC, the fp32 torch reference of the unpack, the
+    standalone unpack kernel and the host C++ unpack."""
     raw = _dev_bytes(size)
     gpu.fill_random(raw.data_ptr(), size, 11)  # random bf16 bit patterns, NaN/Inf included
     packed_n = gpu.fp8_packed_size(size, chunk, block)
     packed = _dev_bytes(packed_n)
     gpu.fp8_pack_chunks(raw.data_ptr(), size, chunk, block, packed.data_ptr())
     out = _dev_bytes(size)
-    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr(), max_blocks=max_blocks,
-                                 store=store)
+    crcs = gpu.fp8_verify_unpack(packed.data_ptr(), size, chunk, block, out.data_ptr(), cus=cus)
     pchunk = chunk // 2 + chunk // 2 // block * 4
     assert crcs == gpu.crc32c_chunks(packed.data_ptr(), packed_n, pchunk)
     host = packed.cpu().numpy().tobytes()
@@ -260,9 +314,45 @@ def test_fp8_fused_verify_unpack(gpu, size, chunk, block, max_blocks, store):
         n = min(chunk, size - off) // 2
         base = packed.data_ptr() + c * pchunk
         gpu.fp8_unpack(base, base + n, n, ref.data_ptr() + off, block)
+        _assert_bf16_bits_equal(out[off : off + 2 * n].view(torch.bfloat16),
+                                _torch_unpack(packed[c * pchunk : c * pchunk + pchunk], 2 * n, block))
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     assert out.cpu().numpy().tobytes() == gpu.fp8_unpack_layer_host(host, size, chunk, block)
+
+
+@pytest.mark.parametrize("block,cus", [(128, 0), (128, 128), (32, 0), (512, 32), (64, 1)])
+def test_fp8_fused_batch(gpu, block, cus):
+    """The engine's launch: up to crc32c_batch_max independent packed chunks of
+    mixed sizes (full 64 MiB grid chunks, a layer's short last chunk, chunks
+    below one 16 KiB segment) in one launch; every CRC equals the host CRC of
+    its packed bytes and every bf16 output the fp32 torch reference. The same
+    workspace serves two launches (the kernel leaves its fold words zeroed)."""
+    nmax = gpu.crc32c_batch_max()
+    lens = [[64 << 20, (3 << 20) + 8 * block, 4 * block, (16 << 10) + 2 * block, 1 << 20][i % 5] for i in range(nmax)]
+    lens = [n - n % (2 * block) for n in lens]
+    chunks = []
+    for i, n in enumerate(lens):
+        raw = _dev_bytes(n)
+        gpu.fill_random(raw.data_ptr(), n, 500 + i)
+        p = _dev_bytes(gpu.fp8_packed_size(n, n, block))
+        gpu.fp8_pack_chunks(raw.data_ptr(), n, n, block, p.data_ptr())
+        chunks.append((p, n))
+    ws = torch.zeros(gpu.crc32c_batch_workspace_bytes(), dtype=torch.uint8, device="cuda")
+    for rep in range(2):
+        outs = [_dev_bytes(n) for _, n in chunks]
+        crc = torch.zeros(nmax, dtype=torch.int32, device="cuda")
+        gpu.fp8_verify_unpack_batch_async([(p.data_ptr(), n, o.data_ptr()) for (p, n), o in zip(chunks, outs)],
+                                          block, crc.data_ptr(), ws.data_ptr(), 0, cus)
+        torch.cuda.synchronize()
+        got = [int(x) & 0xFFFFFFFF for x in crc.cpu().tolist()]
+        assert got == [gpu.crc32c(p.cpu().numpy().tobytes()) for p, _ in chunks], rep
+        for (p, n), o in zip(chunks, outs):
+            _assert_bf16_bits_equal(o.view(torch.bfloat16), _torch_unpack(p, n, block))
+    # the synchronous binding agrees
+    outs = [_dev_bytes(n) for _, n in chunks]
+    assert gpu.fp8_verify_unpack_batch([(p.data_ptr(), n, o.data_ptr()) for (p, n), o in zip(chunks, outs)],
+                                       block, 0, cus) == got
 
 
 def test_fp8_fused_verify_unpack_detects_corruption(gpu):
