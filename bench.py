@@ -32,6 +32,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BASELINE_METRIC = "aggregate GB/s + time-to-full-placement, 80×1 GiB layers, mode 1, 8 ranks"
 
 
+def metric_name(layers: int, layer_mib: int, mode: int, ranks: int) -> str:
+    """BASELINE.json's metric with the workload and rank count this run measured
+    (equal to BASELINE_METRIC for the headline config at 8 ranks)."""
+    size = f"{layer_mib // 1024} GiB" if layer_mib % 1024 == 0 else f"{layer_mib} MiB"
+    return (f"aggregate GB/s + time-to-full-placement, {layers}×{size} layers, mode {mode}, "
+            f"{ranks} rank{'s' if ranks != 1 else ''}")
+
+
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE or 1)")
@@ -43,10 +51,7 @@ def parse_args(argv=None):
     p.add_argument("--chunk-mib", type=int, default=64)
     p.add_argument("--tier", default="host", choices=["host", "device", "disk"])
     p.add_argument("--seeding", default="random", choices=["random", "leader", "uniform"])
-    p.add_argument("--copies", type=int, default=1)
-    p.add_argument("--assignment", default="replicate", choices=["replicate", "pipeline"])
-    p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--copies", type=int, default=1, help="holders per layer in the initial seeding")
     p.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
                    help="mode 1 owner choice when a layer has several holders (--copies > 1); links also "
                         "relays around links the plan knows to be slow")
@@ -54,9 +59,8 @@ def parse_args(argv=None):
                    help="seconds one session (step) may take before the rank gives up (also the P2P group timeout)")
     p.add_argument("--pull-window", type=int, default=0,
                    help="mode 2 jobs in flight per sender (0 = one per peer; round-4 sim at N=8, 50 GB/s links, "
-                        "closed loop on: 7 -> 265 ms, 10 -> 294, 14 -> 388 - with more jobs than links the "
-                        "concurrent transfers share each link and the busy-time estimate reads it low; round 2, "
-                        "before the closed loop: 14 -> 241, profiles/r4_predict_mode2.jsonl)")
+                        "closed loop on: 7 -> 265 ms, 10 -> 294, 14 -> 388, profiles/r4_predict_mode2.jsonl). "
+                        "REAL-NODE GUESS: settled by config.per_link_busy_GBps in mode 2")
     p.add_argument("--storage", default="", help="disk tier directory")
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0: scatter+relay P2P, ncclBroadcast, or leader fan-out")
@@ -72,36 +76,25 @@ def parse_args(argv=None):
     p.add_argument("--node-disk-gbps", type=float, default=None,
                    help="--tier disk: the node's one NVMe read rate shared by every rank's disk readers and planned "
                         "as one budget by mode 3 (default 13.3, profiles/r1_diskspeed.log; 0 = per-rank, unpaced)")
-    p.add_argument("--reserve-cus", type=int, default=-1,
-                   help="CUs the verify/copy kernels leave free for RCCL when --verify-cus is 0 (-1: 32 when N > 1)")
+    # Defaults measured on a real MI355X cite their evidence; the ones only a
+    # real 8-GPU node can settle name the JSON field that will (REAL-NODE GUESS).
     p.add_argument("--verify-cus", type=int, default=-1,
                    help="the verify stream runs on the last N CUs only, RCCL lanes and copies on the others (-1: 32, "
                         "4 CUs on each XCD, when N > 1 - 128 with --store bf16 - and 0 alone; 0: all shared). "
-                        "bin/contention: a 64-workgroup copy keeps 99.6 %% of its rate beside 450 GB/s of verify "
-                        "on the last 32 CUs (profiles/r4_contention)")
-    p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX", help="RCCL communicator minCTAs:maxCTAs")
-    p.add_argument("--nccl-register", action="store_true", help="ncclCommRegister every HBM layer slot")
+                        "Evidence: bin/contention on one MI355X, a 64-workgroup copy keeps 99.6 %% of its rate "
+                        "beside 450 GB/s of verify on the last 32 CUs (profiles/r4_contention); the fused bf16 "
+                        "verify needs 128 at 7 x 153 GB/s of ingress (scripts/verify_bench.py --cus 128). "
+                        "REAL-NODE GUESS at N = 8: settled by config.verify_busy_frac_rank0 and per_link_busy_GBps")
     p.add_argument("--lanes", type=int, default=0,
                    help="comm lanes (RCCL communicator + stream + dedicated HW queue each); 0 = one lane per "
-                        "directed link on up to 8 ranks (14 at N = 8), world-1 per-distance lanes beyond")
-    p.add_argument("--comm-init", default="split", choices=["parallel", "split"],
-                   help="lane communicators: split from the world communicator one after another (split, the "
-                        "default: 16.3-17.1 s vs 18.7-19.1 s for parallel at 8 ranks on one GPU, profiles/r3_init2), "
-                        "or one unique id each, initialized together (parallel); the JSON records both phases per lane")
+                        "directed link on up to 8 ranks (14 at N = 8), world-1 per-distance lanes beyond. "
+                        "REAL-NODE GUESS (schedule evidence: the sim's RCCL round model, tests/test_timing_sim.py); "
+                        "settled by config.per_link_busy_GBps and comm_init_ms_per_lane / comm_connect_ms_per_lane")
     p.add_argument("--probe-mib", type=int, default=256,
                    help="N > 1: untimed pre-flight probe of every directed link with this many MiB "
-                        "(all lanes at once, then each pair alone); 0 = skip")
-    p.add_argument("--probe-timeout", type=float, default=30.0,
-                   help="seconds the probe waits for a lane before naming it stalled and failing the attempt")
-    p.add_argument("--no-adapt-links", action="store_true",
-                   help="plan every session on the fixed link estimates instead of the per-link rates the ranks "
-                        "measured (probe + earlier sessions' busy throughput, EWMA)")
-    p.add_argument("--no-hierarchical", action="store_true",
-                   help="ranks on several hosts: plan every dest from the holders directly instead of importing a "
-                        "layer once per host and relaying it over that host's xGMI (mode 1, links policy)")
-    p.add_argument("--no-fallback", action="store_true",
-                   help="N > 1 under torchrun: run the worker in this process (no supervised fresh-process "
-                        "attempts with fallback data-plane settings)")
+                        "(all lanes at once, then each pair alone); 0 = skip. Its rates floor the closed loop's "
+                        "link capacities for the first sessions. REAL-NODE GUESS for the size: settled by "
+                        "config.probe_lane_GBps (concurrent vs solo) against per_link_busy_GBps")
     p.add_argument("--inject", action="append", default=[], metavar="SPEC",
                    help="fault injection (utils/faults.py), e.g. slow-link=0:1:20G (rank 0 -> 1 capped at 20 GB/s)")
     p.add_argument("--source-pool", type=int, default=0,
@@ -150,14 +143,14 @@ def load_supervise():
 def fallback_attempts(args, world):
     """The supervised attempts at N > 1: as asked; then round 2's data plane
     (one lane per ring distance - world-1 communicators and HW queues instead
-    of 14 - split from the world communicator one by one); then that without
-    RCCL's P2P/IPC transport (host shared memory between the GPUs)."""
+    of 14); then that without RCCL's P2P/IPC transport (host shared memory
+    between the GPUs). Lane communicators are split from the world one."""
     Attempt = load_supervise().Attempt
     atts = [Attempt("")]
-    if args.lanes == 0 and world > 2 or args.comm_init != "split":
-        atts.append(Attempt(f"lanes={world - 1}, split comm init", ["--lanes", str(world - 1), "--comm-init", "split"]))
-    atts.append(Attempt(f"lanes={world - 1}, split comm init, NCCL_P2P_DISABLE=1",
-                        ["--lanes", str(world - 1), "--comm-init", "split"], {"NCCL_P2P_DISABLE": "1"}))
+    if args.lanes == 0 and world > 2:
+        atts.append(Attempt(f"lanes={world - 1}", ["--lanes", str(world - 1)]))
+    atts.append(Attempt(f"lanes={world - 1}, NCCL_P2P_DISABLE=1", ["--lanes", str(world - 1)],
+                        {"NCCL_P2P_DISABLE": "1"}))
     return atts
 
 
@@ -201,7 +194,7 @@ def main(argv=None) -> int:
     sys.path.insert(0, HERE)
     sup = load_supervise()
 
-    if world > 1 and not os.environ.get(sup.ENV_PREFIX) and not args.no_fallback and sup.agent_store_available():
+    if world > 1 and not os.environ.get(sup.ENV_PREFIX) and sup.agent_store_available():
         return supervise(args, world, rank)
     chan = sup.WorkerChannel.from_env()
     try:
@@ -278,7 +271,7 @@ def worker(args, world, rank, chan) -> int:
 
     layer_bytes = args.layer_mib << 20
     cfg = make_workload(world, args.layers, layer_bytes, seeding=args.seeding, tier=args.tier, copies=args.copies,
-                        seed=args.seed, assignment=args.assignment, chunk_bytes=args.chunk_mib << 20)
+                        seed=0, assignment="replicate", chunk_bytes=args.chunk_mib << 20)
     total_bytes = delivered_bytes(cfg)
 
     from distributed_llm_dissemination_amd.__main__ import nccl_ids
@@ -300,7 +293,7 @@ def worker(args, world, rank, chan) -> int:
     node_key = "b" + hashlib.blake2b(run_tag.encode(), digest_size=6).hexdigest()
     disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else (13.3 if args.tier == "disk" else 0.0)
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
-                 verify=not args.no_verify, payload_seed=args.seed, registry={rank: listen_addr(bool(hosts))},
+                 verify=True, payload_seed=0, registry={rank: listen_addr(bool(hosts))},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
                  store=args.store, group_timeout_s=min(300.0, args.timeout),
                  engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(rank)},
@@ -324,7 +317,7 @@ def worker(args, world, rank, chan) -> int:
     if world > 1 and args.probe_mib > 0:
         beat("probe")
         try:
-            probe = rt.probe_links(args.probe_mib << 20, timeout_s=args.probe_timeout)
+            probe = rt.probe_links(args.probe_mib << 20, timeout_s=30.0)
         except RuntimeError as e:
             failed(str(e))
         log(f"link probe: {probe.get('probe_ms')} ms; concurrent GB/s {probe.get('concurrent')}")
@@ -333,10 +326,10 @@ def worker(args, world, rank, chan) -> int:
                          {p: g * 1e9 for p, g in probe.get("concurrent_in", {}).items() if g})
 
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
-    policy = dict(seed=args.seed, pull_window=args.pull_window or max(1, world - 1),
+    policy = dict(seed=0, pull_window=args.pull_window or max(1, world - 1),
                   owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective",
-                  adapt_links=not args.no_adapt_links, hierarchical=not args.no_hierarchical)
+                  adapt_links=True, hierarchical=True)
 
     def step(timed: bool, i: int):
         beat(f"{'step' if timed else 'warmup'} {i}")
@@ -390,8 +383,9 @@ def worker(args, world, rank, chan) -> int:
     value = total_bytes * args.steps / total / 1e9
     if rank == 0:
         out = {
-            "metric": BASELINE_METRIC,
-            "ranks": world,  # the metric names the 8-rank config; this line measured `ranks` of it
+            "metric": metric_name(args.layers, args.layer_mib, args.mode, world),
+            "baseline_metric": BASELINE_METRIC,  # BASELINE.json's name; `metric` says what this run measured
+            "ranks": world,
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
@@ -407,12 +401,12 @@ def worker(args, world, rank, chan) -> int:
                 "model": f"{args.layers}x{args.layer_mib}MiB layers (Llama-3-70B-sized shards)",
                 "global_batch": None,
                 "seq_len": None,
-                "parallelism": f"dp{world} (full replication)" if args.assignment == "replicate" else f"pp{world}",
+                "parallelism": f"dp{world} (full replication)",
                 "mode": args.mode,
                 "tier": args.tier,
                 "seeding": args.seeding,
                 "chunk_mib": args.chunk_mib,
-                "verify": not args.no_verify,
+                "verify": True,
                 "bytes_per_step": total_bytes,
                 "time_to_full_placement_s": round(ms_per_step / 1e3, 6),
                 "leader_time_to_deliver_s": round(last.time_to_deliver_s, 6) if last else None,
@@ -465,7 +459,7 @@ def worker(args, world, rank, chan) -> int:
             # per lane, rank 0: communicator set-up and connects (settles parallel vs split on a real node)
             out["config"]["comm_init_ms_per_lane"] = [round(x, 1) for x in es.lane_init_ms]
             out["config"]["comm_connect_ms_per_lane"] = [round(x, 1) for x in es.lane_connect_ms]
-            out["config"]["comm_init"] = args.comm_init
+            out["config"]["comm_init"] = "split"
             # the verify stream's CUs (the last ones of the mask; RCCL and copies on the rest)
             out["config"]["verify_cus"] = (args.verify_cus if args.verify_cus >= 0
                                            else 128 if args.store == "bf16" else 32)
@@ -483,7 +477,7 @@ def worker(args, world, rank, chan) -> int:
             out["config"]["per_link_busy_GBps"] = busy
             # the per directed link rates the leader's last plan used (measured, closed loop)
             plan = rt.plan_link_bw()
-            out["config"]["adapt_links"] = not args.no_adapt_links
+            out["config"]["adapt_links"] = True
             out["config"]["plan_link_GBps"] = {f"{a}->{b}": round(v / 1e9, 2) for (a, b), v in sorted(plan.items())}
             if any(all_probe):
                 # untimed pre-flight probe: GB/s per directed link (sender's device time)

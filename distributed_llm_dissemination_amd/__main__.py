@@ -142,12 +142,12 @@ def build_parser() -> argparse.ArgumentParser:
 
 def engine_opts(args) -> dict:
     """Planned-engine (rccl) knobs from the CLI."""
-    opts = {"reserve_cus": args.reserve_cus,
+    opts = {"reserve_cus": int(getattr(args, "reserve_cus", -1)),
             "verify_cus": int(getattr(args, "verify_cus", -1)),
             "suspect_s": getattr(args, "suspect_timeout", 10.0),
             "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0)),
             "comm_init": getattr(args, "comm_init", "split")}
-    if args.nccl_ctas:
+    if getattr(args, "nccl_ctas", ""):
         lo, _, hi = args.nccl_ctas.partition(":")
         opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)
     return opts

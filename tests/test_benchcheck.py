@@ -16,7 +16,7 @@ def test_a_real_8_gpu_run_passes():
 
 
 def test_fallbacks_and_shared_gpu_runs_fail():
-    assert real_multi_gpu_problems(_line(fallback="lanes=7, split comm init, NCCL_P2P_DISABLE=1"), 8, 14)
+    assert real_multi_gpu_problems(_line(fallback="lanes=7, NCCL_P2P_DISABLE=1"), 8, 14)
     assert real_multi_gpu_problems(_line(engine="rccl-socket, all ranks on one GPU (schedule rehearsal)"), 8, 14)
     assert real_multi_gpu_problems(_line(lanes=7), 8, 14)
 

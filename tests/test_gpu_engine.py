@@ -23,7 +23,10 @@ def test_host_tier_promotion_all_modes(gpu, mode):
             res = rt.run(mode, timeout=60)
             assert res.ok, res.error
             assert res.engine_stats["verify_failures"] == 0
-            assert res.engine_stats["bytes_verified"] == 6 * (6 * MiB + 4096) or mode == 3 or True
+            # every staged byte checked exactly once, in every mode (mode 3's
+            # self-jobs included): the same count the sim backend gives
+            assert res.engine_stats["bytes_staged"] == 6 * (6 * MiB + 4096)
+            assert res.engine_stats["bytes_verified"] == 6 * (6 * MiB + 4096)
             for l in range(6):
                 assert rt.layer_bytes(l) == gpu.fill_random_host(6 * MiB + 4096, layer_seed(0, l))
     finally:

@@ -68,8 +68,6 @@ def n(request):
 @pytest.mark.parametrize("mode,extra", [(1, []), (2, ["--pull-window", "2"]), (3, []), (0, ["--seeding", "leader"]),
                                         (0, ["--seeding", "leader", "--bcast", "collective"]),
                                         (1, ["--pack", "fp8", "--layer-mib", "96"]),
-                                        (1, ["--nccl-ctas", "4:16", "--reserve-cus", "64"]),
-                                        (1, ["--nccl-register"]),
                                         (1, ["--pack", "fp8", "--store", "bf16", "--layer-mib", "96"]),
                                         (1, ["--inject", "slow-link=0:1:2G"]),
                                         (1, ["--seeding", "uniform", "--source-pool", "3"])])

@@ -553,3 +553,25 @@ def test_mode2_planned_dest_loads_its_own_lower_tier_copy():
 
     (res,), _ = run_cluster(cfg, 2, pull_window=1, inspect=inspect)
     assert res[1].engine_stats["bytes_staged"] == 2 * MiB
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_single_rank_verifies_every_staged_byte_once(mode):
+    """One rank promoting 6 host-tier layers (the GPU engine test's workload,
+    tests/test_gpu_engine.py): every staged byte is CRC-checked exactly once
+    in every mode - the staging checks go out in batches of up to 16 chunks
+    (PlannedEngine::flush_stage_checks) - session after session."""
+    size = 6 * MiB + 4096
+    cfg = make_workload(1, 6, size, tier="host", chunk_bytes=MiB)
+    rt = Runtime(cfg, 0, engine="sim", chunk_bytes=MiB, registry={0: "127.0.0.1:0"}, sim_key=f"one{next(_keys)}")
+    try:
+        for _ in range(2):
+            res = rt.run(mode, timeout=60)
+            assert res.ok, res.error
+            assert res.engine_stats["bytes_staged"] == 6 * size
+            assert res.engine_stats["bytes_verified"] == 6 * size
+            assert res.engine_stats["verify_failures"] == 0
+            for l in range(6):
+                assert rt.layer_bytes(l) == expected_image(rt, l, size)
+    finally:
+        rt.close()

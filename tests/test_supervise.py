@@ -79,5 +79,5 @@ def test_bench_supervisor_runs_the_fallback_attempts_on_cpu(tmp_path):
     r = _torchrun(3, ["bench.py", "--gpus", "3", "--steps", "1", "--warmup", "0", "--layers", "3",
                       "--layer-mib", "1"], {})
     assert r.returncode != 0
-    for k, label in enumerate(["", " (lanes=2, split comm init)", " (lanes=2, split comm init, NCCL_P2P_DISABLE=1)"]):
+    for k, label in enumerate(["", " (lanes=2)", " (lanes=2, NCCL_P2P_DISABLE=1)"]):
         assert f"attempt {k}{label}: starting worker" in r.stderr, r.stderr[-3000:]
