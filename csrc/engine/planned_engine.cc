@@ -752,10 +752,11 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
     want = jc->second;
     known = true;
   }
-  // The check joins the staging batch (flush_stage_checks): one verify launch
-  // per kVerifyBatch staged chunks instead of one per chunk.
-  StageCheck sc;
-  sc.ev = e;
+  // The check joins the pending batch (flush_checks): one verify launch per
+  // kVerifyBatch staged chunks instead of one per chunk.
+  PendingCheck sc;
+  sc.wait = e;
+  sc.held = true;
   ev_hold(e);
   if (cfg_.unpack_store) {
     // fused: check the packed chunk and write its bf16 image (one pass)
@@ -776,8 +777,8 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
     sc.has_req = true;
   }
   sc.piece = p;
-  stage_checks_.push_back(sc);
-  if (stage_checks_.size() >= size_t(kVerifyBatch)) flush_stage_checks();
+  pending_checks_.push_back(sc);
+  if (++pending_reqs_ >= kVerifyBatch) flush_checks();
   if (bounce) {
     // The bounce buffer is free again once its H2D copy has landed - not after
     // the chunk's CRC check: the verify queue is in order, and a check queued
@@ -790,22 +791,41 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   stats_.bytes_staged += slen;
 }
 
-void PlannedEngine::flush_stage_checks() {
-  if (stage_checks_.empty()) return;
-  Verify v;
-  v.t0 = stage_checks_.front().t0;
-  std::vector<Backend::CheckReq> reqs;
-  std::vector<Ev> waits;
-  for (auto& sc : stage_checks_) {
-    if (sc.has_req) reqs.push_back(sc.req);
-    if (std::find(waits.begin(), waits.end(), sc.ev) == waits.end()) waits.push_back(sc.ev);
-    v.pieces.push_back(sc.piece);
-    v.slots.push_back(sc.slot);
+// The checks queued since the last flush (staged chunks, and the chunks the
+// P2P groups of this issue pass landed) go to the verify queue as batches of
+// up to kVerifyBatch chunk checks, each batch one Backend::verify behind the
+// landings of its own chunks only, so verification keeps pipelining behind
+// staging and transfers.
+void PlannedEngine::flush_checks() {
+  size_t i = 0;
+  while (i < pending_checks_.size()) {
+    Verify v;
+    v.t0 = pending_checks_[i].t0;
+    std::vector<Backend::CheckReq> reqs;
+    std::vector<Ev> waits;
+    size_t j = i;
+    for (; j < pending_checks_.size(); ++j) {
+      const PendingCheck& pc = pending_checks_[j];
+      if (pc.has_req && reqs.size() == size_t(kVerifyBatch)) break;
+      if (pc.has_req) reqs.push_back(pc.req);
+      if (pc.wait && std::find(waits.begin(), waits.end(), pc.wait) == waits.end()) waits.push_back(pc.wait);
+      v.pieces.push_back(pc.piece);
+      v.slots.push_back(pc.slot);
+    }
+    v.ev = backend_->verify(reqs, waits);
+    verifies_.push_back(std::move(v));
+    i = j;
   }
-  v.ev = backend_->verify(reqs, waits);
-  for (auto& sc : stage_checks_) ev_drop(sc.ev);
-  stage_checks_.clear();
-  verifies_.push_back(std::move(v));
+  drop_pending_checks();
+}
+
+void PlannedEngine::drop_pending_checks() {
+  for (auto& pc : pending_checks_)
+    if (pc.held) ev_drop(pc.wait);
+  pending_checks_.clear();
+  pending_reqs_ = 0;
+  for (Ev e : owned_waits_) backend_->release(e);
+  owned_waits_.clear();
 }
 
 int PlannedEngine::ensure_chunk(Layer& L, LayerID id, int64_t c, bool want_landed) {
@@ -987,6 +1007,7 @@ bool PlannedEngine::issue_some() {
   // staged or received, pacing, in-flight cap) does not hold the others.
   bool progress = false;
   for (int lane = 0; lane < lanes_; ++lane) progress |= issue_lane(lane);
+  flush_checks();  // the chunks this pass's groups land (and staged): batched checks
   return progress;
 }
 
@@ -1129,9 +1150,7 @@ bool PlannedEngine::issue_lane(int lane) {
     // Receivers: chunks are valid behind `g` on this lane; check them on the
     // verify queue. With one lane a later send of the chunk is ordered behind
     // `g` on the same queue; with several, it waits for a mark on this lane.
-    Verify v;
     Ev mark = 0;
-    std::vector<Backend::CheckReq> checks;
     for (auto& p : group) {
       if (p.kind != Kind::Recv) continue;
       Layer& L = layers_[p.layer];
@@ -1146,26 +1165,27 @@ bool PlannedEngine::issue_lane(int lane) {
       } else {
         set_chunk_ev(L, p.chunk, 0);  // pending on the comm queue itself: later sends are ordered behind it
       }
-      uint32_t slot = ~0u;
+      // The chunk's check joins the pending batch behind this group's landing
+      // (flush_checks at the end of the issue pass): the chunks every lane
+      // landed in one pass share verify launches.
+      PendingCheck pc;
+      pc.piece = p;
+      pc.wait = landed_ev;  // alive until the flush: the group is polled after it
       if (cfg_.unpack_store && p.full) {
         // fused check + dequantization of the landed packed chunk
         const uint32_t s = crc_slot();
-        checks.push_back(unpack_req(L, p.chunk, s));
-        if (cfg_.verify && p.has_crc) slot = s;
+        pc.req = unpack_req(L, p.chunk, s);
+        pc.has_req = true;
+        if (cfg_.verify && p.has_crc) pc.slot = s;
       } else if (cfg_.verify && p.has_crc && p.full) {
-        slot = crc_slot();
-        checks.push_back(Backend::CheckReq{L.dev + p.off, p.len, slot});
+        pc.slot = crc_slot();
+        pc.req = Backend::CheckReq{L.dev + p.off, p.len, pc.slot};
+        pc.has_req = true;
       }
-      v.pieces.push_back(p);
-      v.slots.push_back(slot);
+      pending_reqs_ += pc.has_req ? 1 : 0;
+      pending_checks_.push_back(pc);
     }
-    // Every chunk this group landed is checked by one batched verify (one
-    // launch per kVerifyBatch chunks, the fold inside it).
-    if (!v.pieces.empty()) {
-      v.ev = backend_->verify(checks, {landed_ev});
-      verifies_.push_back(std::move(v));
-    }
-    if (landed_ev != g) backend_->release(landed_ev);
+    if (landed_ev != g) owned_waits_.push_back(landed_ev);  // released after the flush
     {
       std::lock_guard<std::mutex> lk(stats_mu_);
       stats_.groups++;
@@ -1277,11 +1297,8 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
     backend_->release(v.ev);
   }
   verifies_.clear();
-  for (auto& sc : stage_checks_) {
-    aborted++;
-    ev_drop(sc.ev);
-  }
-  stage_checks_.clear();
+  aborted += int64_t(pending_checks_.size());
+  drop_pending_checks();
   for (auto& b : bounce_busy_) {  // every queue drained in the backend's shrink: the copies are done
     ev_drop(b.first);
     bounce_free_.push_back(b.second);
@@ -1331,7 +1348,7 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
 }
 
 void PlannedEngine::poll() {
-  flush_stage_checks();  // what this pass staged: one batched check
+  flush_checks();  // what was staged since the issue pass: batched checks
   const auto now = std::chrono::steady_clock::now();
   for (int lane = 0; lane < lanes_; ++lane) {
     auto& infl = inflight_[size_t(lane)];
@@ -1543,8 +1560,7 @@ void PlannedEngine::run() {
         for (auto& q : ops_) q.clear();
         for (auto& q : inflight_) q.clear();
         verifies_.clear();
-        for (auto& sc : stage_checks_) ev_drop(sc.ev);
-        stage_checks_.clear();
+        drop_pending_checks();
         local_wait_.clear();
         std::lock_guard<std::mutex> lk(req_mu_);
         busy_ = false;

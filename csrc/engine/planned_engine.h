@@ -289,11 +289,12 @@ class PlannedEngine : public DataEngine {
     std::vector<Piece> pieces;
     std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
   };
-  struct StageCheck {  // a staged chunk whose check waits for the staging batch
+  struct PendingCheck {  // a landed or staged chunk whose check waits for the next flush_checks
     Piece piece;
-    Ev ev = 0;                  // its staging copy (held)
+    Ev wait = 0;                // its landing: a staging copy (held: ev_hold) or a P2P group / its corrupt mark
+    bool held = false;
     uint32_t slot = ~0u;        // result slot, ~0u = not verified
-    bool has_req = false;
+    bool has_req = false;       // a check (plain or fused) to launch; else only the landing to wait for
     Backend::CheckReq req{};
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   };
@@ -344,7 +345,7 @@ class PlannedEngine : public DataEngine {
       if (!q.empty()) return false;
     for (auto& q : inflight_)
       if (!q.empty()) return false;
-    return verifies_.empty() && stage_checks_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty() &&
+    return verifies_.empty() && pending_checks_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty() &&
            bounce_busy_.empty();
   }
   int lane_for(int peer, bool send) const {
@@ -385,8 +386,9 @@ class PlannedEngine : public DataEngine {
   uint32_t crc_slot();
   // unpack_store: the fused check of chunk c (packed at L.dev) into its bf16 slot.
   Backend::CheckReq unpack_req(Layer& L, int64_t c, uint32_t slot);
-  // Launch the checks of the chunks staged since the last flush as one verify.
-  void flush_stage_checks();
+  // Launch the pending checks as batched verifies (flush_checks), or forget them.
+  void flush_checks();
+  void drop_pending_checks();
   void fail(const std::string& what);
   int64_t src_len(const Layer& L, int64_t c) const;  // source bytes of chunk c
   int64_t src_grid(const Layer& L) const { return cfg_.pack == 1 && !L.src_packed ? cfg_.chunk_bytes : grid_; }
@@ -411,7 +413,9 @@ class PlannedEngine : public DataEngine {
   std::vector<std::deque<Piece>> ops_;          // per lane, key order
   std::vector<std::deque<Inflight>> inflight_;  // per lane
   std::deque<Verify> verifies_;
-  std::vector<StageCheck> stage_checks_;  // staged chunks whose checks are not launched yet
+  std::vector<PendingCheck> pending_checks_;  // checks not launched yet (staged and landed chunks)
+  int pending_reqs_ = 0;                      // of them, chunk checks to launch
+  std::vector<Ev> owned_waits_;               // landing events the engine releases after the flush
   std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
   std::deque<std::pair<LayerID, int64_t>> local_wait_;  // local promotions deferred by tier pacing
   // keys of the queued (not yet posted) sends of each chunk: relay cuts, and
