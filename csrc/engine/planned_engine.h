@@ -478,6 +478,9 @@ class PlannedEngine : public DataEngine {
 };
 
 constexpr uint32_t kCrcSlots = 1u << 16;
+// Token-bucket keys (PlannedEngine::pace_ready): a mode-3 job, a rate-capped
+// peer link, a source tier.
+constexpr uint64_t kPaceJob = 1ull << 62, kPacePeer = 2ull << 62, kPaceTier = 3ull << 62;
 // Chunks per verify launch (kern::kCrcBatchMax): at 64 MiB source chunks a
 // batch of 16 is 1 GiB of bf16 per launch, where the fused kernel runs at
 // its streaming rate; one chunk alone fills less than a round of the chip.

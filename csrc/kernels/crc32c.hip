@@ -1,10 +1,12 @@
-// Per-chunk CRC32C on gfx950 (receiver-side verification of every landed chunk).
+// CRC32C on gfx950 (receiver-side verification of every landed chunk), and
+// the fused CRC32C + fp8 -> bf16 dequantization of packed chunks.
 //
 // CRC is a serial recurrence, so the kernel works with raw (un-inverted) CRC
 // registers, which are linear over GF(2):
 //   raw(A || B) = shift(raw(A), |B|) xor raw(B),  shift(r, L) = r * x^(8L) mod P.
 // Decomposition:
-//  * a chunk is cut into 16 KiB segments; one wave owns a segment;
+//  * a chunk is cut into 16 KiB segments; one wave owns a segment (the last,
+//    partial round of a launch's grid: half a segment, see once_split);
 //  * a segment is 4 blocks of 4 KiB, and lane l owns the contiguous 64-B piece
 //    l of every block. Within a piece the classic slice-by-4 recurrence runs
 //    (s ^= word; s = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3]): one table lookup per
@@ -14,15 +16,19 @@
 //    multiply by a per-lane constant (x^(8*64*(63-lane))), then the lanes are
 //    XOR-reduced with cross-lane shuffles: a segment's value is its raw CRC;
 //  * the wave then shifts that value to the END OF ITS CHUNK - x^(8*16 KiB*j)
-//    from one table indexed by the segments that follow it, then x^(8*rem)
-//    for a chunk whose last segment is short (wave-uniform products);
-//  * a second, small kernel (one workgroup per chunk) XORs a chunk's segment
-//    values and adds the init/xorout term, writing the standard CRC32C.
-// The constants depend on nothing but the segment geometry (chunks up to
-// 1 GiB): one upload per device, never a per-length table (a length-keyed
-// table grew with every new piece size and re-allocated mid-session).
+//    from three 1024-entry levels of a table, then x^(8*rem) for a chunk whose
+//    last segment is short (wave-uniform products);
+//  * the fold runs in the same launch: a workgroup XORs its waves' values per
+//    chunk and adds them to the chunk's {acc, count} words with device-scope
+//    atomics; the workgroup that completes the count writes the standard
+//    CRC32C (fold_add below). The separate fold launch this replaced cost
+//    8.4-9.6 us per 64 MiB chunk in the round-4 engine traces.
+// One launch covers a regular chunk grid (ChunkGeo) or up to kCrcBatchMax
+// independent chunks (BatchGeo: the chunks one P2P issue pass or one staging
+// batch landed). The constants depend on nothing but the segment geometry
+// (chunks up to 16 TiB): one upload per device, never a per-length table.
 // The result is the exact CRC32C of each chunk for any chunk length that is a
-// multiple of 16 (the buffer's final chunk may have any length).
+// multiple of 16 (a buffer's final chunk, and a batch item, may have any length).
 //
 // Loads stay coalesced: each 16-B load instruction of a wave reads one whole
 // KiB (lane m + 16 r: word r of piece 16 j + m of KiB j), and a 4x4 register
@@ -35,31 +41,28 @@
 // LDS layout (MI355X_MICROARCH.md, LDS): a ds_read_b32 is served in two groups
 // of 32 lanes over 32 banks, and data-dependent indices into a plain table
 // conflict (2x the useful LDS cycles in round 1, profiles/r1_counters). Every
-// table entry is stored 32 times, replica r in bank r, and lane l reads replica
-// l & 31: conflict-free by construction. The 4 byte tables take 128 KiB (two
-// per 64 KiB: entry b at row b * 256 B, odd table at +128 B), so the address
-// of byte k of s is (b << 8) | (half * 128 + replica * 4) | (pair << 16): ONE
-// v_perm_b32 of s with a per-lane constant, then the ds_read_b32. With the
-// 16 KiB of shift tables that is 144 KiB: one 1024-thread workgroup per CU.
+// table entry is stored R times, replica r in bank r, and lane l reads replica
+// l mod R: R = 32 is conflict-free by construction (144 KiB: one workgroup
+// per CU); the verify kernel uses R = 16 (lanes l and l + 16 share a bank, up
+// to 2-way conflicts) in 72 KiB, so two 512-thread workgroups share a CU and
+// one fills its tables and waits for its first loads while the other computes.
+// The address of byte k of s is ONE v_perm_b32 of s with a per-lane constant,
+// then the ds_read_b32.
 //
-// History (profiles/r2_crc_ab): nibble tables on strided 16-B words (40
-// lookups per 16 B; 2.7 TB/s on 1 GiB, 31 us per 64 MiB chunk), the same on
-// byte-addressed nibble tables with a rolling prefetch (3.3 TB/s), an MFMA
-// GF(2) product (2.3 TB/s), slice-by-4 on directly loaded pieces (3.1 TB/s)
-// and with 4 independent recurrences per lane (2.3-2.5 TB/s) all lost to this
-// kernel: 5.76 TB/s on 1 GiB (186.5 us, kernel trace; the same load shape with
-// no math reads at 6.8 TB/s), 16.6 us + 4.5 us fold per single 64 MiB chunk.
-// Per 16 KiB segment a wave issues ~256 v_perm + ~130 v_bitop3 (3-input XORs)
-// for the lookups, 64 permlane swaps and ~160 VALU for the branch-free shift to
-// the chunk end (the divergent multiply loop cost 212 us per GiB).
-// Two recurrences per lane (blocks 0-1 and 2-3, joined by an 8 KiB shift
-// table in the last 16 KiB of LDS) measured 229 us: the chain latency is not
-// what bounds it. Round 4 (fused kernel, profiles/r4_chains): four chains per
-// lane, one per block, joined by 4096-byte shifts, measured the same as one
-// chain (160.4 vs 157.9 us main kernel at 512 MiB, 29.6 vs 30.3 at 64 MiB):
-// the ~9 us a launch pays over the same kernel without CRC math is the first
-// and last waves' ~600 VALU + 256 LDS lookups per lane per segment with
-// nothing to hide behind, not the length of the dependency chain.
+// History (profiles/r2_crc_ab, r4_*): nibble tables on strided 16-B words (40
+// lookups per 16 B; 2.7 TB/s on 1 GiB), the same on byte-addressed nibble
+// tables with a rolling prefetch (3.3 TB/s), an MFMA GF(2) product (2.3 TB/s),
+// slice-by-4 on directly loaded pieces (3.1 TB/s) and with 4 independent
+// recurrences per lane (2.3-2.5 TB/s) all lost to the slice-by-4-on-pieces
+// scheme above: 5.76 TB/s on 1 GiB as a persistent walk (round 2). Round 4's
+// fused kernel found one segment per wave faster than any persistent walk for
+// read+write (vmcnt counts loads and stores in order: a walking wave's next
+// loads wait behind its stores; bin/walkprobe, profiles/r4_walk*), and two
+// recurrences per lane or four chains per block measured the same as one
+// chain: the cost a launch pays over the copy is its first and last waves'
+// ~600 VALU + 256 LDS lookups per lane per segment with nothing to hide
+// behind. Round 5 removed the walk, the separate fold kernels and the store
+// variants from the library and batches the engine's chunks per launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -347,6 +350,16 @@ __device__ __forceinline__ uint32_t seg_full(u32x4_t (&w)[4 * kBlocksPerSeg], co
 }
 
 
+// Workgroup barrier for LDS hand-offs only: it waits for this wave's LDS
+// operations, not for its global stores. __syncthreads() also drains vmcnt,
+// which would hold every wave at the barrier until its bf16 stores are
+// acknowledged (the workgroup's 80 KiB of LDS stay allocated meanwhile).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // One segment per wave: the wave issues its segment's loads (and the scales)
 // BEFORE the workgroup fills the LDS tables, then runs the segment and exits.
 // On gfx9 one in-order counter (vmcnt) covers loads and stores, so a walking
@@ -459,7 +472,7 @@ __device__ __forceinline__ uint32_t slice_half(const Geo& geo, int64_t g, bool h
   const uint32_t v = h ? half_seg<1, Visit, R>(cur, have, full, sc, lds, visit, w)
                        : half_seg<0, Visit, R>(cur, have, full, sc, lds, visit, w);
   if (h == 1 && lane == 0) xch[stride * (wave >> 1)] = v;
-  __syncthreads();
+  lds_barrier();
   return h == 0 && have ? to_chunk_end(cur, v ^ xch[stride * (wave >> 1)], sc) : 0;
 }
 
@@ -738,7 +751,7 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
     *reinterpret_cast<uint32_t*>(slots + wave * kSlot + 16) = val;
     *reinterpret_cast<int64_t*>(slots + wave * kSlot + 24) = item;
   }
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) {
     uint32_t vs[kWaves16];
     int64_t its[kWaves16];
