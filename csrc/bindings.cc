@@ -310,6 +310,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("peer_busy_ms", &PlannedStats::peer_busy_ms)
       .def_readonly("peer_send_busy_ms", &PlannedStats::peer_send_busy_ms)
       .def_readonly("peer_recv_busy_ms", &PlannedStats::peer_recv_busy_ms)
+      .def_readonly("verify_calls", &PlannedStats::verify_calls)
+      .def_readonly("verify_chunks", &PlannedStats::verify_chunks)
       .def_readonly("lane_busy_ms", &PlannedStats::lane_busy_ms)
       .def_readonly("lanes", &PlannedStats::lanes)
       .def_readonly("comm_init_ms", &PlannedStats::comm_init_ms)

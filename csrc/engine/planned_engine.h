@@ -169,6 +169,8 @@ struct PlannedStats {
   // device time the verify stream spent on checks (landing met -> check done):
   // against the session's wall time, the occupancy of the verify CUs
   double verify_busy_ms = 0;
+  int64_t verify_calls = 0;   // Backend::verify calls (one event each; one launch per <= 16 chunks)
+  int64_t verify_chunks = 0;  // chunk checks they carried (verify_chunks / verify_calls: the batching)
   // log2(us) histograms: bucket b counts latencies in [2^b, 2^(b+1)) us
   std::vector<int64_t> group_us_hist = std::vector<int64_t>(32, 0);  // P2P group issue -> complete
   std::vector<int64_t> land_us_hist = std::vector<int64_t>(32, 0);   // chunk issue -> landed + verified

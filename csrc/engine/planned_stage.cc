@@ -75,6 +75,11 @@ void PlannedEngine::partial_landed(Layer& L, const Piece& p, std::vector<Verify>
     reqs.push_back(Backend::CheckReq{L.dev + a, b - a, slot});
   }
   v.ev = backend_->verify(reqs, {});
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.verify_calls++;
+    stats_.verify_chunks += int64_t(reqs.size());
+  }
   v.pieces.push_back(f);
   v.slots.push_back(slot);
   out.push_back(std::move(v));
@@ -339,6 +344,9 @@ void PlannedEngine::flush_checks() {
     v.ev = backend_->verify(reqs, waits);
     verifies_.push_back(std::move(v));
     i = j;
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.verify_calls++;
+    stats_.verify_chunks += int64_t(reqs.size());
   }
   drop_pending_checks();
 }

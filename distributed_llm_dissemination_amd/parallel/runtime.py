@@ -983,7 +983,7 @@ class Runtime:
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
                       "suspects", "shrinks", "aborted_pieces", "paced", "order_violations", "disk_wait_ms",
-                      "group_us_hist", "land_us_hist", "verify_busy_ms")
+                      "group_us_hist", "land_us_hist", "verify_busy_ms", "verify_calls", "verify_chunks")
         }
 
     def topology_link_bw(self, xgmi_gbps: float, pcie_gbps: float = 25.0,

@@ -571,6 +571,9 @@ def test_single_rank_verifies_every_staged_byte_once(mode):
             assert res.engine_stats["bytes_staged"] == 6 * size
             assert res.engine_stats["bytes_verified"] == 6 * size
             assert res.engine_stats["verify_failures"] == 0
+            # 6 layers x 7 chunks, checked in batches of up to 16 per verify
+            assert res.engine_stats["verify_chunks"] == 42
+            assert res.engine_stats["verify_calls"] <= 42 // 4, res.engine_stats
             for l in range(6):
                 assert rt.layer_bytes(l) == expected_image(rt, l, size)
     finally:
