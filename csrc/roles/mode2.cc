@@ -114,8 +114,14 @@ bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID
       if (sender == node || jd.second.state != JobState::Pending || load_[sender] == 0 ||
           eff(node_rate) < eff(sender_rate))
         continue;
-      // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
       const NodeID dest = jd.first.first;
+      // planned engines: a dest's own load of a layer it holds (sender == dest,
+      // min_loaded_sender) is never stolen - that dest also stages the layer's
+      // chunks into the same HBM slot for its own sends, so a peer's transfer
+      // would write them a second time while they are being staged and checked
+      // (TSAN, the crossing mode-2 selftest)
+      if (e_->planned() && sender == dest) continue;
+      // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
       if (host_of(node) != host_of(dest) && host_of(sender) == host_of(dest) && multi_host()) continue;
       double ttf = perf_.count(sender) ? perf_[sender].first * double(load_[sender]) : 1e300;
       Cand c{l.first, jd.first, sender, cnt, ttf};

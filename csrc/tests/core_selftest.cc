@@ -99,7 +99,9 @@ static void ring(bool tcp, int mode) {
 // Planned engine on the simulated fabric: 4 ranks, full replication.
 // die >= 0: that rank stops dead after two groups (elastic recovery path;
 // every layer then has two holders). crossing: two holders per layer and
-// mode-2 chunk jobs, so steals hand out crossing sends of the same chunk.
+// mode-2 chunk jobs: steals move jobs between the holders, never a dest's own
+// load of a layer it holds (that would write its chunks twice: the race TSAN
+// found here in round 5).
 static void planned_sim(int mode, double corrupt = 0, int die = -1, bool crossing = false) {
   const int n = 4, L = 6;
   const int64_t chunk = 1 << 16, size = 3 * chunk + 100;

@@ -156,17 +156,18 @@ def test_mode2_range_jobs(n):
 
 
 @pytest.mark.parametrize("n", [2, 4])
-def test_crossing_jobs_keep_key_order(n):
-    """Both ends hold every layer (copies = n) and mode-2 steals hand out
-    crossing jobs: rank a sends chunk c to b while b sends c to a, in one batch
-    on two lanes. A recv must not be posted ahead of this rank's earlier-key
-    send of the same chunk, or that send would wait on the recv's mark (a
-    larger key) and the two ranks could wait on each other - the rare mode-2
-    hang. The engine counts every send that waits on a larger-key recv."""
+def test_mode2_dest_holding_a_layer_loads_it_itself(n):
+    """Every rank holds every layer (copies = n): mode 2 makes each dest load
+    its own copy (min_loaded_sender) and no peer steals such a job - that dest
+    also stages the layer's chunks into the same HBM slot for its own sends, so
+    a stolen job would write a chunk twice while it is being staged and checked
+    (TSAN caught it in the crossing selftest). No bytes cross ranks, every
+    byte is staged once per rank, and no send ever waits on a larger-key recv."""
     cfg = make_workload(n, 6, 4 * MiB, tier="host", seeding="random", copies=n, chunk_bytes=MiB)
     outs, _ = run_cluster(cfg, 2, sessions=4, pull_window=2, pull_job_bytes=MiB)
     assert sum(r.engine_stats["order_violations"] for res in outs for r in res) == 0
-    assert sum(r.engine_stats["bytes_sent"] for res in outs for r in res) > 0  # jobs did cross ranks
+    assert sum(r.engine_stats["bytes_sent"] for res in outs for r in res) == 0
+    assert all(r.engine_stats["bytes_staged"] == 6 * 4 * MiB for res in outs for r in res)
 
 
 def test_repeated_sessions_reset_state():
