@@ -5,8 +5,10 @@
 // registers, which are linear over GF(2):
 //   raw(A || B) = shift(raw(A), |B|) xor raw(B),  shift(r, L) = r * x^(8L) mod P.
 // Decomposition:
-//  * a chunk is cut into 16 KiB segments; one wave owns a segment (the last,
-//    partial round of a launch's grid: half a segment, see once_split);
+//  * a chunk is cut into 16 KiB segments; one wave owns a segment at a time
+//    (the fused kernel: one segment per wave, the last, partial round of its
+//    grid half a segment, see once_split; the CRC-only kernel: a walk over a
+//    per-workgroup range of segments);
 //  * a segment is 4 blocks of 4 KiB, and lane l owns the contiguous 64-B piece
 //    l of every block. Within a piece the classic slice-by-4 recurrence runs
 //    (s ^= word; s = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3]): one table lookup per
@@ -19,8 +21,8 @@
 //    from three 1024-entry levels of a table, then x^(8*rem) for a chunk whose
 //    last segment is short (wave-uniform products);
 //  * the fold runs in the same launch: a workgroup XORs its waves' values per
-//    chunk and adds them to the chunk's {acc, count} words with device-scope
-//    atomics; the workgroup that completes the count writes the standard
+//    chunk (in LDS) and adds them to the chunk's {acc, count} words with
+//    device-scope atomics; the workgroup that completes the count writes the standard
 //    CRC32C (fold_add below). The separate fold launch this replaced cost
 //    8.4-9.6 us per 64 MiB chunk in the round-4 engine traces.
 // One launch covers a regular chunk grid (ChunkGeo) or up to kCrcBatchMax
@@ -43,9 +45,10 @@
 // conflict (2x the useful LDS cycles in round 1, profiles/r1_counters). Every
 // table entry is stored R times, replica r in bank r, and lane l reads replica
 // l mod R: R = 32 is conflict-free by construction (144 KiB: one workgroup
-// per CU); the verify kernel uses R = 16 (lanes l and l + 16 share a bank, up
-// to 2-way conflicts) in 72 KiB, so two 512-thread workgroups share a CU and
-// one fills its tables and waits for its first loads while the other computes.
+// per CU, the CRC-only walk); the fused kernel uses R = 16 (lanes l and l + 16
+// share a bank, up to 2-way conflicts) in 72 KiB, so two 512-thread workgroups
+// share a CU and one fills its tables and waits for its first loads while the
+// other computes.
 // The address of byte k of s is ONE v_perm_b32 of s with a per-lane constant,
 // then the ds_read_b32.
 //
@@ -61,8 +64,9 @@
 // recurrences per lane or four chains per block measured the same as one
 // chain: the cost a launch pays over the copy is its first and last waves'
 // ~600 VALU + 256 LDS lookups per lane per segment with nothing to hide
-// behind. Round 5 removed the walk, the separate fold kernels and the store
-// variants from the library and batches the engine's chunks per launch.
+// behind. Round 5 removed the separate fold kernels and the store variants
+// from the library, batches the engine's chunks per launch, and keeps the walk
+// (tables filled once per CU, no stores) for the CRC-only check only.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -705,8 +709,8 @@ __device__ __forceinline__ void fold_workgroup(const Geo& geo, const uint32_t* v
 // workgroups with 16 table replicas (72 KiB of LDS, + 8 KiB of bf16 staging
 // with an unpack): two workgroups per CU, so one fills its tables and waits
 // for its first loads while the other computes. Workgroups [split_block, ..)
-// take half segments (once_split). BLOCK = 0: CRC only; else the fused fp8
-// unpack with that scale block.
+// take half segments (once_split). BLOCK: the fp8 scale block of the fused
+// unpack (the CRC-only check is crc_walk_kernel below).
 // Round 4 measured this shape against the alternatives for the fused path
 // (profiles/r4_nt, r4_kernels_final: 5.3-5.5 TB/s at 512 MiB vs 4.66 for the
 // persistent walk with staged stores, 3.6-4.1 for the walk's other store
@@ -719,19 +723,19 @@ template <class Geo, int BLOCK>
 __global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
 verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, const uint32_t* __restrict__ sc,
                      uint32_t* __restrict__ acc) {
-  constexpr bool kUnpack = BLOCK > 0;
-  using Visit = std::conditional_t<kUnpack, UnpackVisit<kUnpack ? BLOCK : 128>, NoVisit>;
-  // Per wave after the tables: its 1 KiB bf16 staging slot (fused) or 32 B.
-  // Bytes 16-31 of a wave's slot carry its fold value and item to thread 0
-  // (its staging is done by then; word 0 may hold a half-pair hand-over).
-  // Two 80 KiB workgroups fill the CU's 160 KiB: not one more byte to spare.
-  constexpr uint32_t kSlot = kUnpack ? 1024 : 32;
+  static_assert(BLOCK > 0, "fused only");
+  using Visit = UnpackVisit<BLOCK>;
+  // Per wave after the tables: its 1 KiB bf16 staging slot. Bytes 16-31 of a
+  // wave's slot carry its fold value and item to thread 0 (its staging is done
+  // by then; word 0 may hold a half-pair hand-over). Two 80 KiB workgroups
+  // fill the CU's 160 KiB: not one more byte to spare.
+  constexpr uint32_t kSlot = 1024;
   __shared__ uint4 lds_raw[(LdsLayout<16>::kBytes + kWaves16 * kSlot) / 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
   uint8_t* slots = lds + LdsLayout<16>::kBytes;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   Visit v{};
-  if constexpr (kUnpack) v.slot = slots + wave * kSlot;
+  v.slot = slots + wave * kSlot;
   uint32_t val;
   int64_t item = -1;
   if (int64_t(blockIdx.x) < split_block) {
@@ -762,6 +766,112 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
     }
     fold_workgroup<Geo, kWaves16>(geo, vs, its, acc);
   }
+}
+
+// The CRC-only check: a walk. With no stores there is no in-order vmcnt to
+// fear (the reason the fused kernel runs one segment per wave), so one
+// 1024-thread workgroup per CU fills its 32-replica (conflict-free) tables
+// ONCE and its 16 waves walk the workgroup's contiguous range of segments:
+// wave w takes g0 + w, g0 + w + 16, ..., and loads block b of its next
+// segment as soon as block b of the current one is consumed (pinned with
+// sched_barrier: left alone, the compiler sinks those loads behind the math),
+// so 16 KiB stay in flight per wave. The round-2 walk ran at 5.76 TB/s on
+// 1 GiB; one segment per wave with the tables filled per 8 segments measured
+// 3.8 TB/s for CRC alone (profiles/r5_verify/per_launch.txt).
+// The fold: a wave accumulates its values while its item does not change and
+// hands each run to the workgroup's LDS slot of that item (ds atomics); at
+// the end the workgroup adds one value per item to the global {acc, count}
+// (fold_add) - one pair of device-scope atomics per (workgroup, item), 16
+// per 64 MiB item in a 16-chunk batch, instead of one per 8 segments.
+constexpr int kWalkWaves = 16, kWalkSlots = 256;
+
+// One wave's walk over segments g = first, first + step, ... < end: the
+// segment value (at its chunk's end) goes to sink(seg, value) on lane 0.
+template <class Geo, class Sink>
+__device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t end, int64_t step,
+                                         const uint32_t* __restrict__ sc, const Slice4T<32>& st, Sink sink) {
+  const int lane = threadIdx.x & 63;
+  const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
+  int64_t g = first;
+  if (g >= end) return;
+  NoVisit visit;
+  Seg cur = geo(g);
+  // invariant at the loop top: w holds cur's words if cur is a full segment
+  u32x4_t w[4 * kBlocksPerSeg];
+  {
+    const auto r = seg_rsrc(cur.p, cur.len == kSegBytes);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {  // in order: every path issues w[0..15] oldest first
+      w[i] = seg_load(r, lo, i);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  for (; g < end; g += step) {
+    const int64_t gn = g + step;
+    Seg nxt = cur;  // no next segment: loads against an empty resource
+    bool nfull = false;
+    if (gn < end) {
+      nxt = geo(gn);
+      nfull = nxt.len == kSegBytes;
+    }
+    const auto rn = seg_rsrc(nxt.p, nfull);
+    uint32_t s;
+    if (cur.len == kSegBytes) {
+      const uint32_t rowc = sc[kLanePow + lane];
+      s = 0;
+#pragma unroll
+      for (int b = 0; b < kBlocksPerSeg; ++b) {
+        row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
+        s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
+#pragma unroll
+        for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[4 * b + j] = seg_load(rn, lo, 4 * b + j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      s = wave_xor_dpp(multmodp_unrolled(rowc, s));
+    } else {
+      s = slice_partial(cur, sc, st, lane, visit);
+    }
+    if (lane == 0) sink(cur, to_chunk_end(cur, s, sc));
+    if (cur.len != kSegBytes) {  // (rare) w did not take the next segment's words yet
+#pragma unroll
+      for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
+        w[i] = seg_load(rn, lo, i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    cur = nxt;
+  }
+}
+
+template <class Geo>
+__global__ void __launch_bounds__(kWalkWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
+crc_walk_kernel(const Geo geo, int64_t total_segs, int64_t per_wg, const uint32_t* __restrict__ sc,
+                uint32_t* __restrict__ acc) {
+  __shared__ uint4 lds_raw[(LdsLayout<32>::kBytes + kWalkSlots * 8) / 16];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
+  uint32_t* fx = reinterpret_cast<uint32_t*>(lds + LdsLayout<32>::kBytes);  // per item slot: XOR
+  uint32_t* fn = fx + kWalkSlots;                                            // ... and segment count
+  const int64_t g0 = int64_t(blockIdx.x) * per_wg, g1 = min(g0 + per_wg, total_segs);
+  if (g0 >= g1) return;  // whole workgroup
+  for (int i = threadIdx.x; i < 2 * kWalkSlots; i += blockDim.x) fx[i] = 0;
+  const int64_t first_item = geo(g0).chunk;
+  load_lds<32>(lds, sc);  // once per workgroup; its barrier also publishes the zeroed slots
+  const Slice4T<32> st(lds);
+  // two LDS atomics per 16 KiB segment (the host keeps a range within kWalkSlots items)
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: g and its Seg in SGPRs
+  crc_walk(geo, g0 + wave, g1, kWalkWaves, sc, st, [=](const Seg& sg, uint32_t v) {
+    const int slot = int(sg.chunk - first_item);
+    atomicXor(&fx[slot], v);
+    atomicAdd(&fn[slot], 1u);
+  });
+  lds_barrier();
+  const int64_t nslots = geo(g1 - 1).chunk - first_item + 1;
+  for (int64_t t = threadIdx.x; t < nslots; t += blockDim.x)
+    if (fn[t]) fold_add(geo, first_item + t, fx[t], fn[t], acc);
 }
 
 // Per-device constant tables (one upload per device, before any RCCL traffic:
@@ -878,15 +988,33 @@ OnceGrid once_split(int64_t total_segs, int cus) {
   return OnceGrid{full, unsigned(full + (half_segs + kWaves16 / 2 - 1) / (kWaves16 / 2))};
 }
 
+int64_t segs_of(int64_t n) { return (n + kSegBytes - 1) / kSegBytes; }
+
+// Fewest segments of any item but the last (bounds the items one walk range spans).
+int64_t min_item_segs(const ChunkGeo& g) { return g.spc; }
+int64_t min_item_segs(const BatchGeo&) { return 1 << 20; }  // at most kCrcBatchMax items in all
+
 template <class Geo>
 hipError_t launch(const Geo& geo, int64_t total_segs, int block, const uint32_t* consts, void* ws, hipStream_t s,
                   int cus) {
   if (total_segs <= 0) return hipSuccess;
+  auto* acc = static_cast<uint32_t*>(ws);
+  if (block == 0) {
+    // CRC only: one walking workgroup per CU the stream may use, each a
+    // contiguous range of segments (at least one per wave)
+    const int dc = device_cus();
+    const int64_t wgs = std::max<int64_t>(
+        1, std::min<int64_t>(cus > 0 ? std::min(cus, dc) : dc, (total_segs + kWalkWaves - 1) / kWalkWaves));
+    // a range spans at most kWalkSlots items: one LDS slot each (items of
+    // at least min_item_segs segments; a batch holds at most kCrcBatchMax)
+    const int64_t per_wg = std::min((total_segs + wgs - 1) / wgs, (kWalkSlots - 2) * min_item_segs(geo));
+    crc_walk_kernel<Geo><<<dim3(unsigned((total_segs + per_wg - 1) / per_wg)), dim3(kWalkWaves * 64), 0, s>>>(
+        geo, total_segs, per_wg, consts, acc);
+    return hipGetLastError();
+  }
   const OnceGrid og = once_split(total_segs, cus);
   const dim3 grid(og.blocks), tpb(kWaves16 * 64);
-  auto* acc = static_cast<uint32_t*>(ws);
   switch (block) {
-    case 0: verify_once16_kernel<Geo, 0><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
     case 32: verify_once16_kernel<Geo, 32><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
     case 64: verify_once16_kernel<Geo, 64><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
     case 128: verify_once16_kernel<Geo, 128><<<grid, tpb, 0, s>>>(geo, total_segs, og.split_block, consts, acc); break;
@@ -897,7 +1025,6 @@ hipError_t launch(const Geo& geo, int64_t total_segs, int block, const uint32_t*
   return hipGetLastError();
 }
 
-int64_t segs_of(int64_t n) { return (n + kSegBytes - 1) / kSegBytes; }
 
 // A ChunkGeo over `bytes` in `chunk_bytes` chunks (the caller checked alignment).
 hipError_t chunk_geo(const void* src, int64_t bytes, int64_t chunk_bytes, uint32_t* crc_out, ChunkGeo* g,

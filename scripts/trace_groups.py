@@ -4,7 +4,7 @@ grouped by kernel and grid size (the grid tells a 1-, 4-, 8- or 16-chunk batch
 apart): launches, mean / min us, and us per 64 MiB source chunk when the
 grid's workgroups say how many segments it covered.
 
-    python scripts/trace_groups.py <kernel_trace.csv> [--chunk-mib 64] [--match verify_once16]
+    python scripts/trace_groups.py <kernel_trace.csv> [--chunk-mib 64] [--match crc_walk]
 """
 
 import argparse
@@ -16,7 +16,7 @@ from collections import OrderedDict
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--match", default="verify_once16|crc32c|fold")
+    ap.add_argument("--match", default="verify_once16|crc_walk|crc32c|fold")
     args = ap.parse_args()
     pat = re.compile(args.match)
     groups = OrderedDict()
