@@ -32,6 +32,7 @@ LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -L/o
 CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/core/fp8.cc csrc/core/trace.cc csrc/transport/inproc.cc \
              csrc/transport/tcp.cc csrc/store/store.cc csrc/sched/maxflow.cc csrc/sched/lp.cc csrc/roles/node.cc \
              csrc/roles/mode01.cc csrc/roles/mode2.cc csrc/roles/mode3.cc csrc/roles/multihost.cc \
+             csrc/roles/recovery.cc csrc/roles/dispatch.cc \
              csrc/engine/host_engine.cc csrc/engine/planned_engine.cc csrc/engine/planned_stage.cc \
              csrc/engine/planned_recovery.cc csrc/engine/sim_backend.cc
 BIND_SRC  := csrc/bindings.cc

@@ -742,442 +742,6 @@ void Node::finish_if_satisfied() {
   sig_cv_.notify_all();
 }
 
-// ------------------------------------------- elastic recovery (planned data plane)
-//
-// The reference only sketches this (Leader interface TODOs `update(a)` and
-// `crash(n node)`, distributor/node.go:215-219; a dead sender hangs the run,
-// SURVEY §5.3).
-// A rank whose P2P group stalls or fails reports the group's peers (Suspect).
-// The leader probes them over the control plane; for peers that are gone it
-// starts a recovery generation: the dead nodes leave the status and the
-// assignment, every survivor shrinks the RCCL communicator around them
-// (ncclCommShrink with NCCL_SHRINK_ABORT: in-flight groups are aborted) and
-// resets what was in flight, and once all survivors have confirmed
-// (ShrinkDone) the leader re-plans every unacked (dest, layer) from a live
-// holder. Pairs without a live holder are dropped (logged, counted).
-void Node::on_suspect(const MessagePtr& m) {
-  if (!started_ || satisfied_) return;
-  std::vector<NodeID> gone;
-  for (NodeID p : m->peers) {
-    if (p == cfg_.id || dead_nodes_.count(p) || !status_.count(p)) continue;
-    if (!t_->alive(p)) gone.push_back(p);
-  }
-  if (gone.empty()) {
-    log::info(int64_t(cfg_.id)).u("from", m->src).i("peers", int64_t(m->peers.size()))
-        .msg("suspect report: every named peer answers; waiting");
-    return;
-  }
-  shrink_gen_++;
-  for (NodeID d : gone) dead_nodes_.insert(d);
-  int64_t dropped = 0;
-  {
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    for (NodeID d : gone) {
-      status_.erase(d);
-      auto a = assignment_.find(d);
-      if (a != assignment_.end()) {
-        dropped += int64_t(a->second.size());
-        assignment_.erase(a);
-      }
-    }
-    stats_.recoveries++;
-    stats_.dropped += dropped;
-  }
-  for (NodeID d : gone) initial_status_.erase(d);
-  // Planning state of the interrupted schedule: re-planned from scratch.
-  pending_jobs_.clear();
-  jobs_.clear();
-  load_.clear();
-  inflight_.clear();
-  outstanding_.clear();
-  shrink_wait_.clear();
-  for (auto& kv : status_) shrink_wait_.insert(kv.first);
-  log::warn(int64_t(cfg_.id)).u("generation", shrink_gen_).i("dead", int64_t(gone.size()))
-      .i("survivors", int64_t(shrink_wait_.size())).i("dropped_assignments", dropped)
-      .msg("rank(s) dead: shrinking the communicator and re-planning");
-  trace::mark("dissem.recovery");
-  Message s;
-  s.type = MsgType::Shrink;
-  s.seq = shrink_gen_;
-  s.peers.assign(dead_nodes_.begin(), dead_nodes_.end());
-  s.payload_str = e_->new_comm_id();  // the survivors' new communicator (RCCL unique id)
-  for (NodeID n : std::set<NodeID>(shrink_wait_)) send_msg(n, s);
-}
-
-void Node::on_shrink_done(const MessagePtr& m) {
-  if (m->seq != shrink_gen_ || !shrink_wait_.erase(m->src)) return;
-  if (shrink_wait_.empty()) replan_after_shrink();
-}
-
-void Node::replan_after_shrink() {
-  const Location target = e_->target();
-  std::map<NodeID, int64_t> planned;  // bytes per sender in this re-plan (spread the load)
-  std::vector<std::pair<NodeID, LayerID>> lost;
-  int64_t jobs = 0;
-  for (auto& kv : assignment_) {
-    const NodeID dest = kv.first;
-    for (auto& l : kv.second) {
-      const LayerID layer = l.first;
-      auto st = status_.find(dest);
-      if (st != status_.end() && at(st->second, layer, target)) continue;
-      if (st != status_.end() && st->second.count(layer)) {
-        add_job(dest, dest, layer, 0, -1);  // its own copy in another tier: promote it
-        ++jobs;
-        continue;
-      }
-      NodeID best = kClientID;
-      for (auto& o : status_) {
-        if (o.first == dest || !o.second.count(layer)) continue;
-        if (best == kClientID || planned[o.first] < planned[best]) best = o.first;
-      }
-      if (best == kClientID) {
-        lost.push_back({dest, layer});
-        continue;
-      }
-      planned[best] += layer_size(layer);
-      add_job(best, dest, layer, 0, -1);
-      ++jobs;
-    }
-  }
-  for (auto& dl : lost) {
-    log::error(int64_t(cfg_.id)).u("dest", dl.first).u("layer", dl.second)
-        .msg("no live holder of the layer: dropping it from the assignment");
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    assignment_[dl.first].erase(dl.second);
-    stats_.dropped++;
-  }
-  log::info(int64_t(cfg_.id)).u("generation", shrink_gen_).i("jobs", jobs).msg("re-planned after recovery");
-  flush_batch();
-  finish_if_satisfied();
-}
-
-void Node::on_range_ack(const MessagePtr& m) {
-  // A range of a layer landed at m->src: range jobs it completes are retired.
-  if (cfg_.mode != 2) return;
-  auto lj = jobs_.find(m->layer);
-  if (lj == jobs_.end()) return;
-  std::vector<JobKey> done;
-  for (auto& kv : lj->second) {
-    if (kv.first.first != m->src) continue;
-    Job& j = kv.second;
-    const int64_t a = std::max(kv.first.second, m->offset);
-    const int64_t b = std::min(kv.first.second + j.size, m->offset + m->data_size);
-    if (a < b) j.got.add(a, b);
-    if (j.got.covered() >= j.size) done.push_back(kv.first);
-  }
-  for (auto& k : done) retire_job(m->layer, k);
-  if (!done.empty()) flush_batch();
-}
-
-void Node::retire_job(LayerID layer, const JobKey& key) {
-  auto lj = jobs_.find(layer);
-  if (lj == jobs_.end()) return;
-  auto jt = lj->second.find(key);
-  if (jt == lj->second.end()) return;
-  Job job = jt->second;
-  lj->second.erase(jt);
-  if (job.state == JobState::Sending) {
-    double dur = double(log::now_us() - job.t_us);
-    auto& pf = perf_[job.sender];
-    pf.first = pf.second == 0 ? dur : 0.5 * pf.first + 0.5 * dur;  // EWMA (quirk Q9)
-    pf.second++;
-    inflight_[job.sender] = std::max(0, inflight_[job.sender] - 1);
-    log::info(int64_t(cfg_.id)).u("node", job.sender).u("layerID", layer).i("offset", key.second)
-        .f("duration[ms]", dur / 1e3).msg("job completed");
-  } else {
-    load_[job.sender] = std::max<int64_t>(0, load_[job.sender] - 1);
-  }
-  while (inflight_[job.sender] < cfg_.pull_window && assign_new_job(job.sender)) {
-  }
-}
-
-// ------------------------------------------------------- failure handling
-
-void Node::track(NodeID sender, NodeID dest, LayerID layer, int64_t off, int64_t size) {
-  if (cfg_.job_timeout_s <= 0 || !is_leader_) return;
-  outstanding_[{dest, layer}].push_back({sender, off, size, log::now_us()});
-}
-
-NodeID Node::alternative_owner(LayerID layer, NodeID dest, NodeID avoid) {
-  // Any live holder of the layer (announced or acked since), the least busy first.
-  std::map<NodeID, int> busy;
-  for (auto& kv : outstanding_)
-    for (auto& o : kv.second) busy[o.sender]++;
-  NodeID best = kClientID;
-  int best_busy = INT_MAX;
-  for (auto& kv : status_) {
-    NodeID n = kv.first;
-    if (n == dest || n == avoid || suspects_.count(n) || !kv.second.count(layer)) continue;
-    if (busy[n] < best_busy) {
-      best = n;
-      best_busy = busy[n];
-    }
-  }
-  return best;
-}
-
-void Node::on_tick() {
-  if (!started_ || satisfied_ || cfg_.job_timeout_s <= 0 || e_->planned()) return;
-  const int64_t now = log::now_us();
-  struct Expired {
-    NodeID dest;
-    LayerID layer;
-    Outstanding o;
-  };
-  std::vector<Expired> expired;
-  for (auto it = outstanding_.begin(); it != outstanding_.end();) {
-    auto& v = it->second;
-    for (auto o = v.begin(); o != v.end();) {
-      double allow = cfg_.job_timeout_s + (cfg_.job_min_rate > 0 ? double(o->size) / cfg_.job_min_rate : 0.0);
-      if (double(now - o->t_us) / 1e6 > allow) {
-        expired.push_back({it->first.first, it->first.second, *o});
-        o = v.erase(o);
-      } else {
-        ++o;
-      }
-    }
-    it = v.empty() ? outstanding_.erase(it) : std::next(it);
-  }
-  for (auto& e : expired) {
-    if (!suspects_.count(e.o.sender) && e.o.sender != cfg_.id && e.o.sender != e.dest) {
-      suspects_.insert(e.o.sender);
-      std::lock_guard<std::mutex> lk(sig_mu_);
-      stats_.suspects++;
-    }
-    int& n = redispatches_[{e.dest, e.layer, e.o.off}];
-    NodeID alt = alternative_owner(e.layer, e.dest, e.o.sender);
-    if (alt == kClientID || ++n > cfg_.max_redispatch) {
-      log::error(int64_t(cfg_.id)).u("layer", e.layer).u("dest", e.dest).u("sender", e.o.sender)
-          .msg(alt == kClientID ? "job deadline expired and no other owner holds the layer"
-                                : "job deadline expired too often; giving up on this range");
-      track(e.o.sender, e.dest, e.layer, e.o.off, e.o.size);  // keep watching the original sender
-      continue;
-    }
-    log::warn(int64_t(cfg_.id)).u("layer", e.layer).u("dest", e.dest).u("sender", e.o.sender).u("new_sender", alt)
-        .i("offset", e.o.off).i("size", e.o.size).msg("job deadline expired: re-dispatching from another owner");
-    {
-      std::lock_guard<std::mutex> lk(sig_mu_);
-      stats_.redispatched++;
-    }
-    if (cfg_.mode == 2) {
-      // Keep the pull scheduler's books: the job now belongs to `alt`.
-      auto lj = jobs_.find(e.layer);
-      if (lj != jobs_.end()) {
-        auto jt = lj->second.find({e.dest, e.o.off});
-        if (jt != lj->second.end()) {
-          if (jt->second.state == JobState::Sending) inflight_[jt->second.sender] = std::max(0, inflight_[jt->second.sender] - 1);
-          jt->second.sender = alt;
-          jt->second.state = JobState::Sending;
-          jt->second.t_us = now;
-          inflight_[alt]++;
-        }
-      }
-    }
-    if (e.o.off == 0 && e.o.size >= layer_size(e.layer)) {
-      retransmit(e.layer, alt, e.dest);
-    } else {
-      track(alt, e.dest, e.layer, e.o.off, e.o.size);
-      if (alt == cfg_.id) {
-        send_layer(e.dest, e.layer, e.o.off, e.o.size, 0);
-      } else {
-        Message f;
-        f.type = MsgType::FlowRetransmit;
-        f.layer = e.layer;
-        f.dest = e.dest;
-        f.offset = e.o.off;
-        f.data_size = e.o.size;
-        send_msg(alt, f);
-      }
-    }
-  }
-  if (cfg_.mode == 2 && !expired.empty()) {
-    // Pending jobs queued on a suspect move to live senders.
-    for (auto& lj : jobs_)
-      for (auto& jd : lj.second)
-        if (jd.second.state == JobState::Pending && suspects_.count(jd.second.sender)) {
-          load_[jd.second.sender] = std::max<int64_t>(0, load_[jd.second.sender] - 1);
-          NodeID s = min_loaded_sender(lj.first, jd.first.first);
-          if (s == kClientID) continue;
-          jd.second.sender = s;
-          load_[s]++;
-        }
-    for (auto& kv : load_)
-      if (!suspects_.count(kv.first))
-        while (inflight_[kv.first] < cfg_.pull_window && assign_new_job(kv.first)) {
-        }
-  }
-}
-
-void Node::on_nack(const MessagePtr& m) {
-  // A receiver's chunk failed its CRC (planned engines): re-send that range,
-  // preferably from a holder that had the layer before the session started
-  // (its copy was checked against the manifest when it was staged).
-  const NodeID dest = m->src, bad = m->dest;
-  {
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    stats_.nacks++;
-  }
-  std::vector<NodeID> cand;
-  for (auto& kv : initial_status_)
-    if (kv.first != dest && kv.first != bad && kv.second.count(m->layer)) cand.push_back(kv.first);
-  NodeID src = bad;
-  if (!cand.empty()) src = cand[size_t(rng_() % cand.size())];
-  log::warn(int64_t(cfg_.id)).u("layer", m->layer).u("dest", dest).u("bad_sender", bad).u("new_sender", src)
-      .i("offset", m->offset).i("size", m->data_size).msg("chunk failed its CRC: re-sending");
-  if (!e_->planned()) return;
-  add_job(src, dest, m->layer, m->offset, m->data_size);
-  flush_batch();
-}
-
-void Node::add_job(NodeID src, NodeID dst, LayerID layer, int64_t offset, int64_t size, int phase, int64_t rate) {
-  XferJob j;
-  j.rate = rate;
-  j.src = src;
-  j.dst = dst;
-  j.layer = layer;
-  j.total = layer_size(layer);
-  j.offset = offset;
-  j.size = size < 0 ? j.total - offset : size;
-  auto it = manifests_.find(layer);
-  j.chunk_bytes = e_->chunk_bytes();
-  if (it != manifests_.end() && it->second.chunk_bytes > 0) {
-    j.chunk_bytes = it->second.chunk_bytes;
-    int64_t first = j.offset / j.chunk_bytes;
-    int64_t last = (j.offset + j.size + j.chunk_bytes - 1) / j.chunk_bytes;
-    for (int64_t c = first; c < last && c < int64_t(it->second.crc.size()); ++c) j.crc.push_back(it->second.crc[size_t(c)]);
-  } else if (auto pc = partial_crc_.find(layer); pc != partial_crc_.end() && pc->second.first > 0) {
-    // No whole copy announced a manifest: the chunks partial holders vouched
-    // for. One unknown chunk leaves the job unverified (never a wrong CRC).
-    j.chunk_bytes = pc->second.first;
-    const int64_t first = j.offset / j.chunk_bytes, last = (j.offset + j.size + j.chunk_bytes - 1) / j.chunk_bytes;
-    for (int64_t c = first; c < last; ++c) {
-      auto ci = pc->second.second.find(c);
-      if (ci == pc->second.second.end()) {
-        j.crc.clear();
-        break;
-      }
-      j.crc.push_back(ci->second);
-    }
-  }
-  pending_jobs_.push_back({j, phase});
-}
-
-void Node::merge_partial_manifest(LayerID layer, const CrcManifest& m,
-                                  const std::vector<std::pair<int64_t, int64_t>>& ranges) {
-  if (m.chunk_bytes <= 0) return;
-  auto& pc = partial_crc_[layer];
-  if (pc.first && pc.first != m.chunk_bytes) return;  // another grid: keep the first
-  pc.first = m.chunk_bytes;
-  const int64_t total = layer_size(layer);
-  for (int64_t c = 0; c < int64_t(m.crc.size()); ++c) {
-    const int64_t a = c * m.chunk_bytes, b = total > 0 ? std::min(a + m.chunk_bytes, total) : a + m.chunk_bytes;
-    bool inside = false;
-    for (auto& r : ranges) inside = inside || (r.first <= a && r.second >= b);
-    if (inside) pc.second.emplace(c, m.crc[size_t(c)]);
-  }
-}
-
-void Node::flush_batch() {
-  // Assign global sequence numbers: by phase (relay hops after the hops that
-  // feed them), then round-robin over (src, dst) pairs so that consecutive
-  // sequence numbers spread over distinct xGMI links. This runs between
-  // "timer start" and the first byte on any link: jobs are moved, not copied,
-  // and the leader's own batch goes last (its engine starts staging the
-  // moment it lands, beside the encoding of everyone else's).
-  if (pending_jobs_.empty()) return;
-  trace::Scoped tr("dissem.flush_batch");
-  std::map<std::pair<int, std::pair<NodeID, NodeID>>, std::vector<size_t>> groups;  // (phase, (src, dst)) -> jobs
-  for (size_t i = 0; i < pending_jobs_.size(); ++i)
-    groups[{pending_jobs_[i].phase, {pending_jobs_[i].job.src, pending_jobs_[i].job.dst}}].push_back(i);
-  std::map<NodeID, Message> per_rank;
-  for (auto g = groups.begin(); g != groups.end();) {
-    const int phase = g->first.first;
-    auto end = g;
-    while (end != groups.end() && end->first.first == phase) ++end;
-    for (size_t round = 0;; ++round) {
-      bool any = false;
-      for (auto pr = g; pr != end; ++pr) {
-        if (round >= pr->second.size()) continue;
-        any = true;
-        XferJob& j = pending_jobs_[pr->second[round]].job;
-        j.seq = next_seq_++;
-        if (j.dst == kAllRanks) {
-          for (auto& st : status_)
-            if (st.first != j.src) per_rank[st.first].jobs.push_back(j);
-          per_rank[j.src].jobs.push_back(std::move(j));
-        } else if (j.dst == j.src) {
-          per_rank[j.src].jobs.push_back(std::move(j));
-        } else {
-          // a sender that announced the layer's manifest checks its staging
-          // against its own CRCs: its copy of the job goes without them
-          auto mh = manifest_holders_.find(j.layer);
-          const bool own = mh != manifest_holders_.end() && mh->second.count(j.src);
-          XferJob sj;
-          sj.seq = j.seq;
-          sj.src = j.src;
-          sj.dst = j.dst;
-          sj.layer = j.layer;
-          sj.offset = j.offset;
-          sj.size = j.size;
-          sj.total = j.total;
-          sj.chunk_bytes = j.chunk_bytes;
-          sj.rate = j.rate;
-          if (!own) sj.crc = j.crc;
-          per_rank[j.src].jobs.push_back(std::move(sj));
-          per_rank[j.dst].jobs.push_back(std::move(j));
-        }
-      }
-      if (!any) break;
-    }
-    g = end;
-  }
-  pending_jobs_.clear();
-  const uint64_t batch = next_batch_++;
-  int64_t njobs = 0;
-  std::vector<std::pair<NodeID, Message>> out;
-  out.reserve(per_rank.size());
-  for (auto& kv : per_rank)
-    if (kv.first != cfg_.id) out.emplace_back(kv.first, std::move(kv.second));
-  if (auto self = per_rank.find(cfg_.id); self != per_rank.end()) out.emplace_back(self->first, std::move(self->second));
-  for (auto& o : out) {
-    o.second.type = MsgType::XferBatch;
-    o.second.batch = batch;
-    o.second.src = cfg_.id;
-    o.second.epoch = cfg_.epoch;
-    njobs += int64_t(o.second.jobs.size());
-  }
-  try {
-    t_->send_many(out);
-  } catch (const std::exception& e) {
-    log::error(int64_t(cfg_.id)).s("error", e.what()).msg("failed to send xfer_batch");
-  }
-  log::debug(int64_t(cfg_.id)).u("batch", batch).i("job_copies", njobs).msg("dispatched transfer batch");
-}
-
-void Node::retransmit(LayerID layer, NodeID owner, NodeID dest) {
-  // node.go:611-626; the leader's own sends are asynchronous (quirk Q4).
-  {
-    std::lock_guard<std::mutex> lk(sig_mu_);
-    stats_.jobs_dispatched++;
-  }
-  if (e_->planned()) {
-    add_job(owner, dest, layer, 0, -1);
-    return;
-  }
-  track(owner, dest, layer, 0, layer_size(layer));
-  if (owner == cfg_.id) {
-    LayerSrc src;
-    int64_t rate = store_.get(layer, &src) ? src.meta.limit_rate : 0;
-    send_layer(dest, layer, 0, -1, rate);
-    return;
-  }
-  Message r;
-  r.type = MsgType::Retransmit;
-  r.layer = layer;
-  r.dest = dest;
-  send_msg(owner, r);
-}
-
 // ------------------------------------------------------------------- client
 
 ClientNode::ClientNode(NodeID node_id, std::shared_ptr<Transport> t, const LayersSrc& layers)

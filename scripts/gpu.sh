@@ -12,6 +12,7 @@
 #   check      GPU tests, smoke(), 1-GPU headline bench
 #   verify     receive-side kernels at the engine's launch size: tests + scripts/verify_bench.py + kernel trace
 #   profile    kernel traces of the headline bench and the fp8 --store bf16 receive path
+#   pmc        counters of the two verify kernels at the engine's full-batch launch (3 passes)
 #   multirank  multi-rank RCCL rehearsal on one GPU (ranks share device 0)
 #   shared8    the driver's `bench.py --gpus 8` path at 8 ranks on one GPU (every mode)
 #   shared24   the driver's N = 2 and N = 4 scaling points (`bench.py --gpus 2/4`) on one GPU
@@ -47,6 +48,17 @@ case "$RECIPE" in
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fp8_bf16 -o fp8b -- \
       python3 bench.py --pack fp8 --store bf16 --layers 20 --layer-mib 3072 --steps 2 --warmup 1 \
       > $OUT/fp8_bf16.json 2> $OUT/fp8_bf16.log
+    ;;
+  pmc)
+    VB="python3 scripts/verify_bench.py --only-full-batch --reps 5"
+    timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
+      SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq -o sq -- $VB \
+      > $OUT/sq.json 2> $OUT/sq.err &&
+    timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- $VB \
+      > $OUT/fetch.json 2> $OUT/fetch.err &&
+    timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- $VB \
+      > $OUT/write.json 2> $OUT/write.err &&
+    python3 scripts/pmc_summary.py $OUT/sq $OUT/fetch $OUT/write > $OUT/pmc_summary.md
     ;;
   multirank)
     timeout -k 10 1100 $PYTEST tests/test_gpu_multirank.py > $OUT/pytest.log 2>&1

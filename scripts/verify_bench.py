@@ -17,7 +17,10 @@ distinct buffers, cycled), and every case is checked once against the host CRC
 and the standalone unpack. Run it under rocprofv3 --kernel-trace --stats for the
 per-kernel device times (the HIP-event numbers here include launch gaps).
 
-    python scripts/verify_bench.py [--reps 40] [--pool 24]
+    python scripts/verify_bench.py [--reps 40] [--pool 24] [--cus N] [--only-full-batch]
+
+--only-full-batch runs just the full-batch launches of both kernels (and the
+checks), so a rocprofv3 --pmc pass sees one launch shape per kernel.
 """
 
 import argparse
@@ -50,7 +53,9 @@ def main():
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--pool", type=int, default=24, help="distinct 64 MiB chunks cycled through (>= 16)")
     ap.add_argument("--cus", type=int, default=0, help="CUs the launches size their grid for (0: all)")
+    ap.add_argument("--only-full-batch", action="store_true", help="only the full-batch launches (counter runs)")
     args = ap.parse_args()
+    full_only = args.only_full_batch
     pool = max(16, args.pool)
     nmax = _core.crc32c_batch_max()
     out = {"chunk_MiB": CHUNK >> 20, "pool_chunks": pool, "cus": args.cus}
@@ -70,11 +75,12 @@ def main():
         calls[0] += 1
         _core.crc32c_chunks_async(bufs[i].data_ptr(), CHUNK, CHUNK, res.data_ptr(), ws.data_ptr(), 0, args.cus)
 
-    t = timed(crc_single, args.reps)
-    out["crc_single_us_per_chunk"] = round(t * 1e6, 1)
-    out["crc_single_GBps"] = round(CHUNK / t / 1e9, 1)
+    if not full_only:
+        t = timed(crc_single, args.reps)
+        out["crc_single_us_per_chunk"] = round(t * 1e6, 1)
+        out["crc_single_GBps"] = round(CHUNK / t / 1e9, 1)
     for k in (1, 4, 8, 16):
-        if k > nmax:
+        if k > nmax or (full_only and k != nmax):
             continue
         calls[0] = 0
 
@@ -91,13 +97,15 @@ def main():
     _core.crc32c_batch_async([(b.data_ptr(), CHUNK) for b in bufs[:nmax]], res.data_ptr(), ws.data_ptr(), 0, args.cus)
     torch.cuda.synchronize()
     out["crc_batch_matches_host"] = [x & 0xFFFFFFFF for x in res.cpu().tolist()] == want
-    big = torch.empty(16 * CHUNK, dtype=torch.uint8, device="cuda")
-    _core.fill_random(big.data_ptr(), big.numel(), 5)
-    wsb = torch.zeros(_core.crc32c_workspace_bytes(big.numel(), CHUNK), dtype=torch.uint8, device="cuda")
-    t = timed(lambda: _core.crc32c_chunks_async(big.data_ptr(), big.numel(), CHUNK, res.data_ptr(), wsb.data_ptr(), 0,
-                                                args.cus), args.reps // 2)
-    out["crc_bulk_1GiB_GBps"] = round(big.numel() / t / 1e9, 1)
-    del big, bufs
+    if not full_only:
+        big = torch.empty(16 * CHUNK, dtype=torch.uint8, device="cuda")
+        _core.fill_random(big.data_ptr(), big.numel(), 5)
+        wsb = torch.zeros(_core.crc32c_workspace_bytes(big.numel(), CHUNK), dtype=torch.uint8, device="cuda")
+        t = timed(lambda: _core.crc32c_chunks_async(big.data_ptr(), big.numel(), CHUNK, res.data_ptr(),
+                                                    wsb.data_ptr(), 0, args.cus), args.reps // 2)
+        out["crc_bulk_1GiB_GBps"] = round(big.numel() / t / 1e9, 1)
+        del big
+    del bufs
 
     # ---- fused CRC32C + fp8 -> bf16 of packed 64 MiB source chunks
     src = torch.empty(CHUNK, dtype=torch.uint8, device="cuda")
@@ -119,11 +127,12 @@ def main():
         _core.fp8_verify_unpack_async(packed[i].data_ptr(), CHUNK, CHUNK, BLOCK, outs[i].data_ptr(), res.data_ptr(),
                                       ws.data_ptr(), 0, args.cus)
 
-    t = timed(fused_single, args.reps)
-    out["fused_single_us_per_chunk"] = round(t * 1e6, 1)
-    out["fused_single_GBps"] = round(moved / t / 1e9, 1)
+    if not full_only:
+        t = timed(fused_single, args.reps)
+        out["fused_single_us_per_chunk"] = round(t * 1e6, 1)
+        out["fused_single_GBps"] = round(moved / t / 1e9, 1)
     for k in (1, 4, 8, 16):
-        if k > nmax:
+        if k > nmax or (full_only and k != nmax):
             continue
         calls[0] = 0
 
@@ -153,6 +162,9 @@ def main():
         _core.fp8_unpack(packed[j].data_ptr(), packed[j].data_ptr() + n, n, ref.data_ptr(), BLOCK)
         ok = ok and torch.equal(ref, outs[j])
     out["fused_batch_bf16_matches_unpack"] = ok
+    if full_only:
+        print(json.dumps(out))
+        return
     # references: the standalone unpack of one chunk, a torch copy of 64 MiB
     t = timed(lambda: _core.fp8_unpack(packed[0].data_ptr(), packed[0].data_ptr() + n, n, ref.data_ptr(), BLOCK),
               args.reps)

@@ -71,6 +71,33 @@ def test_crc32c_cus_and_workspace_reuse(gpu, n, chunk, cus):
         assert int(ws.count_nonzero()) == 0  # the launch left its fold words zeroed
 
 
+@pytest.mark.parametrize(
+    "n,chunk",
+    [
+        ((8 << 20) + 16, 16 << 10),  # 513 one-segment chunks: a range capped at the LDS fold slots
+        (7 << 20, 48 << 10),  # 3-segment chunks
+        ((2 << 20) + 48, 4 << 10),  # chunks shorter than a segment
+    ],
+)
+@pytest.mark.parametrize("cus", [1, 2])
+def test_crc32c_walk_ranges_spanning_many_chunks(gpu, n, chunk, cus):
+    """The CRC-only walk gives each workgroup a contiguous range of segments and
+    folds it per chunk in LDS slots: with one or two CUs a range would span
+    hundreds of small chunks, so the host caps it at the slot count and
+    launches more workgroups."""
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 77 + n)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
+    ws = torch.zeros(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+    out = torch.zeros(len(want), dtype=torch.int32, device="cuda")
+    gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, cus)
+    torch.cuda.synchronize()
+    assert [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()] == want
+    assert int(ws.count_nonzero()) == 0
+
+
 def test_crc32c_batch_matches_host(gpu):
     # the chunks one P2P group lands: independent buffers of mixed sizes
     sizes = [64 << 20, (1 << 20) + 16, 100 << 10, 16, 48 << 10, 3 * (16 << 10) + 32]
