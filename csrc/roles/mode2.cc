@@ -177,13 +177,13 @@ bool Node::assign_new_job(NodeID node) {
     j.t_us = log::now_us();
     load_[node] = std::max<int64_t>(0, load_[node] - 1);
     inflight_[node]++;
-    log::debug(int64_t(cfg_.id)).u("node", node).u("layer", layer).i("offset", key.second)
+    log::debug(int64_t(cfg_.id)).u("node", node).u("dest", key.first).u("layer", layer).i("offset", key.second)
         .msg("pass a job initially assigned");
     dispatch_range(layer, node, key.first, key.second, j.size);
     return true;
   }
   if (rarest_stealable_job(node, &layer, &key, &victim)) {
-    log::debug(int64_t(cfg_.id)).u("layer", layer)
+    log::debug(int64_t(cfg_.id)).u("layer", layer).u("node", node).u("dest", key.first)
         .msg("steal a job from the most loaded node (" + std::to_string(victim) + ") to node " + std::to_string(node));
     load_[victim] = std::max<int64_t>(0, load_[victim] - 1);
     Job& j = jobs_[layer][key];

@@ -152,7 +152,7 @@ void Node::retire_job(LayerID layer, const JobKey& key) {
     pf.first = pf.second == 0 ? dur : 0.5 * pf.first + 0.5 * dur;  // EWMA (quirk Q9)
     pf.second++;
     inflight_[job.sender] = std::max(0, inflight_[job.sender] - 1);
-    log::info(int64_t(cfg_.id)).u("node", job.sender).u("layerID", layer).i("offset", key.second)
+    log::info(int64_t(cfg_.id)).u("node", job.sender).u("dest", key.first).u("layerID", layer).i("offset", key.second)
         .f("duration[ms]", dur / 1e3).msg("job completed");
   } else {
     load_[job.sender] = std::max<int64_t>(0, load_[job.sender] - 1);
