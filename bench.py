@@ -75,7 +75,10 @@ def parse_args(argv=None):
                         "mode 0 then stages one slice of every layer per rank over its own PCIe (config #2)")
     p.add_argument("--node-disk-gbps", type=float, default=None,
                    help="--tier disk: the node's one NVMe read rate shared by every rank's disk readers and planned "
-                        "as one budget by mode 3 (default 13.3, profiles/r1_diskspeed.log; 0 = per-rank, unpaced)")
+                        "as one budget by mode 3 (0 = per-rank, unpaced). Default: unpaced at N = 1 (one rank has the "
+                        "NVMe alone; paced at 13.3 it read exactly 13.30 GB/s where this box's file->HBM pipeline "
+                        "does 15.3, profiles/r5_disk/); 13.3 at N > 1, REAL-NODE GUESS from the round-1 box's NVMe "
+                        "(profiles/r1_diskspeed.log), settled by bin/diskspeed on the node and stage_GBps_rank0")
     # Defaults measured on a real MI355X cite their evidence; the ones only a
     # real 8-GPU node can settle name the JSON field that will (REAL-NODE GUESS).
     p.add_argument("--verify-cus", type=int, default=-1,
@@ -291,7 +294,8 @@ def worker(args, world, rank, chan) -> int:
     run_tag = os.environ.get("DLD_SUP_PREFIX", "") + os.environ.get("MASTER_PORT", "") + os.environ.get(
         "TORCHELASTIC_RUN_ID", "") if world > 1 else str(os.getpid())
     node_key = "b" + hashlib.blake2b(run_tag.encode(), digest_size=6).hexdigest()
-    disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else (13.3 if args.tier == "disk" else 0.0)
+    disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else (
+        13.3 if args.tier == "disk" and world > 1 else 0.0)
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=True, payload_seed=0, registry={rank: listen_addr(bool(hosts))},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
