@@ -74,11 +74,11 @@ def parse_args(argv=None):
                    help="host-tier layers in node-shared pinned memory (POSIX shm, hipHostRegister in every rank); "
                         "mode 0 then stages one slice of every layer per rank over its own PCIe (config #2)")
     p.add_argument("--node-disk-gbps", type=float, default=None,
-                   help="--tier disk: the node's one NVMe read rate shared by every rank's disk readers and planned "
-                        "as one budget by mode 3 (0 = per-rank, unpaced). Default: unpaced at N = 1 (one rank has the "
-                        "NVMe alone; paced at 13.3 it read exactly 13.30 GB/s where this box's file->HBM pipeline "
-                        "does 15.3, profiles/r5_disk/); 13.3 at N > 1, REAL-NODE GUESS from the round-1 box's NVMe "
-                        "(profiles/r1_diskspeed.log), settled by bin/diskspeed on the node and stage_GBps_rank0")
+                   help="--tier disk: the node's one NVMe read rate (GB/s) shared by every rank's disk readers and "
+                        "planned as one budget by mode 3 (0 = per-rank, unpaced). Default: unpaced at N = 1 (one rank "
+                        "has the NVMe alone; paced at 13.3 it read exactly 13.30 GB/s, unpaced 20.3, "
+                        "profiles/r5_disk/); at N > 1 MEASURED before the run by an O_DIRECT read probe on each host "
+                        "(utils/diskprobe.py; JSON node_disk_GBps, node_disk_source)")
     # Defaults measured on a real MI355X cite their evidence; the ones only a
     # real 8-GPU node can settle name the JSON field that will (REAL-NODE GUESS).
     p.add_argument("--verify-cus", type=int, default=-1,
@@ -294,8 +294,22 @@ def worker(args, world, rank, chan) -> int:
     run_tag = os.environ.get("DLD_SUP_PREFIX", "") + os.environ.get("MASTER_PORT", "") + os.environ.get(
         "TORCHELASTIC_RUN_ID", "") if world > 1 else str(os.getpid())
     node_key = "b" + hashlib.blake2b(run_tag.encode(), digest_size=6).hexdigest()
-    disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else (
-        13.3 if args.tier == "disk" and world > 1 else 0.0)
+    disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else 0.0
+    disk_source = "flag" if args.node_disk_gbps is not None else "unpaced"
+    if args.tier == "disk" and args.node_disk_gbps is None and world > 1:
+        # the node's one NVMe, shared by every rank: measured once per host
+        # (utils/diskprobe.py), the slowest host's rate for all; 13.3 (the
+        # round-1 box, profiles/r1_diskspeed.log) where O_DIRECT is unavailable
+        from distributed_llm_dissemination_amd.utils.diskprobe import read_rate_gbps
+
+        mine = None
+        if int(os.environ.get("LOCAL_RANK", "0")) == 0:  # one probe per host (ranks sharing a GPU included)
+            mine = read_rate_gbps(args.storage or os.path.join(os.getcwd(), "storage"))
+            log(f"node NVMe read rate: {mine if mine is None else round(mine, 2)} GB/s (O_DIRECT probe)")
+        rates = [None] * world
+        dist.all_gather_object(rates, mine)
+        got = [r for r in rates if r]
+        disk_gbps, disk_source = (min(got), "measured") if got else (13.3, "default")
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=True, payload_seed=0, registry={rank: listen_addr(bool(hosts))},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
@@ -421,7 +435,8 @@ def worker(args, world, rank, chan) -> int:
                 "pack": args.pack,
                 "payload": "bf16 layer shards as raw bytes, moved bit-exact (CRC32C per chunk)",
                 **({"host_share": True} if args.host_share else {}),
-                **({"node_disk_GBps": disk_gbps} if args.tier == "disk" else {}),
+                **({"node_disk_GBps": round(disk_gbps, 2), "node_disk_source": disk_source}
+                   if args.tier == "disk" else {}),
             },
         }
         if args.pack != "none":
