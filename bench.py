@@ -58,9 +58,11 @@ def parse_args(argv=None):
     p.add_argument("--timeout", type=float, default=120.0,
                    help="seconds one session (step) may take before the rank gives up (also the P2P group timeout)")
     p.add_argument("--pull-window", type=int, default=0,
-                   help="mode 2 jobs in flight per sender (0 = one per peer; round-4 sim at N=8, 50 GB/s links, "
-                        "closed loop on: 7 -> 265 ms, 10 -> 294, 14 -> 388, profiles/r4_predict_mode2.jsonl). "
-                        "REAL-NODE GUESS: settled by config.per_link_busy_GBps in mode 2")
+                   help="mode 2 jobs in flight per sender (0 = two per peer). Round-5 sim (closed loop on, 50 GB/s "
+                        "links): N = 8: 7 -> 262-270 ms, 10 -> 248, 14 -> 245, 21 -> 270; N = 4: 3 -> 589, 6 -> 465; "
+                        "N = 2: 1 -> 1794, 2 -> 875 (a rank's loads of its own layers hold window slots too; "
+                        "profiles/r5_predict_mode2_windows.jsonl). REAL-NODE GUESS: settled by "
+                        "config.per_link_busy_GBps in mode 2")
     p.add_argument("--storage", default="", help="disk tier directory")
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0: scatter+relay P2P, ncclBroadcast, or leader fan-out")
@@ -344,7 +346,7 @@ def worker(args, world, rank, chan) -> int:
                          {p: g * 1e9 for p, g in probe.get("concurrent_in", {}).items() if g})
 
     engine_note = f"{rt.engine.stats().lanes} comm lanes" if world > 1 else ""
-    policy = dict(seed=0, pull_window=args.pull_window or max(1, world - 1),
+    policy = dict(seed=0, pull_window=args.pull_window or max(1, 2 * (world - 1)),
                   owner_policy=args.owner_policy,
                   relay=args.bcast == "relay", collective=args.bcast == "collective",
                   adapt_links=True, hierarchical=True)

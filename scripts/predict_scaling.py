@@ -188,7 +188,8 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                 extra = {"stage_gbps": pcie_gbps / scale} if plan_links else {}
                 if plan_links and hosts > 1:
                     extra["nic_gbps"] = nic_gbps / scale
-                r.prepare(mode, **{"pull_window": max(1, n - 1), "adapt_links": adapt_links, **extra, **(policy or {})})
+                r.prepare(mode, **{"pull_window": max(1, 2 * (n - 1)), "adapt_links": adapt_links, **extra,
+                                   **(policy or {})})
             res = [None] * n
             sent0 = [r.link_stats()["sent"] for r in rts]
             staged0 = [r.engine.stats().bytes_staged for r in rts]
@@ -302,7 +303,7 @@ def main() -> int:
     ap.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
                     help="mode 1's owner choice (bench.py's default: links)")
     ap.add_argument("--pull-window", type=int, default=0,
-                    help="mode 2: jobs in flight per sender (0: N - 1; bench.py's default is 2 (N - 1))")
+                    help="mode 2: jobs in flight per sender (0: 2 (N - 1), as bench.py)")
     args = ap.parse_args()
     common = dict(steps=args.steps, warmup=args.warmup, probe_mib=args.probe_mib)
     _core.set_log_level(3)
