@@ -326,13 +326,10 @@ __device__ __forceinline__ u32x4_t seg_load(__amdgpu_buffer_rsrc_t r, int lo, in
 // registers: per block, the visit sees the block's 4 words (as loaded, with
 // their byte offsets in the chunk), then the transpose hands lane l its piece
 // and the slice-by-4 chain runs; the lanes' registers are shifted to the
-// segment end (lanec = x^(8*64*(63-lane))) and XOR-reduced. `between(b)` runs
-// after block b (the persistent walk issues the next segment's block-b loads
-// there). CRC = false (diagnostic only) keeps the visits and drops the math.
-template <class Visit, bool CRC, class ST, class Between>
+// segment end (lanec = x^(8*64*(63-lane))) and XOR-reduced.
+template <class Visit, class ST>
 __device__ __forceinline__ uint32_t seg_full(u32x4_t (&w)[4 * kBlocksPerSeg], const Seg& cur, const ST& st,
-                                             Visit& visit, const uint32_t* __restrict__ lanec, int lo,
-                                             Between between) {
+                                             Visit& visit, const uint32_t* __restrict__ lanec, int lo) {
   // s holds (register ^ next word) between steps: 16 mix steps per block,
   // the block's first word folded into the gap shift before it
   uint32_t s = 0;
@@ -340,17 +337,13 @@ __device__ __forceinline__ uint32_t seg_full(u32x4_t (&w)[4 * kBlocksPerSeg], co
   for (int b = 0; b < kBlocksPerSeg; ++b) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) visit.word(w[4 * b + j], cur.seg_start + b * kBlockBytes + j * 1024 + lo, 4 * b + j);
-    if constexpr (CRC) {
-      row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
-      s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
+    row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
+    s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
 #pragma unroll
-      for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
-    }
+    for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
     __builtin_amdgcn_sched_barrier(0);
-    between(b);
   }
-  if constexpr (CRC) s = wave_xor_dpp(multmodp_unrolled(lanec[threadIdx.x & 63], s));
-  return s;
+  return wave_xor_dpp(multmodp_unrolled(lanec[threadIdx.x & 63], s));
 }
 
 
@@ -397,7 +390,7 @@ __device__ __forceinline__ uint32_t slice_once(const Geo& geo, int64_t g, bool h
   const Slice4T<R> st(lds);
   visit.begin(cur);
   uint32_t s;
-  if (full) s = seg_full<Visit, true>(w, cur, st, visit, sc + kLanePow, lo, [](int) {});
+  if (full) s = seg_full(w, cur, st, visit, sc + kLanePow, lo);
   else s = slice_partial(cur, sc, st, lane, visit);
   return to_chunk_end(cur, s, sc);
 }
@@ -775,9 +768,11 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
 // wave w takes g0 + w, g0 + w + 16, ..., and loads block b of its next
 // segment as soon as block b of the current one is consumed (pinned with
 // sched_barrier: left alone, the compiler sinks those loads behind the math),
-// so 16 KiB stay in flight per wave. The round-2 walk ran at 5.76 TB/s on
-// 1 GiB; one segment per wave with the tables filled per 8 segments measured
-// 3.8 TB/s for CRC alone (profiles/r5_verify/per_launch.txt).
+// so 16 KiB stay in flight per wave. One segment per wave with the tables
+// filled per 8 segments measured 3.8 TB/s for CRC alone (profiles/r5_verify/);
+// this walk 5.67 TB/s on 1 GiB and 12.6 us per 64 MiB chunk in 16-chunk
+// launches, 0.94-1.0 TB/s on the 32 CUs of the verify stream with peers
+// (profiles/r5_walk/).
 // The fold: a wave accumulates its values while its item does not change and
 // hands each run to the workgroup's LDS slot of that item (ds atomics); at
 // the end the workgroup adds one value per item to the global {acc, count}
