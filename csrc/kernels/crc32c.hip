@@ -38,7 +38,7 @@
 // 16 VALU per 64 B of lane data) hands lane l its piece l. Loading the pieces
 // directly (every lane 16 B of its own piece per instruction: 64 separate
 // 64-B spans) reads at 3.5-4.0 TB/s against 6.8 for whole KiBs in the same
-// 16-KiB-per-wave shape (kern::read_seg probe, profiles/r2_crc_ab).
+// 16-KiB-per-wave shape (round 2's read-shape probe kernel, profiles/r2_crc_ab).
 //
 // LDS layout (MI355X_MICROARCH.md, LDS): a ds_read_b32 is served in two groups
 // of 32 lanes over 32 banks, and data-dependent indices into a plain table
