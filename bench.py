@@ -43,14 +43,21 @@ def metric_name(layers: int, layer_mib: int, mode: int, ranks: int) -> str:
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE or 1)")
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--mode", type=int, default=1, choices=[0, 1, 2, 3])
-    p.add_argument("--layers", type=int, default=80)
-    p.add_argument("--layer-mib", type=int, default=1024)
-    p.add_argument("--chunk-mib", type=int, default=64)
-    p.add_argument("--tier", default="host", choices=["host", "device", "disk"])
-    p.add_argument("--seeding", default="random", choices=["random", "leader", "uniform"])
+    p.add_argument("--steps", type=int, default=5, help="timed sessions")
+    p.add_argument("--warmup", type=int, default=1, help="untimed sessions first")
+    p.add_argument("--mode", type=int, default=1, choices=[0, 1, 2, 3],
+                   help="distribution mode (BASELINE config #3: 1, peer retransmission)")
+    p.add_argument("--layers", type=int, default=80, help="layers (config #3: 80)")
+    p.add_argument("--layer-mib", type=int, default=1024, help="MiB per layer (config #3: 1 GiB)")
+    p.add_argument("--chunk-mib", type=int, default=64,
+                   help="chunk grid: P2P message, CRC unit and staging copy. N = 1 reads the same at 32-256 "
+                        "(56.87-56.98 GB/s, profiles/r5_chunk/). REAL-NODE GUESS at N > 1: settled by "
+                        "config.per_link_busy_GBps")
+    p.add_argument("--tier", default="host", choices=["host", "device", "disk"],
+                   help="where the seeded layers live: pinned host memory (config #3), HBM, NVMe (config #4)")
+    p.add_argument("--seeding", default="random", choices=["random", "leader", "uniform"],
+                   help="InitialLayers: balanced random permutation (config #3), all on the leader (config #2), "
+                        "or i.i.d. uniform owners")
     p.add_argument("--copies", type=int, default=1, help="holders per layer in the initial seeding")
     p.add_argument("--owner-policy", default="links", choices=["random", "balanced", "links"],
                    help="mode 1 owner choice when a layer has several holders (--copies > 1); links also "
