@@ -313,7 +313,10 @@ def worker(args, world, rank, chan) -> int:
 
         mine = None
         if int(os.environ.get("LOCAL_RANK", "0")) == 0:  # one probe per host (ranks sharing a GPU included)
-            mine = read_rate_gbps(args.storage or os.path.join(os.getcwd(), "storage"))
+            try:  # never leave the other ranks waiting in the gather below
+                mine = read_rate_gbps(args.storage or os.path.join(os.getcwd(), "storage"))
+            except Exception as e:  # noqa: BLE001 - e.g. a full or read-only disk: keep the default
+                log(f"node NVMe probe failed: {e}")
             log(f"node NVMe read rate: {mine if mine is None else round(mine, 2)} GB/s (O_DIRECT probe)")
         rates = [None] * world
         dist.all_gather_object(rates, mine)
