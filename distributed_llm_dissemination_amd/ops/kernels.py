@@ -69,14 +69,16 @@ def fill_random_(t: torch.Tensor, seed: int) -> torch.Tensor:
 
 def crc32c(t: torch.Tensor, chunk_bytes: int = 0) -> torch.Tensor:
     """CRC32C (Castagnoli) of every `chunk_bytes` chunk of `t`'s bytes (whole
-    tensor when 0), as an int32 GPU tensor holding the uint32 bit patterns."""
+    tensor when 0), as an int32 GPU tensor holding the uint32 bit patterns. One
+    chunk may have any length; several need a chunk size that is a multiple of
+    16 (every chunk starts 16-B aligned)."""
     _check_dev(t, "t")
     n = _nbytes(t)
-    chunk = chunk_bytes or n
+    chunk = min(chunk_bytes or n, n)
     if n <= 0:
         return torch.empty(0, dtype=torch.int32, device=t.device)
-    if chunk % 16:
-        raise ValueError("chunk_bytes must be a multiple of 16")
+    if chunk < n and chunk % 16:
+        raise ValueError("chunk_bytes must be a multiple of 16 when the tensor holds several chunks")
     nchunks = (n + chunk - 1) // chunk
     out = torch.empty(nchunks, dtype=torch.int32, device=t.device)
     # the fold words of the launch: zeroed (kernels.h: the kernel leaves them zeroed)

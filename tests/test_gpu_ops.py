@@ -57,6 +57,31 @@ def test_fp8_layer_fused_verify_unpack():
     assert torch.equal(y, torch.cat(parts))
 
 
+def test_fp8_verify_unpack_chunks_batch_vs_torch_fp32():
+    """The engine's batched form through the op: independent packed chunks of
+    mixed sizes (a full 64 MiB chunk, a layer's short tail, small ones) in one
+    launch; CRCs against the op's plain CRC of each packed image, bf16 against
+    torch's e4m3fn -> f32 x scale -> bf16 of the same bytes."""
+    sizes = [64 << 20, (3 << 20) + 8192, 256, 1 << 20]
+    chunks, refs = [], []
+    for i, src in enumerate(sizes):
+        torch.manual_seed(i)
+        x = (torch.randn(src // 2, device="cuda") * (10.0 ** (i - 2))).to(torch.bfloat16)
+        packed = ops.fp8_pack_layer(x, (src + 4095) // 4096 * 4096)  # one chunk: [q: src/2][scales f32]
+        n = src // 2
+        q, sc = packed[:n].view(torch.float8_e4m3fn), packed[n:].view(torch.float32)
+        refs.append((q.float().view(-1, 128) * sc[:, None]).view(-1).to(torch.bfloat16))
+        chunks.append((packed, src))
+    outs, crcs = ops.fp8_verify_unpack_chunks(chunks)
+    assert ops.crc32c_values(crcs) == [ops.crc32c_values(ops.crc32c(p))[0] for p, _ in chunks]
+    for y, ref in zip(outs, refs):
+        torch.testing.assert_close(y, ref, rtol=0, atol=0)
+    with pytest.raises(ValueError):
+        ops.fp8_verify_unpack_chunks([(chunks[0][0], 100)])  # not a whole number of scale blocks
+    with pytest.raises(ValueError):
+        ops.fp8_verify_unpack_chunks(chunks * 5)  # more than one launch holds
+
+
 def test_ops_reject_bad_operands():
     x = torch.zeros(100, dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):
@@ -65,5 +90,10 @@ def test_ops_reject_bad_operands():
         ops.fp8_pack(x.float(), 4)
     with pytest.raises(ValueError):
         ops.crc32c(torch.zeros(64, dtype=torch.uint8), 16)  # host tensor
+    with pytest.raises(ValueError):
+        ops.crc32c(torch.zeros(64, dtype=torch.uint8, device="cuda"), 24)  # several chunks, not 16-B aligned
+    # one chunk of any length is fine (a packed chunk's image: 128 q bytes + 8 of scales)
+    odd = torch.zeros(136, dtype=torch.uint8, device="cuda")
+    assert ops.crc32c_values(ops.crc32c(odd)) == [_core.crc32c(bytes(136))]
     with pytest.raises(ValueError):
         ops.fp8_verify_unpack(torch.zeros(16, dtype=torch.uint8, device="cuda"), 1 << 20, 1 << 20)
