@@ -175,6 +175,8 @@ def fp8_verify_unpack_chunks(chunks: List[Tuple[torch.Tensor, int]], block: int 
     dev = chunks[0][0].device
     for packed, src_len in chunks:
         _check_dev(packed, "packed", torch.uint8)
+        if packed.device != dev:
+            raise ValueError("every chunk of one launch must be on the same GPU")
         if src_len <= 0 or src_len % (2 * block):
             raise ValueError("src_len must be a positive multiple of 2 * block")
         need = src_len // 2 + src_len // 2 // block * 4
