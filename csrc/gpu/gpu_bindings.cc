@@ -81,15 +81,6 @@ void register_gpu_bindings(PyObject* module) {
   }, py::arg("data"), py::arg("crc") = 0);
   m.def("crc32c_shift", &crc32c_shift);
   m.def("crc32c_multmodp", &crc32c_multmodp);
-  m.def("read_seg_async", [](uint64_t src, int64_t n, uint64_t out, int blocks, int layout, bool roll,
-                             uint64_t stream) {
-    check(kern::read_seg(reinterpret_cast<const void*>(src), n, reinterpret_cast<uint32_t*>(out), blocks, layout, roll,
-                         as_stream(stream)), "read_seg");
-  });
-  m.def("read_xor_async", [](uint64_t src, int64_t n, uint64_t out, int blocks, int depth, uint64_t stream) {
-    check(kern::read_xor(reinterpret_cast<const void*>(src), n, reinterpret_cast<uint32_t*>(out), blocks, depth,
-                         as_stream(stream)), "read_xor");
-  }, py::arg("src"), py::arg("nbytes"), py::arg("out"), py::arg("blocks"), py::arg("depth") = 4, py::arg("stream") = 0);
   m.def("fill_random_host", [](int64_t n, uint64_t seed, int64_t offset) {
     std::string out(size_t(n), '\0');
     {

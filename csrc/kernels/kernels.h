@@ -6,10 +6,10 @@
 // between workgroups. The hardware's round-robin of workgroups over the 8 XCDs
 // therefore needs no remapping (there is no L2 reuse to keep on one XCD); what
 // matters is enough bytes in flight per CU (HBM latency) and, for CRC32C, the
-// LDS table layout (crc32c.hip). fill and CRC32C size their grids to the CU
-// count (256) times the workgroups a CU holds and grid-stride beyond that;
-// fp8 pack/unpack give every lane one 8-element group (a 64 MiB chunk is
-// 16k workgroups, far more than the chip holds at once).
+// LDS table layout (crc32c.hip). fill sizes its grid to the CU count (256)
+// times the workgroups a CU holds and grid-strides beyond that; the CRC32C
+// grids are described below; fp8 pack/unpack give every lane one 8-element
+// group (a 64 MiB chunk is 16k workgroups, far more than the chip holds at once).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -25,24 +25,18 @@ hipError_t fill_random(void* dst, int64_t bytes, uint64_t seed, hipStream_t s);
 void fill_random_host(void* dst, int64_t bytes, uint64_t seed, int64_t offset = 0);
 // Test helper: hold stream s until *flag != 0 (host-mapped) or max_iters ~3 us sleeps.
 hipError_t spin_until(const uint32_t* flag, uint64_t max_iters, uint64_t* iters, hipStream_t s);
-// Read-bandwidth probe: XOR of [src, src+bytes) into blocks*4 dwords at out
-// (bytes % 16 == 0); `depth` 16-B loads in flight per lane (1, 2, 4, 8).
-hipError_t read_xor(const void* src, int64_t bytes, uint32_t* out, int blocks, int depth, hipStream_t s);
-// Segment-read probe (the CRC kernels' load shape, no compute): 16 KiB per
-// wave, 1024-thread workgroups, `blocks` of them; layout 0 = 64-B lane pieces,
-// 1 = strided 16-B words; roll = prefetch the next segment while consuming.
-// out: blocks * 1024 dwords; bytes % 16384 == 0.
-hipError_t read_seg(const void* src, int64_t bytes, uint32_t* out, int blocks, int layout, bool roll, hipStream_t s);
 
 // ---- crc32c.hip: CRC32C verification (and the fused fp8 unpack) on gfx950.
-// One kernel shape serves every entry point: one 16 KiB segment per wave,
-// 512-thread workgroups, two per CU, and the fold of a chunk's segments done
-// inside the same launch (device-scope atomics on a {acc, count} pair per
-// item in `workspace`; crc32c.hip). A workspace must be zeroed ONCE (e.g.
-// hipMemsetAsync) before its first use; every launch leaves it zeroed again.
-// Launches that share a workspace must be ordered (one stream).
-// `cus`: the CUs the launch's stream may use (a CU-masked verify stream); the
-// grid's last partial round is sized for them. 0 = the whole device.
+// Two kernels: the CRC-only check walks (one 1024-thread workgroup per CU,
+// each a contiguous range of 16 KiB segments), the fused check + unpack runs
+// one segment per wave (512-thread workgroups, two per CU). Both fold a
+// chunk's segments inside the same launch (device-scope atomics on a
+// {acc, count} pair per item in `workspace`; crc32c.hip). A workspace must be
+// zeroed ONCE (e.g. hipMemsetAsync) before its first use; every launch leaves
+// it zeroed again. Launches that share a workspace must be ordered (one stream).
+// `cus`: the CUs the launch's stream may use (a CU-masked verify stream): the
+// walk launches one workgroup per such CU, the fused kernel sizes its grid's
+// last partial round for them. 0 = the whole device.
 //
 // out[c] (device or host-mapped memory) receives the standard CRC32C of chunk
 // c of [src, src+bytes). src 16-B aligned; chunk_bytes a multiple of 16
