@@ -463,6 +463,9 @@ def worker(args, world, rank, chan) -> int:
             vb = last.engine_stats.get("verify_busy_ms")
             if vb is not None and last.seconds > 0:  # occupancy of the verify CUs in the last session
                 out["config"]["verify_busy_frac_rank0"] = round(vb / (last.seconds * 1e3), 3)
+            nck = last.engine_stats.get("verify_chunks")
+            if vb is not None and nck:  # device time of the batched checks per checked chunk
+                out["config"]["verify_us_per_chunk_rank0"] = round(vb * 1e3 / nck, 1)
             st = last.engine_stats.get("bytes_staged")
             if st and last.seconds > 0:  # this rank's host -> HBM rate over the session (PCIe bound: ~57 GB/s)
                 out["config"]["stage_GBps_rank0"] = round(st / last.seconds / 1e9, 2)
