@@ -772,7 +772,10 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
 // filled per 8 segments measured 3.8 TB/s for CRC alone (profiles/r5_verify/);
 // this walk 5.67 TB/s on 1 GiB and 12.6 us per 64 MiB chunk in 16-chunk
 // launches, 0.94-1.0 TB/s on the 32 CUs of the verify stream with peers
-// (profiles/r5_walk/).
+// (profiles/r5_walk/). Issuing the first segment's loads before the table
+// fill (slice_once's order) measured slower here - 28 vs 24 us for a lone
+// chunk, 13.3 vs 12.6 per chunk in a batch (verify_bench_*loads_before_fill):
+// the fill's own table loads then wait behind them in the in-order vmcnt.
 // The fold: a wave accumulates its values while its item does not change and
 // hands each run to the workgroup's LDS slot of that item (ds atomics); at
 // the end the workgroup adds one value per item to the global {acc, count}
