@@ -365,6 +365,11 @@ __device__ __forceinline__ void lds_barrier() {
 // in 160 us where one-segment waves took 139 and a plain one-shot grid 131
 // (bin/walkprobe, profiles/r4_walk*/). A CU streams many short-lived waves
 // instead, and the table fill is paid per workgroup of WAVES segments.
+// (The fill's own table reads, issued after the data loads, can only be
+// waited for together with them; reading the tables into registers first and
+// storing them after the data loads measured the same - 17.9 vs 18.0 us per
+// 64 MiB chunk batched, profiles/r5_fill_order/: the CU's other workgroup
+// already covers the fill.)
 // Returns the segment's value at its chunk's end (to_chunk_end).
 template <class Geo, class Visit, int R, int WAVES>
 __device__ __forceinline__ uint32_t slice_once(const Geo& geo, int64_t g, bool have, const uint32_t* __restrict__ sc,
