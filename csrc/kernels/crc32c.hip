@@ -781,6 +781,9 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
 // fill (slice_once's order) measured slower here - 28 vs 24 us for a lone
 // chunk, 13.3 vs 12.6 per chunk in a batch (verify_bench_*loads_before_fill):
 // the fill's own table loads then wait behind them in the in-order vmcnt.
+// Reading the tables into registers first, then the segment, then storing
+// the tables, measured neutral: 25.9 us lone, 12.6 batched, 5.78 TB/s on
+// 1 GiB (profiles/r5_fill_order/).
 // The fold: a wave accumulates its values while its item does not change and
 // hands each run to the workgroup's LDS slot of that item (ds atomics); at
 // the end the workgroup adds one value per item to the global {acc, count}
