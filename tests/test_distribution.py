@@ -358,11 +358,11 @@ def test_mode2_host_engine_keeps_the_fastest_source(core, tmp_path):
         peer = c.node(2, 2, {5: core.LayerSrc.inmem(data)})
         peer.announce()
         wait_status(leader, 2)  # the session starts once the dest (the only Assignment key) announces
-        t0 = time.time()
         exec_distribution(leader, [dest], assignment)
         assert peer.wait_ready(5.0)
         assert dest.layer(5).host_bytes() == data
-        assert time.time() - t0 < 0.4  # a disk load would take ~0.27 s + the startup
+        # the bytes came over the peer's connection, none from the dest's own disk
+        # (byte counters, not wall time: a timing bound flaked under parallel test load)
         assert c.ts[2].bytes_sent >= size and c.ts[1].bytes_sent == 0
     finally:
         c.close()
