@@ -406,17 +406,13 @@ PYBIND11_MODULE(_core, m) {
   });
   // token bucket (core/ratelimit.h): pace `total` bytes at `rate` B/s; returns
   // (seconds elapsed, piece sizes) - unit-test hook
+  // The pacing schedule of `total` bytes on a virtual clock: (seconds the
+  // bucket made the caller wait, piece sizes) - exact, whatever the host load.
   m.def("token_bucket_pace", [](int64_t total, int64_t rate, int64_t burst) {
     std::vector<int64_t> pieces;
-    double secs;
-    {
-      py::gil_scoped_release nogil;
-      TokenBucket tb(rate, burst);
-      auto t0 = std::chrono::steady_clock::now();
-      tb.paced(total, [&](int64_t, int64_t n) { pieces.push_back(n); });
-      secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    }
-    return py::make_tuple(secs, pieces);
+    BasicTokenBucket<VirtualClock> tb(rate, burst);
+    tb.paced(total, [&](int64_t, int64_t n) { pieces.push_back(n); });
+    return py::make_tuple(tb.clock().now(), pieces);
   }, py::arg("total"), py::arg("rate"), py::arg("burst") = TokenBucket::kDefaultBurst);
   // fp8 wire/storage format (core/fp8.h), host reference
   m.def("fp8_packed_size", &fp8::packed_size, py::arg("src_bytes"), py::arg("src_chunk"), py::arg("block") = 128);

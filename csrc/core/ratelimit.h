@@ -13,17 +13,33 @@
 
 namespace dissem {
 
-class TokenBucket {
+// The bucket's clock: real time and a real sleep for the data paths, or a
+// virtual clock whose sleep advances it (tests: exact, host-load independent).
+struct SteadyClock {
+  double now() const {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void sleep(double secs) { std::this_thread::sleep_for(std::chrono::duration<double>(secs)); }
+};
+struct VirtualClock {
+  double t = 0;
+  double now() const { return t; }
+  void sleep(double secs) { t += secs; }
+};
+
+template <class Clock = SteadyClock>
+class BasicTokenBucket {
  public:
   static constexpr int64_t kDefaultBurst = 256 * 1024;
 
-  explicit TokenBucket(int64_t rate_bps, int64_t burst = kDefaultBurst)
-      : rate_(rate_bps), burst_(std::max<int64_t>(burst, 1)), tokens_(double(burst_)),
-        last_(std::chrono::steady_clock::now()) {}
+  explicit BasicTokenBucket(int64_t rate_bps, int64_t burst = kDefaultBurst, Clock clock = Clock())
+      : rate_(rate_bps), burst_(std::max<int64_t>(burst, 1)), tokens_(double(burst_)), clock_(clock),
+        last_(clock_.now()) {}
 
   bool unlimited() const { return rate_ <= 0; }
   int64_t burst() const { return burst_; }
   int64_t rate() const { return rate_; }
+  const Clock& clock() const { return clock_; }
 
   // Blocks until n bytes may pass (n <= burst is the intended use).
   void wait(int64_t n) {
@@ -31,8 +47,7 @@ class TokenBucket {
     refill();
     tokens_ -= double(n);
     if (tokens_ < 0) {
-      double secs = -tokens_ / double(rate_);
-      std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+      clock_.sleep(-tokens_ / double(rate_));
       refill();
     }
   }
@@ -52,15 +67,18 @@ class TokenBucket {
 
  private:
   void refill() {
-    auto now = std::chrono::steady_clock::now();
-    double dt = std::chrono::duration<double>(now - last_).count();
+    const double now = clock_.now();
+    const double dt = now - last_;
     last_ = now;
     tokens_ = std::min(double(burst_), tokens_ + dt * double(rate_));
   }
   int64_t rate_;
   int64_t burst_;
   double tokens_;
-  std::chrono::steady_clock::time_point last_;
+  Clock clock_;
+  double last_;
 };
+
+using TokenBucket = BasicTokenBucket<>;
 
 }  // namespace dissem
