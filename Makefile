@@ -29,7 +29,7 @@ HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Icsrc -I$(ROCM)/includ
              -fvisibility=hidden
 LDFLAGS   := -shared -L$(TORCHLIB) -Wl,-rpath,$(TORCHLIB) -lamdhip64 -lrccl -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrocprofiler-sdk-roctx -lpthread
 
-CORE_SRC  := csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/core/fp8.cc csrc/core/trace.cc csrc/transport/inproc.cc \
+CORE_SRC  := csrc/core/vclock.cc csrc/core/json.cc csrc/core/log.cc csrc/core/wire.cc csrc/core/crc32c.cc csrc/core/fp8.cc csrc/core/trace.cc csrc/transport/inproc.cc \
              csrc/transport/tcp.cc csrc/store/store.cc csrc/sched/maxflow.cc csrc/sched/lp.cc csrc/roles/node.cc \
              csrc/roles/mode01.cc csrc/roles/mode2.cc csrc/roles/mode3.cc csrc/roles/multihost.cc \
              csrc/roles/recovery.cc csrc/roles/dispatch.cc \

@@ -11,6 +11,7 @@
 #include "core/log.h"
 #include "core/ratelimit.h"
 #include "core/trace.h"
+#include "core/vclock.h"
 #include "core/wire.h"
 #include "engine/engine.h"
 #include "engine/planned_engine.h"
@@ -25,6 +26,31 @@ namespace py = pybind11;
 using namespace dissem;
 
 namespace {
+
+// Barrier for the threads of an in-process simulation (a threading.Barrier
+// would hold a clock-counted thread busy and stop model time).
+class VBarrier {
+ public:
+  explicit VBarrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const uint64_t gen = gen_;
+    if (++count_ >= n_) {
+      count_ = 0;
+      ++gen_;
+      lk.unlock();
+      cv_.notify_all();
+      return;
+    }
+    cv_.wait(lk, [&] { return gen_ != gen; });
+  }
+
+ private:
+  std::mutex mu_;
+  CondVar cv_;
+  int n_, count_ = 0;
+  uint64_t gen_ = 0;
+};
 
 std::shared_ptr<HostBuffer> buffer_from_py(const py::object& obj) {
   py::buffer buf = py::reinterpret_borrow<py::buffer>(obj);
@@ -390,6 +416,36 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("wait_s", &SimTiming::wait_s)
       .def_readwrite("recv_delay_s", &SimTiming::recv_delay_s);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
+  // Virtual clock (core/vclock.h): the simulator in model time. Python threads
+  // that drive a session's ranks are counted by the clock between adopt() and
+  // release() (reserve first, from the thread that starts them).
+  m.def("vclock_enable", [](bool on) { vclock::enable(on); });
+  m.def("vclock_enabled", &vclock::enabled);
+  m.def("vclock_now", &vclock::now, "seconds: model time when the virtual clock is on, else the steady clock");
+  m.def("vclock_reserve", &vclock::reserve, py::arg("n"));
+  m.def("vclock_adopt", [] { vclock::adopt("python"); });
+  m.def("vclock_release", &vclock::release);
+  m.def("vclock_sleep", [](double s) {
+    py::gil_scoped_release nogil;
+    vclock::sleep_for(s);
+  });
+  m.def("vclock_stats", [] {
+    auto st = vclock::stats();
+    py::dict d;
+    d["t"] = st.t;
+    d["busy"] = st.busy;
+    d["blocked"] = st.blocked;
+    d["timers"] = st.timers;
+    d["advances"] = st.advances;
+    return d;
+  });
+  m.def("vclock_describe", &vclock::describe);
+  py::class_<VBarrier, std::shared_ptr<VBarrier>>(m, "VBarrier", "a thread barrier that waits in model time")
+      .def(py::init<int>())
+      .def("wait", [](VBarrier& b) {
+        py::gil_scoped_release nogil;
+        b.wait();
+      });
   m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
   m.def("sim_read", [](uint64_t ptr, int64_t n) {
     return py::bytes(reinterpret_cast<const char*>(ptr), size_t(n));

@@ -10,6 +10,8 @@
 #include <mutex>
 #include <optional>
 
+#include "core/vclock.h"
+
 namespace dissem {
 
 // Timed condition wait on a system_clock deadline. libstdc++ lowers
@@ -21,6 +23,11 @@ bool cv_wait_for(std::condition_variable& cv, Lock& lk, double seconds, Pred pre
   auto dl = std::chrono::system_clock::now() +
             std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(seconds));
   return cv.wait_until(lk, dl, pred);
+}
+// The same on a CondVar (model time when the virtual clock is on).
+template <class Pred>
+bool cv_wait_for(CondVar& cv, std::unique_lock<std::mutex>& lk, double seconds, Pred pred) {
+  return cv.wait_for_s(lk, seconds, pred);
 }
 
 template <class T>
@@ -78,7 +85,7 @@ class BlockingQueue {
 
  private:
   mutable std::mutex mu_;
-  std::condition_variable cv_;
+  CondVar cv_;
   std::deque<T> q_;
   bool closed_ = false;
 };

@@ -11,15 +11,16 @@
 #include <cstdint>
 #include <thread>
 
+#include "core/vclock.h"
+
 namespace dissem {
 
-// The bucket's clock: real time and a real sleep for the data paths, or a
-// virtual clock whose sleep advances it (tests: exact, host-load independent).
+// The bucket's clock: the process clock (real time, or the simulator's model
+// time when core/vclock.h is on), or a private virtual clock whose sleep
+// advances it (unit tests: exact, host-load independent).
 struct SteadyClock {
-  double now() const {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-  }
-  void sleep(double secs) { std::this_thread::sleep_for(std::chrono::duration<double>(secs)); }
+  double now() const { return vclock::now(); }
+  void sleep(double secs) { vclock::sleep_for(secs); }
 };
 struct VirtualClock {
   double t = 0;

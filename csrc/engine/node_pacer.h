@@ -24,6 +24,8 @@
 #include <string>
 #include <thread>
 
+#include "core/vclock.h"
+
 namespace dissem {
 
 class NodePacer {
@@ -52,6 +54,7 @@ class NodePacer {
   NodePacer& operator=(const NodePacer&) = delete;
 
   static int64_t now_ns() {
+    if (vclock::enabled()) return int64_t(vclock::now() * 1e9);  // simulated node: model time
     timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return int64_t(ts.tv_sec) * 1000000000ll + ts.tv_nsec;
@@ -67,7 +70,7 @@ class NodePacer {
       start = cur > now ? cur : now;
     } while (!next_->compare_exchange_weak(cur, start + dur, std::memory_order_acq_rel, std::memory_order_relaxed));
     const int64_t wait = start - now;
-    if (wait > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(wait));
+    if (wait > 0) vclock::sleep_for(double(wait) * 1e-9);
     return wait > 0 ? wait : 0;
   }
 

@@ -57,9 +57,8 @@ void dump_stack_handler(int) {
   backtrace_symbols_fd(frames, n, 2);
 }
 
-size_t log2_bucket(std::chrono::steady_clock::time_point since) {
-  const int64_t us =
-      std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - since).count();
+size_t log2_bucket(double since) {
+  const int64_t us = int64_t((vclock::now() - since) * 1e6);
   size_t b = 0;
   while (b < 31 && (int64_t(1) << (b + 1)) <= us) ++b;
   return b;
@@ -95,23 +94,23 @@ PlannedEngine::PlannedEngine(const PlannedConfig& cfg, std::unique_ptr<Backend> 
   stats_.lane_connect_ms = backend_->lane_connect_ms();
   for (int r = 0; r < cfg_.world; ++r) node_rank_[cfg_.rank_nodes[size_t(r)]] = r;
   self_node_ = cfg_.rank_nodes[size_t(cfg_.rank)];
-  th_ = std::thread([this] { run(); });
-  monitor_ = std::thread([this] { monitor_loop(); });
+  th_ = vclock::spawn([this] { run(); }, "engine-issue");
+  monitor_ = vclock::spawn([this] { monitor_loop(); }, "engine-monitor");
 }
 
 void PlannedEngine::monitor_loop() {
   int64_t reported = 0;
   while (!stop_req_) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    vclock::sleep_for(0.25);
     {
       // the issue thread loops every ~20 us while it has work: a loop counter that
       // stands still for 5 s means it is stuck outside any marked backend call
       const int64_t t = loop_ticks_.load();
-      const auto now = std::chrono::steady_clock::now();
+      const double now = vclock::now();
       if (t != last_ticks_) {
         last_ticks_ = t;
         ticks_since_ = now;
-      } else if (now - ticks_since_ > std::chrono::seconds(5) && !call_what_.load() && !idle_flag_.load()) {
+      } else if (now - ticks_since_ > 5.0 && !call_what_.load() && !idle_flag_.load()) {
         ticks_since_ = now;
         log::warn(int64_t(self_node_)).i("loop_ticks", t).msg("issue thread not looping (stuck outside backend calls)");
         if (!stack_dumped_ && getenv("DISSEM_STACK_DUMP")) {
@@ -393,7 +392,7 @@ void PlannedEngine::run_probe(ProbeJob& job) {
     bool done = false;
   };
   std::vector<G> groups;
-  const auto t0 = std::chrono::steady_clock::now();
+  const double t0 = vclock::now();
   for (auto& kv : by_lane) {
     std::vector<XOp> xops;
     for (size_t i : kv.second) {
@@ -410,7 +409,7 @@ void PlannedEngine::run_probe(ProbeJob& job) {
   }
   size_t left = groups.size();
   while (left > 0) {
-    const auto now = std::chrono::steady_clock::now();
+    const double now = vclock::now();
     for (auto& g : groups) {
       if (g.done) continue;
       const int r = backend_->query(g.ev);
@@ -418,15 +417,15 @@ void PlannedEngine::run_probe(ProbeJob& job) {
       g.done = true;
       --left;
       double ms = r > 0 ? backend_->group_ms(g.ev) : -1;
-      if (r > 0 && ms < 0) ms = std::chrono::duration<double, std::milli>(now - t0).count();
+      if (r > 0 && ms < 0) ms = (now - t0) * 1e3;
       for (size_t i : g.ops) {
         job.ops[i].done = r > 0;
         job.ops[i].ms = ms;
       }
       backend_->release(g.ev);
     }
-    if (left == 0 || std::chrono::duration<double>(now - t0).count() > job.timeout_s) break;
-    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (left == 0 || now - t0 > job.timeout_s) break;
+    vclock::sleep_for(200e-6);
   }
   if (left == 0) {
     for (uint8_t* b : bufs) backend_->free(b);
@@ -466,7 +465,7 @@ void PlannedEngine::set_chunk_ev(Layer& L, int64_t c, Ev e) {
 // is exactly `rate`.
 bool PlannedEngine::pace_ready(uint64_t key, int64_t rate, int64_t n) {
   if (rate <= 0) return true;
-  const auto now = std::chrono::steady_clock::now();
+  const double now = vclock::now();
   Pace& p = pace_[key];
   // Mode-3 job buckets hold two chunks: the plan runs every link at exactly its
   // capacity (size/T per job), so a job held back behind staging or its lane
@@ -482,7 +481,7 @@ bool PlannedEngine::pace_ready(uint64_t key, int64_t rate, int64_t n) {
   }
   p.rate = double(rate);
   p.burst = std::max(p.burst, cap);
-  p.tokens = std::min(p.burst, p.tokens + std::chrono::duration<double>(now - p.last).count() * p.rate);
+  p.tokens = std::min(p.burst, p.tokens + (now - p.last) * p.rate);
   p.last = now;
   return p.tokens >= double(n) - 0.5;
 }
@@ -594,7 +593,7 @@ bool PlannedEngine::issue_lane(int lane) {
   bool progress = false;
   auto& q = ops_[size_t(lane)];
   auto& infl = inflight_[size_t(lane)];
-  const auto now = std::chrono::steady_clock::now();
+  const double now = vclock::now();
   const int cap = std::max(4, cfg_.max_inflight_groups / lanes_);
   while (!q.empty() && int(infl.size()) < cap && !failed_) {
     std::vector<Piece> group;
@@ -786,7 +785,7 @@ bool PlannedEngine::issue_lane(int lane) {
 
 void PlannedEngine::poll() {
   flush_checks();  // what was staged since the issue pass: batched checks
-  const auto now = std::chrono::steady_clock::now();
+  const double now = vclock::now();
   for (int lane = 0; lane < lanes_; ++lane) {
     auto& infl = inflight_[size_t(lane)];
     while (!infl.empty()) {
@@ -797,9 +796,8 @@ void PlannedEngine::poll() {
         // block its lane forever. Report the in-flight peers to the leader
         // (which probes them and shrinks the communicator around a dead one);
         // fail if nothing resolves it.
-        double age = std::chrono::duration<double>(now - head.t0).count();
-        if (node_ && cfg_.suspect_s > 0 && age > cfg_.suspect_s &&
-            now - last_suspect_ > std::chrono::duration<double>(std::max(cfg_.suspect_s, 1.0))) {
+        double age = now - head.t0;
+        if (node_ && cfg_.suspect_s > 0 && age > cfg_.suspect_s && now - last_suspect_ > std::max(cfg_.suspect_s, 1.0)) {
           // Not (yet) a failure: if the peers are alive the group may still
           // complete. Name every in-flight peer: the group at the head may be
           // waiting on a live rank that itself waits on the dead one.
@@ -988,7 +986,7 @@ void PlannedEngine::take_requests(bool block) {
 void PlannedEngine::run() {
   try {
     backend_->init_thread();
-    auto last_async_check = std::chrono::steady_clock::now();
+    double last_async_check = vclock::now();
     while (!stop_req_) {
       take_requests(idle());
       if (stop_req_) break;
@@ -1010,7 +1008,7 @@ void PlannedEngine::run() {
         reqs_.clear();
         busy_ = false;
         idle_cv_.notify_all();
-        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        vclock::sleep_for(0.005);
         continue;
       }
       loop_ticks_.fetch_add(1, std::memory_order_relaxed);
@@ -1019,15 +1017,15 @@ void PlannedEngine::run() {
       bool progress = issue_some();
       poll();
       if (recovering_ && cfg_.group_timeout_s > 0 &&
-          std::chrono::steady_clock::now() - recover_since_ > std::chrono::duration<double>(cfg_.group_timeout_s))
+          vclock::now() - recover_since_ > cfg_.group_timeout_s)
         fail("data plane stalled and the leader did not shrink the communicator");
       {
         std::lock_guard<std::mutex> lk(req_mu_);
         busy_ = !idle() || !reqs_.empty();
         if (!busy_) idle_cv_.notify_all();
       }
-      auto now = std::chrono::steady_clock::now();
-      if (now - last_async_check > std::chrono::milliseconds(100)) {
+      const double now = vclock::now();
+      if (now - last_async_check > 0.1) {
         last_async_check = now;
         std::string e = backend_->async_error();
         if (!e.empty() && !recovering_) {
@@ -1044,12 +1042,12 @@ void PlannedEngine::run() {
       if (progress || completions_ != quiet_mark_ || idle()) {
         quiet_mark_ = completions_;
         quiet_since_ = now;
-      } else if (cfg_.suspect_s > 0 && now - quiet_since_ > std::chrono::duration<double>(cfg_.suspect_s)) {
+      } else if (cfg_.suspect_s > 0 && now - quiet_since_ > cfg_.suspect_s) {
         quiet_since_ = now;
         log::warn(int64_t(self_node_)).s("state", describe_stall()).f("quiet_s", cfg_.suspect_s)
             .msg("data plane waiting: no group issued or completed");
       }
-      if (!progress && !idle()) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if (!progress && !idle()) vclock::sleep_for(20e-6);
     }
   } catch (const std::exception& e) {
     fail(e.what());

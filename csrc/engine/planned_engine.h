@@ -42,6 +42,7 @@
 #include <tuple>
 #include <vector>
 
+#include "core/vclock.h"
 #include "engine/backend.h"
 #include "engine/engine.h"
 #include "engine/node_pacer.h"
@@ -287,7 +288,7 @@ class PlannedEngine : public DataEngine {
   };
   struct Verify {  // landing (recv group or staging copy) awaiting its check
     Ev ev = 0;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    double t0 = vclock::now();
     std::vector<Piece> pieces;
     std::vector<uint32_t> slots;  // CRC result slots, ~0u = not verified
   };
@@ -298,7 +299,7 @@ class PlannedEngine : public DataEngine {
     uint32_t slot = ~0u;        // result slot, ~0u = not verified
     bool has_req = false;       // a check (plain or fused) to launch; else only the landing to wait for
     Backend::CheckReq req{};
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    double t0 = vclock::now();
   };
   struct DiskRead {  // chunk of a disk-tier layer: pread into a bounce buffer, then H2D
     LayerID layer;
@@ -326,14 +327,14 @@ class PlannedEngine : public DataEngine {
   void run_probe(ProbeJob& job);
   struct Inflight {  // a P2P group on a comm lane
     Ev ev;
-    std::chrono::steady_clock::time_point t0;
+    double t0;
     std::vector<int> peers;  // partner ranks
     std::vector<int> send_peers;  // ranks it sends to (point-to-point)
     std::vector<int> recv_peers;  // ranks it receives from (point-to-point)
   };
   struct Pace {  // token bucket, non-blocking (burst: one chunk; mode-3 jobs two, see pace_ready)
     double rate = 0, tokens = 0, burst = 0;
-    std::chrono::steady_clock::time_point last{};
+    double last = 0;
   };
 
   void run();
@@ -404,7 +405,7 @@ class PlannedEngine : public DataEngine {
   uint32_t crc_next_ = 0;
 
   std::mutex req_mu_;
-  std::condition_variable req_cv_, idle_cv_;
+  CondVar req_cv_, idle_cv_;
   std::deque<Req> reqs_;
   bool busy_ = false;
   uint64_t resets_done_ = 0;
@@ -427,7 +428,7 @@ class PlannedEngine : public DataEngine {
   std::map<Ev, int> evref_;
   std::map<uint64_t, Pace> pace_;
   bool recovering_ = false;  // issue thread: waiting for the leader's Shrink
-  std::chrono::steady_clock::time_point recover_since_, last_suspect_;
+  double recover_since_ = 0, last_suspect_ = -1e300;  // vclock::now() seconds
   int64_t groups_issued_ = 0;
   std::atomic<bool> dead_{false};  // fault injection: this rank "crashed"
 
@@ -436,7 +437,7 @@ class PlannedEngine : public DataEngine {
   std::deque<std::pair<Ev, uint8_t*>> bounce_busy_;  // H2D copy event -> its bounce buffer
   std::deque<DiskRead> disk_wait_;                 // waiting for a bounce buffer
   std::mutex disk_mu_;
-  std::condition_variable disk_cv_;
+  CondVar disk_cv_;
   std::deque<DiskRead> disk_todo_, disk_done_;
   std::vector<std::thread> readers_;
   int disk_inflight_ = 0;
@@ -461,17 +462,16 @@ class PlannedEngine : public DataEngine {
     }
     ~CallMark() { e->call_what_ = nullptr; }
     static int64_t now_us() {
-      return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
-          .count();
+      return vclock::now_us();
     }
   };
   std::atomic<int64_t> loop_ticks_{0};  // issue-thread loop iterations (monitor: liveness)
   std::atomic<bool> idle_flag_{true};
   int64_t last_ticks_ = -1;             // monitor thread only
   bool stack_dumped_ = false;           // monitor thread only (DISSEM_STACK_DUMP)
-  std::chrono::steady_clock::time_point ticks_since_ = std::chrono::steady_clock::now();
+  double ticks_since_ = vclock::now();
   int64_t completions_ = 0, quiet_mark_ = 0;  // completed groups; the count at the last progress check
-  std::chrono::steady_clock::time_point quiet_since_ = std::chrono::steady_clock::now();
+  double quiet_since_ = vclock::now();
   std::atomic<const char*> call_what_{nullptr};
   std::atomic<int64_t> call_since_us_{0};
   std::atomic<int> call_lane_{0};

@@ -64,7 +64,7 @@ std::string PlannedEngine::describe_stall() const {
 void PlannedEngine::suspect(const std::vector<int>& peers, const std::string& why, bool broken) {
   if (broken && !recovering_) {
     recovering_ = true;  // the communicator is unusable until the Shrink
-    recover_since_ = std::chrono::steady_clock::now();
+    recover_since_ = vclock::now();
   }
   Message m;
   m.type = MsgType::Suspect;

@@ -161,7 +161,7 @@ void PlannedEngine::submit_disk(Layer& L, LayerID id, int64_t c) {
       bounce_all_.push_back(b);
       bounce_free_.push_back(b);
     }
-    for (int i = 0; i < std::max(1, cfg_.disk_readers); ++i) readers_.emplace_back([this] { reader_loop(); });
+    for (int i = 0; i < std::max(1, cfg_.disk_readers); ++i) readers_.push_back(vclock::spawn([this] { reader_loop(); }, "disk-reader"));
   }
   L.st[size_t(c)] = 3;
   DiskRead d;

@@ -14,6 +14,11 @@
 // len / stage_bps. With copy_bytes = false no payload moves (timing-only runs
 // of full-size schedules in little memory). Multi-host fabrics (host, nic_bps)
 // also charge a cross-host transfer to both ends' NICs.
+//
+// Every time here is vclock::now(): with the virtual clock on (core/vclock.h)
+// the queues below wait in model time and a session's length is its modeled
+// makespan, the same on every run and any host load; off, they sleep the
+// modeled times on the wall clock.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -30,6 +35,7 @@
 #include "core/crc32c.h"
 #include "core/fp8.h"
 #include "core/queue.h"
+#include "core/vclock.h"
 #include "engine/backend.h"
 #include "engine/planned_engine.h"
 
@@ -40,32 +46,39 @@ namespace {
 struct SimEvent {
   std::atomic<int> state{0};  // 0 pending, 1 done, -1 failed
   double ms = -1;             // groups: time on the lane from dependencies met to completion
+  std::mutex mu;
+  CondVar cv;                 // state left 0 (queues waiting on it as a dependency)
+  void set(int st) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      state = st;
+    }
+    cv.notify_all();
+  }
 };
-
-using Clock = std::chrono::steady_clock;
 
 struct Posted {
   uint8_t* ptr;
   int64_t len;
   bool done = false;
   bool bad = false;
-  Clock::time_point done_at{};  // timing model: when the link finishes this transfer
-  Clock::time_point posted = Clock::now();
+  double done_at = 0;               // timing model: when the link finishes this transfer (vclock::now() s)
+  double posted = vclock::now();
   double injected_s = 0;  // fault injection: this post came that late (SimTiming::recv_delay_s)
   double model_s = 0;     // modeled device time of the op (see Fabric::post)
 };
 
 struct Fabric {
   std::mutex mu;
-  std::condition_variable cv;
+  CondVar cv;
   bool aborted = false;  // a survivor shrank this communicator: every wait fails now
   // (lane, src, dst) -> sends, recvs
   std::map<std::tuple<int, int, int>, std::pair<std::deque<Posted*>, std::deque<Posted*>>> ch;
   SimFabricStats stats;
   std::set<int> crashed;  // fault injection: ranks whose posts no longer move bytes
   SimTiming timing;
-  std::map<std::pair<int, int>, Clock::time_point> link_free;  // timing model: directed link busy until
-  std::map<int, Clock::time_point> nic_out_free, nic_in_free;   // timing model: per-rank NIC busy until
+  std::map<std::pair<int, int>, double> link_free;  // timing model: directed link busy until
+  std::map<int, double> nic_out_free, nic_in_free;   // timing model: per-rank NIC busy until
 
   double link_rate(int src, int dst) const {
     auto it = timing.link.find({src, dst});
@@ -107,8 +120,8 @@ struct Fabric {
           // The transfer is done when its last queue is.
           // both ends posted: the transfer may start (timed from the posts
           // themselves, not from when this thread got the fabric's lock)
-          const auto now = std::max(s->posted, r->posted);
-          const auto dur = std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(s->len) / bps));
+          const double now = std::max(s->posted, r->posted);
+          const double dur = double(s->len) / bps;
           auto& free_at = link_free[{src, dst}];
           free_at = std::max(now, free_at) + dur;
           auto done = free_at;
@@ -127,7 +140,7 @@ struct Fabric {
           // its receive. How late the simulator's own threads got to either
           // post never enters it, so rates derived from it (the closed loop's
           // busy throughput) are the same on an idle or a loaded host.
-          const double span = std::chrono::duration<double>(done - std::max(s->posted, r->posted)).count();
+          const double span = done - std::max(s->posted, r->posted);
           s->model_s = span + r->injected_s;
           r->model_s = span;
         }
@@ -174,13 +187,13 @@ struct Fabric {
       return true;
     });
     if (!ok || aborted) return false;
-    Clock::time_point until{};
+    double until = 0;
     for (auto& o : ops) {
       if (o->bad) return false;
       until = std::max(until, o->done_at);
     }
     lk.unlock();
-    std::this_thread::sleep_until(until);  // the links are still moving these bytes
+    vclock::sleep_until(until);  // the links are still moving these bytes
     return true;
   }
 };
@@ -222,7 +235,7 @@ std::shared_ptr<Fabric> fabric(const std::string& key, const Fabric* inherit = n
 
 class Queue {
  public:
-  Queue() : th_([this] { loop(); }) {}
+  Queue() : th_(vclock::spawn([this] { loop(); }, "sim-queue")) {}
   ~Queue() { stop(); }
   void push(std::function<void()> fn) {
     {
@@ -266,18 +279,15 @@ class Queue {
     }
   }
   std::mutex mu_;
-  std::condition_variable cv_;
+  CondVar cv_;
   std::deque<std::function<void()>> q_;
   bool stop_ = false, running_ = false;
   std::thread th_;
 };
 
 bool wait_event(const std::shared_ptr<SimEvent>& e, double timeout_s) {
-  auto dl = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
-  while (e->state.load() == 0) {
-    if (std::chrono::steady_clock::now() > dl) return false;
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
-  }
+  std::unique_lock<std::mutex> lk(e->mu);
+  e->cv.wait_for_s(lk, timeout_s, [&] { return e->state.load() != 0; });
   return e->state.load() > 0;
 }
 
@@ -308,21 +318,19 @@ class SimBackend : public Backend {
   }
 
   // Staging occupies the copy queue for n / stage_bps (timing model).
-  void stage_delay(Clock::time_point t0, int64_t n) {
+  void stage_delay(double t0, int64_t n) {
     const double bps = fab_->timing.stage_bps;
-    if (bps > 0)
-      std::this_thread::sleep_until(
-          t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(double(n) / bps)));
+    if (bps > 0) vclock::sleep_until(t0 + double(n) / bps);
   }
 
   Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {
     auto [id, ev] = make_event();
     const bool copy = fab_->timing.copy_bytes;
     copy_.push([=] {
-      const auto t0 = Clock::now();
+      const double t0 = vclock::now();
       if (copy) memcpy(dst, src, size_t(n));
       stage_delay(t0, n);
-      ev->state = 1;
+      ev->set(1);
     });
     return id;
   }
@@ -331,11 +339,11 @@ class SimBackend : public Backend {
     auto [id, ev] = make_event();
     const bool copy = fab_->timing.copy_bytes;
     copy_.push([=] {
-      const auto t0 = Clock::now();
+      const double t0 = vclock::now();
       const int64_t n = n_src / 2;
       if (copy) fp8::pack_host(reinterpret_cast<const uint16_t*>(src), n, dst, reinterpret_cast<float*>(dst + n), block);
       stage_delay(t0, n_src);
-      ev->state = 1;
+      ev->set(1);
     });
     return id;
   }
@@ -345,14 +353,14 @@ class SimBackend : public Backend {
     comm_.at(size_t(lane))->push([=] {
       const uint32_t pat = 0xA5A5A5A5u;
       memcpy(p, &pat, 4);
-      ev->state = 1;
+      ev->set(1);
     });
     return id;
   }
 
   Ev mark(int lane) override {
     auto [id, ev] = make_event();
-    comm_.at(size_t(lane))->push([=] { ev->state = 1; });
+    comm_.at(size_t(lane))->push([=] { ev->set(1); });
     return id;
   }
 
@@ -368,7 +376,7 @@ class SimBackend : public Backend {
         if (!d || !wait_event(d, fab->timing.wait_s)) {
           set_error(std::string("group dependency failed: event ") + std::to_string(waits[i]) +
                     (d ? (d->state.load() < 0 ? " failed" : " timed out") : " was already released"));
-          ev->state = -1;
+          ev->set(-1);
           return;
         }
       }
@@ -376,7 +384,7 @@ class SimBackend : public Backend {
       if (auto rd = fab->timing.recv_delay_s.find(rank); rd != fab->timing.recv_delay_s.end() && rd->second > 0)
         for (auto& o : ops)
           if (!o.send && !o.bcast) {
-            std::this_thread::sleep_for(std::chrono::duration<double>(rd->second));
+            vclock::sleep_for(rd->second);
             injected = rd->second;
             break;
           }
@@ -420,7 +428,7 @@ class SimBackend : public Backend {
         }
         if (o.peer < 0 || o.peer >= world_ || o.peer == rank) {
           set_error("bad peer");
-          ev->state = -1;
+          ev->set(-1);
           return;
         }
         posted.push_back(mk(o));
@@ -439,7 +447,7 @@ class SimBackend : public Backend {
       if (!fab->wait_all(posted, fab->timing.wait_s)) {
         fab->cancel(posted);
         set_error("P2P group did not complete (deadlock or size mismatch)");
-        ev->state = -1;
+        ev->set(-1);
         return;
       }
       // The group's device time: its longest op in the model (ops of one group
@@ -447,7 +455,7 @@ class SimBackend : public Backend {
       double ms = 0;
       for (auto& p : posted) ms = std::max(ms, p->model_s * 1e3);
       ev->ms = ms;
-      ev->state = 1;
+      ev->set(1);
     });
     return id;
   }
@@ -466,7 +474,7 @@ class SimBackend : public Backend {
     verify_.push([=] {
       for (auto& d : deps)
         if (!d || !wait_event(d, fab_->timing.wait_s)) {
-          ev->state = -1;
+          ev->set(-1);
           return;
         }
       for (const CheckReq& r : reqs) {
@@ -480,7 +488,7 @@ class SimBackend : public Backend {
         if (copy)
           fp8::unpack_host(r.p, reinterpret_cast<const float*>(r.p + n), n, reinterpret_cast<uint16_t*>(r.out), r.block);
       }
-      ev->state = 1;
+      ev->set(1);
     });
     return id;
   }

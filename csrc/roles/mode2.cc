@@ -174,7 +174,7 @@ bool Node::assign_new_job(NodeID node) {
   if (rarest_own_job(node, &layer, &key)) {
     Job& j = jobs_[layer][key];
     j.state = JobState::Sending;
-    j.t_us = log::now_us();
+    j.t_us = vclock::now_us();
     load_[node] = std::max<int64_t>(0, load_[node] - 1);
     inflight_[node]++;
     log::debug(int64_t(cfg_.id)).u("node", node).u("dest", key.first).u("layer", layer).i("offset", key.second)
@@ -189,7 +189,7 @@ bool Node::assign_new_job(NodeID node) {
     Job& j = jobs_[layer][key];
     j.sender = node;
     j.state = JobState::Sending;
-    j.t_us = log::now_us();
+    j.t_us = vclock::now_us();
     inflight_[node]++;
     dispatch_range(layer, node, key.first, key.second, j.size);
     return true;

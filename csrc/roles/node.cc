@@ -92,14 +92,14 @@ Node::~Node() {
 
 void Node::start() {
   if (running_.exchange(true)) return;
-  loop_th_ = std::thread([this] { loop(); });
+  loop_th_ = vclock::spawn([this] { loop(); }, "node-loop");
   if (is_leader_) {
     // A leader whose assignment names only itself gets no announce: check once at start.
     auto m = std::make_shared<Message>();
     m->type = MsgType::Tick;
     m->epoch = cfg_.epoch;
     t_->inject(m);
-    if (cfg_.job_timeout_s > 0) tick_th_ = std::thread([this] { ticker(); });
+    if (cfg_.job_timeout_s > 0) tick_th_ = vclock::spawn([this] { ticker(); }, "node-tick");
   }
 }
 
@@ -581,7 +581,7 @@ void Node::start_distribution() {
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     started_ = true;
-    t_start_us_ = log::now_us();
+    t_start_us_ = vclock::now_us();
     stats_.bytes_planned = planned;
     sig_cv_.notify_all();
   }
@@ -668,7 +668,7 @@ void Node::start_distribution() {
     {
       std::lock_guard<std::mutex> lk(sig_mu_);
       satisfied_ = true;
-      t_ready_us_ = log::now_us();
+      t_ready_us_ = vclock::now_us();
       stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
     }
     log::info(int64_t(cfg_.id)).msg("timer stop: startup");
@@ -732,7 +732,7 @@ void Node::finish_if_satisfied() {
   {
     std::lock_guard<std::mutex> lk(sig_mu_);
     satisfied_ = true;
-    t_ready_us_ = log::now_us();
+    t_ready_us_ = vclock::now_us();
     stats_.time_to_deliver_s = double(t_ready_us_ - t_start_us_) / 1e6;
   }
   log::info(int64_t(cfg_.id)).f("time_to_deliver_s", stats_.time_to_deliver_s).msg("timer stop: startup");

@@ -19,6 +19,7 @@
 #include <set>
 #include <thread>
 
+#include "core/vclock.h"
 #include "engine/engine.h"
 #include "store/store.h"
 #include "transport/transport.h"
@@ -263,14 +264,14 @@ class Node {
   std::set<NodeID> shrink_wait_;    // survivors whose ShrinkDone is outstanding
   std::thread tick_th_;
   std::mutex tick_mu_;
-  std::condition_variable tick_cv_;
+  CondVar tick_cv_;
   bool tick_stop_ = false;
 
   // cross-thread signalling
   std::mutex sig_mu_;
-  std::condition_variable sig_cv_;
+  CondVar sig_cv_;
   bool started_ = false, satisfied_ = false, ready_ = false;
-  int64_t t_start_us_ = 0, t_ready_us_ = 0;
+  int64_t t_start_us_ = 0, t_ready_us_ = 0;  // vclock::now_us (model time in simulations)
   uint64_t session_range_ = 0;  // roctx range: timer start -> assignment satisfied
   NodeStats stats_;
   std::set<LayerID> acked_;

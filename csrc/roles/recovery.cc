@@ -147,7 +147,7 @@ void Node::retire_job(LayerID layer, const JobKey& key) {
   Job job = jt->second;
   lj->second.erase(jt);
   if (job.state == JobState::Sending) {
-    double dur = double(log::now_us() - job.t_us);
+    double dur = double(vclock::now_us() - job.t_us);
     auto& pf = perf_[job.sender];
     pf.first = pf.second == 0 ? dur : 0.5 * pf.first + 0.5 * dur;  // EWMA (quirk Q9)
     pf.second++;
@@ -165,7 +165,7 @@ void Node::retire_job(LayerID layer, const JobKey& key) {
 
 void Node::track(NodeID sender, NodeID dest, LayerID layer, int64_t off, int64_t size) {
   if (cfg_.job_timeout_s <= 0 || !is_leader_) return;
-  outstanding_[{dest, layer}].push_back({sender, off, size, log::now_us()});
+  outstanding_[{dest, layer}].push_back({sender, off, size, vclock::now_us()});
 }
 
 NodeID Node::alternative_owner(LayerID layer, NodeID dest, NodeID avoid) {
@@ -188,7 +188,7 @@ NodeID Node::alternative_owner(LayerID layer, NodeID dest, NodeID avoid) {
 
 void Node::on_tick() {
   if (!started_ || satisfied_ || cfg_.job_timeout_s <= 0 || e_->planned()) return;
-  const int64_t now = log::now_us();
+  const int64_t now = vclock::now_us();
   struct Expired {
     NodeID dest;
     LayerID layer;

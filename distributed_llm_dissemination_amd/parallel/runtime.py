@@ -782,7 +782,7 @@ class Runtime:
         (separately launched processes); the reference fails on the first dial error.
         """
         node = self._node
-        t0 = time.perf_counter()
+        t0 = _core.vclock_now()  # the steady clock; model time in a virtual-clock simulation
         if not self.is_leader:
             deadline = time.monotonic() + announce_retry_s
             while True:
@@ -794,7 +794,7 @@ class Runtime:
                         raise
                     time.sleep(0.1)
         ok = node.wait_ready(timeout)
-        t1 = time.perf_counter()
+        t1 = _core.vclock_now()
         err = ""
         if self.engine is not None:
             err = self.engine.error()
@@ -1042,11 +1042,11 @@ class Runtime:
                 raise RuntimeError(f"link probe ({what}) stalled after {timeout_s:.0f} s on node {self.node_id}: {desc}")
             return got
 
-        t0 = time.perf_counter()
+        t0 = _core.vclock_now()
         self._barrier()
         got = run([(p, True, nbytes) for p in peers] + [(p, False, nbytes) for p in peers], "concurrent")
         self._barrier()
-        conc_ms = (time.perf_counter() - t0) * 1e3
+        conc_ms = (_core.vclock_now() - t0) * 1e3
         out: Dict[str, object] = {
             "bytes": nbytes,
             "concurrent": {self.node_ids[o["peer"]]: _sig(nbytes / (o["ms"] / 1e3) / 1e9) if o["ms"] > 0 else None
@@ -1070,7 +1070,7 @@ class Runtime:
                         run([(a, False, nbytes)], f"solo {self.node_ids[a]}->{self.node_ids[b]}")
             self._barrier()
             out["solo"] = rates
-        out["probe_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        out["probe_ms"] = round((_core.vclock_now() - t0) * 1e3, 1)
         return out
 
     def link_bytes(self) -> Dict[str, Dict[int, int]]:

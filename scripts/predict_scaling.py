@@ -6,8 +6,15 @@ The schedule is the real one - leader plan, sequence numbers, lanes, groups,
 staging waits - executed by the same engine code that drives RCCL; the sim
 backend charges every staging copy len / PCIe and every P2P transfer
 len / link on its directed link. Sizes are scaled down by --scale with the
-rates scaled by the same factor, so every chunk takes its full-size time and a
-session takes its full-size wall time in a fraction of the memory.
+rates scaled by the same factor, so every chunk takes its full-size time in a
+fraction of the memory.
+
+By default everything runs on the virtual clock (core/vclock.h,
+parallel/simclock.py): the simulator waits in model time, so a session's
+predicted length is its modeled makespan - the same number on every run and
+on any host load - plus the leader's plan time measured on this CPU (the plan
+is real CPU work that does not get faster with the fabric). --wall runs the
+older wall-clock mode (every modeled time slept, --slowdown x slower).
 
     python scripts/predict_scaling.py --link-gbps 50 64 --ns 1 2 4 8
     python scripts/predict_scaling.py --ns 8 --mode0                 # BASELINE config #2
@@ -21,6 +28,7 @@ aggregate GB/s value bench.py would report (N x 80 GiB / T).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -31,6 +39,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_llm_dissemination_amd import _core  # noqa: E402
 from distributed_llm_dissemination_amd.models.catalog import delivered_bytes, make_workload  # noqa: E402
+from distributed_llm_dissemination_amd.parallel import simclock  # noqa: E402
 from distributed_llm_dissemination_amd.parallel.runtime import Runtime  # noqa: E402
 
 MiB = 1 << 20
@@ -43,7 +52,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
             adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
             nic_gbps: float = 50.0, host_lane_classes: int = 0, probe_mib: int = 256, warmup: int = 1,
-            recv_delay=None, slow_after_probe: bool = False) -> dict:
+            recv_delay=None, slow_after_probe: bool = False, virtual: bool = True) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others
@@ -73,17 +82,22 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     hosts: the N ranks sit in this many hosts (N / hosts GPUs each, an xGMI mesh
     inside a host); a transfer between hosts also occupies both GPUs' NICs at
     nic_gbps per direction (one NIC per GPU).
-    slowdown: run every rate this many times slower and divide the measured time
-    by it (keeps the simulator's own per-op thread overhead small next to the
-    modeled transfer times)."""
+    slowdown: wall-clock mode only (virtual=False): run every rate this many
+    times slower and divide the measured time by it (keeps the simulator's own
+    per-op thread overhead small next to the modeled transfer times).
+    virtual (default): model time (see the module docstring); `model_ms` lists
+    each session's modeled makespan without the plan time."""
+    if virtual:
+        slowdown = 1.0  # model time has no simulator overhead to dilute
     plan_link_gbps = (plan_link_gbps if plan_link_gbps is not None else link_gbps) / slowdown
     level = _core.log_level()
     _core.set_log_level(3)  # per-event JSON lines on stderr would be part of the timed sessions
     try:
-        return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
-                        seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
-                        disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib, warmup,
-                        {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe)
+        with (simclock.virtual_clock() if virtual else contextlib.nullcontext()):
+            return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
+                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
+                            disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib,
+                            warmup, {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe)
     finally:
         _core.set_log_level(level)
 
@@ -147,34 +161,36 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             (s, d), frac = slow_link
             cfg.links[s][d] = int(bw * frac)
     disk = dict(storage_path=storage, node_disk_gbps=disk_gbps / scale, node_key=key) if tier == "disk" else {}
-    bar = threading.Barrier(n)
-    rts = [Runtime(cfg, i, engine="sim", registry={i: "127.0.0.1:0"}, chunk_bytes=cb, sim_key=key, verify=False,
+    virtual = _core.vclock_enabled()
+    if virtual:
+        # model time: in-process transport (no socket reader threads the clock
+        # cannot count) and a barrier that waits in model time
+        bar = simclock.barrier(n)
+        reg = {i: f"{key}/{i}" for i in range(n)}
+        rt_kw = dict(transport="inproc", registry=reg)
+    else:
+        bar = threading.Barrier(n).wait
+        rt_kw = {}
+    rts = [Runtime(cfg, i, engine="sim", chunk_bytes=cb, sim_key=key, verify=False,
                    poison=False, engine_opts={"lanes": lanes, "host_lane_classes": host_lane_classes}, pack=pack,
-                   host_share=host_share, barrier=bar.wait, **disk)
+                   host_share=host_share, barrier=bar, **(rt_kw or {"registry": {i: "127.0.0.1:0"}}), **disk)
            for i in range(n)]
     if host_share:
         for r in rts:
             r.unlink_shared()
-    reg = {i: r.transport.address() for i, r in enumerate(rts)}
-    for r in rts:
-        r.transport.set_registry(reg)
-    times, flow_Ts, plans, cached, walls = [], [], [], [], []
+    if not virtual:
+        reg = {i: r.transport.address() for i, r in enumerate(rts)}
+        for r in rts:
+            r.transport.set_registry(reg)
+    times, flow_Ts, plans, cached, walls, models = [], [], [], [], [], []
     flow_T = 0.0
     plan_links_used = {}
     probe_GBps = None
     try:
         if n > 1 and probe_mib > 0 and adapt_links:
             # bench.py's untimed pre-flight probe (concurrent pass): floors the link capacities
-            got = [None] * n
-
-            def pr(i):
-                got[i] = rts[i].probe_links(max(cb, (probe_mib << 20) // scale), timeout_s=600, solo=False)
-
-            ths = [threading.Thread(target=pr, args=(i,)) for i in range(n)]
-            for th in ths:
-                th.start()
-            for th in ths:
-                th.join()
+            nb = max(cb, (probe_mib << 20) // scale)
+            got, _ = simclock.run_ranks([lambda r=r: r.probe_links(nb, timeout_s=600, solo=False) for r in rts])
             for r, g in zip(rts, got):
                 r.observe_probe({p: v * 1e9 for p, v in g.get("concurrent", {}).items() if v},
                                 {p: v * 1e9 for p, v in g.get("concurrent_in", {}).items() if v})
@@ -190,25 +206,20 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                     extra["nic_gbps"] = nic_gbps / scale
                 r.prepare(mode, **{"pull_window": max(1, 2 * (n - 1)), "adapt_links": adapt_links, **extra,
                                    **(policy or {})})
-            res = [None] * n
             sent0 = [r.link_stats()["sent"] for r in rts]
             staged0 = [r.engine.stats().bytes_staged for r in rts]
-
-            def go(i):
-                res[i] = rts[i].execute(600)
-
-            ths = [threading.Thread(target=go, args=(i,)) for i in range(n)]
-            t0 = time.perf_counter()
-            for th in ths:
-                th.start()
-            for th in ths:
-                th.join()
-            wall = time.perf_counter() - t0
+            w0 = time.perf_counter()
+            res, span = simclock.run_ranks([lambda r=r: r.execute(600) for r in rts])
+            walls.append(time.perf_counter() - w0)
             if not all(x.ok for x in res):
                 raise RuntimeError([x.error for x in res if not x.ok])
             plan_s = res[0].plan_ms / 1e3
-            walls.append(wall)
-            times.append((wall - plan_s) / slowdown + plan_s)
+            if virtual:
+                # model time: the plan ran while the clock stood still - charge it at its CPU cost
+                models.append(span)
+                times.append(span + plan_s)
+            else:
+                times.append((span - plan_s) / slowdown + plan_s)
             plans.append(res[0].plan_ms)
             cached.append(res[0].plan_cached)
             flow_T = res[0].flow_T
@@ -239,6 +250,9 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             "seeding": seeding, **({"policy": policy} if policy else {}), **({"host_share": True} if host_share else {}),
             "lanes": lanes_used, "ms_per_step": round(sec * 1e3, 1), "min_ms": round(min(timed) * 1e3, 1),
             "warmup": warmup, "times_ms": [round(x * 1e3, 1) for x in times],
+            **({"clock": "virtual", "model_ms": [round(x * 1e3, 3) for x in models],
+                "model_ms_per_step": round(sum(models[warmup:] or models) / len(models[warmup:] or models) * 1e3, 3),
+                "wall_s": round(sum(walls), 2)} if virtual else {"clock": "wall"}),
             "plan_ms": [round(x, 2) for x in plans], "plan_cached": cached,
             **({"probe_GBps": probe_GBps} if probe_GBps else {}),
             **({"flow_T_ms": [round(x / slowdown * 1e3, 1) for x in flow_Ts]} if any(flow_Ts) else {}),
