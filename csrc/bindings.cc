@@ -414,7 +414,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("host", &SimTiming::host)
       .def_readwrite("nic_bps", &SimTiming::nic_bps)
       .def_readwrite("wait_s", &SimTiming::wait_s)
-      .def_readwrite("recv_delay_s", &SimTiming::recv_delay_s);
+      .def_readwrite("recv_delay_s", &SimTiming::recv_delay_s)
+      .def_readwrite("serialize_lanes", &SimTiming::serialize_lanes);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   // Virtual clock (core/vclock.h): the simulator in model time. Python threads
   // that drive a session's ranks are counted by the clock between adopt() and

@@ -213,6 +213,10 @@ struct SimTiming {
   // many seconds late (its peers' sends wait for it, as an RCCL send waits
   // for the matching receive): the closed loop must not read that as slow links.
   std::map<int, double> recv_delay_s;
+  // Fault injection for the schedule tests: every comm lane of a rank runs on
+  // ONE queue (its groups one after another, as if the lanes were one stream).
+  // The model-time upper bounds in tests/test_timing_sim.py must catch it.
+  bool serialize_lanes = false;
 };
 
 // In-process simulated fabric: ranks of one "communicator" share `comm_key`.

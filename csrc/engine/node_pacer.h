@@ -70,7 +70,10 @@ class NodePacer {
       start = cur > now ? cur : now;
     } while (!next_->compare_exchange_weak(cur, start + dur, std::memory_order_acq_rel, std::memory_order_relaxed));
     const int64_t wait = start - now;
-    if (wait > 0) vclock::sleep_for(double(wait) * 1e-9);
+    // A simulated node has no device to serve the read: the reader holds the
+    // bytes only at the end of its slot, as a real pread returns then.
+    const int64_t until = vclock::enabled() ? wait + dur : wait;
+    if (until > 0) vclock::sleep_for(double(until) * 1e-9);
     return wait > 0 ? wait : 0;
   }
 

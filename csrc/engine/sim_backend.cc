@@ -350,7 +350,7 @@ class SimBackend : public Backend {
 
   Ev corrupt(uint8_t* p, int lane) override {
     auto [id, ev] = make_event();
-    comm_.at(size_t(lane))->push([=] {
+    lane_q(lane).push([=] {
       const uint32_t pat = 0xA5A5A5A5u;
       memcpy(p, &pat, 4);
       ev->set(1);
@@ -360,7 +360,7 @@ class SimBackend : public Backend {
 
   Ev mark(int lane) override {
     auto [id, ev] = make_event();
-    comm_.at(size_t(lane))->push([=] { ev->set(1); });
+    lane_q(lane).push([=] { ev->set(1); });
     return id;
   }
 
@@ -370,7 +370,7 @@ class SimBackend : public Backend {
     for (Ev w : waits) deps.push_back(lookup(w));
     int rank = rank_;
     auto fab = fab_;
-    comm_.at(size_t(lane))->push([=] {
+    lane_q(lane).push([=] {
       for (size_t i = 0; i < deps.size(); ++i) {
         auto& d = deps[i];
         if (!d || !wait_event(d, fab->timing.wait_s)) {
@@ -549,6 +549,7 @@ class SimBackend : public Backend {
     events_[id] = e;
     return {id, e};
   }
+  Queue& lane_q(int lane) { return *comm_.at(fab_->timing.serialize_lanes ? 0 : size_t(lane)); }
   std::shared_ptr<SimEvent> lookup(Ev e) {
     if (!e) return nullptr;
     std::lock_guard<std::mutex> lk(ev_mu_);

@@ -52,7 +52,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             slowdown: float = 1.0, tier: str = "host", pack: str = "none", plan_link_gbps=None,
             adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
             nic_gbps: float = 50.0, host_lane_classes: int = 0, probe_mib: int = 256, warmup: int = 1,
-            recv_delay=None, slow_after_probe: bool = False, virtual: bool = True) -> dict:
+            recv_delay=None, slow_after_probe: bool = False, virtual: bool = True,
+            serialize_lanes: bool = False) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others
@@ -86,7 +87,9 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     times slower and divide the measured time by it (keeps the simulator's own
     per-op thread overhead small next to the modeled transfer times).
     virtual (default): model time (see the module docstring); `model_ms` lists
-    each session's modeled makespan without the plan time."""
+    each session's modeled makespan without the plan time.
+    serialize_lanes: fault injection - each rank's comm lanes share one queue
+    (SimTiming.serialize_lanes); the schedule tests' upper bounds must catch it."""
     if virtual:
         slowdown = 1.0  # model time has no simulator overhead to dilute
     plan_link_gbps = (plan_link_gbps if plan_link_gbps is not None else link_gbps) / slowdown
@@ -97,7 +100,8 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             return _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                             seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
                             disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib,
-                            warmup, {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe)
+                            warmup, {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe,
+                            serialize_lanes)
     finally:
         _core.set_log_level(level)
 
@@ -105,7 +109,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
              policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False,
              hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1, recv_delay=None,
-             slow_after_probe=False):
+             slow_after_probe=False, serialize_lanes=False):
     import shutil
     import tempfile
 
@@ -114,7 +118,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
                            storage, host_share, hosts, nic_gbps, host_lane_classes, probe_mib, warmup, recv_delay,
-                           slow_after_probe)
+                           slow_after_probe, serialize_lanes)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
@@ -123,7 +127,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
                 policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
                 host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1,
-                recv_delay=None, slow_after_probe=False):
+                recv_delay=None, slow_after_probe=False, serialize_lanes=False):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -131,6 +135,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     t.copy_bytes = False
     t.wait_s = 600.0  # congested schedules queue transfers behind their links and NICs for long
     t.stage_bps = pcie_gbps * 1e9 / scale
+    t.serialize_lanes = serialize_lanes
     t.link_bps = link_gbps * 1e9 / scale
     slow = {}
     if slow_link is not None:
@@ -270,6 +275,31 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             **({"planned_T_ms": round(flow_T * 1e3 / slowdown, 1)} if flow_T > 0 else {})}
 
 
+def closed_form_ms(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, link_gbps: float = 50.0,
+                   pcie_gbps: float = 57.5, tier: str = "host", disk_gbps: float = 13.3, mode0: bool = False) -> float:
+    """The physical lower bound of one step, in ms.
+
+    Modes 1-3, random seeding (the headline): every GPU stages its 1/N of the
+    layers over its PCIe and receives 1/N from each peer over that link, both
+    overlapped: total / N / min(PCIe, link) (N = 1: total / PCIe); from the
+    node's one NVMe (tier "disk") at least total / NVMe.
+    Mode 0 (config #2, the leader holds every layer): each receiver takes
+    every byte in over its N - 1 links, total / (N - 1) / link; from host
+    memory (tier "host") the leader's PCIe carries every byte too."""
+    total = layers * layer_bytes
+    if mode0:
+        if n < 2:
+            return 0.0
+        t = total / (n - 1) / (link_gbps * 1e9)
+        if tier == "host":
+            t = max(t, total / (pcie_gbps * 1e9))
+        return t * 1e3
+    t = total / n / min(pcie_gbps * 1e9, link_gbps * 1e9 if n > 1 else float("inf"))
+    if tier == "disk":
+        t = max(t, total / (disk_gbps * 1e9))
+    return t * 1e3
+
+
 def modeled_ms(link_bytes, staged, n, link_gbps, pcie_gbps, slow_link=None) -> float:
     """A load-independent lower bound of a session from its bytes accounting:
     the busiest directed link's bytes / its rate, or the busiest rank's staged
@@ -294,7 +324,9 @@ def main() -> int:
     ap.add_argument("--scale", type=int, default=1024)
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--mode", type=int, default=1)
-    ap.add_argument("--slowdown", type=float, default=4.0)
+    ap.add_argument("--slowdown", type=float, default=4.0, help="--wall only: rates this many times slower")
+    ap.add_argument("--wall", action="store_true",
+                    help="the wall-clock simulator (sleeps every modeled time) instead of model time")
     ap.add_argument("--layers", type=int, default=80)
     ap.add_argument("--layer-mib", type=int, default=1024)
     ap.add_argument("--tier", choices=["host", "disk"], default="host",
@@ -319,7 +351,7 @@ def main() -> int:
     ap.add_argument("--pull-window", type=int, default=0,
                     help="mode 2: jobs in flight per sender (0: 2 (N - 1), as bench.py)")
     args = ap.parse_args()
-    common = dict(steps=args.steps, warmup=args.warmup, probe_mib=args.probe_mib)
+    common = dict(steps=args.steps, warmup=args.warmup, probe_mib=args.probe_mib, virtual=not args.wall)
     _core.set_log_level(3)
     if args.mode0:
         for lg in args.link_gbps:
@@ -335,6 +367,9 @@ def main() -> int:
                                     mode=0, slowdown=args.slowdown, seeding="leader", tier=tier,
                                     policy={"relay": relay, "collective": coll, "hierarchical": not args.flat},
                                     hosts=args.hosts, nic_gbps=args.nic_gbps, **common)
+                        if args.hosts == 1:
+                            r["closed_form_ms"] = round(closed_form_ms(n, link_gbps=lg, pcie_gbps=args.pcie_gbps,
+                                                                       tier=tier, mode0=True), 1)
                         print(json.dumps(r), flush=True)
         return 0
     for lg in args.link_gbps:
@@ -347,11 +382,9 @@ def main() -> int:
             # closed form: every GPU stages 80/N GiB over PCIe and gets
             # 80/N GiB from each peer over its link; both overlap
             if args.pack == "none" and args.hosts == 1:
-                total = args.layers * (args.layer_mib << 20)
-                bound = total / n / min(args.pcie_gbps * 1e9, lg * 1e9 if n > 1 else 1e30)
-                if args.tier == "disk":  # every byte leaves the node's one NVMe once
-                    bound = max(bound, total / (args.disk_gbps * 1e9))
-                r["closed_form_ms"] = round(bound * 1e3, 1)
+                r["closed_form_ms"] = round(closed_form_ms(n, layers=args.layers, layer_bytes=args.layer_mib << 20,
+                                                           link_gbps=lg, pcie_gbps=args.pcie_gbps, tier=args.tier,
+                                                           disk_gbps=args.disk_gbps), 1)
             print(json.dumps(r), flush=True)
     return 0
 
