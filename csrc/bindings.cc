@@ -116,7 +116,8 @@ PYBIND11_MODULE(_core, m) {
       .value("Transport", MsgType::Transport)
       .value("Nack", MsgType::Nack)
       .value("Bcast", MsgType::Bcast)
-      .value("Landed", MsgType::Landed);
+      .value("Landed", MsgType::Landed)
+      .value("XferBatch", MsgType::XferBatch);
   m.attr("CLIENT_ID") = py::int_(kClientID);
 
   py::class_<LayerMeta>(m, "LayerMeta")
@@ -139,6 +140,18 @@ PYBIND11_MODULE(_core, m) {
       });
 
   // ---- messages / codec
+  py::class_<XferJob>(m, "XferJob")
+      .def(py::init<>())
+      .def_readwrite("seq", &XferJob::seq)
+      .def_readwrite("src", &XferJob::src)
+      .def_readwrite("dst", &XferJob::dst)
+      .def_readwrite("layer", &XferJob::layer)
+      .def_readwrite("offset", &XferJob::offset)
+      .def_readwrite("size", &XferJob::size)
+      .def_readwrite("total", &XferJob::total)
+      .def_readwrite("chunk_bytes", &XferJob::chunk_bytes)
+      .def_readwrite("crc", &XferJob::crc)
+      .def_readwrite("rate", &XferJob::rate);
   py::class_<Message, MessagePtr>(m, "Message")
       .def(py::init<>())
       .def_readwrite("type", &Message::type)
@@ -158,6 +171,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("chunk_bytes", &Message::chunk_bytes)
       .def_readwrite("crc", &Message::crc)
       .def_readwrite("seq", &Message::seq)
+      .def_readwrite("batch", &Message::batch)
+      .def_readwrite("order", &Message::order)
+      .def_readwrite("jobs", &Message::jobs)
       .def_readwrite("peers", &Message::peers)
       .def_readwrite("src_addr", &Message::src_addr)
       .def_readwrite("payload_str", &Message::payload_str)
@@ -173,6 +189,8 @@ PYBIND11_MODULE(_core, m) {
   });
   m.def("encode_envelope", [](const Message& x) { return py::bytes(encode_envelope(x)); });
   m.def("decode_envelope", [](const std::string& s) { return decode_envelope(Json::parse(s)); });
+  m.def("decode_envelope_text", [](const std::string& s) { return decode_envelope_text(s.data(), s.size()); },
+        "the transport's decoder (transfer batches take the fast path)");
   m.def("json_roundtrip", [](const std::string& s) { return Json::parse(s).dump(); });
   m.def("json_parse_prefix", [](const std::string& s) {
     Json out;
@@ -415,7 +433,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("nic_bps", &SimTiming::nic_bps)
       .def_readwrite("wait_s", &SimTiming::wait_s)
       .def_readwrite("recv_delay_s", &SimTiming::recv_delay_s)
-      .def_readwrite("serialize_lanes", &SimTiming::serialize_lanes);
+      .def_readwrite("serialize_lanes", &SimTiming::serialize_lanes)
+      .def_readwrite("trace", &SimTiming::trace);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   // Virtual clock (core/vclock.h): the simulator in model time. Python threads
   // that drive a session's ranks are counted by the clock between adopt() and
@@ -448,6 +467,11 @@ PYBIND11_MODULE(_core, m) {
         b.wait();
       });
   m.def("sim_fabric_bytes", [](const std::string& key) { return sim_fabric_stats(key).bytes; });
+  m.def("sim_fabric_trace", [](const std::string& key) {
+    auto st = sim_fabric_stats(key);
+    return py::make_tuple(st.transfers, st.stages);
+  }, "(transfers [(src, dst, start_s, end_s, bytes)], stages [(rank, start_s, end_s, bytes)]) with SimTiming.trace");
+  m.def("sim_fabric_clear_trace", [](const std::string& key) { sim_clear_trace(key); });
   m.def("sim_read", [](uint64_t ptr, int64_t n) {
     return py::bytes(reinterpret_cast<const char*>(ptr), size_t(n));
   });

@@ -216,6 +216,7 @@ Json encode_payload(const Message& m) {
     case MsgType::XferBatch: {
       src_id();
       p["Batch"] = Json(uint64_t(m.batch));
+      if (m.order) p["Order"] = Json(uint64_t(m.order));
       Json arr = Json::array();
       for (auto& j : m.jobs) {
         Json e = Json::array();
@@ -386,7 +387,12 @@ std::string encode_xfer_batch(const Message& m) {
     }
     o.ch(']');
   }
-  o.lit("],\"SrcID\":");
+  o.lit("]");
+  if (m.order) {
+    o.lit(",\"Order\":");
+    o.num(uint64_t(m.order));
+  }
+  o.lit(",\"SrcID\":");
   o.num(uint64_t(m.src));
   o.lit("},\"src\":\"");
   o.num(uint64_t(m.src));
@@ -482,6 +488,8 @@ bool decode_xfer_payload(Cur& c, Message& m) {
       m.batch = c.num<uint64_t>();
     } else if (k == "Epoch") {
       m.epoch = c.num<uint64_t>();
+    } else if (k == "Order") {
+      m.order = c.num<uint8_t>();
     } else if (k == "SrcID") {
       m.src = c.num<uint64_t>();
     } else if (k == "Jobs") {
@@ -613,6 +621,7 @@ MessagePtr decode_envelope(const Json& env) {
       break;
     case MsgType::XferBatch:
       m->batch = p.get_u64("Batch");
+      m->order = uint8_t(p.get_u64("Order", 0));
       if (auto* arr = p.find("Jobs"); arr && arr->is_array()) {
         for (auto& e : arr->as_array()) {
           const auto& a = e.as_array();

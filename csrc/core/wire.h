@@ -89,6 +89,11 @@ struct Message {
   std::vector<NodeID> peers;    // Bcast participants; Suspect / Shrink node lists
   // XferBatch / Announce extensions
   uint64_t batch = 0;
+  // XferBatch: how lanes order its pieces - 0 chunk-major (chunk index, then
+  // sequence number: every job of a batch advances chunk by chunk together,
+  // as paced mode-3 jobs must), 1 job-major (sequence number, then chunk:
+  // mode-2 pull jobs, so a sender's links stay on the layer its copy queue stages)
+  uint8_t order = 0;
   std::vector<XferJob> jobs;
   std::map<LayerID, CrcManifest> manifest;
   PartialLayers partial_layers;  // Announce extension: layers held only in these byte ranges

@@ -25,6 +25,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 namespace dissem {
@@ -186,6 +187,9 @@ inline int lane_of_hosts(int src, int dst, int world, int lanes, int hosts, int 
 
 struct SimFabricStats {
   int64_t matched = 0, bytes = 0;
+  // SimTiming::trace: every timed transfer as (src, dst, start s, end s, bytes)
+  std::vector<std::tuple<int, int, double, double, int64_t>> transfers;
+  std::vector<std::tuple<int, double, double, int64_t>> stages;  // (rank, start s, end s, bytes)
 };
 
 // Timing model of the simulated fabric (all rates in bytes/s, 0 = instant).
@@ -217,11 +221,15 @@ struct SimTiming {
   // ONE queue (its groups one after another, as if the lanes were one stream).
   // The model-time upper bounds in tests/test_timing_sim.py must catch it.
   bool serialize_lanes = false;
+  // Record every timed transfer and staging copy (sim_fabric_trace): the
+  // per-link timelines that show where a schedule leaves links idle.
+  bool trace = false;
 };
 
 // In-process simulated fabric: ranks of one "communicator" share `comm_key`.
 std::unique_ptr<Backend> make_sim_backend(const std::string& comm_key, int rank, int world, int lanes = 1);
 SimFabricStats sim_fabric_stats(const std::string& comm_key);
+void sim_clear_trace(const std::string& comm_key);
 // Set the timing model of a fabric (before its ranks start moving bytes).
 void sim_set_timing(const std::string& comm_key, const SimTiming& t);
 

@@ -290,7 +290,9 @@ bool PlannedEngine::on_message(const MessagePtr& m) {
       r.comm_id = m->payload_str;
       reqs_.push_back(std::move(r));
     } else {
-      reqs_.push_back(Req{Req::Batch, m->jobs, 0, 0, 0});
+      Req r{Req::Batch, m->jobs, 0, 0, 0};
+      r.order = m->order;
+      reqs_.push_back(std::move(r));
     }
     busy_ = true;
   }
@@ -490,7 +492,7 @@ void PlannedEngine::pace_take(uint64_t key, int64_t rate, int64_t n) {
   if (rate > 0) pace_[key].tokens -= double(n);
 }
 
-void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
+void PlannedEngine::add_batch(std::vector<XferJob>& jobs, uint8_t order) {
   std::sort(jobs.begin(), jobs.end(), [](const XferJob& a, const XferJob& b) { return a.seq < b.seq; });
   std::vector<Piece> pieces;
   const int64_t cb = grid_;
@@ -532,7 +534,13 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
       // Ordering key (batch, chunk index in the layer, seq): a relay of chunk c
       // (a later phase, so a larger seq) always sorts after the recv of chunk c
       // it forwards, whatever byte ranges the two jobs cover.
-      Piece p{kind, j.seq, c, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
+      // Job-major batches (mode 2) order a lane job by job instead (pidx =
+      // seq, then chunk): a sender's pull jobs start as acks return, so its
+      // lanes hold different layers, and chunk-major order would interleave
+      // them - a lane waiting on layer B's chunk 0 while the copy queue stages
+      // layer A for the others (sim, N = 8: 224 -> 216 ms, bound 214.7).
+      const int64_t pidx = order == 1 ? int64_t((j.seq << 24) | uint64_t(c)) : c;
+      Piece p{kind, j.seq, pidx, peer, j.layer, pos, e - pos, L.size, c, pos == c * cb && e == cend};
       p.src_node = j.src;
       p.bcast = bcast;
       p.rate = j.rate;
@@ -555,15 +563,29 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
     return a.pidx != b.pidx ? a.pidx < b.pidx : a.seq < b.seq;
   });
   for (auto& p : pieces) {
-    if (p.kind == Kind::Local) {
-      // Local promotions take no part in the P2P order: stage right away so PCIe
-      // runs ahead of the xGMI rounds that forward the same chunks.
-      Layer& L = layer(p.layer);
-      if (ensure_chunk(L, p.layer, p.chunk, true) < 0) fail("no source to load layer " + std::to_string(p.layer));
-      continue;
-    }
+    if (p.kind == Kind::Local) continue;
     if (p.kind == Kind::Send && !p.bcast) fwd_pending_[{p.layer, p.chunk}].insert(key_of(p));
     ops_[size_t(p.lane)].push_back(p);
+  }
+  for (auto& p : pieces) {
+    if (p.kind != Kind::Local) continue;
+    // Local promotions take no part in the P2P order. A chunk this rank also
+    // sends is staged when its first send needs it (the lanes' key order), so
+    // a promotion never queues a layer on the copy queue ahead of the chunks
+    // the links are waiting for (mode 2 at N = 8: a self-load of the layer
+    // being sent staged all 16 chunks at once and the lanes' next layer
+    // waited ~17 ms behind them). Any other chunk stages right away, so PCIe
+    // runs ahead of the xGMI rounds that forward the same chunks.
+    // While this rank has sends queued, other promotions trickle in at most
+    // kPromoteAhead chunks at a time (issue_some) instead of queueing whole
+    // layers ahead of the sends' chunks.
+    Layer& L = layer(p.layer);
+    if (L.st[size_t(p.chunk)] == 0 && !fwd_pending_.empty()) {
+      L.want[size_t(p.chunk)] = 1;
+      deferred_local_.push_back({p.layer, p.chunk});
+      continue;
+    }
+    if (ensure_chunk(L, p.layer, p.chunk, true) < 0) fail("no source to load layer " + std::to_string(p.layer));
   }
   int64_t ns = 0, nr = 0;
   for (auto& p : pieces) (p.kind == Kind::Send ? ns : nr) += p.kind == Kind::Local ? 0 : 1;
@@ -573,6 +595,23 @@ void PlannedEngine::add_batch(std::vector<XferJob>& jobs) {
 
 bool PlannedEngine::issue_some() {
   if (recovering_ || dead_) return false;
+  // Promotions left to a send whose staging they would share: once the send
+  // staged the chunk (or no longer will: cancelled by a re-plan) they are done
+  // (the chunk's check reports it landed, L.want) or staged here.
+  for (auto it = promoting_.begin(); it != promoting_.end();)
+    it = layers_[it->first].st[size_t(it->second)] == 1 ? std::next(it) : promoting_.erase(it);
+  for (size_t n = deferred_local_.size(); n > 0 && !failed_; --n) {
+    auto lc = deferred_local_.front();
+    deferred_local_.pop_front();
+    Layer& L = layers_[lc.first];
+    if (L.st[size_t(lc.second)] != 0) continue;
+    if (fwd_pending_.count(lc) || (!fwd_pending_.empty() && promoting_.size() >= size_t(kPromoteAhead))) {
+      deferred_local_.push_back(lc);
+      continue;
+    }
+    if (ensure_chunk(L, lc.first, lc.second, true) < 0) fail("no source to load layer " + std::to_string(lc.first));
+    if (L.st[size_t(lc.second)] == 1) promoting_.insert(lc);
+  }
   // Local promotions held back by tier pacing.
   for (size_t n = local_wait_.size(); n > 0 && !failed_; --n) {
     auto lc = local_wait_.front();
@@ -914,7 +953,7 @@ void PlannedEngine::take_requests(bool block) {
   for (auto& r : got) {
     switch (r.type) {
       case Req::Batch:
-        add_batch(r.jobs);
+        add_batch(r.jobs, r.order);
         break;
       case Req::Load: {
         Layer& L = layer(r.layer);
@@ -942,6 +981,8 @@ void PlannedEngine::take_requests(bool block) {
         }
         pace_.clear();
         local_wait_.clear();
+        deferred_local_.clear();
+        promoting_.clear();
         fwd_pending_.clear();
         std::lock_guard<std::mutex> lk(req_mu_);
         resets_done_++;
@@ -997,6 +1038,8 @@ void PlannedEngine::run() {
         verifies_.clear();
         drop_pending_checks();
         local_wait_.clear();
+        deferred_local_.clear();
+        promoting_.clear();
         std::lock_guard<std::mutex> lk(req_mu_);
         busy_ = false;
         idle_cv_.notify_all();

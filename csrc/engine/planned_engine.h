@@ -236,7 +236,7 @@ class PlannedEngine : public DataEngine {
   struct Piece {
     Kind kind;
     uint64_t seq;
-    int64_t pidx;  // chunk index inside its layer (ordering key after the batch)
+    int64_t pidx;  // ordering key after the batch: the chunk index, or seq << 24 | chunk (job-major)
     int peer;      // rank
     LayerID layer;
     int64_t off, len, total;
@@ -252,6 +252,8 @@ class PlannedEngine : public DataEngine {
     int64_t rate = 0;    // job pacing (B/s, 0 = unlimited)
     uint64_t batch = 0;  // add_batch ordinal (most significant part of the key)
   };
+  // Key: (batch, pidx, seq). Chunk-major batches (Message::order 0) set pidx to
+  // the chunk index, job-major ones (order 1) to seq << 24 | chunk index.
   using Key = std::tuple<uint64_t, int64_t, uint64_t>;
   static Key key_of(const Piece& p) { return Key{p.batch, p.pidx, p.seq}; }
   struct PartChunk {
@@ -323,6 +325,7 @@ class PlannedEngine : public DataEngine {
     std::string comm_id;       // Shrink: the survivors' new communicator id
     const uint8_t* base = nullptr;  // HostReady: host copy; `off` = bytes present, `len` = total
     ProbeJob* probe = nullptr;  // Probe
+    uint8_t order = 0;          // Batch: Message::order
   };
   void run_probe(ProbeJob& job);
   struct Inflight {  // a P2P group on a comm lane
@@ -339,7 +342,7 @@ class PlannedEngine : public DataEngine {
 
   void run();
   void take_requests(bool block);
-  void add_batch(std::vector<XferJob>& jobs);
+  void add_batch(std::vector<XferJob>& jobs, uint8_t order);
   bool issue_some();
   bool issue_lane(int lane);
   void poll();
@@ -349,6 +352,7 @@ class PlannedEngine : public DataEngine {
     for (auto& q : inflight_)
       if (!q.empty()) return false;
     return verifies_.empty() && pending_checks_.empty() && disk_inflight_ == 0 && disk_wait_.empty() && local_wait_.empty() &&
+           deferred_local_.empty() &&
            bounce_busy_.empty();
   }
   int lane_for(int peer, bool send) const {
@@ -421,6 +425,8 @@ class PlannedEngine : public DataEngine {
   std::vector<Ev> owned_waits_;               // landing events the engine releases after the flush
   std::vector<std::pair<LayerID, int64_t>> restage_;  // local chunks to stage again (bad CRC)
   std::deque<std::pair<LayerID, int64_t>> local_wait_;  // local promotions deferred by tier pacing
+  std::deque<std::pair<LayerID, int64_t>> deferred_local_;  // promotions held back behind queued sends
+  std::set<std::pair<LayerID, int64_t>> promoting_;  // of them, staged and not yet resident
   // keys of the queued (not yet posted) sends of each chunk: relay cuts, and
   // recvs of a chunk held back behind this rank's earlier-key send of it
   std::map<std::pair<LayerID, int64_t>, std::multiset<Key>> fwd_pending_;
@@ -487,5 +493,8 @@ constexpr uint64_t kPaceJob = 1ull << 62, kPacePeer = 2ull << 62, kPaceTier = 3u
 // batch of 16 is 1 GiB of bf16 per launch, where the fused kernel runs at
 // its streaming rate; one chunk alone fills less than a round of the chip.
 constexpr int kVerifyBatch = 16;
+// Promotions (loads of a rank's own layers) staged ahead of the chunks its
+// queued sends need: at most this many at a time (PlannedEngine::add_batch).
+constexpr int kPromoteAhead = 2;
 
 }  // namespace dissem

@@ -119,6 +119,8 @@ void PlannedEngine::do_shrink(const std::vector<NodeID>& dead_nodes, uint64_t ge
   for (auto& q : ops_) q.clear();
   restage_.clear();
   local_wait_.clear();
+  deferred_local_.clear();
+  promoting_.clear();
   fwd_pending_.clear();
   for (auto& kv : layers_) {
     Layer& L = kv.second;

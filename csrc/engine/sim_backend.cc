@@ -133,6 +133,7 @@ struct Fabric {
             done = std::max({done, o, i});
           }
           s->done_at = r->done_at = done;
+          if (timing.trace) stats.transfers.emplace_back(src, dst, done - dur, done, s->len);
           // Modeled device time of each op: from the later of the two posts
           // (the transfer cannot start before both ends are there) to the end
           // on its link - queueing behind the link's earlier transfers
@@ -320,7 +321,12 @@ class SimBackend : public Backend {
   // Staging occupies the copy queue for n / stage_bps (timing model).
   void stage_delay(double t0, int64_t n) {
     const double bps = fab_->timing.stage_bps;
-    if (bps > 0) vclock::sleep_until(t0 + double(n) / bps);
+    if (bps <= 0) return;
+    if (fab_->timing.trace) {
+      std::lock_guard<std::mutex> lk(fab_->mu);
+      fab_->stats.stages.emplace_back(rank_, t0, t0 + double(n) / bps, n);
+    }
+    vclock::sleep_until(t0 + double(n) / bps);
   }
 
   Ev stage(uint8_t* dst, const uint8_t* src, int64_t n) override {
@@ -584,6 +590,13 @@ void sim_set_timing(const std::string& comm_key, const SimTiming& t) {
   std::lock_guard<std::mutex> lk(f->mu);
   f->timing = t;
   f->link_free.clear();
+}
+
+void sim_clear_trace(const std::string& comm_key) {
+  auto f = fabric(comm_key);
+  std::lock_guard<std::mutex> lk(f->mu);
+  f->stats.transfers.clear();
+  f->stats.stages.clear();
 }
 
 SimFabricStats sim_fabric_stats(const std::string& comm_key) {

@@ -124,6 +124,7 @@ void Node::flush_batch() {
   for (auto& o : out) {
     o.second.type = MsgType::XferBatch;
     o.second.batch = batch;
+    o.second.order = cfg_.mode == 2 ? 1 : 0;  // pull jobs: job-major lanes (Message::order)
     o.second.src = cfg_.id;
     o.second.epoch = cfg_.epoch;
     njobs += int64_t(o.second.jobs.size());

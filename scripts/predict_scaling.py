@@ -53,7 +53,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
             nic_gbps: float = 50.0, host_lane_classes: int = 0, probe_mib: int = 256, warmup: int = 1,
             recv_delay=None, slow_after_probe: bool = False, virtual: bool = True,
-            serialize_lanes: bool = False) -> dict:
+            serialize_lanes: bool = False, trace: bool = False) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others
@@ -101,7 +101,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
                             seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
                             disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib,
                             warmup, {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe,
-                            serialize_lanes)
+                            serialize_lanes, trace)
     finally:
         _core.set_log_level(level)
 
@@ -109,7 +109,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
              policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False,
              hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1, recv_delay=None,
-             slow_after_probe=False, serialize_lanes=False):
+             slow_after_probe=False, serialize_lanes=False, trace=False):
     import shutil
     import tempfile
 
@@ -118,7 +118,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
                            storage, host_share, hosts, nic_gbps, host_lane_classes, probe_mib, warmup, recv_delay,
-                           slow_after_probe, serialize_lanes)
+                           slow_after_probe, serialize_lanes, trace)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
@@ -127,7 +127,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
                 policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
                 host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1,
-                recv_delay=None, slow_after_probe=False, serialize_lanes=False):
+                recv_delay=None, slow_after_probe=False, serialize_lanes=False, trace=False):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -136,6 +136,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     t.wait_s = 600.0  # congested schedules queue transfers behind their links and NICs for long
     t.stage_bps = pcie_gbps * 1e9 / scale
     t.serialize_lanes = serialize_lanes
+    t.trace = trace
     t.link_bps = link_gbps * 1e9 / scale
     slow = {}
     if slow_link is not None:
@@ -213,6 +214,8 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                                    **(policy or {})})
             sent0 = [r.link_stats()["sent"] for r in rts]
             staged0 = [r.engine.stats().bytes_staged for r in rts]
+            if trace:
+                _core.sim_fabric_clear_trace(key)
             w0 = time.perf_counter()
             res, span = simclock.run_ranks([lambda r=r: r.execute(600) for r in rts])
             walls.append(time.perf_counter() - w0)
@@ -240,6 +243,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                         link_bytes[(i, p)] = d * scale
             staged = [(r.engine.stats().bytes_staged - staged0[i]) * scale for i, r in enumerate(rts)]
         lanes_used = rts[0].engine.stats().lanes
+        trace_last = _core.sim_fabric_trace(key) if trace else None
         rts_est = [dict(r.link_est) for r in rts]  # per rank: the send-side busy-throughput EWMA per peer (B/s)
         rts_est_in = [dict(r.link_est_in) for r in rts]  # ... and the receive-side one per peer
     finally:
@@ -272,6 +276,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
             "modeled_ms_last": round(modeled_ms(link_bytes, staged, n, link_gbps * slowdown, pcie_gbps * slowdown,
                                                  slow_link) * 1e3, 1),
             "value_GBps": round(total / sec / 1e9, 1), "scale": scale,
+            **({"trace_last": trace_last} if trace else {}),
             **({"planned_T_ms": round(flow_T * 1e3 / slowdown, 1)} if flow_T > 0 else {})}
 
 

@@ -126,52 +126,59 @@ def test_mode3_hbm_ingress_budget_binds_the_plan():
 
 @pytest.mark.parametrize("n", [1, 2, 4, 8])
 @pytest.mark.parametrize("mode", [1, 3])
-def test_headline_schedule_within_5pct_of_the_link_bound(mode, n):
+def test_headline_schedule_within_3pct_of_the_link_bound(mode, n):
     """The headline schedule (80 x 1 GiB, random seeding, at 1/1024 size with
     rates scaled alike): every GPU stages exactly 80/N GiB over PCIe and every
     directed link carries exactly 80/N GiB, so the step cannot beat
-    85.9 GB / (N * min(PCIe, link)); modes 1 and 3 stay within 5 % of it in
-    model time, every session (the warm-up one too)."""
+    85.9 GB / (N * min(PCIe, link)); modes 1 and 3 stay within 3 % of it in
+    model time, every session (the warm-up one too). Measured: +0.14 / 0.28 /
+    0.56 % at N = 2 / 4 / 8 - one chunk's staging before the first transfer."""
     r = predict_scaling.predict(n, mode=mode, steps=1, **HEADLINE)
     bound = predict_scaling.closed_form_ms(n)
     assert r["staged_GiB_last"] == [pytest.approx(80 / n, rel=1e-3)] * n, r
     assert len(r["link_GiB_last"]) == n * (n - 1), r
     assert all(v == pytest.approx(80 / n, rel=1e-3) for v in r["link_GiB_last"].values()), r
     for ms in r["model_ms"]:
-        assert bound * 0.999 <= ms <= bound * 1.05, (n, mode, r["model_ms"], bound)
+        assert bound * 0.999 <= ms <= bound * 1.03, (n, mode, r["model_ms"], bound)
     if mode == 3 and n > 1:
         assert r["planned_T_ms"] == pytest.approx(bound, rel=1e-3), r
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-def test_mode0_relay_within_8pct_of_ingress_bound(n):
+def test_mode0_relay_within_3pct_of_ingress_bound(n):
     """BASELINE config #2: the leader holds all 80 layers in HBM; the relay
     broadcast scatters 1/(N-1) of each layer and every receiver relays its
     slice to the others, so each receiver's N - 1 ingress links carry every
-    byte: T >= 85.9 GB / (N - 1) / link. The schedule stays within 8 %."""
+    byte: T >= 85.9 GB / (N - 1) / link. The schedule stays within 3 %
+    (measured +0.0 / 0.31 / 0.63 % at N = 2 / 4 / 8)."""
     r = predict_scaling.predict(n, mode=0, steps=1, seeding="leader", tier="device",
                                 policy={"relay": True, "collective": False}, **{k: v for k, v in HEADLINE.items()
                                                                                if k != "policy"})
     bound = predict_scaling.closed_form_ms(n, tier="device", mode0=True)
     for ms in r["model_ms"]:
-        assert bound * 0.999 <= ms <= bound * 1.08, (n, r["model_ms"], bound)
+        assert bound * 0.999 <= ms <= bound * 1.03, (n, r["model_ms"], bound)
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-def test_mode2_pull_schedule_within_bound(n):
+def test_mode2_pull_schedule_within_3pct_of_the_bound(n):
     """Mode 2 (pull / steal, node.go:741-807, :909-1073) on the headline
-    workload: jobs are dispatched as acks return, so links see gaps the
-    static plans do not have; it stays within 10 % of the same bound."""
+    workload: jobs are dispatched as acks return, yet it stays within 3 % of
+    the same bound (measured +0.39 / 0.28 / 0.56 % at N = 2 / 4 / 8), every
+    session. Two things keep its links fed (scripts/sim_timeline.py showed
+    the idle stretches): pull batches are job-major on the lanes
+    (Message.order), and a rank's loads of its own layers never queue whole
+    layers on its copy queue ahead of the chunks its sends wait for
+    (PlannedEngine kPromoteAhead). Before: 224-241 ms at N = 8."""
     r = predict_scaling.predict(n, mode=2, steps=1, **HEADLINE)
     bound = predict_scaling.closed_form_ms(n)
     for ms in r["model_ms"]:
-        assert bound * 0.999 <= ms <= bound * 1.10, (n, r["model_ms"], bound)
+        assert bound * 0.999 <= ms <= bound * 1.03, (n, r["model_ms"], bound)
 
 
 def test_upper_bounds_catch_serialized_lanes():
     """The bounds above have teeth: with every rank's comm lanes forced onto
     one queue (SimTiming.serialize_lanes - as if the 14 lanes of N = 8 were
-    one stream) the same schedule misses the 5 % bound by far."""
+    one stream) the same schedule misses the 3 % bound by far."""
     bound = predict_scaling.closed_form_ms(8)
     r = predict_scaling.predict(8, mode=1, steps=1, warmup=0, serialize_lanes=True, **HEADLINE)
     assert min(r["model_ms"]) > 1.5 * bound, (r["model_ms"], bound)

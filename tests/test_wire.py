@@ -99,3 +99,32 @@ def test_json_unicode_and_big_ints(core):
     s = '{"a":"\\u00e9\\ud83d\\ude00","b":18446744073709551615,"c":-5,"d":1.5e3}'
     out = json.loads(core.json_roundtrip(s))
     assert out == {"a": "é😀", "b": 18446744073709551615, "c": -5, "d": 1500.0}
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_xfer_batch_fast_path_matches_dom(core, order):
+    """Transfer batches are written straight to text and read back by a cursor
+    (wire.cc fast path): the text must equal the JSON DOM's, and both decoders
+    give back every job field, the CRCs and the lane order (Message.order:
+    1 = job-major lanes for mode-2 pull batches, omitted when 0)."""
+    m = _msg(core, core.MsgType.XferBatch, src=0, epoch=3, batch=7, order=order)
+    jobs = []
+    for k in range(3):
+        j = core.XferJob()
+        j.seq, j.src, j.dst, j.layer = 10 + k, k, k + 1, 40 + k
+        j.offset, j.size, j.total, j.chunk_bytes = k * 4096, 8192, 65536, 4096
+        j.crc = [0xDEADBEEF, k, 0xFFFFFFFF]
+        j.rate = 0 if k else 123456
+        jobs.append(j)
+    m.jobs = jobs
+    text = core.encode_envelope(m)
+    env = json.loads(text)
+    assert ("Order" in env["payload"]) == (order == 1)
+    assert core.json_roundtrip(text.decode()) == text.decode()  # sorted keys, no whitespace: the DOM's own text
+    for back in (core.decode_envelope(text.decode()), core.decode_envelope_text(text.decode())):
+        assert back.type == core.MsgType.XferBatch and back.batch == 7 and back.order == order and back.epoch == 3
+        got = [(j.seq, j.src, j.dst, j.layer, j.offset, j.size, j.total, j.chunk_bytes, list(j.crc), j.rate)
+               for j in back.jobs]
+        want = [(j.seq, j.src, j.dst, j.layer, j.offset, j.size, j.total, j.chunk_bytes, list(j.crc), j.rate)
+                for j in jobs]
+        assert got == want
