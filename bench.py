@@ -71,6 +71,9 @@ def parse_args(argv=None):
                         "profiles/r5_predict_mode2_windows.jsonl). REAL-NODE GUESS: settled by "
                         "config.per_link_busy_GBps in mode 2")
     p.add_argument("--storage", default="", help="disk tier directory")
+    p.add_argument("--allow-buffered", action="store_true",
+                   help="--tier disk: accept a run whose layer files sit on a memory file system or were read "
+                        "without O_DIRECT (the JSON says so); by default such a run fails, since its rate is not a disk's")
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0: scatter+relay P2P, ncclBroadcast, or leader fan-out")
     p.add_argument("--pack", default="none", choices=["none", "fp8"],
@@ -322,6 +325,26 @@ def worker(args, world, rank, chan) -> int:
         dist.all_gather_object(rates, mine)
         got = [r for r in rates if r]
         disk_gbps, disk_source = (min(got), "measured") if got else (13.3, "default")
+    disk_info = {}
+    if args.tier == "disk":
+        from distributed_llm_dissemination_amd.utils.diskprobe import refusal, storage_info
+
+        st = storage_info(args.storage or os.path.join(os.getcwd(), "storage"))
+        from distributed_llm_dissemination_amd.utils.config import SOURCE_DISK
+
+        mine_bytes = sum(cfg.node(rank).initial_layers.get(SOURCE_DISK, {}).values())
+        fit = int(st["avail_bytes"] * 0.97 // layer_bytes)
+        disk_info = {"storage_fs": st["fs"], "storage_device": st["device"], "storage_mount": st["mount"],
+                     "storage_avail_GB": round(st["avail_bytes"] / 1e9, 1), "layers_fit_on_storage": fit}
+        log(f"disk tier on {st['mount']} ({st['fs']}, {st['device']}): {st['avail_bytes'] / 1e9:.1f} GB free, "
+            f"this rank writes {mine_bytes / 1e9:.1f} GB")
+        why = refusal(st["fs"], "o_direct", args.allow_buffered)
+        if why:
+            failed(f"--tier disk: {why}; pass --allow-buffered to run anyway")
+        if mine_bytes > st["avail_bytes"] * 0.97:
+            failed(f"--tier disk: this rank's {mine_bytes / 1e9:.1f} GB of layer files do not fit the "
+                   f"{st['avail_bytes'] / 1e9:.1f} GB free on {st['mount']} (at most {fit} layers of "
+                   f"{args.layer_mib} MiB): pass --layers {fit} or another --storage")
     rt = Runtime(cfg, rank, engine="rccl", transport="tcp", chunk_bytes=args.chunk_mib << 20,
                  verify=True, payload_seed=0, registry={rank: listen_addr(bool(hosts))},
                  barrier=barrier, nccl_uid=uid, device=local_rank, storage_path=args.storage, pack=args.pack,
@@ -361,8 +384,12 @@ def worker(args, world, rank, chan) -> int:
                   relay=args.bcast == "relay", collective=args.bcast == "collective",
                   adapt_links=True, hierarchical=True)
 
+    cache_left = []  # --tier disk: fraction of a layer file still in the page cache before each session
+
     def step(timed: bool, i: int):
         beat(f"{'step' if timed else 'warmup'} {i}")
+        if args.tier == "disk":
+            cache_left.append(rt.drop_disk_cache())  # conf/exe.sh:17: every run starts cold
         rt.prepare(args.mode, **policy)
         barrier()
         torch.cuda.synchronize()
@@ -384,12 +411,33 @@ def worker(args, world, rank, chan) -> int:
     times = []
     plans = []  # leader (rank 0): the plan of every timed step - it runs after "timer start"
     last = None
+    disk_bytes = {"direct": 0, "buffered": 0}
     for i in range(args.steps):
         dt, last = step(True, i)
         times.append(dt)
         plans.append(last)
+        disk_bytes["direct"] += last.engine_stats.get("disk_direct_bytes", 0)
+        disk_bytes["buffered"] += last.engine_stats.get("disk_buffered_bytes", 0)
         log(f"step {i}: {dt * 1e3:.1f} ms ({total_bytes / dt / 1e9:.1f} GB/s) ttd={last.time_to_deliver_s * 1e3:.1f} ms")
     beat("measured")
+    if args.tier == "disk":
+        if world > 1:
+            got = [None] * world
+            dist.all_gather_object(got, (disk_bytes, max(cache_left, default=-1.0)))
+            disk_bytes = {k: sum(g[0][k] for g in got) for k in disk_bytes}
+            left = max(g[1] for g in got)
+        else:
+            left = max(cache_left, default=-1.0)
+        from distributed_llm_dissemination_amd.utils.diskprobe import read_mode, refusal
+
+        mode_ = read_mode(disk_bytes["direct"], disk_bytes["buffered"])
+        disk_info.update({"disk_read_mode": mode_, "disk_direct_GB": round(disk_bytes["direct"] / 1e9, 2),
+                          "disk_buffered_GB": round(disk_bytes["buffered"] / 1e9, 2),
+                          "page_cache_dropped": left >= 0, "page_cache_resident_max": round(left, 4)})
+        why = refusal(disk_info["storage_fs"], mode_, args.allow_buffered)
+        if why:
+            failed(f"--tier disk: {why} ({disk_bytes['buffered'] / 1e9:.1f} GB buffered); pass --allow-buffered "
+                   f"to report it anyway")
     total = sum(times)
     # Per directed link over the timed steps: bytes this rank sent to each peer,
     # and the device time of the P2P groups that sent to it.
@@ -447,7 +495,7 @@ def worker(args, world, rank, chan) -> int:
                 "pack": args.pack,
                 "payload": "bf16 layer shards as raw bytes, moved bit-exact (CRC32C per chunk)",
                 **({"host_share": True} if args.host_share else {}),
-                **({"node_disk_GBps": round(disk_gbps, 2), "node_disk_source": disk_source}
+                **({"node_disk_GBps": round(disk_gbps, 2), "node_disk_source": disk_source, **disk_info}
                    if args.tier == "disk" else {}),
             },
         }

@@ -257,6 +257,8 @@ PYBIND11_MODULE(_core, m) {
       .def("register_pipe", &Transport::register_pipe)
       .def("address", &Transport::address)
       .def("set_registry", &Transport::set_registry)
+      .def("set_max_envelope", &Transport::set_max_envelope, "largest control envelope a peer may send (bytes)")
+      .def("set_max_payload", &Transport::set_max_payload, "largest layer message DataSize / TotalSize (bytes)")
       .def("add_peer", &Transport::add_peer)
       .def("registry", &Transport::registry)
       .def_property_readonly("bytes_sent", [](const Transport& t) { return t.bytes_sent.load(); })
@@ -296,6 +298,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("poison", &PlannedConfig::poison)
       .def_readwrite("max_inflight_groups", &PlannedConfig::max_inflight_groups)
       .def_readwrite("group_peers", &PlannedConfig::group_peers)
+      .def_readwrite("disk_o_direct", &PlannedConfig::disk_o_direct)
       .def_readwrite("disk_readers", &PlannedConfig::disk_readers)
       .def_readwrite("disk_ring", &PlannedConfig::disk_ring)
       .def_readwrite("pack", &PlannedConfig::pack)
@@ -365,6 +368,8 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("comm_reform_ms", &PlannedStats::comm_reform_ms)
       .def_readonly("paced", &PlannedStats::paced)
       .def_readonly("disk_wait_ms", &PlannedStats::disk_wait_ms)
+      .def_readonly("disk_direct_bytes", &PlannedStats::disk_direct_bytes)
+      .def_readonly("disk_buffered_bytes", &PlannedStats::disk_buffered_bytes)
       .def_readonly("order_violations", &PlannedStats::order_violations);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")
       .def("provision", [](PlannedEngine& e, LayerID l, int64_t n) {
@@ -439,6 +444,14 @@ PYBIND11_MODULE(_core, m) {
   // Virtual clock (core/vclock.h): the simulator in model time. Python threads
   // that drive a session's ranks are counted by the clock between adopt() and
   // release() (reserve first, from the thread that starts them).
+  m.def("file_cache_drop", [](const std::string& p) {
+    py::gil_scoped_release nogil;
+    return file_cache_drop(p);
+  }, "write back and evict a file's page-cache pages; returns the fraction still resident");
+  m.def("file_cache_resident", [](const std::string& p) {
+    py::gil_scoped_release nogil;
+    return file_cache_resident(p);
+  }, "fraction of a file's pages in the page cache (mincore)");
   m.def("vclock_enable", [](bool on) { vclock::enable(on); });
   m.def("vclock_enabled", &vclock::enabled);
   m.def("vclock_now", &vclock::now, "seconds: model time when the virtual clock is on, else the steady clock");

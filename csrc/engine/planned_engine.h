@@ -76,6 +76,7 @@ struct PlannedConfig {
   std::map<NodeID, int64_t> link_rate;  // cap this rank's sends to a node (B/s; slow-link injection)
   int group_peers = 1;             // ops per peer and direction per group
   int disk_readers = 4;            // NVMe reader threads (O_DIRECT pread into pinned bounce buffers)
+  bool disk_o_direct = true;       // false: buffered preads (tests of the fallback reporting)
   int disk_ring = 8;               // pinned bounce buffers of chunk_bytes each
   // One NVMe shared by every rank of the node: > 0 paces this rank's disk
   // reads through a node-wide budget of this many B/s (engine/node_pacer.h),
@@ -166,6 +167,9 @@ struct PlannedStats {
   double comm_reform_ms = 0;  // last elastic re-form (abort + re-init after a shrink)
   int64_t paced = 0;  // issue attempts a token bucket deferred
   double disk_wait_ms = 0;  // time disk reads waited for the node-wide read budget
+  // disk-tier bytes read with O_DIRECT (past every page cache of this OS) and
+  // buffered (the filesystem refused O_DIRECT: they may come from memory)
+  int64_t disk_direct_bytes = 0, disk_buffered_bytes = 0;
   int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
   // device time the verify stream spent on checks (landing met -> check done):
   // against the session's wall time, the occupancy of the verify CUs

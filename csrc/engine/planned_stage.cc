@@ -218,6 +218,7 @@ void PlannedEngine::pump_disk() {
 
 void PlannedEngine::reader_loop() {
   std::map<std::string, int> fds;
+  std::map<std::string, bool> direct;  // path -> opened with O_DIRECT
   for (;;) {
     DiskRead d;
     {
@@ -229,8 +230,16 @@ void PlannedEngine::reader_loop() {
     }
     int& fd = fds[d.path];
     if (fd <= 0) {
-      fd = ::open(d.path.c_str(), O_RDONLY | O_DIRECT | O_CLOEXEC);
-      if (fd < 0) fd = ::open(d.path.c_str(), O_RDONLY | O_CLOEXEC);  // e.g. tmpfs: no O_DIRECT
+      fd = cfg_.disk_o_direct ? ::open(d.path.c_str(), O_RDONLY | O_DIRECT | O_CLOEXEC) : -1;
+      direct[d.path] = fd >= 0;
+      if (fd < 0) {
+        // e.g. an old tmpfs: no O_DIRECT. Still read, but say so: these bytes
+        // may come from the page cache, and the stats count them apart
+        // (disk_buffered_bytes; bench.py refuses such a run without --allow-buffered).
+        fd = ::open(d.path.c_str(), O_RDONLY | O_CLOEXEC);
+        if (cfg_.disk_o_direct)
+          log::warn(int64_t(self_node_)).s("path", d.path).msg("O_DIRECT refused: buffered disk reads");
+      }
     }
     // O_DIRECT needs 4 KiB aligned lengths; the bounce buffer holds a whole chunk.
     const int64_t want = std::min<int64_t>(((d.len + 4095) / 4096) * 4096, cfg_.chunk_bytes);
@@ -246,6 +255,10 @@ void PlannedEngine::reader_loop() {
       got += r;
     }
     d.ok = got >= d.len;
+    {
+      std::lock_guard<std::mutex> lk(stats_mu_);
+      (direct[d.path] ? stats_.disk_direct_bytes : stats_.disk_buffered_bytes) += got;
+    }
     {
       std::lock_guard<std::mutex> lk(disk_mu_);
       disk_done_.push_back(std::move(d));

@@ -1,5 +1,10 @@
 #include "store/store.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -165,6 +170,40 @@ int64_t LayerStore::landed_bytes(LayerID id) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = slots_.find(id);
   return it == slots_.end() ? 0 : it->second.landed.covered();
+}
+
+double file_cache_resident(const std::string& path) {
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -1;
+  struct stat st {};
+  double frac = -1;
+  if (fstat(fd, &st) == 0 && st.st_size > 0) {
+    void* p = mmap(nullptr, size_t(st.st_size), PROT_READ, MAP_SHARED, fd, 0);
+    if (p != MAP_FAILED) {
+      const long page = sysconf(_SC_PAGESIZE);
+      const size_t pages = (size_t(st.st_size) + size_t(page) - 1) / size_t(page);
+      std::vector<unsigned char> v(pages);
+      if (mincore(p, size_t(st.st_size), v.data()) == 0) {
+        size_t in = 0;
+        for (unsigned char b : v) in += b & 1;
+        frac = double(in) / double(pages);
+      }
+      munmap(p, size_t(st.st_size));
+    }
+  } else if (st.st_size == 0) {
+    frac = 0;
+  }
+  ::close(fd);
+  return frac;
+}
+
+double file_cache_drop(const std::string& path) {
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -1;
+  (void)fdatasync(fd);  // dirty pages cannot be dropped
+  (void)posix_fadvise(fd, 0, 0, POSIX_FADV_DONTNEED);
+  ::close(fd);
+  return file_cache_resident(path);
 }
 
 }  // namespace dissem

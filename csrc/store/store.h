@@ -78,4 +78,12 @@ class LayerStore {
   std::map<LayerID, Slot> slots_;
 };
 
+// Disk-tier layer files and this OS's page cache (reference: conf/exe.sh:17
+// drops every cache before a run). file_cache_drop writes back and evicts the
+// file's cached pages (fdatasync + POSIX_FADV_DONTNEED); both return the
+// fraction of the file's pages still resident (mincore), so a benchmark can
+// show its reads did not come from memory. -1: the file could not be mapped.
+double file_cache_drop(const std::string& path);
+double file_cache_resident(const std::string& path);
+
 }  // namespace dissem

@@ -408,17 +408,65 @@ class TcpTransport : public Transport {
     return true;
   }
 
+  // Framing: the extent of the next envelope (a JSON object) in the growing
+  // receive buffer, resumed where the previous call stopped - a rescan from
+  // the start on every recv is quadratic in an envelope's size. Strings and
+  // escapes are tracked so braces inside them do not count; the decoder
+  // validates the rest.
+  class EnvelopeScan {
+   public:
+    // End of the first complete object in buf[0, len), or 0 while incomplete.
+    size_t next(const char* buf, size_t len) {
+      for (; pos_ < len; ++pos_) {
+        const char c = buf[pos_];
+        if (str_) {
+          if (esc_) esc_ = false;
+          else if (c == '\\') esc_ = true;
+          else if (c == '"') str_ = false;
+          continue;
+        }
+        if (depth_ == 0 && c != '{') {
+          if (c == ' ' || c == '\n' || c == '\r' || c == '\t') continue;
+          throw std::runtime_error("envelope does not start with '{'");
+        }
+        if (c == '"') {
+          str_ = true;
+        } else if (c == '{' || c == '[') {
+          if (++depth_ > 256) throw std::runtime_error("envelope nesting too deep");
+        } else if (c == '}' || c == ']') {
+          if (--depth_ == 0) {
+            const size_t end = pos_ + 1;
+            *this = EnvelopeScan();
+            return end;
+          }
+        }
+      }
+      return 0;
+    }
+
+   private:
+    size_t pos_ = 0;
+    int depth_ = 0;
+    bool str_ = false, esc_ = false;
+  };
+
   void read_loop(int fd, uint64_t id) {
     std::string buf;
+    EnvelopeScan scan;
     for (;;) {
       size_t used = 0;
       try {
-        used = Json::scan_prefix(buf.data(), buf.size());  // one envelope's extent, no DOM
+        used = scan.next(buf.data(), buf.size());
       } catch (const std::exception& e) {
         log::error(-1).s("error", e.what()).msg("failed to decode envelope");
         break;
       }
       if (used == 0) {
+        if (int64_t(buf.size()) > max_envelope_.load()) {
+          log::error(-1).i("bytes", int64_t(buf.size())).i("limit", max_envelope_.load())
+              .msg("envelope larger than the limit: disconnecting the peer");
+          break;
+        }
         if (!fill(fd, buf, buf.size() + 1)) break;
         continue;
       }
@@ -446,6 +494,16 @@ class TcpTransport : public Transport {
   }
 
   bool receive_layer(int fd, std::string& buf, MessagePtr m) {
+    // A header's sizes come from the wire: check them before anything is
+    // allocated or written (a lying peer must not make this process reserve
+    // its DataSize, nor land bytes past its TotalSize).
+    const int64_t cap = max_payload_.load();
+    if (m->data_size < 0 || m->offset < 0 || m->total_size < 0 || m->data_size > cap || m->total_size > cap ||
+        (m->total_size > 0 && m->offset + m->data_size > m->total_size)) {
+      log::error(-1).i("layerID", int64_t(m->layer)).i("layer_size", m->data_size).i("total_size", m->total_size)
+          .i("offset", m->offset).i("limit", cap).msg("refused layer header: disconnecting the peer");
+      return false;
+    }
     log::info(-1).i("layerID", int64_t(m->layer)).i("layer_size", m->data_size).i("total_size", m->total_size)
         .msg("start receiving layer");
     int64_t t0 = log::now_us();

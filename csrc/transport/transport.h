@@ -108,6 +108,15 @@ class Transport {
   std::atomic<int64_t> bytes_sent{0};
   std::atomic<int64_t> bytes_received{0};
 
+  // Limits on what a peer may make this transport buffer (TCP): one control
+  // envelope, and one layer message's payload (its DataSize / TotalSize - the
+  // runtime sets the largest layer of its config). A peer past either is
+  // disconnected before anything is allocated.
+  static constexpr int64_t kDefaultMaxEnvelope = 64ll << 20;
+  static constexpr int64_t kDefaultMaxPayload = 64ll << 30;
+  void set_max_envelope(int64_t n) { max_envelope_ = n; }
+  void set_max_payload(int64_t n) { max_payload_ = n; }
+
  protected:
   bool lookup(NodeID id, std::string* addr) const {
     std::lock_guard<std::mutex> lk(reg_mu_);
@@ -131,6 +140,8 @@ class Transport {
   LandingFn landing_;
   ProgressFn progress_;
   BlockingQueue<MessagePtr> inbox_;
+  std::atomic<int64_t> max_envelope_{kDefaultMaxEnvelope};
+  std::atomic<int64_t> max_payload_{kDefaultMaxPayload};
 };
 
 std::shared_ptr<Transport> make_inproc_transport(const std::string& addr, const AddrRegistry& reg);

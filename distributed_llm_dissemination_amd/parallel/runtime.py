@@ -241,6 +241,7 @@ class Runtime:
         self.link_slow_streak: Dict[tuple, int] = {}  # (dir, peer): observations below LINK_SLOW x the median
         self.link_level: Dict[str, float] = {}  # dir -> the uniform level every normal link reports (B/s)
         self._links0: Optional[Dict[str, Dict[int, float]]] = None
+        self.disk_paths: List[str] = []  # this rank's disk-tier layer files
 
         reg = dict(registry) if registry is not None else cfg.registry()
         if transport == "inproc":
@@ -250,6 +251,9 @@ class Runtime:
             self.transport = _core.tcp_transport(addr, reg)
             reg[node_id] = self.transport.address()
             self.transport.set_registry(reg)
+            # a layer message's sizes come from the wire: nothing larger than this
+            # config's largest layer is accepted (tcp.cc receive_layer)
+            self.transport.set_max_payload(max([cfg.layer_size, *cfg.layer_sizes().values()]))
 
         if engine in ("rccl", "sim"):
             pcfg = _core.PlannedConfig()
@@ -399,6 +403,7 @@ class Runtime:
                     layers[l] = _core.LayerSrc.client(size, rate)
                 elif st == SOURCE_DISK or (self.storage_path and st != SOURCE_DEVICE):
                     path = self._disk_layer(l, size, seed)
+                    self.disk_paths.append(path)
                     # the file holds the source bytes; the layer's size is its slot size
                     layers[l] = _core.LayerSrc.disk(path, self.slot_sizes[l], rate, _core.SourceType(st))
                     if gpu:
@@ -668,6 +673,16 @@ class Runtime:
                     f.write(self._source_bytes(layer, size, seed, off, n))
             os.replace(tmp, path)
         return path
+
+    def drop_disk_cache(self) -> float:
+        """Write back and evict this rank's disk-tier layer files from the page
+        cache (the reference drops every cache before a run, conf/exe.sh:17);
+        returns the largest fraction of any file still resident afterwards
+        (0.0 = every read of the next session goes to the device; -1: no files)."""
+        worst = -1.0
+        for p in self.disk_paths:
+            worst = max(worst, _core.file_cache_drop(p))
+        return worst
 
     # ---------------------------------------------------------- sessions
     def run(self, mode: int, *, timeout: float = 600.0, **policy) -> SessionResult:
@@ -983,6 +998,7 @@ class Runtime:
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
                       "suspects", "shrinks", "aborted_pieces", "paced", "order_violations", "disk_wait_ms",
+                      "disk_direct_bytes", "disk_buffered_bytes",
                       "group_us_hist", "land_us_hist", "verify_busy_ms", "verify_calls", "verify_chunks")
         }
 

@@ -13,6 +13,11 @@ is bin/diskspeed.
 
 Returns None where O_DIRECT is not available (tmpfs, some overlay mounts): the
 caller keeps its default then.
+
+``storage_info`` says what a directory sits on (file system type, device,
+free bytes: /proc/mounts + statvfs), for the benchmark's JSON: a rate read
+from tmpfs, or through a loop device whose backing file the host caches, is
+not an NVMe rate.
 """
 
 from __future__ import annotations
@@ -21,9 +26,52 @@ import mmap
 import os
 import threading
 import time
-from typing import Optional
+from typing import Dict, Optional
 
 _ALIGN = 4096
+MEMORY_FS = {"tmpfs", "ramfs", "devtmpfs", "hugetlbfs"}
+
+
+def read_mode(direct_bytes: int, buffered_bytes: int) -> str:
+    """What a disk-tier session's reads were: "o_direct" (every byte past this
+    OS's page cache), "buffered" (none), "mixed", or "none" (nothing read)."""
+    if direct_bytes <= 0 and buffered_bytes <= 0:
+        return "none"
+    if buffered_bytes <= 0:
+        return "o_direct"
+    return "buffered" if direct_bytes <= 0 else "mixed"
+
+
+def refusal(fs: str, mode: str, allow_buffered: bool) -> Optional[str]:
+    """Why a disk-tier benchmark must not report its rate as a disk's (None: it may)."""
+    if allow_buffered:
+        return None
+    if fs in MEMORY_FS:
+        return f"the layer files sit on {fs} (memory), not a disk"
+    if mode in ("buffered", "mixed"):
+        return "layer files were read without O_DIRECT (the file system refused it): reads may come from memory"
+    return None
+
+
+def storage_info(directory: str) -> Dict[str, object]:
+    """The mount holding `directory`: {"fs", "device", "mount", "avail_bytes"}
+    (fs "?" when /proc/mounts is unreadable)."""
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.realpath(directory)
+    best = ("", "?", "?")
+    try:
+        with open("/proc/mounts") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) < 3:
+                    continue
+                dev, mnt, fs = parts[0], parts[1].replace("\\040", " "), parts[2]
+                if (path == mnt or path.startswith(mnt.rstrip("/") + "/")) and len(mnt) >= len(best[0]):
+                    best = (mnt, dev, fs)
+    except OSError:
+        pass
+    st = os.statvfs(path)
+    return {"fs": best[2], "device": best[1], "mount": best[0] or "?", "avail_bytes": st.f_bavail * st.f_frsize}
 
 
 def read_rate_gbps(directory: str, size_bytes: int = 1 << 30, block_bytes: int = 16 << 20,
@@ -37,14 +85,18 @@ def read_rate_gbps(directory: str, size_bytes: int = 1 << 30, block_bytes: int =
     path = os.path.join(directory, f".diskprobe.{os.getpid()}")
     bufs = [mmap.mmap(-1, block) for _ in range(max(1, readers))]  # page-aligned, as O_DIRECT needs
     try:
-        # bytes that do not compress or dedupe: a storage layer that does either
-        # would report a rate real layers never see
-        pattern = os.urandom(block)
+        # bytes that do not compress or dedupe - different in every block: a
+        # storage layer that did either would report a rate real layers never see
+        import numpy as np
+
+        rng = np.random.default_rng(int.from_bytes(os.urandom(8), "little"))
         fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
         try:
             for i in range(nblocks):
-                os.pwrite(fd, pattern, i * block)
+                os.pwrite(fd, rng.bytes(block), i * block)
             os.fsync(fd)
+            # the written pages must not serve the reads below from this OS's cache
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
         finally:
             os.close(fd)
         try:
