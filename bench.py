@@ -335,7 +335,8 @@ def worker(args, world, rank, chan) -> int:
         mine_bytes = sum(cfg.node(rank).initial_layers.get(SOURCE_DISK, {}).values())
         fit = int(st["avail_bytes"] * 0.97 // layer_bytes)
         disk_info = {"storage_fs": st["fs"], "storage_device": st["device"], "storage_mount": st["mount"],
-                     "storage_avail_GB": round(st["avail_bytes"] / 1e9, 1), "layers_fit_on_storage": fit}
+                     "storage_avail_GB": round(st["avail_bytes"] / 1e9, 1), "layers_fit_on_storage": fit,
+                     **({"storage_note": st["note"]} if "note" in st else {})}
         log(f"disk tier on {st['mount']} ({st['fs']}, {st['device']}): {st['avail_bytes'] / 1e9:.1f} GB free, "
             f"this rank writes {mine_bytes / 1e9:.1f} GB")
         why = refusal(st["fs"], "o_direct", args.allow_buffered)

@@ -733,7 +733,19 @@ bool PlannedEngine::issue_lane(int lane) {
       } else {
         recvd += p.len;
       }
-      xops.push_back(XOp{p.kind == Kind::Send, p.peer, L.dev + p.off, p.len, p.bcast});
+      uint8_t* at = L.dev + p.off;
+      if (p.kind == Kind::Recv && !p.bcast && p.full) {
+        // A chunk this rank stages (or reads from disk), or already holds: a
+        // mode-2 steal of a dest's own load, a re-dispatch. The peer's copy
+        // lands beside it, is checked there and dropped - the live slot keeps
+        // exactly one writer.
+        const uint8_t s = L.st[size_t(p.chunk)];
+        if (s == 1 || s == 2 || s == 3) {
+          p.scratch = backend_->alloc(p.len);
+          at = p.scratch;
+        }
+      }
+      xops.push_back(XOp{p.kind == Kind::Send, p.peer, at, p.len, p.bcast});
     }
     Ev g;
     {
@@ -758,7 +770,7 @@ bool PlannedEngine::issue_lane(int lane) {
       std::uniform_real_distribution<double> u(0.0, 1.0);
       for (auto& p : group) {
         if (p.kind != Kind::Recv || p.len < 4 || u(inject_rng_) >= cfg_.inject_corrupt) continue;
-        Ev c = backend_->corrupt(layers_[p.layer].dev + p.off, lane);
+        Ev c = backend_->corrupt(p.scratch ? p.scratch : layers_[p.layer].dev + p.off, lane);
         if (landed_ev != g) backend_->release(landed_ev);
         landed_ev = c;
         injected++;
@@ -771,6 +783,20 @@ bool PlannedEngine::issue_lane(int lane) {
     for (auto& p : group) {
       if (p.kind != Kind::Recv) continue;
       Layer& L = layers_[p.layer];
+      if (p.scratch) {
+        // the chunk's state stays its staging's; only the peer's copy is checked
+        PendingCheck pc;
+        pc.piece = p;
+        pc.wait = landed_ev;
+        if (cfg_.verify && p.has_crc) {
+          pc.slot = crc_slot();
+          pc.req = Backend::CheckReq{p.scratch, p.len, pc.slot};
+          pc.has_req = true;
+        }
+        pending_reqs_ += pc.has_req ? 1 : 0;
+        pending_checks_.push_back(pc);
+        continue;
+      }
       L.st[size_t(p.chunk)] = 1;
       L.rkey[size_t(p.chunk)] = key_of(p);
       if (lanes_ > 1 && !p.bcast) {
@@ -892,6 +918,19 @@ void PlannedEngine::poll() {
     for (size_t i = 0; i < it->pieces.size(); ++i) {
       const Piece& p = it->pieces[i];
       Layer& L = layers_[p.layer];
+      if (p.scratch) {
+        const bool bad = it->slots[i] != ~0u && backend_->crc_result(it->slots[i]) != p.crc;
+        backend_->free(p.scratch);
+        {
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          stats_.scratch_landings++;
+          stats_.verify_failures += bad ? 1 : 0;  // the peer's copy; the local one stands
+        }
+        // landed for the leader once the local copy is resident (its staging's check)
+        if (L.st[size_t(p.chunk)] == 2) landed(p);
+        else L.want[size_t(p.chunk)] = 1;
+        continue;
+      }
       if (it->slots[i] != ~0u) {
         uint32_t got = backend_->crc_result(it->slots[i]);
         if (got != p.crc) {

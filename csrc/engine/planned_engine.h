@@ -171,6 +171,7 @@ struct PlannedStats {
   // buffered (the filesystem refused O_DIRECT: they may come from memory)
   int64_t disk_direct_bytes = 0, disk_buffered_bytes = 0;
   int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
+  int64_t scratch_landings = 0;  // recvs of chunks already staged / resident here (landed in scratch)
   // device time the verify stream spent on checks (landing met -> check done):
   // against the session's wall time, the occupancy of the verify CUs
   double verify_busy_ms = 0;
@@ -255,6 +256,10 @@ class PlannedEngine : public DataEngine {
     int lane = 0;
     int64_t rate = 0;    // job pacing (B/s, 0 = unlimited)
     uint64_t batch = 0;  // add_batch ordinal (most significant part of the key)
+    // A recv of a chunk this rank is already staging, or holds: it lands in this
+    // scratch buffer instead of the live slot (issue_lane), so no byte of a
+    // chunk is ever written by two copies at once.
+    uint8_t* scratch = nullptr;
   };
   // Key: (batch, pidx, seq). Chunk-major batches (Message::order 0) set pidx to
   // the chunk index, job-major ones (order 1) to seq << 24 | chunk index.

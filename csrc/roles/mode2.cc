@@ -115,12 +115,11 @@ bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID
           eff(node_rate) < eff(sender_rate))
         continue;
       const NodeID dest = jd.first.first;
-      // planned engines: a dest's own load of a layer it holds (sender == dest,
-      // min_loaded_sender) is never stolen - that dest also stages the layer's
-      // chunks into the same HBM slot for its own sends, so a peer's transfer
-      // would write them a second time while they are being staged and checked
-      // (TSAN, the crossing mode-2 selftest)
-      if (e_->planned() && sender == dest) continue;
+      // A dest's own load of a layer it holds (sender == dest) is stolen like
+      // any job (node.go:1036-1042): e.g. a peer holding it in memory relieves
+      // a dest reading it from a slow tier. If that dest also stages the chunks
+      // (for its own sends), the peer's copy lands in scratch (PlannedEngine
+      // issue_lane), never a second time into the live slot.
       // several hosts: a job its dest's own host serves (xGMI) is not stolen across the network
       if (host_of(node) != host_of(dest) && host_of(sender) == host_of(dest) && multi_host()) continue;
       double ttf = perf_.count(sender) ? perf_[sender].first * double(load_[sender]) : 1e300;

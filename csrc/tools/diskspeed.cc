@@ -1,12 +1,17 @@
 // diskspeed: calibrate the NVMe -> pinned host -> HBM staging path
 // (reference: diskspeed/main.go, which only times a buffered ReadAt into RAM).
 //
-//   bin/diskspeed -path FILE [-chunk MiB] [-depth N] [-device D] [-no-direct]
+//   bin/diskspeed -path FILE [-path FILE ...] [-chunk MiB] [-depth N] [-device D] [-no-direct]
 //
-// Reports three rates: file -> pinned host (O_DIRECT preads on `depth` reader
-// threads), pinned host -> HBM (hipMemcpyAsync), and the overlapped pipeline
-// file -> pinned ring -> HBM, which is what the disk tier of the data engine
-// does. Use the numbers as `Sources` rates in a topology config.
+// Every -path adds a file (e.g. all layer files of a bench run: the rate over
+// tens of GiB, not the ramp of one file). Reports three rates over all of
+// them: file -> pinned host (O_DIRECT preads on `depth` reader threads),
+// pinned host -> HBM (hipMemcpyAsync), and the overlapped pipeline
+// file -> pinned ring -> HBM with `depth` readers, each handing its chunk to
+// the copy stream - what the disk tier of the data engine does (its reader
+// threads and bounce ring, planned_stage.cc). Evict the files from the page
+// cache first (bench.py does; Runtime.drop_disk_cache) or the first pass
+// reads memory. Use the numbers as `Sources` rates in a topology config.
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
 #include <sys/stat.h>
@@ -17,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -34,58 +40,73 @@ static double now() {
     }                                                                                \
   } while (0)
 
+struct Chunk {
+  int file;
+  int64_t off, len;
+};
+
 int main(int argc, char** argv) {
-  std::string path;
+  std::vector<std::string> paths;
   int64_t chunk = 64ll << 20;
   int depth = 4, device = 0;
   bool direct = true;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
-    if (a == "-path" && i + 1 < argc) path = argv[++i];
+    if (a == "-path" && i + 1 < argc) paths.push_back(argv[++i]);
     else if (a == "-chunk" && i + 1 < argc) chunk = atoll(argv[++i]) << 20;
     else if (a == "-depth" && i + 1 < argc) depth = atoi(argv[++i]);
     else if (a == "-device" && i + 1 < argc) device = atoi(argv[++i]);
     else if (a == "-no-direct") direct = false;
   }
-  if (path.empty()) {
-    printf("usage: -path [file path] [-chunk MiB] [-depth N] [-device D] [-no-direct]\n");
+  if (paths.empty() || depth < 1 || chunk <= 0) {
+    printf("usage: -path [file path] [-path ...] [-chunk MiB] [-depth N] [-device D] [-no-direct]\n");
     return 0;
   }
-  struct stat st;
-  if (stat(path.c_str(), &st) != 0) {
-    perror("stat");
-    return 1;
-  }
-  const int64_t size = st.st_size;
-  int fd = open(path.c_str(), O_RDONLY | (direct ? O_DIRECT : 0));
-  if (fd < 0 && direct) {
-    fprintf(stderr, "O_DIRECT not supported here, falling back to buffered reads\n");
-    direct = false;
-    fd = open(path.c_str(), O_RDONLY);
-  }
-  if (fd < 0) {
-    perror("open");
-    return 1;
+  std::vector<int> fds;
+  std::vector<Chunk> chunks;
+  int64_t total = 0;
+  for (size_t f = 0; f < paths.size(); ++f) {
+    struct stat st;
+    if (stat(paths[f].c_str(), &st) != 0) {
+      perror(paths[f].c_str());
+      return 1;
+    }
+    int fd = open(paths[f].c_str(), O_RDONLY | (direct ? O_DIRECT : 0));
+    if (fd < 0 && direct) {
+      fprintf(stderr, "O_DIRECT not supported here, falling back to buffered reads\n");
+      direct = false;
+      fd = open(paths[f].c_str(), O_RDONLY);
+    }
+    if (fd < 0) {
+      perror("open");
+      return 1;
+    }
+    fds.push_back(fd);
+    for (int64_t off = 0; off < st.st_size; off += chunk)
+      chunks.push_back(Chunk{int(f), off, std::min<int64_t>(chunk, st.st_size - off)});
+    total += st.st_size;
   }
   CHECK(hipSetDevice(device));
-  std::vector<void*> ring(static_cast<size_t>(depth));
+  const int ring_n = 2 * depth;  // pinned bounce buffers (the engine's disk_ring)
+  std::vector<void*> ring(static_cast<size_t>(ring_n));
   for (auto& p : ring) CHECK(hipHostMalloc(&p, size_t(chunk), hipHostMallocDefault));
+  const int dev_slots = 64;  // HBM destination: a 4 GiB ring at 64 MiB chunks, whatever the file sizes
   void* dev = nullptr;
-  CHECK(hipMalloc(&dev, size_t(size)));
+  CHECK(hipMalloc(&dev, size_t(chunk) * dev_slots));
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
-  const int64_t n = (size + chunk - 1) / chunk;
+  const int64_t n = int64_t(chunks.size());
 
   auto read_chunk = [&](int64_t c, void* buf) {
-    int64_t off = c * chunk, len = std::min(chunk, size - off);
-    int64_t want = direct ? ((len + 4095) / 4096) * 4096 : len;
+    const Chunk& k = chunks[size_t(c)];
+    int64_t want = direct ? ((k.len + 4095) / 4096) * 4096 : k.len;
     int64_t got = 0;
-    while (got < len) {
-      ssize_t r = pread(fd, static_cast<char*>(buf) + got, size_t(want - got), off + got);
+    while (got < k.len) {
+      ssize_t r = pread(fds[size_t(k.file)], static_cast<char*>(buf) + got, size_t(want - got), k.off + got);
       if (r <= 0) break;
       got += r;
     }
-    return len;
+    return k.len;
   };
 
   // 1) file -> pinned host, `depth` readers
@@ -97,40 +118,58 @@ int main(int argc, char** argv) {
       for (int64_t c; (c = next++) < n;) read_chunk(c, ring[size_t(r)]);
     });
   for (auto& t : th) t.join();
-  double t_read = now() - t0;
+  const double t_read = now() - t0;
 
-  // 2) pinned host -> HBM
+  // 2) pinned host -> HBM (the same number of chunks, from the ring)
   t0 = now();
-  for (int64_t c = 0; c < n; ++c) {
-    int64_t off = c * chunk, len = std::min(chunk, size - off);
-    CHECK(hipMemcpyAsync(static_cast<char*>(dev) + off, ring[size_t(c % depth)], size_t(len), hipMemcpyHostToDevice, s));
-  }
+  for (int64_t c = 0; c < n; ++c)
+    CHECK(hipMemcpyAsync(static_cast<char*>(dev) + (c % dev_slots) * chunk, ring[size_t(c % ring_n)],
+                         size_t(chunks[size_t(c)].len), hipMemcpyHostToDevice, s));
   CHECK(hipStreamSynchronize(s));
-  double t_h2d = now() - t0;
+  const double t_h2d = now() - t0;
 
-  // 3) overlapped: read chunk c+1.. while chunk c copies (ring of `depth` pinned buffers)
-  std::vector<hipEvent_t> ev(static_cast<size_t>(depth));
+  // 3) overlapped: `depth` readers, each reads its next chunk into a free ring
+  // slot and hands it to the copy stream; a slot is free again once its copy landed
+  std::vector<hipEvent_t> ev(static_cast<size_t>(ring_n));
   for (auto& e : ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  std::vector<bool> used(static_cast<size_t>(ring_n), false);
+  std::mutex mu;
+  next = 0;
+  th.clear();
   t0 = now();
-  for (int64_t c = 0; c < n; ++c) {
-    int slot = int(c % depth);
-    if (c >= depth) CHECK(hipEventSynchronize(ev[size_t(slot)]));
-    int64_t len = read_chunk(c, ring[size_t(slot)]);
-    CHECK(hipMemcpyAsync(static_cast<char*>(dev) + c * chunk, ring[size_t(slot)], size_t(len), hipMemcpyHostToDevice, s));
-    CHECK(hipEventRecord(ev[size_t(slot)], s));
-  }
+  for (int r = 0; r < depth; ++r)
+    th.emplace_back([&] {
+      for (int64_t c; (c = next++) < n;) {
+        const int slot = int(c % ring_n);
+        bool wait;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          wait = used[size_t(slot)];
+        }
+        if (wait) CHECK(hipEventSynchronize(ev[size_t(slot)]));
+        const int64_t len = read_chunk(c, ring[size_t(slot)]);
+        std::lock_guard<std::mutex> lk(mu);
+        CHECK(hipMemcpyAsync(static_cast<char*>(dev) + (c % dev_slots) * chunk, ring[size_t(slot)], size_t(len),
+                             hipMemcpyHostToDevice, s));
+        CHECK(hipEventRecord(ev[size_t(slot)], s));
+        used[size_t(slot)] = true;
+      }
+    });
+  for (auto& t : th) t.join();
   CHECK(hipStreamSynchronize(s));
-  double t_pipe = now() - t0;
+  const double t_pipe = now() - t0;
 
-  const double mib = double(size) / (1 << 20);
-  printf("File size: %lld\n", (long long)size);
+  const double mib = double(total) / (1 << 20);
+  printf("Files: %zu, bytes: %lld\n", paths.size(), (long long)total);
   printf("Time to load: %.3fs\n", t_read);
   printf("Throughput: %.2f MiB/s (file -> pinned host, %s, depth %d)\n", mib / t_read, direct ? "O_DIRECT" : "buffered",
          depth);
   printf("H2D: %.2f MiB/s (pinned -> HBM)\n", mib / t_h2d);
-  printf("Pipeline: %.2f MiB/s (file -> pinned ring -> HBM)\n", mib / t_pipe);
-  printf("{\"bytes\": %lld, \"read_MiBps\": %.1f, \"h2d_MiBps\": %.1f, \"pipeline_MiBps\": %.1f}\n", (long long)size,
-         mib / t_read, mib / t_h2d, mib / t_pipe);
-  close(fd);
+  printf("Pipeline: %.2f MiB/s (file -> pinned ring -> HBM, %d readers)\n", mib / t_pipe, depth);
+  printf("{\"files\": %zu, \"bytes\": %lld, \"direct\": %s, \"depth\": %d, \"read_GBps\": %.2f, \"h2d_GBps\": %.2f, "
+         "\"pipeline_GBps\": %.2f}\n",
+         paths.size(), (long long)total, direct ? "true" : "false", depth, double(total) / t_read / 1e9,
+         double(total) / t_h2d / 1e9, double(total) / t_pipe / 1e9);
+  for (int fd : fds) close(fd);
   return 0;
 }

@@ -71,7 +71,12 @@ def storage_info(directory: str) -> Dict[str, object]:
     except OSError:
         pass
     st = os.statvfs(path)
-    return {"fs": best[2], "device": best[1], "mount": best[0] or "?", "avail_bytes": st.f_bavail * st.f_frsize}
+    out = {"fs": best[2], "device": best[1], "mount": best[0] or "?", "avail_bytes": st.f_bavail * st.f_frsize}
+    if best[2] == "overlay" or best[1].startswith("/dev/loop"):
+        # what O_DIRECT cannot promise here: the layer below is the host's
+        out["note"] = ("container overlay / loop device: O_DIRECT bypasses this OS's page cache, but the store "
+                       "below it belongs to the host and may serve reads from the host's memory")
+    return out
 
 
 def read_rate_gbps(directory: str, size_bytes: int = 1 << 30, block_bytes: int = 16 << 20,

@@ -115,15 +115,18 @@ case "$RECIPE" in
     # every file's page-cache pages evicted before every session, O_DIRECT reads counted (the
     # JSON's disk_read_mode / storage_fs / page_cache_resident_max); DISK_LAYERS layers of 1 GiB
     # (80 when the disk holds them - the JSON's layers_fit_on_storage says what does), then
-    # bin/diskspeed on files of the same run (O_DIRECT at depth 4 and 8), after evicting them again
+    # bin/diskspeed over ALL files of the same run (O_DIRECT, 4 and 8 readers), evicted again first
     L=${DISK_LAYERS:-72}
     df -hT . > $OUT/df.txt 2>&1; lsblk -o NAME,SIZE,TYPE,ROTA,MOUNTPOINT >> $OUT/df.txt 2>&1
     timeout -k 10 900 python bench.py --tier disk --layers $L --steps 2 --warmup 1 \
       > $OUT/bench_disk.json 2> $OUT/bench_disk.log &&
-    python -c "import sys; sys.path.insert(0, '.'); from distributed_llm_dissemination_amd import _core; \
-print([round(_core.file_cache_drop(f'storage/layers/0/{l}.layer'), 4) for l in range($L)])" > $OUT/cache_drop.txt &&
-    timeout -k 10 120 bin/diskspeed -path storage/layers/0/0.layer > $OUT/diskspeed.log 2>&1 &&
-    timeout -k 10 120 bin/diskspeed -path storage/layers/0/1.layer -depth 8 > $OUT/diskspeed_d8.log 2>&1 &&
+    DROP="import sys; sys.path.insert(0, '.'); from distributed_llm_dissemination_amd import _core; \
+print(max(_core.file_cache_drop(f'storage/layers/0/{l}.layer') for l in range($L)))"
+    FILES=$(for l in $(seq 0 $((L - 1))); do echo "-path storage/layers/0/$l.layer"; done)
+    python -c "$DROP" > $OUT/cache_drop.txt &&
+    timeout -k 10 300 bin/diskspeed $FILES -depth 4 > $OUT/diskspeed_all_d4.log 2>&1 &&
+    python -c "$DROP" >> $OUT/cache_drop.txt &&
+    timeout -k 10 300 bin/diskspeed $FILES -depth 8 > $OUT/diskspeed_all_d8.log 2>&1 &&
     rm -rf storage
     ;;
   fp8)

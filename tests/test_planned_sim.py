@@ -158,16 +158,21 @@ def test_mode2_range_jobs(n):
 @pytest.mark.parametrize("n", [2, 4])
 def test_mode2_dest_holding_a_layer_loads_it_itself(n):
     """Every rank holds every layer (copies = n): mode 2 makes each dest load
-    its own copy (min_loaded_sender) and no peer steals such a job - that dest
-    also stages the layer's chunks into the same HBM slot for its own sends, so
-    a stolen job would write a chunk twice while it is being staged and checked
-    (TSAN caught it in the crossing selftest). No bytes cross ranks, every
-    byte is staged once per rank, and no send ever waits on a larger-key recv."""
+    its own copy first (min_loaded_sender), and an idle peer may steal such a
+    job as the reference allows (node.go:1036-1042). A rank whose chunk is
+    both staged here (for its own sends or load) and sent by a peer keeps one
+    writer per byte: the peer's copy lands in scratch (scratch_landings).
+    Every byte arrives (run_cluster compares every layer), every byte sent is
+    received, each chunk is held once per rank, and no send ever waits on a
+    larger-key recv."""
     cfg = make_workload(n, 6, 4 * MiB, tier="host", seeding="random", copies=n, chunk_bytes=MiB)
     outs, _ = run_cluster(cfg, 2, sessions=4, pull_window=2, pull_job_bytes=MiB)
     assert sum(r.engine_stats["order_violations"] for res in outs for r in res) == 0
-    assert sum(r.engine_stats["bytes_sent"] for res in outs for r in res) == 0
-    assert all(r.engine_stats["bytes_staged"] == 6 * 4 * MiB for res in outs for r in res)
+    for res in outs:
+        assert sum(r.engine_stats["bytes_sent"] for r in res) == sum(r.engine_stats["bytes_recv"] for r in res)
+        for r in res:  # staged or received - a scratch landing is a received duplicate of a staged chunk
+            held = r.engine_stats["bytes_staged"] + r.engine_stats["bytes_recv"] - r.engine_stats["scratch_landings"] * MiB
+            assert held == 6 * 4 * MiB, r.engine_stats
 
 
 def test_repeated_sessions_reset_state():
@@ -542,9 +547,9 @@ def test_mode0_host_share_layers_with_fewer_chunks_than_ranks():
 
 def test_mode2_planned_dest_loads_its_own_lower_tier_copy():
     """Mode 2 on the planned (GPU) engine: a dest that holds a layer in a lower
-    tier (pinned host) loads it itself rather than receiving it from a peer
-    into the HBM slot it is also staging (the race TSAN caught, round 3); the
-    peer sends nothing of it."""
+    tier (pinned host) loads it itself (min_loaded_sender); its one job is
+    dispatched at once (window 1), so there is nothing pending for the peer to
+    steal and the peer sends nothing of it."""
     cfg = make_workload(2, 2, 2 * MiB, tier="host", seeding="leader", chunk_bytes=MiB)
     cfg.assignment = {0: [0, 1], 1: [0]}
     cfg.nodes[1].initial_layers = {2: {0: 2 * MiB}}  # rank 1 holds layer 0 in host memory too
@@ -579,3 +584,26 @@ def test_single_rank_verifies_every_staged_byte_once(mode):
                 assert rt.layer_bytes(l) == expected_image(rt, l, size)
     finally:
         rt.close()
+
+
+def test_mode2_slow_self_load_is_stolen_by_a_faster_peer():
+    """rank 1 holds layer 0 in a slow tier (LimitRate 4 MB/s) and
+    must load it; rank 0 holds it in memory, unpaced. Rank 1 starts on its
+    first range job itself (min_loaded_sender, window 1); rank 0, done with its
+    own load, steals rank 1's pending ranges (node.go:1036-1042: the thief is
+    at least as fast) and sends them. Byte counters: rank 1 staged the chunks
+    of the ranges it started (the first, maybe one more before rank 0 is idle)
+    and received the others from rank 0, every chunk once; every byte of the
+    layer is checked at rank 1 (run_cluster)."""
+    from distributed_llm_dissemination_amd.utils.config import SOURCE_MEM
+
+    cfg = make_workload(2, 1, 4 * MiB, tier="host", seeding="leader", chunk_bytes=MiB)
+    cfg.assignment = {0: [0], 1: [0]}
+    cfg.nodes[1].initial_layers = {SOURCE_MEM: {0: 4 * MiB}}
+    cfg.nodes[1].sources = {SOURCE_MEM: 4_000_000}
+
+    (res,), _ = run_cluster(cfg, 2, pull_window=1, pull_job_bytes=MiB)
+    staged, recv = res[1].engine_stats["bytes_staged"], res[1].engine_stats["bytes_recv"]
+    assert MiB <= staged <= 2 * MiB and recv >= 2 * MiB, res[1].engine_stats  # the slow tier was relieved
+    assert staged + recv == 4 * MiB and res[1].engine_stats["scratch_landings"] == 0
+    assert res[0].engine_stats["bytes_sent"] == recv
