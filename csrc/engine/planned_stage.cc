@@ -320,7 +320,8 @@ void PlannedEngine::stage_from(Layer& L, LayerID id, int64_t c, const uint8_t* s
   }
   sc.piece = p;
   pending_checks_.push_back(sc);
-  if (++pending_reqs_ >= kVerifyBatch) flush_checks();
+  pending_reqs_ += sc.has_req ? 1 : 0;  // checks to launch, as issue_lane counts them
+  if (pending_reqs_ >= kVerifyBatch) flush_checks();
   if (bounce) {
     // The bounce buffer is free again once its H2D copy has landed - not after
     // the chunk's CRC check: the verify queue is in order, and a check queued

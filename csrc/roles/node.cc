@@ -446,17 +446,58 @@ int64_t Node::layer_size(LayerID l) {
 }
 
 // A directed link s -> d is timed at both ends: s reports it with its send
-// rates, d with its receive rates. Each end's P2P time includes waiting for the
-// other end to post, so the faster reading is the link's (the later poster
-// timed the transfer alone); the announces arrive in any order.
+// rates, d with its receive rates (the announces arrive in any order).
 void Node::merge_link_rates(NodeID src, const std::map<NodeID, int64_t>& out, const std::map<NodeID, int64_t>& in) {
-  for (auto& kv : out) {
-    int64_t& v = measured_links_[{src, kv.first}];
-    v = std::max(v, kv.second);
-  }
-  for (auto& kv : in) {
-    int64_t& v = measured_links_[{kv.first, src}];
-    v = std::max(v, kv.second);
+  for (auto& kv : out) reported_out_[{src, kv.first}] = kv.second;
+  for (auto& kv : in) reported_in_[{kv.first, src}] = kv.second;
+}
+
+// The rate a link is planned on. Each end's P2P time includes waiting for the
+// other end to post, so normally the FASTER reading is the link's (the later
+// poster timed the transfer alone: a late receiver must not read as a slow
+// link). But a rank reports one level for all its normal links
+// (Runtime.link_report), so a node whose egress is slow on EVERY link reports
+// a low level while each receiver still reports its own (fast) level until it
+// has flagged the link over LINK_SLOW_SESSIONS sessions: the faster reading
+// would hide it. A node whose level lies below kSlowNode of the median level
+// of its direction is such a node: its links plan on the SLOWER reading.
+void Node::merged_link_rates() {
+  constexpr double kSlowNode = 0.7;  // Runtime.LINK_SLOW
+  auto levels = [](const std::map<std::pair<NodeID, NodeID>, int64_t>& rep, bool by_src) {
+    std::map<NodeID, std::vector<int64_t>> per;
+    for (auto& kv : rep)
+      if (kv.second > 0) per[by_src ? kv.first.first : kv.first.second].push_back(kv.second);
+    std::map<NodeID, int64_t> lvl;
+    for (auto& kv : per) {
+      std::sort(kv.second.begin(), kv.second.end());
+      lvl[kv.first] = kv.second[kv.second.size() / 2];
+    }
+    return lvl;
+  };
+  auto slow_nodes = [&](const std::map<NodeID, int64_t>& lvl) {
+    std::vector<int64_t> v;
+    for (auto& kv : lvl) v.push_back(kv.second);
+    std::set<NodeID> slow;
+    if (v.empty()) return slow;
+    std::sort(v.begin(), v.end());
+    const double med = double(v[v.size() / 2]);
+    for (auto& kv : lvl)
+      if (double(kv.second) < kSlowNode * med) slow.insert(kv.first);
+    return slow;
+  };
+  const std::set<NodeID> slow_out = slow_nodes(levels(reported_out_, true));
+  const std::set<NodeID> slow_in = slow_nodes(levels(reported_in_, false));
+  measured_links_.clear();
+  for (auto& kv : reported_out_) measured_links_[kv.first] = kv.second;
+  for (auto& kv : reported_in_) {
+    auto it = measured_links_.find(kv.first);
+    if (it == measured_links_.end()) {
+      measured_links_[kv.first] = kv.second;
+    } else if (slow_out.count(kv.first.first) || slow_in.count(kv.first.second)) {
+      it->second = std::min(it->second, kv.second);
+    } else {
+      it->second = std::max(it->second, kv.second);
+    }
   }
 }
 
@@ -586,6 +627,7 @@ void Node::start_distribution() {
     sig_cv_.notify_all();
   }
   initial_status_ = status_;
+  merged_link_rates();
   if (cfg_.adapt_links && !measured_links_.empty()) {
     // Closed loop: plan on the capacities the senders measured (reported with
     // their announces) instead of the estimates; links nobody measured keep

@@ -243,7 +243,11 @@ class Node {
   };
   std::vector<PendingJob> pending_jobs_;
   uint64_t next_seq_ = 1, next_batch_ = 1;
-  std::map<std::pair<NodeID, NodeID>, int64_t> measured_links_;  // leader: reported link rates (B/s)
+  std::map<std::pair<NodeID, NodeID>, int64_t> measured_links_;  // leader: merged link rates (B/s, merged_link_rates)
+  // leader: per directed link, the sender's report (timed at the sending end)
+  // and the receiver's (timed at the receiving end)
+  std::map<std::pair<NodeID, NodeID>, int64_t> reported_out_, reported_in_;
+  void merged_link_rates();
   std::map<LayerID, CrcManifest> manifests_;  // whole copies' manifests
   std::map<LayerID, std::set<NodeID>> manifest_holders_;  // who announced a whole copy's manifest
   // chunk CRCs vouched for by partial copies: layer -> (grid, chunk -> crc)

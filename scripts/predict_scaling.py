@@ -57,6 +57,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others
+    (or a list of such pairs: several slow links)
     (slow_after_probe: only from the first session on - the probe saw it at full speed).
     plan_links: the leader's plan knows every link's capacity (config Links)
     and every GPU's staging rate, at the simulated (scaled) rates: mode 1 with
@@ -138,12 +139,10 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     t.serialize_lanes = serialize_lanes
     t.trace = trace
     t.link_bps = link_gbps * 1e9 / scale
-    slow = {}
-    if slow_link is not None:
-        (s, d), frac = slow_link
-        slow = {(s, d): link_gbps * 1e9 / scale * frac}
-        if not slow_after_probe:
-            t.link = slow
+    slows = _slow_list(slow_link)
+    slow = {(s, d): link_gbps * 1e9 / scale * frac for (s, d), frac in slows}
+    if slow and not slow_after_probe:
+        t.link = slow
     if recv_delay:
         t.recv_delay_s = dict(recv_delay)
     per_host = max(1, n // max(1, hosts))
@@ -163,8 +162,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
         nic_bw = int(nic_gbps * 1e9 / scale)
         cfg.links = {s: {d: (bw if host_of[s] == host_of[d] else min(bw, nic_bw)) for d in range(n) if d != s}
                      for s in range(n)}
-        if slow_link is not None:
-            (s, d), frac = slow_link
+        for (s, d), frac in slows:
             cfg.links[s][d] = int(bw * frac)
     disk = dict(storage_path=storage, node_disk_gbps=disk_gbps / scale, node_key=key) if tier == "disk" else {}
     virtual = _core.vclock_enabled()
@@ -305,6 +303,13 @@ def closed_form_ms(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, link
     return t * 1e3
 
 
+def _slow_list(slow_link):
+    """slow_link as a list of ((s, d), frac)."""
+    if not slow_link:
+        return []
+    return [slow_link] if isinstance(slow_link[0][0], int) else list(slow_link)
+
+
 def modeled_ms(link_bytes, staged, n, link_gbps, pcie_gbps, slow_link=None) -> float:
     """A load-independent lower bound of a session from its bytes accounting:
     the busiest directed link's bytes / its rate, or the busiest rank's staged
@@ -312,9 +317,7 @@ def modeled_ms(link_bytes, staged, n, link_gbps, pcie_gbps, slow_link=None) -> f
     simulated threads does not enter it)."""
     t = 0.0
     for (s, d), b in link_bytes.items():
-        rate = link_gbps * 1e9
-        if slow_link is not None and (s, d) == tuple(slow_link[0]):
-            rate *= slow_link[1]
+        rate = link_gbps * 1e9 * dict((tuple(k), f) for k, f in _slow_list(slow_link)).get((s, d), 1.0)
         t = max(t, b / rate)
     for b in staged:
         t = max(t, b / (pcie_gbps * 1e9))

@@ -390,3 +390,22 @@ def test_predicted_disk_tier_is_bound_by_the_node_nvme():
     assert sum(r["staged_GiB_last"]) == pytest.approx(16, rel=1e-3), r
     for ms in r["model_ms"]:
         assert bound * 0.99 <= ms / 1e3 <= bound * 1.05, (r["model_ms"], bound)
+
+
+def test_closed_loop_plans_a_node_with_slow_egress_on_every_link():
+    """node 0's egress runs at half speed on EVERY link. Node 0
+    reports one level for all its links - its own median, low - while each
+    receiver reports the link at its uniform (fast) level until it has
+    flagged it over two observations. Taking the faster of the two ends, as
+    for a late receiver, would hide the slow egress; a node whose level lies
+    below 0.7 of the median level is planned on the slower reading
+    (Node::merged_link_rates), so already the first session plans node 0's
+    links at their measured 25 GB/s and moves bytes off them."""
+    slow = [((0, d), 0.5) for d in range(1, 8)]
+    kw = dict(layers=32, mode=1, probe_mib=1024, **HEADLINE)
+    r = predict_scaling.predict(8, slow_link=slow, steps=1, warmup=0, **kw)
+    plan = r["plan_link_GBps_last"]
+    assert all(plan[f"0->{d}"] == pytest.approx(25.0, abs=0.5) for d in range(1, 8)), plan
+    assert all(plan[f"{s}->{d}"] == pytest.approx(50.0, abs=0.5) for s in range(1, 8) for d in range(8) if d != s), plan
+    blind = predict_scaling.predict(8, slow_link=slow, steps=1, warmup=0, adapt_links=False, **kw)
+    assert max(r["model_ms"]) < 0.8 * max(blind["model_ms"]), (r["model_ms"], blind["model_ms"])
