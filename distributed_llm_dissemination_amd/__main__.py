@@ -63,12 +63,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--engine", default="auto", choices=["auto", "host", "rccl"],
                    help="data plane: host (TCP into RAM, the reference) or rccl (RCCL/xGMI into HBM); "
                         "auto = rccl under torchrun with a GPU visible, else host")
-    p.add_argument("--transport", default=None, choices=["tcp", "rccl"], help="alias: tcp = --engine host")
     p.add_argument("--chunk-mib", type=int, default=64)
-    p.add_argument("--chunk-bytes", type=int, default=0, help="chunk grid in bytes (overrides --chunk-mib)")
     p.add_argument("--pack", default="none", choices=["none", "fp8"],
                    help="fp8: bf16 layers are packed to block-scaled e4m3fn on staging (wire + HBM format)")
-    p.add_argument("--pack-block", type=int, default=128, help="elements per fp8 scale")
     p.add_argument("--store", default="packed", choices=["packed", "bf16"],
                    help="with --pack fp8: bf16 = also keep each layer dequantized to bf16 in HBM (fused "
                         "verify+unpack kernel on every landed chunk)")
@@ -78,18 +75,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "tiny, llama3-8b, llama3-70b, llama3.1-405b; LayerSize must equal the preset's layer "
                         "bytes) instead of random bytes; after delivery each rank runs its layers' forward pass "
                         "on the received parameters")
-    p.add_argument("--streams-per-peer", type=int, default=1,
-                   help="P2P ops per peer and direction in one RCCL group")
-    p.add_argument("--reserve-cus", type=int, default=-1,
-                   help="rccl: CUs the verify/copy kernels leave free for RCCL when --verify-cus is 0 (-1: 32 "
-                        "with peers, else 0)")
     p.add_argument("--verify-cus", type=int, default=-1,
                    help="rccl: the verify stream runs on the last N CUs only, RCCL lanes and copies on the others "
                         "(-1: 32 - CUs 28-31 of each XCD - with peers, 128 with --store bf16, 0 alone; 0: shared)")
-    p.add_argument("--nccl-ctas", default="", metavar="MIN:MAX",
-                   help="rccl: communicator CTA bounds (ncclConfig minCTAs/maxCTAs; channels per P2P peer)")
-    p.add_argument("--nccl-register", action="store_true",
-                   help="rccl: register every HBM layer slot with the communicator (ncclCommRegister)")
     p.add_argument("--lanes", type=int, default=0,
                    help="rccl: independent comm lanes (RCCL communicator + HIP stream + dedicated HW queue "
                         "each); 0 = one lane per directed link on up to 8 ranks (14 at 8 ranks), world-1 "
@@ -100,10 +88,6 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--node-disk-gbps", type=float, default=0.0,
                    help="rccl: one NVMe shared by every rank of the node at this read rate (disk readers share it; "
                         "mode 3 plans it as one budget); 0 = per-rank disks")
-    p.add_argument("--comm-init", default="split", choices=["parallel", "split"],
-                   help="rccl: lane communicators split from the world communicator one by one (split, the "
-                        "default: faster at 8 shared ranks, profiles/r3_init2), or one unique id each, initialized "
-                        "together in one group (parallel)")
     p.add_argument("--suspect-timeout", type=float, default=10.0,
                    help="rccl: report a P2P group stalled this long to the leader, which probes the peers and "
                         "shrinks the communicator around dead ranks (elastic recovery; 0 = only on failure)")
@@ -111,7 +95,6 @@ def build_parser() -> argparse.ArgumentParser:
                    help="fault injection: drop-chunk=P | kill-rank=R@T | slow-link=S:D:RATE")
     p.add_argument("--job-timeout", type=float, default=0.0,
                    help="leader: re-dispatch a job not acked within this many seconds (+ bytes/--job-min-rate)")
-    p.add_argument("--job-min-rate", type=float, default=0.0)
     p.add_argument("--max-retries", type=int, default=4, help="CRC failures of one chunk before giving up")
     p.add_argument("--persist-dir", default="",
                    help="after delivery, write this node's layers + CRC manifest here; on start, announce "
@@ -123,34 +106,20 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--pull-window", type=int, default=1)
     p.add_argument("--pull-job-mib", type=int, default=0,
                    help="mode 2: split layers into jobs of this many MiB (0 = one job per layer, reference)")
-    p.add_argument("--no-relay", action="store_true", help="mode 0 on rccl: leader fan-out instead of relay")
     p.add_argument("--bcast", default="relay", choices=["relay", "collective", "fanout"],
                    help="mode 0 on rccl: relay = scatter + peer relay over all xGMI links; collective = "
                         "ncclBroadcast per layer; fanout = leader sends every copy")
-    p.add_argument("--xgmi-link-gbps", type=float, default=None,
-                   help="rccl: plan each GPU pair's link (probed xGMI topology) at this GB/s when the config has "
-                        "no Links (default 50; 0 = no link tier)")
-    p.add_argument("--pcie-gbps", type=float, default=None,
-                   help="rccl: plan each GPU's host->HBM staging at this GB/s (mode 3; default 55; 0 = unlimited)")
-    p.add_argument("--no-verify", action="store_true")
     p.add_argument("--timeout", type=float, default=3600.0)
     p.add_argument("--json-summary", action="store_true")
-    p.add_argument("--example-config", action="store_true")
-    p.add_argument("--log-file", default="")
     return p
 
 
 def engine_opts(args) -> dict:
-    """Planned-engine (rccl) knobs from the CLI."""
-    opts = {"reserve_cus": int(getattr(args, "reserve_cus", -1)),
-            "verify_cus": int(getattr(args, "verify_cus", -1)),
-            "suspect_s": getattr(args, "suspect_timeout", 10.0),
-            "nccl_register": bool(getattr(args, "nccl_register", False)), "lanes": int(getattr(args, "lanes", 0)),
-            "comm_init": getattr(args, "comm_init", "split")}
-    if getattr(args, "nccl_ctas", ""):
-        lo, _, hi = args.nccl_ctas.partition(":")
-        opts["nccl_min_ctas"], opts["nccl_max_ctas"] = int(lo or 0), int(hi or 0)
-    return opts
+    """Planned-engine (rccl) knobs from the CLI (bench.py shares them); the
+    other PlannedConfig fields keep their defaults - set them through
+    Runtime(engine_opts=...)."""
+    return {"verify_cus": int(getattr(args, "verify_cus", -1)), "suspect_s": getattr(args, "suspect_timeout", 10.0),
+            "lanes": int(getattr(args, "lanes", 0)), "comm_init": getattr(args, "comm_init", "split")}
 
 
 def nccl_ids(core, world: int, args) -> bytes:
@@ -162,13 +131,6 @@ def nccl_ids(core, world: int, args) -> bytes:
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL across rank processes
-    if args.example_config:
-        from .utils.config import example_config
-
-        print(json.dumps(example_config().to_json(), indent=2))
-        return 0
-    if args.transport:
-        args.engine = "host" if args.transport == "tcp" else "rccl"
     torchrun_rank = os.environ.get("RANK")
     if args.engine == "auto":
         args.engine = "host"
@@ -186,8 +148,6 @@ def main(argv=None) -> int:
     from .utils.config import ConfigError, load_config
 
     _core.set_log_level(0 if args.v else 1)  # cmd/main.go:38-42
-    if args.log_file:
-        _core.set_log_file(args.log_file)
     try:
         cfg = load_config(args.f)
         leader = cfg.leader()
@@ -263,11 +223,11 @@ def main(argv=None) -> int:
                   f"(layers {sorted(bad)[:8]} differ)", file=sys.stderr)
             return 2
     rt = Runtime(cfg, my_id, engine=args.engine, storage_path=args.s,
-                 chunk_bytes=args.chunk_bytes or (args.chunk_mib << 20),
-                 verify=not args.no_verify and args.verify != "none", registry=registry, barrier=barrier,
-                 nccl_uid=uid, device=device, pack=args.pack, pack_block=args.pack_block, store=args.store,
+                 chunk_bytes=args.chunk_mib << 20,
+                 verify=args.verify != "none", registry=registry, barrier=barrier,
+                 nccl_uid=uid, device=device, pack=args.pack, store=args.store,
                  inject_corrupt=faults.drop_chunk, max_retries=args.max_retries,
-                 host_link_rate=faults.link_rates_from(my_id), group_peers=args.streams_per_peer,
+                 host_link_rate=faults.link_rates_from(my_id),
                  persist_dir=args.persist_dir,
                  engine_opts={**engine_opts(args), "link_rate": faults.link_rates_from(my_id)},
                  host_share=args.host_share and args.engine == "rccl", node_disk_gbps=args.node_disk_gbps,
@@ -303,10 +263,8 @@ def main(argv=None) -> int:
     if args.owner_policy is None:
         args.owner_policy = "links" if args.engine == "rccl" else "random"
     policy = dict(seed=args.seed, owner_policy=args.owner_policy, pull_window=args.pull_window,
-                  relay=not args.no_relay and args.bcast != "fanout", collective=args.bcast == "collective",
-                  job_timeout_s=args.job_timeout, job_min_rate=args.job_min_rate,
-                  pull_job_bytes=args.pull_job_mib << 20, xgmi_link_gbps=args.xgmi_link_gbps,
-                  stage_gbps=args.pcie_gbps)
+                  relay=args.bcast != "fanout", collective=args.bcast == "collective",
+                  job_timeout_s=args.job_timeout, pull_job_bytes=args.pull_job_mib << 20)
     rt.prepare(args.m, **policy)
     if barrier:
         barrier()
