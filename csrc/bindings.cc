@@ -440,7 +440,9 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("wait_s", &SimTiming::wait_s)
       .def_readwrite("recv_delay_s", &SimTiming::recv_delay_s)
       .def_readwrite("serialize_lanes", &SimTiming::serialize_lanes)
-      .def_readwrite("trace", &SimTiming::trace);
+      .def_readwrite("trace", &SimTiming::trace)
+      .def_readwrite("verify_bps", &SimTiming::verify_bps)
+      .def_readwrite("verify_launch_s", &SimTiming::verify_launch_s);
   m.def("sim_set_timing", &sim_set_timing, py::arg("comm_key"), py::arg("timing"));
   // Virtual clock (core/vclock.h): the simulator in model time. Python threads
   // that drive a session's ranks are counted by the clock between adopt() and

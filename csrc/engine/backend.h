@@ -84,6 +84,9 @@ class Backend {
     uint32_t slot;
     uint8_t* out = nullptr;
     int block = 0;
+    // The CRC the engine expects. Only the timing-only simulator uses it
+    // (SimTiming::copy_bytes false moves no bytes, so it reports this value).
+    uint32_t expect = 0;
   };
   virtual Ev verify(const std::vector<CheckReq>& reqs, const std::vector<Ev>& waits) = 0;
   virtual int query(Ev e) = 0;  // 1 done, 0 pending, -1 failed
@@ -221,6 +224,13 @@ struct SimTiming {
   // ONE queue (its groups one after another, as if the lanes were one stream).
   // The model-time upper bounds in tests/test_timing_sim.py must catch it.
   bool serialize_lanes = false;
+  // The verify queue's device time: every launch costs verify_launch_s plus
+  // its bytes (packed bytes read; the fused unpack's bf16 writes are not
+  // charged) at verify_bps - the measured CRC walk on the verify stream's CUs
+  // (profiles/r5_walk: ~1 TB/s on 32 CUs, ~24 us for a lone 64 MiB chunk on
+  // all). 0 = instant, as before.
+  double verify_bps = 0;
+  double verify_launch_s = 0;
   // Record every timed transfer and staging copy (sim_fabric_trace): the
   // per-link timelines that show where a schedule leaves links idle.
   bool trace = false;

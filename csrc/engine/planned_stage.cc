@@ -69,10 +69,12 @@ void PlannedEngine::partial_landed(Layer& L, const Piece& p, std::vector<Verify>
   if (cfg_.unpack_store) {
     const uint32_t s = crc_slot();
     reqs.push_back(unpack_req(L, f.chunk, s));
+    reqs.back().expect = f.crc;
     if (f.has_crc) slot = s;
   } else if (f.has_crc) {
     slot = crc_slot();
     reqs.push_back(Backend::CheckReq{L.dev + a, b - a, slot});
+    reqs.back().expect = f.crc;
   }
   v.ev = backend_->verify(reqs, {});
   {
@@ -350,7 +352,10 @@ void PlannedEngine::flush_checks() {
     for (; j < pending_checks_.size(); ++j) {
       const PendingCheck& pc = pending_checks_[j];
       if (pc.has_req && reqs.size() == size_t(kVerifyBatch)) break;
-      if (pc.has_req) reqs.push_back(pc.req);
+      if (pc.has_req) {
+        reqs.push_back(pc.req);
+        reqs.back().expect = pc.piece.has_crc ? pc.piece.crc : 0;
+      }
       if (pc.wait && std::find(waits.begin(), waits.end(), pc.wait) == waits.end()) waits.push_back(pc.wait);
       v.pieces.push_back(pc.piece);
       v.slots.push_back(pc.slot);

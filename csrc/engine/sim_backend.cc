@@ -483,8 +483,21 @@ class SimBackend : public Backend {
           ev->set(-1);
           return;
         }
+      const SimTiming& tm = fab_->timing;
+      if (tm.verify_bps > 0 || tm.verify_launch_s > 0) {
+        int64_t bytes = 0;
+        for (const CheckReq& r : reqs) bytes += r.out ? fp8::packed_len(r.n, r.block) : r.n;
+        const double dur = tm.verify_launch_s + (tm.verify_bps > 0 ? double(bytes) / tm.verify_bps : 0.0);
+        const double t0 = vclock::now();
+        vclock::sleep_until(t0 + dur);
+        ev->ms = dur * 1e3;
+      }
       for (const CheckReq& r : reqs) {
         if (r.n <= 0) continue;
+        if (!copy) {  // timing-only run: no bytes moved, the check is charged above and passes
+          results_[r.slot] = r.expect;
+          continue;
+        }
         if (!r.out) {
           results_[r.slot] = crc32c(r.p, size_t(r.n));
           continue;

@@ -61,6 +61,23 @@ NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
   return found ? best : kClientID;
 }
 
+// Planned engines: a sender's loads of its own layers (sender == dest, the
+// min_loaded_sender choice for a dest holding a layer in another tier) take no
+// network window slot - they stage over PCIe, not a link - but have a window
+// of one of their own, so the rest stay pending (stealable by a faster peer)
+// and a sender's links always have pull_window jobs queued: with the loads in
+// the network window, a lane at N = 2 waited one chunk's staging per layer for
+// its next job (sim with the verify model: 910 vs 862 ms, bound 859). The
+// engine keeps such loads from queueing whole layers ahead of its sends
+// (PlannedEngine kPromoteAhead). Host engines count every job in one window,
+// as the reference pulls one job per sender (node.go:764-807).
+constexpr int kSelfWindow = 1;
+
+bool Node::job_room(NodeID sender, NodeID dest) {
+  if (self_job(sender, dest)) return self_inflight_[sender] < kSelfWindow;
+  return inflight_[sender] < cfg_.pull_window;
+}
+
 bool Node::rarest_own_job(NodeID node, LayerID* layer, JobKey* key) {
   // node.go:981-1010 (ties: lowest layer id, then lowest (dest, offset))
   bool ok = false;
@@ -72,6 +89,7 @@ bool Node::rarest_own_job(NodeID node, LayerID* layer, JobKey* key) {
     if (lj == jobs_.end()) continue;
     for (auto& jd : lj->second) {
       if (jd.second.sender != node || jd.second.state != JobState::Pending) continue;
+      if (!job_room(node, jd.first.first)) continue;
       size_t cnt = owners_[l.first].size();
       if (!ok || cnt < min_owners || (cnt == min_owners && l.first < *layer)) {
         min_owners = cnt;
@@ -115,6 +133,7 @@ bool Node::rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID
           eff(node_rate) < eff(sender_rate))
         continue;
       const NodeID dest = jd.first.first;
+      if (!job_room(node, dest)) continue;
       // A dest's own load of a layer it holds (sender == dest) is stolen like
       // any job (node.go:1036-1042): e.g. a peer holding it in memory relieves
       // a dest reading it from a slow tier. If that dest also stages the chunks
@@ -164,7 +183,7 @@ void Node::dispatch_range(LayerID layer, NodeID sender, NodeID dest, int64_t off
   send_msg(sender, f);
 }
 
-bool Node::assign_new_job(NodeID node) {
+bool Node::assign_new_job(NodeID node, bool steal) {
   // node.go:909-945
   LayerID layer = 0;
   JobKey key{0, 0};
@@ -175,13 +194,13 @@ bool Node::assign_new_job(NodeID node) {
     j.state = JobState::Sending;
     j.t_us = vclock::now_us();
     load_[node] = std::max<int64_t>(0, load_[node] - 1);
-    inflight_[node]++;
+    job_slots(node, key.first)++;
     log::debug(int64_t(cfg_.id)).u("node", node).u("dest", key.first).u("layer", layer).i("offset", key.second)
         .msg("pass a job initially assigned");
     dispatch_range(layer, node, key.first, key.second, j.size);
     return true;
   }
-  if (rarest_stealable_job(node, &layer, &key, &victim)) {
+  if (steal && rarest_stealable_job(node, &layer, &key, &victim)) {
     log::debug(int64_t(cfg_.id)).u("layer", layer).u("node", node).u("dest", key.first)
         .msg("steal a job from the most loaded node (" + std::to_string(victim) + ") to node " + std::to_string(node));
     load_[victim] = std::max<int64_t>(0, load_[victim] - 1);
@@ -189,7 +208,7 @@ bool Node::assign_new_job(NodeID node) {
     j.sender = node;
     j.state = JobState::Sending;
     j.t_us = vclock::now_us();
-    inflight_[node]++;
+    job_slots(node, key.first)++;
     dispatch_range(layer, node, key.first, key.second, j.size);
     return true;
   }
@@ -278,8 +297,14 @@ void Node::schedule_mode2() {
   for (auto& kv : assignment_) kick.insert(kv.first);
   for (auto& kv : load_)
     if (kv.second > 0) kick.insert(kv.first);
+  // Every node takes its own jobs first, then steals: kicked one after
+  // another, an early node would otherwise steal a later one's jobs before
+  // that node had started any (e.g. a dest's load of its own copy).
   for (NodeID n : kick)
-    while (inflight_[n] < cfg_.pull_window && assign_new_job(n)) {
+    while (assign_new_job(n, false)) {
+    }
+  for (NodeID n : kick)
+    while (assign_new_job(n)) {
     }
 }
 

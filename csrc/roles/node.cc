@@ -763,7 +763,7 @@ void Node::on_ack(const MessagePtr& m) {
     for (auto& k : done) retire_job(m->layer, k);
   }
   // The destination now owns a copy it can serve (status grew above): let it pull too.
-  while (inflight_[m->src] < cfg_.pull_window && assign_new_job(m->src)) {
+  while (assign_new_job(m->src)) {
   }
   flush_batch();
 }

@@ -198,7 +198,7 @@ class Node {
   void schedule_mode3();
   // mode 2 (node.go:628-1073); a job is (layer, dest, byte range)
   using JobKey = std::pair<NodeID, int64_t>;  // (dest, offset) within jobs_[layer]
-  bool assign_new_job(NodeID node);
+  bool assign_new_job(NodeID node, bool steal = true);
   NodeID min_loaded_sender(LayerID layer, NodeID dest);
   bool rarest_own_job(NodeID node, LayerID* layer, JobKey* key);
   bool rarest_stealable_job(NodeID node, LayerID* layer, JobKey* key, NodeID* victim);
@@ -234,7 +234,13 @@ class Node {
   };
   std::map<LayerID, std::map<JobKey, Job>> jobs_;
   std::map<NodeID, int64_t> load_;        // senderLoadCounter
-  std::map<NodeID, int> inflight_;        // jobs currently sending per sender
+  std::map<NodeID, int> inflight_;        // jobs currently sending per sender (network jobs)
+  // planned engines: a sender's loads of its own layers in flight, a window of
+  // their own beside the network one (mode2.cc, kSelfWindow)
+  std::map<NodeID, int> self_inflight_;
+  bool self_job(NodeID sender, NodeID dest) const { return sender == dest && e_->planned(); }
+  bool job_room(NodeID sender, NodeID dest);
+  int& job_slots(NodeID sender, NodeID dest) { return (self_job(sender, dest) ? self_inflight_ : inflight_)[sender]; }
   std::map<NodeID, std::pair<double, uint64_t>> perf_;  // sender -> (EWMA job us, count) (quirk Q9)
   // planned data plane (leader): jobs awaiting dispatch, sequence numbers, CRC manifests
   struct PendingJob {

@@ -59,6 +59,7 @@ void Node::on_suspect(const MessagePtr& m) {
   jobs_.clear();
   load_.clear();
   inflight_.clear();
+  self_inflight_.clear();
   outstanding_.clear();
   shrink_wait_.clear();
   for (auto& kv : status_) shrink_wait_.insert(kv.first);
@@ -151,13 +152,14 @@ void Node::retire_job(LayerID layer, const JobKey& key) {
     auto& pf = perf_[job.sender];
     pf.first = pf.second == 0 ? dur : 0.5 * pf.first + 0.5 * dur;  // EWMA (quirk Q9)
     pf.second++;
-    inflight_[job.sender] = std::max(0, inflight_[job.sender] - 1);
+    int& slots = job_slots(job.sender, key.first);
+    slots = std::max(0, slots - 1);
     log::info(int64_t(cfg_.id)).u("node", job.sender).u("dest", key.first).u("layerID", layer).i("offset", key.second)
         .f("duration[ms]", dur / 1e3).msg("job completed");
   } else {
     load_[job.sender] = std::max<int64_t>(0, load_[job.sender] - 1);
   }
-  while (inflight_[job.sender] < cfg_.pull_window && assign_new_job(job.sender)) {
+  while (assign_new_job(job.sender)) {
   }
 }
 
@@ -235,11 +237,14 @@ void Node::on_tick() {
       if (lj != jobs_.end()) {
         auto jt = lj->second.find({e.dest, e.o.off});
         if (jt != lj->second.end()) {
-          if (jt->second.state == JobState::Sending) inflight_[jt->second.sender] = std::max(0, inflight_[jt->second.sender] - 1);
+          if (jt->second.state == JobState::Sending) {
+            int& slots = job_slots(jt->second.sender, e.dest);
+            slots = std::max(0, slots - 1);
+          }
           jt->second.sender = alt;
           jt->second.state = JobState::Sending;
           jt->second.t_us = now;
-          inflight_[alt]++;
+          job_slots(alt, e.dest)++;
         }
       }
     }
@@ -273,7 +278,7 @@ void Node::on_tick() {
         }
     for (auto& kv : load_)
       if (!suspects_.count(kv.first))
-        while (inflight_[kv.first] < cfg_.pull_window && assign_new_job(kv.first)) {
+        while (assign_new_job(kv.first)) {
         }
   }
 }

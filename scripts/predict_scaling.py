@@ -44,6 +44,11 @@ from distributed_llm_dissemination_amd.parallel.runtime import Runtime  # noqa: 
 
 MiB = 1 << 20
 _n = [0]
+# The verify queue's device time (GB/s of checked bytes, us per launch), from
+# scripts/verify_bench.py on one MI355X (profiles/r5_walk): with peers the
+# verify stream owns 32 CUs - 0.94 TB/s in 16-chunk launches, 77 us for a lone
+# 64 MiB chunk; alone it has every CU - 5.3 TB/s, 24 us for a lone chunk.
+VERIFY_MODEL = {"peers": (940.0, 6.0), "alone": (5300.0, 11.4)}
 
 
 def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
@@ -53,7 +58,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
             adapt_links: bool = True, disk_gbps: float = 13.3, host_share: bool = False, hosts: int = 1,
             nic_gbps: float = 50.0, host_lane_classes: int = 0, probe_mib: int = 256, warmup: int = 1,
             recv_delay=None, slow_after_probe: bool = False, virtual: bool = True,
-            serialize_lanes: bool = False, trace: bool = False) -> dict:
+            serialize_lanes: bool = False, trace: bool = False, verify_model: bool = True) -> dict:
     """Timed sessions of the headline workload at 1/scale size; returns the full-size prediction.
 
     slow_link=((s, d), frac): that directed link runs at frac of the others
@@ -90,7 +95,10 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
     virtual (default): model time (see the module docstring); `model_ms` lists
     each session's modeled makespan without the plan time.
     serialize_lanes: fault injection - each rank's comm lanes share one queue
-    (SimTiming.serialize_lanes); the schedule tests' upper bounds must catch it."""
+    (SimTiming.serialize_lanes); the schedule tests' upper bounds must catch it.
+    verify_model (default): every landed and staged chunk is CRC-checked on the
+    rank's verify queue, which costs its measured device time (VERIFY_MODEL:
+    the CRC walk on 32 CUs with peers, on all CUs alone); False: no checks."""
     if virtual:
         slowdown = 1.0  # model time has no simulator overhead to dilute
     plan_link_gbps = (plan_link_gbps if plan_link_gbps is not None else link_gbps) / slowdown
@@ -102,7 +110,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
                             seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links,
                             disk_gbps / slowdown, host_share, hosts, nic_gbps / slowdown, host_lane_classes, probe_mib,
                             warmup, {r: v * slowdown for r, v in (recv_delay or {}).items()}, slow_after_probe,
-                            serialize_lanes, trace)
+                            serialize_lanes, trace, verify_model)
     finally:
         _core.set_log_level(level)
 
@@ -110,7 +118,7 @@ def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int 
 def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
              policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, host_share=False,
              hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1, recv_delay=None,
-             slow_after_probe=False, serialize_lanes=False, trace=False):
+             slow_after_probe=False, serialize_lanes=False, trace=False, verify_model=True):
     import shutil
     import tempfile
 
@@ -119,7 +127,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
         return _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link,
                            seeding, policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps,
                            storage, host_share, hosts, nic_gbps, host_lane_classes, probe_mib, warmup, recv_delay,
-                           slow_after_probe, serialize_lanes, trace)
+                           slow_after_probe, serialize_lanes, trace, verify_model)
     finally:
         if storage:
             shutil.rmtree(storage, ignore_errors=True)
@@ -128,7 +136,7 @@ def _predict(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, l
 def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode, lanes, steps, slow_link, seeding,
                 policy, plan_links, slowdown, tier, pack, plan_link_gbps, adapt_links, disk_gbps, storage,
                 host_share=False, hosts=1, nic_gbps=50.0, host_lane_classes=0, probe_mib=256, warmup=1,
-                recv_delay=None, slow_after_probe=False, serialize_lanes=False, trace=False):
+                recv_delay=None, slow_after_probe=False, serialize_lanes=False, trace=False, verify_model=True):
     pcie_gbps, link_gbps = pcie_gbps / slowdown, link_gbps / slowdown
     key = f"predict{os.getpid()}_{_n[0]}"
     _n[0] += 1
@@ -138,6 +146,10 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     t.stage_bps = pcie_gbps * 1e9 / scale
     t.serialize_lanes = serialize_lanes
     t.trace = trace
+    if verify_model:
+        gbps, launch_us = VERIFY_MODEL["peers" if n > 1 else "alone"]
+        t.verify_bps = gbps / slowdown * 1e9 / scale
+        t.verify_launch_s = launch_us * 1e-6 * slowdown
     t.link_bps = link_gbps * 1e9 / scale
     slows = _slow_list(slow_link)
     slow = {(s, d): link_gbps * 1e9 / scale * frac for (s, d), frac in slows}
@@ -175,7 +187,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
     else:
         bar = threading.Barrier(n).wait
         rt_kw = {}
-    rts = [Runtime(cfg, i, engine="sim", chunk_bytes=cb, sim_key=key, verify=False,
+    rts = [Runtime(cfg, i, engine="sim", chunk_bytes=cb, sim_key=key, verify=verify_model,
                    poison=False, engine_opts={"lanes": lanes, "host_lane_classes": host_lane_classes}, pack=pack,
                    host_share=host_share, barrier=bar, **(rt_kw or {"registry": {i: "127.0.0.1:0"}}), **disk)
            for i in range(n)]
@@ -241,6 +253,9 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                         link_bytes[(i, p)] = d * scale
             staged = [(r.engine.stats().bytes_staged - staged0[i]) * scale for i, r in enumerate(rts)]
         lanes_used = rts[0].engine.stats().lanes
+        vs = rts[0].engine.stats()
+        verify_rank0 = {"calls": vs.verify_calls, "chunks": vs.verify_chunks,
+                        "busy_ms_full_size": round(vs.verify_busy_ms / slowdown, 1)}
         trace_last = _core.sim_fabric_trace(key) if trace else None
         rts_est = [dict(r.link_est) for r in rts]  # per rank: the send-side busy-throughput EWMA per peer (B/s)
         rts_est_in = [dict(r.link_est_in) for r in rts]  # ... and the receive-side one per peer
@@ -275,6 +290,7 @@ def _predict_in(n, layers, layer_bytes, chunk, pcie_gbps, link_gbps, scale, mode
                                                  slow_link) * 1e3, 1),
             "value_GBps": round(total / sec / 1e9, 1), "scale": scale,
             **({"trace_last": trace_last} if trace else {}),
+            **({"verify_rank0_all_sessions": verify_rank0} if verify_model else {}),
             **({"planned_T_ms": round(flow_T * 1e3 / slowdown, 1)} if flow_T > 0 else {})}
 
 
