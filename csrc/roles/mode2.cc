@@ -64,14 +64,15 @@ NodeID Node::min_loaded_sender(LayerID layer, NodeID dest) {
 // Planned engines: a sender's loads of its own layers (sender == dest, the
 // min_loaded_sender choice for a dest holding a layer in another tier) take no
 // network window slot - they stage over PCIe, not a link - but have a window
-// of one of their own, so the rest stay pending (stealable by a faster peer)
+// of two of their own (one layer loading while the last one's check and ack
+// complete), so the rest stay pending (stealable by a faster peer)
 // and a sender's links always have pull_window jobs queued: with the loads in
 // the network window, a lane at N = 2 waited one chunk's staging per layer for
 // its next job (sim with the verify model: 910 vs 862 ms, bound 859). The
 // engine keeps such loads from queueing whole layers ahead of its sends
 // (PlannedEngine kPromoteAhead). Host engines count every job in one window,
 // as the reference pulls one job per sender (node.go:764-807).
-constexpr int kSelfWindow = 1;
+constexpr int kSelfWindow = 2;
 
 bool Node::job_room(NodeID sender, NodeID dest) {
   if (self_job(sender, dest)) return self_inflight_[sender] < kSelfWindow;
