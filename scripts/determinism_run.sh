@@ -6,6 +6,9 @@
 # `make -B -j16` on the same CPUs (LOAD=1).
 #
 #   bash scripts/determinism_run.sh [runs=5] [workers=0 (serial) | N (pytest -n N)] [dir=profiles/r6_determinism]
+#
+# Run it from a copy of the tree (TREE=<commit> names it in the summary) when
+# the working tree's extension is rebuilt meanwhile.
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 RUNS=${1:-5}
@@ -24,7 +27,7 @@ if [ "${LOAD:-0}" = 1 ]; then
 fi
 {
   echo "# $RUNS CPU-suite runs ($TAG$([ "${LOAD:-0}" = 1 ] && echo ', beside a looping make -B -j16')), $(nproc) CPUs, $(date -u +%FT%TZ)"
-  echo "# tree: $(git rev-parse --short HEAD)$(git diff --quiet || echo '+dirty')"
+  echo "# tree: ${TREE:-$(git rev-parse --short HEAD)$(git diff --quiet || echo '+dirty')}"
 } >> "$SUMMARY"
 XDIST=()
 [ "$WORKERS" -gt 0 ] && XDIST=(-n "$WORKERS")
