@@ -30,6 +30,7 @@ import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 BASELINE_METRIC = "aggregate GB/s + time-to-full-placement, 80×1 GiB layers, mode 1, 8 ranks"
+PROBE_BYTES = 4 << 30  # node NVMe probe file (N > 1, --tier disk): past typical drive caches
 
 
 def metric_name(layers: int, layer_mib: int, mode: int, ranks: int) -> str:
@@ -306,6 +307,7 @@ def worker(args, world, rank, chan) -> int:
     run_tag = os.environ.get("DLD_SUP_PREFIX", "") + os.environ.get("MASTER_PORT", "") + os.environ.get(
         "TORCHELASTIC_RUN_ID", "") if world > 1 else str(os.getpid())
     node_key = "b" + hashlib.blake2b(run_tag.encode(), digest_size=6).hexdigest()
+    disk_info = {}  # --tier disk: storage, read mode and page-cache facts for the JSON
     disk_gbps = args.node_disk_gbps if args.node_disk_gbps is not None else 0.0
     disk_source = "flag" if args.node_disk_gbps is not None else "unpaced"
     if args.tier == "disk" and args.node_disk_gbps is None and world > 1:
@@ -317,7 +319,7 @@ def worker(args, world, rank, chan) -> int:
         mine = None
         if int(os.environ.get("LOCAL_RANK", "0")) == 0:  # one probe per host (ranks sharing a GPU included)
             try:  # never leave the other ranks waiting in the gather below
-                mine = read_rate_gbps(args.storage or os.path.join(os.getcwd(), "storage"))
+                mine = read_rate_gbps(args.storage or os.path.join(os.getcwd(), "storage"), size_bytes=PROBE_BYTES)
             except Exception as e:  # noqa: BLE001 - e.g. a full or read-only disk: keep the default
                 log(f"node NVMe probe failed: {e}")
             log(f"node NVMe read rate: {mine if mine is None else round(mine, 2)} GB/s (O_DIRECT probe)")
@@ -325,18 +327,18 @@ def worker(args, world, rank, chan) -> int:
         dist.all_gather_object(rates, mine)
         got = [r for r in rates if r]
         disk_gbps, disk_source = (min(got), "measured") if got else (13.3, "default")
-    disk_info = {}
+        if got:
+            disk_info["node_disk_probe_GiB"] = PROBE_BYTES / 2**30  # the probe file's size beside its rate
     if args.tier == "disk":
+        from distributed_llm_dissemination_amd.utils.config import SOURCE_DISK
         from distributed_llm_dissemination_amd.utils.diskprobe import refusal, storage_info
 
         st = storage_info(args.storage or os.path.join(os.getcwd(), "storage"))
-        from distributed_llm_dissemination_amd.utils.config import SOURCE_DISK
-
         mine_bytes = sum(cfg.node(rank).initial_layers.get(SOURCE_DISK, {}).values())
         fit = int(st["avail_bytes"] * 0.97 // layer_bytes)
-        disk_info = {"storage_fs": st["fs"], "storage_device": st["device"], "storage_mount": st["mount"],
-                     "storage_avail_GB": round(st["avail_bytes"] / 1e9, 1), "layers_fit_on_storage": fit,
-                     **({"storage_note": st["note"]} if "note" in st else {})}
+        disk_info.update({"storage_fs": st["fs"], "storage_device": st["device"], "storage_mount": st["mount"],
+                          "storage_avail_GB": round(st["avail_bytes"] / 1e9, 1), "layers_fit_on_storage": fit,
+                          **({"storage_note": st["note"]} if "note" in st else {})})
         log(f"disk tier on {st['mount']} ({st['fs']}, {st['device']}): {st['avail_bytes'] / 1e9:.1f} GB free, "
             f"this rank writes {mine_bytes / 1e9:.1f} GB")
         why = refusal(st["fs"], "o_direct", args.allow_buffered)
