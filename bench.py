@@ -517,6 +517,9 @@ def worker(args, world, rank, chan) -> int:
             nck = last.engine_stats.get("verify_chunks")
             if vb is not None and nck:  # device time of the batched checks per checked chunk
                 out["config"]["verify_us_per_chunk_rank0"] = round(vb * 1e3 / nck, 1)
+                calls = last.engine_stats.get("verify_calls") or 0
+                if calls:  # the batching behind that rate: chunks per verify launch
+                    out["config"]["verify_chunks_per_call_rank0"] = round(nck / calls, 2)
             st = last.engine_stats.get("bytes_staged")
             if st and last.seconds > 0:  # this rank's host -> HBM rate over the session (PCIe bound: ~57 GB/s)
                 out["config"]["stage_GBps_rank0"] = round(st / last.seconds / 1e9, 2)
