@@ -19,6 +19,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -128,35 +129,63 @@ int main(int argc, char** argv) {
   CHECK(hipStreamSynchronize(s));
   const double t_h2d = now() - t0;
 
-  // 3) overlapped: `depth` readers, each reads its next chunk into a free ring
-  // slot and hands it to the copy stream; a slot is free again once its copy landed
+  // 3) overlapped, as the engine's disk tier runs it (planned_stage.cc): a
+  // free list of pinned bounce buffers, `depth` readers each taking the next
+  // chunk and any free buffer, the H2D copy enqueued on two alternating
+  // streams (the engine's two copy queues), and the main thread returning a
+  // buffer to the free list once the event behind its copy has fired.
+  hipStream_t s2;
+  CHECK(hipStreamCreate(&s2));
   std::vector<hipEvent_t> ev(static_cast<size_t>(ring_n));
   for (auto& e : ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  std::vector<bool> used(static_cast<size_t>(ring_n), false);
   std::mutex mu;
+  std::condition_variable cv;
+  std::vector<int> free_slots, busy;
+  for (int i = 0; i < ring_n; ++i) free_slots.push_back(i);
+  int64_t copies = 0, landed = 0;
   next = 0;
   th.clear();
   t0 = now();
   for (int r = 0; r < depth; ++r)
     th.emplace_back([&] {
       for (int64_t c; (c = next++) < n;) {
-        const int slot = int(c % ring_n);
-        bool wait;
+        int slot;
         {
-          std::lock_guard<std::mutex> lk(mu);
-          wait = used[size_t(slot)];
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return !free_slots.empty(); });
+          slot = free_slots.back();
+          free_slots.pop_back();
         }
-        if (wait) CHECK(hipEventSynchronize(ev[size_t(slot)]));
         const int64_t len = read_chunk(c, ring[size_t(slot)]);
         std::lock_guard<std::mutex> lk(mu);
+        hipStream_t cs = (copies++ & 1) ? s2 : s;
         CHECK(hipMemcpyAsync(static_cast<char*>(dev) + (c % dev_slots) * chunk, ring[size_t(slot)], size_t(len),
-                             hipMemcpyHostToDevice, s));
-        CHECK(hipEventRecord(ev[size_t(slot)], s));
-        used[size_t(slot)] = true;
+                             hipMemcpyHostToDevice, cs));
+        CHECK(hipEventRecord(ev[size_t(slot)], cs));
+        busy.push_back(slot);
       }
     });
+  while (true) {  // reclaim buffers whose copy landed
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 0; i < busy.size();) {
+        if (hipEventQuery(ev[size_t(busy[i])]) == hipSuccess) {
+          free_slots.push_back(busy[i]);
+          busy[i] = busy.back();
+          busy.pop_back();
+          ++landed;
+        } else {
+          ++i;
+        }
+      }
+      if (landed == n) break;
+    }
+    cv.notify_all();
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
   for (auto& t : th) t.join();
   CHECK(hipStreamSynchronize(s));
+  CHECK(hipStreamSynchronize(s2));
   const double t_pipe = now() - t0;
 
   const double mib = double(total) / (1 << 20);

@@ -39,6 +39,7 @@ case "$RECIPE" in
     timeout -k 10 400 $PYTEST tests/test_gpu_kernels.py tests/test_gpu_ops.py > $OUT/pytest.log 2>&1 &&
     timeout -k 10 240 python scripts/verify_bench.py > $OUT/vb.json 2> $OUT/vb.err &&
     timeout -k 10 240 python scripts/verify_bench.py --cus 128 > $OUT/vb_cus128.json 2> $OUT/vb_cus128.err &&
+    timeout -k 10 240 python scripts/verify_bench.py --cus 32 > $OUT/vb_cus32.json 2> $OUT/vb_cus32.err &&
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o vb -- \
       python3 scripts/verify_bench.py --reps 20 > $OUT/vb_trace.json 2> $OUT/vb_trace.err
     ;;
