@@ -98,11 +98,13 @@ constexpr uint32_t kLdsBytes = kShLds + 8 * 16 * 128;   // 144 KiB
 // [lanepow: 64 (x^(8*64*(63-l)): lane l's last piece to its segment end)]
 // [segpow: 3 levels x 1024 (x^(8*16 KiB*i*1024^L)): x^(8*16 KiB*j) for any j
 // below 2^30 is the product of at most three entries - chunks up to 16 TiB
-// (one 1 GiB-chunk table capped a single CRC at 1 GiB in round 4)].
+// (one 1 GiB-chunk table capped a single CRC at 1 GiB in round 4)]
+// [walkgap: 8 x 16 nibble tables of the walk's shift from a lane's last piece
+// of one segment to its first piece of the segment 16 later (crc_walk)].
 constexpr int kSegLevels = 3, kSegLevel = 1024;
 constexpr int64_t kMaxSegs = int64_t(1) << (10 * kSegLevels);
 constexpr int kT = 0, kGap = 1024, kPow = kGap + 128, kLanePow = kPow + 1024, kSegPow = kLanePow + 64,
-              kConstWords = kSegPow + kSegLevels * kSegLevel;
+              kWalkGap = kSegPow + kSegLevels * kSegLevel, kConstWords = kWalkGap + 128;
 
 using u32x4_t = unsigned int __attribute__((ext_vector_type(4)));
 
@@ -661,33 +663,34 @@ struct BatchGeo {
 
 // ---- the fold, inside the kernel (no second launch). A chunk's raw CRC is
 // the XOR of its segments' values (each already shifted to the chunk end).
-// Per item the workspace holds {acc, count}: every workgroup XORs the values
-// of its segments of the item into acc (one device-scope atomic per run of
-// its waves that share an item), waits for that atomic to return, then adds
-// its segment count to count; the workgroup whose add completes the item's
-// count takes acc (exchanging in 0), resets count and writes raw ^ init.
-// Both words are back at 0 when the launch ends, so a workspace zeroed once
-// serves every later launch on its stream. Every access to them is a vector
-// atomic, performed where the device's XCDs see one copy of the word.
-// The separate fold launch this replaces cost 8.4-9.6 us per 64 MiB chunk in
-// the round-4 engine traces (profiles/r4_profile), a quarter of the verify.
-// Ordering: the count add is a release at agent scope - it publishes this
-// workgroup's XOR (program order before it); the workgroup whose add completes
-// the count then takes an agent-scope acquire fence, which synchronizes with
-// every earlier release in the count's release sequence, so the exchange reads
-// the complete value by the memory model, not by how this hardware happens to
-// retire atomics. (acq_rel on every add also invalidated every XCD's L2 once
-// per workgroup: the fused kernel went from 18.0 to 32.5 us per chunk.)
+// Per item the workspace holds one 64-bit word {acc (low half), count (high
+// half)}: every workgroup XORs the value of its segments of the item into acc
+// (one device-scope atomic per run of its waves that share an item), then
+// adds its segment count to count, both on that same word; the workgroup
+// whose add completes the item's count has the complete acc in the add's
+// returned value, zeroes the word and writes raw ^ init. Words are back at 0
+// when the launch ends, so a workspace zeroed once serves every later launch
+// on its stream.
+// Ordering by the memory model with relaxed atomics only: a workgroup's XOR
+// and add are RMWs of one location in program order, so the XOR precedes the
+// add in that location's modification order (write-write coherence); the
+// completing add comes after every other add, so after every XOR, and an RMW
+// reads the value just before it - acc complete. (Round 5 put acc and count in
+// two words with an asm dependency between the atomics; release on the count
+// add / acquire in the completer made that formal but the release's L2
+// write-back of the fused kernel's bf16 stores took it from 18.0 to 32.5 us per
+// chunk batched, profiles/r6_verify.) The separate fold launch this replaces
+// cost 8.4-9.6 us per 64 MiB chunk in the round-4 engine traces
+// (profiles/r4_profile), a quarter of the verify.
 template <class Geo>
 __device__ __forceinline__ void fold_add(const Geo& geo, int64_t item, uint32_t x, uint32_t n, uint32_t* acc) {
-  uint32_t* a = acc + 2 * item;
-  __hip_atomic_fetch_xor(a, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t got = __hip_atomic_fetch_add(a + 1, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) + n;
-  if (int64_t(got) == geo.item_segs(item)) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const uint32_t raw = __hip_atomic_exchange(a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *geo.item_out(item) = raw ^ geo.item_init(item);
+  auto* a = reinterpret_cast<unsigned long long*>(acc) + item;
+  __hip_atomic_fetch_xor(a, static_cast<unsigned long long>(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long old =
+      __hip_atomic_fetch_add(a, static_cast<unsigned long long>(n) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (int64_t((old >> 32) + n) == geo.item_segs(item)) {
+    __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *geo.item_out(item) = uint32_t(old) ^ geo.item_init(item);
   }
 }
 
@@ -797,12 +800,34 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
 // (fold_add) - one pair of device-scope atomics per (workgroup, item), 16
 // per 64 MiB item in a 16-chunk batch, instead of one per 8 segments.
 constexpr int kWalkWaves = 16, kWalkSlots = 256;
+// Bytes between the end of a lane's piece in block 3 of segment g and the
+// start of its piece in block 0 of segment g + kWalkWaves (the walk's stride).
+constexpr int64_t kWalkGapBytes = int64_t(kWalkWaves) * kSegBytes - (kBlocksPerSeg - 1) * kBlockBytes - kPieceBytes;
 
-// One wave's walk over segments g = first, first + step, ... < end: the
-// segment value (at its chunk's end) goes to sink(seg, value) on lane 0.
+// s shifted over kWalkGapBytes zeros with `next` folded in (the 16-entry
+// nibble tables at LDS byte `base`: every lane reads one of 16 consecutive
+// words per table, so at most one address per bank - no replicas needed).
+// s = 0 gives next: a run's first segment takes the same path.
+__device__ __forceinline__ uint32_t walk_gap(const uint8_t* lds, uint32_t base, uint32_t s, uint32_t next) {
+  uint32_t r[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) r[n] = lds_word(lds, base + uint32_t(n) * 64u + ((s >> (4 * n)) & 15u) * 4u);
+  using S = Slice4T<32>;
+  return S::x3(S::x3(S::x3(r[0], r[1], r[2]), r[3], r[4]), S::x3(r[5], r[6], r[7]), next);
+}
+
+// One wave's walk over segments g = first, first + kWalkWaves, ... < end.
+// While its next segment is a full one of the same item, a lane carries its
+// CRC state on over the zeros to its piece there (walk_gap: 8 lookups)
+// instead of shifting it to the segment end and reducing the wave (a 32-step
+// GF(2) multiply and a DPP reduction, ~30 % of a segment's VALU work). At a
+// run's end (item change, partial segment or end of range) the state is
+// shifted and reduced once, and sink(seg, value, segments) on lane 0 gets the
+// run's value at the item's end: CRC is linear, so the other waves' segments
+// between (zeros here) add their own values. `gap`: walk_gap's LDS tables.
 template <class Geo, class Sink>
-__device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t end, int64_t step,
-                                         const uint32_t* __restrict__ sc, const Slice4T<32>& st, Sink sink) {
+__device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t end, const uint32_t* __restrict__ sc,
+                                         const Slice4T<32>& st, uint32_t gap, Sink sink) {
   const int lane = threadIdx.x & 63;
   const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
   int64_t g = first;
@@ -820,8 +845,10 @@ __device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t 
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  for (; g < end; g += step) {
-    const int64_t gn = g + step;
+  uint32_t run = 0;  // the lane's state carried from the run's previous segment (0: none)
+  uint32_t nrun = 0;  // segments in the run so far (wave-uniform)
+  for (; g < end; g += kWalkWaves) {
+    const int64_t gn = g + kWalkWaves;
     Seg nxt = cur;  // no next segment: loads against an empty resource
     bool nfull = false;
     if (gn < end) {
@@ -830,13 +857,14 @@ __device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t 
     }
     const auto rn = seg_rsrc(nxt.p, nfull);
     uint32_t s;
+    bool more;  // the run goes on into nxt
     if (cur.len == kSegBytes) {
       const uint32_t rowc = sc[kLanePow + lane];
       s = 0;
 #pragma unroll
       for (int b = 0; b < kBlocksPerSeg; ++b) {
         row_transpose(w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]);
-        s = b ? st.gap(s, w[4 * b][0]) : w[0][0];
+        s = b ? st.gap(s, w[4 * b][0]) : walk_gap(st.lds, gap, run, w[0][0]);
 #pragma unroll
         for (int x = 0; x < 16; ++x) s = st.mix(s, x < 15 ? w[4 * b + ((x + 1) >> 2)][(x + 1) & 3] : 0u);
         __builtin_amdgcn_sched_barrier(0);
@@ -844,11 +872,23 @@ __device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t 
         for (int j = 0; j < 4; ++j) w[4 * b + j] = seg_load(rn, lo, 4 * b + j);
         __builtin_amdgcn_sched_barrier(0);
       }
-      s = wave_xor_dpp(multmodp_unrolled(rowc, s));
-    } else {
+      ++nrun;
+      more = nfull && nxt.chunk == cur.chunk;
+      if (more) {
+        run = s;
+      } else {
+        run = 0;
+        s = wave_xor_dpp(multmodp_unrolled(rowc, s));
+      }
+    } else {  // a partial segment: a run of its own (the one before it ended at the item's full segments)
       s = slice_partial(cur, sc, st, lane, visit);
+      nrun = 1;
+      more = false;
     }
-    if (lane == 0) sink(cur, to_chunk_end(cur, s, sc));
+    if (!more) {
+      if (lane == 0) sink(cur, to_chunk_end(cur, s, sc), nrun);
+      nrun = 0;
+    }
     if (cur.len != kSegBytes) {  // (rare) w did not take the next segment's words yet
 #pragma unroll
       for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
@@ -864,22 +904,25 @@ template <class Geo>
 __global__ void __launch_bounds__(kWalkWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
 crc_walk_kernel(const Geo geo, int64_t total_segs, int64_t per_wg, const uint32_t* __restrict__ sc,
                 uint32_t* __restrict__ acc) {
-  __shared__ uint4 lds_raw[(LdsLayout<32>::kBytes + kWalkSlots * 8) / 16];
+  constexpr uint32_t kFold = LdsLayout<32>::kBytes, kGapT = kFold + kWalkSlots * 8;
+  __shared__ uint4 lds_raw[(kGapT + 8 * 16 * 4) / 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
-  uint32_t* fx = reinterpret_cast<uint32_t*>(lds + LdsLayout<32>::kBytes);  // per item slot: XOR
-  uint32_t* fn = fx + kWalkSlots;                                            // ... and segment count
+  uint32_t* fx = reinterpret_cast<uint32_t*>(lds + kFold);  // per item slot: XOR
+  uint32_t* fn = fx + kWalkSlots;                           // ... and segment count
   const int64_t g0 = int64_t(blockIdx.x) * per_wg, g1 = min(g0 + per_wg, total_segs);
   if (g0 >= g1) return;  // whole workgroup
   for (int i = threadIdx.x; i < 2 * kWalkSlots; i += blockDim.x) fx[i] = 0;
+  for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x)
+    reinterpret_cast<uint32_t*>(lds + kGapT)[i] = sc[kWalkGap + i];
   const int64_t first_item = geo(g0).chunk;
-  load_lds<32>(lds, sc);  // once per workgroup; its barrier also publishes the zeroed slots
+  load_lds<32>(lds, sc);  // once per workgroup; its barrier also publishes the slots and the gap tables
   const Slice4T<32> st(lds);
-  // two LDS atomics per 16 KiB segment (the host keeps a range within kWalkSlots items)
+  // two LDS atomics per run of a wave's segments in one item (the host keeps a range within kWalkSlots items)
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: g and its Seg in SGPRs
-  crc_walk(geo, g0 + wave, g1, kWalkWaves, sc, st, [=](const Seg& sg, uint32_t v) {
+  crc_walk(geo, g0 + wave, g1, sc, st, kGapT, [=](const Seg& sg, uint32_t v, uint32_t n) {
     const int slot = int(sg.chunk - first_item);
     atomicXor(&fx[slot], v);
-    atomicAdd(&fn[slot], 1u);
+    atomicAdd(&fn[slot], n);
   });
   lds_barrier();
   const int64_t nslots = geo(g1 - 1).chunk - first_item + 1;
@@ -939,6 +982,9 @@ uint32_t* device_consts(hipStream_t s) {
   const uint32_t xg = crc32c_xpow8n(kGapBytes);
   for (int n = 0; n < 8; ++n)
     for (uint32_t v = 0; v < 16; ++v) h[size_t(kGap + n * 16 + int(v))] = crc32c_multmodp(xg, v << (4 * n));
+  const uint32_t xw = crc32c_xpow8n(uint64_t(kWalkGapBytes));
+  for (int n = 0; n < 8; ++n)
+    for (uint32_t v = 0; v < 16; ++v) h[size_t(kWalkGap + n * 16 + int(v))] = crc32c_multmodp(xw, v << (4 * n));
   for (int m = 0; m < 1024; ++m) h[size_t(kPow + m)] = crc32c_xpow8n(uint64_t(16) * uint64_t(m));
   for (int l = 0; l < 64; ++l) h[size_t(kLanePow + l)] = crc32c_xpow8n(uint64_t(kPieceBytes) * uint64_t(63 - l));
   // segpow level L, entry i: x^(8 * 16 KiB * i * 1024^L)
@@ -1011,6 +1057,7 @@ template <class Geo>
 hipError_t launch(const Geo& geo, int64_t total_segs, int block, const uint32_t* consts, void* ws, hipStream_t s,
                   int cus) {
   if (total_segs <= 0) return hipSuccess;
+  if (reinterpret_cast<uintptr_t>(ws) & 7) return hipErrorInvalidValue;  // 64-bit fold words
   auto* acc = static_cast<uint32_t*>(ws);
   if (block == 0) {
     // CRC only: one walking workgroup per CU the stream may use, each a

@@ -30,8 +30,8 @@ hipError_t spin_until(const uint32_t* flag, uint64_t max_iters, uint64_t* iters,
 // Two kernels: the CRC-only check walks (one 1024-thread workgroup per CU,
 // each a contiguous range of 16 KiB segments), the fused check + unpack runs
 // one segment per wave (512-thread workgroups, two per CU). Both fold a
-// chunk's segments inside the same launch (device-scope atomics on a
-// {acc, count} pair per item in `workspace`; crc32c.hip). A workspace must be
+// chunk's segments inside the same launch (device-scope atomics on one 64-bit
+// {acc, count} word per item in `workspace`, 8-B aligned; crc32c.hip). A workspace must be
 // zeroed ONCE (e.g. hipMemsetAsync) before its first use; every launch leaves
 // it zeroed again. Launches that share a workspace must be ordered (one stream).
 // `cus`: the CUs the launch's stream may use (a CU-masked verify stream): the

@@ -98,6 +98,18 @@ def main():
     torch.cuda.synchronize()
     out["crc_batch_matches_host"] = [x & 0xFFFFFFFF for x in res.cpu().tolist()] == want
     if not full_only:
+        # a lone chunk's launch by size: the intercept is the launch's fixed
+        # cost (dispatch, table fill, first loads, last wave, fold), the slope its rate
+        for mib in (1, 4, 16, 64):
+            calls[0] = 0
+
+            def crc_lone(mib=mib):
+                i = calls[0] % pool
+                calls[0] += 1
+                _core.crc32c_chunks_async(bufs[i].data_ptr(), mib << 20, mib << 20, res.data_ptr(), ws.data_ptr(), 0,
+                                          args.cus)
+
+            out[f"crc_lone_{mib}MiB_us"] = round(timed(crc_lone, args.reps) * 1e6, 1)
         big = torch.empty(16 * CHUNK, dtype=torch.uint8, device="cuda")
         _core.fill_random(big.data_ptr(), big.numel(), 5)
         wsb = torch.zeros(_core.crc32c_workspace_bytes(big.numel(), CHUNK), dtype=torch.uint8, device="cuda")

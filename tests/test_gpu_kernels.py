@@ -173,6 +173,37 @@ def test_crc32c_detects_single_bit_flip(gpu):
     assert a[:3] == b[:3] and a[3] != b[3]
 
 
+@pytest.mark.parametrize("cus", [2, 32, 0])
+def test_crc32c_walk_runs_carry_exactly(gpu, cus):
+    """With few CUs a wave walks a long run of one chunk's segments and carries
+    its lanes' CRC states from segment to segment (crc_walk's walk_gap): the
+    result matches the host, and a flipped bit in any block of a run's first,
+    middle or last segment - or in a lane's first or last word - changes only
+    its chunk."""
+    n, chunk = (128 << 20) + (16 << 10) + 48, 64 << 20
+    t = _dev_bytes(n)
+    gpu.fill_random(t.data_ptr(), n, 31337)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy().tobytes()
+    want = [gpu.crc32c(host[i : i + chunk]) for i in range(0, n, chunk)]
+    ws = torch.zeros(gpu.crc32c_workspace_bytes(n, chunk), dtype=torch.uint8, device="cuda")
+
+    def crcs():
+        out = torch.zeros(len(want), dtype=torch.int32, device="cuda")
+        gpu.crc32c_chunks_async(t.data_ptr(), n, chunk, out.data_ptr(), ws.data_ptr(), 0, cus)
+        torch.cuda.synchronize()
+        return [int(x) & 0xFFFFFFFF for x in out.cpu().tolist()]
+
+    assert crcs() == want
+    seg = 16 << 10
+    for off in [0, 5 * seg + 3 * 4096 + 63, 1000 * seg + 64 * 37, chunk - 1, chunk + 17 * seg + 2 * 4096 + 4]:
+        t[off] ^= 0x10
+        got = crcs()
+        t[off] ^= 0x10
+        c = off // chunk
+        assert got[c] != want[c] and got[:c] + got[c + 1 :] == want[:c] + want[c + 1 :], off
+
+
 def _scale_exp(amax: torch.Tensor) -> torch.Tensor:
     """core/fp8.h scale: the smallest E >= -126 with amax <= 448 * 2^E (0 if amax == 0), exact in f64."""
     a = amax.double()
