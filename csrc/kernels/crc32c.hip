@@ -91,6 +91,8 @@ constexpr int kPieceBytes = 64;                         // a lane's contiguous p
 constexpr int kBlockBytes = 64 * kPieceBytes;           // 4 KiB
 constexpr int kBlocksPerSeg = kSegBytes / kBlockBytes;  // 4
 constexpr int kGapBytes = kBlockBytes - kPieceBytes;    // between a lane's pieces
+constexpr int kWaves16 = 8;    // waves per workgroup of the fused kernel (512 threads, 16 table replicas)
+constexpr int kWalkWaves = 16;  // ... of the CRC walk (1024 threads, 32 replicas)
 constexpr uint32_t kShLds = 131072;                     // shift tables after the byte tables
 constexpr uint32_t kLdsBytes = kShLds + 8 * 16 * 128;   // 144 KiB
 // Global constants: [T: 4 x 256 (T[k][v]: byte v then k zero bytes)]
@@ -172,8 +174,12 @@ struct LdsLayout {
 };
 static_assert(LdsLayout<32>::kBytes == kLdsBytes, "144 KiB layout");
 
-template <int R = 32>
-__device__ inline void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc) {
+// The fused kernel's fill: one entry per iteration. Its table reads queue
+// behind the segment loads already in flight (one in-order vmcnt), and the
+// CU's other workgroup computes meanwhile; holding more table words in
+// registers here spilled its 128 VGPRs (load_lds below is the walk's).
+template <int R>
+__device__ inline void load_lds_strided(uint8_t* lds, const uint32_t* __restrict__ sc) {
   constexpr int Q = R / 4;  // 16-B stores per entry
   for (int i = threadIdx.x; i < 4 * 256 * Q; i += blockDim.x) {
     const int e = i / Q, q = i % Q, t = e >> 8, b = e & 255;
@@ -185,6 +191,34 @@ __device__ inline void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc) {
     const uint32_t v = sc[kGap + e];
     reinterpret_cast<uint4*>(lds + LdsLayout<R>::kSh + uint32_t(e) * uint32_t(R * 4))[q] = make_uint4(v, v, v, v);
   }
+  __syncthreads();
+}
+
+// The walk's fill by its NT threads: each thread issues all of its table
+// reads together, then writes its 16-B units in address order (consecutive
+// lanes, consecutive units: conflict-free) - one global round trip per
+// workgroup, where the strided loop above waits one per iteration (8) before
+// the walk's first lookup. `walk_gap` (bytes; 0 = none): also copy the 128
+// walk_gap words there.
+template <int R, int NT>
+__device__ __forceinline__ void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc, uint32_t walk_gap = 0) {
+  constexpr int kUnits = 4 * 256 * R / 4, kGapUnits = 8 * 16 * R / 4, K = kUnits / NT;
+  static_assert(kUnits % NT == 0 && kGapUnits <= NT && 128 <= NT, "fill shape");
+  const int tid = threadIdx.x;
+  uint32_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t u = uint32_t(tid + k * NT);  // unit -> (table, byte) of LdsLayout<R>::entry
+    const uint32_t t = R == 32 ? ((u >> 12) << 1) | ((u >> 3) & 1u) : (u >> 2) & 3u;
+    const uint32_t b = R == 32 ? (u >> 4) & 255u : u >> 4;
+    v[k] = sc[kT + t * 256u + b];
+  }
+  const uint32_t gv = tid < kGapUnits ? sc[kGap + tid / (R / 4)] : 0u;
+  const uint32_t wv = walk_gap && tid < 128 ? sc[kWalkGap + tid] : 0u;
+#pragma unroll
+  for (int k = 0; k < K; ++k) reinterpret_cast<uint4*>(lds)[tid + k * NT] = make_uint4(v[k], v[k], v[k], v[k]);
+  if (tid < kGapUnits) reinterpret_cast<uint4*>(lds + LdsLayout<R>::kSh)[tid] = make_uint4(gv, gv, gv, gv);
+  if (walk_gap && tid < 128) reinterpret_cast<uint32_t*>(lds + walk_gap)[tid] = wv;
   __syncthreads();
 }
 
@@ -392,7 +426,7 @@ __device__ __forceinline__ uint32_t slice_once(const Geo& geo, int64_t g, bool h
     }
     visit.advance();
   }
-  load_lds<R>(lds, sc);  // every wave joins the fill and its barrier
+  load_lds_strided<R>(lds, sc);  // every wave joins the fill and its barrier
   if (!have) return 0;
   const Slice4T<R> st(lds);
   visit.begin(cur);
@@ -472,7 +506,7 @@ __device__ __forceinline__ uint32_t slice_half(const Geo& geo, int64_t g, bool h
   u32x4_t w[8];
   if (h) half_load<1>(cur, full, visit, w);
   else half_load<0>(cur, full, visit, w);
-  load_lds<R>(lds, sc);  // every wave joins the fill and its barrier
+  load_lds_strided<R>(lds, sc);  // every wave joins the fill and its barrier
   const uint32_t v = h ? half_seg<1, Visit, R>(cur, have, full, sc, lds, visit, w)
                        : half_seg<0, Visit, R>(cur, have, full, sc, lds, visit, w);
   if (h == 1 && lane == 0) xch[stride * (wave >> 1)] = v;
@@ -726,7 +760,6 @@ __device__ __forceinline__ void fold_workgroup(const Geo& geo, const uint32_t* v
 // the library. Batching several landed chunks into one launch is what makes
 // it fast at the engine's chunk size: one 64 MiB chunk alone is 264
 // workgroups, less than one per CU slot, and ran at 3.0 TB/s (profiles/r4_sizes).
-constexpr int kWaves16 = 8;
 template <class Geo, int BLOCK>
 __global__ void __launch_bounds__(kWaves16 * 64) __attribute__((amdgpu_waves_per_eu(4)))
 verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, const uint32_t* __restrict__ sc,
@@ -799,7 +832,7 @@ verify_once16_kernel(const Geo geo, int64_t total_segs, int64_t split_block, con
 // the end the workgroup adds one value per item to the global {acc, count}
 // (fold_add) - one pair of device-scope atomics per (workgroup, item), 16
 // per 64 MiB item in a 16-chunk batch, instead of one per 8 segments.
-constexpr int kWalkWaves = 16, kWalkSlots = 256;
+constexpr int kWalkSlots = 256;
 // Bytes between the end of a lane's piece in block 3 of segment g and the
 // start of its piece in block 0 of segment g + kWalkWaves (the walk's stride).
 constexpr int64_t kWalkGapBytes = int64_t(kWalkWaves) * kSegBytes - (kBlocksPerSeg - 1) * kBlockBytes - kPieceBytes;
@@ -911,11 +944,12 @@ crc_walk_kernel(const Geo geo, int64_t total_segs, int64_t per_wg, const uint32_
   uint32_t* fn = fx + kWalkSlots;                           // ... and segment count
   const int64_t g0 = int64_t(blockIdx.x) * per_wg, g1 = min(g0 + per_wg, total_segs);
   if (g0 >= g1) return;  // whole workgroup
-  for (int i = threadIdx.x; i < 2 * kWalkSlots; i += blockDim.x) fx[i] = 0;
-  for (int i = threadIdx.x; i < 8 * 16; i += blockDim.x)
-    reinterpret_cast<uint32_t*>(lds + kGapT)[i] = sc[kWalkGap + i];
+  constexpr int NT = kWalkWaves * 64;
+  static_assert(2 * kWalkSlots <= NT, "one slot word per thread");
+  const int tid = threadIdx.x;
+  if (tid < 2 * kWalkSlots) fx[tid] = 0;
   const int64_t first_item = geo(g0).chunk;
-  load_lds<32>(lds, sc);  // once per workgroup; its barrier also publishes the slots and the gap tables
+  load_lds<32, NT>(lds, sc, kGapT);  // once per workgroup; its barrier also publishes the slots
   const Slice4T<32> st(lds);
   // two LDS atomics per run of a wave's segments in one item (the host keeps a range within kWalkSlots items)
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: g and its Seg in SGPRs
@@ -926,7 +960,7 @@ crc_walk_kernel(const Geo geo, int64_t total_segs, int64_t per_wg, const uint32_
   });
   lds_barrier();
   const int64_t nslots = geo(g1 - 1).chunk - first_item + 1;
-  for (int64_t t = threadIdx.x; t < nslots; t += blockDim.x)
+  for (int64_t t = tid; t < nslots; t += NT)
     if (fn[t]) fold_add(geo, first_item + t, fx[t], fn[t], acc);
 }
 

@@ -59,7 +59,7 @@ def supervisor():
                 sup.Attempt("fallback-2", ["--tag", "two"], {"FAKE_EXTRA": "1"})]
     rc, hist = sup.run_attempts([sys.executable, os.path.abspath(__file__), "--worker"], attempts,
                                 json_path=json_path, stall_s=float(os.environ.get("FAKE_STALL_S", "20")),
-                                finish_grace_s=3.0, kill_grace_s=2.0,
+                                finish_grace_s=1.5, kill_grace_s=1.0,
                                 log=lambda m: print(f"[sup {rank}] {m}", file=sys.stderr, flush=True))
     if rank == 0 and rc == 0:
         sup.emit_json(json_path)

@@ -75,10 +75,13 @@ def test_probe_names_a_stalled_lane():
     """Rank 1 never posts its side: rank 0's lanes to and from it stall and the
     probe raises after its timeout, naming them (bench.py then fails the
     attempt and its supervisor starts the fallback)."""
-    rts = _cluster(2)
+    t = _core.SimTiming()
+    t.wait_s = 1.0  # the fabric gives up on the never-matched sends after 1 s (default 30), so close() returns
+    rts = _cluster(2, t)
     try:
         rts[0]._barrier = lambda: None
         with pytest.raises(RuntimeError, match=r"stalled after 0 s on node 0: lane \d+ \(send to node 1\)"):
             rts[0].probe_links(MiB, timeout_s=0.5, solo=False)
     finally:
         rts[1].close()
+        rts[0].close()
