@@ -860,7 +860,7 @@ __device__ __forceinline__ uint32_t walk_gap(const uint8_t* lds, uint32_t base, 
 // between (zeros here) add their own values. `gap`: walk_gap's LDS tables.
 template <class Geo, class Sink>
 __device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t end, const uint32_t* __restrict__ sc,
-                                         const Slice4T<32>& st, uint32_t gap, Sink sink) {
+                                         const Slice4T<32>& st, uint32_t gap, uint32_t* prog, Sink sink) {
   const int lane = threadIdx.x & 63;
   const int lo = kPieceBytes * (lane & 15) + 16 * (lane >> 4);
   int64_t g = first;
@@ -880,6 +880,7 @@ __device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t 
   }
   uint32_t run = 0;  // the lane's state carried from the run's previous segment (0: none)
   uint32_t nrun = 0;  // segments in the run so far (wave-uniform)
+  uint32_t mine = 0;  // segments this wave has done
   for (; g < end; g += kWalkWaves) {
     const int64_t gn = g + kWalkWaves;
     Seg nxt = cur;  // no next segment: loads against an empty resource
@@ -922,6 +923,15 @@ __device__ __forceinline__ void crc_walk(const Geo& geo, int64_t first, int64_t 
       if (lane == 0) sink(cur, to_chunk_end(cur, s, sc), nrun);
       nrun = 0;
     }
+    // Progress-balanced issue: a wave behind its workgroup's average raises its
+    // priority. Left to the arbiter, which favors older waves, the last wave of
+    // a workgroup finished 7-20 us after the first (profiles/r6_walk_anatomy).
+    ++mine;
+    uint32_t tot = 0;
+    if (lane == 0) tot = atomicAdd(prog, 1u) + 1u;
+    tot = __builtin_amdgcn_readfirstlane(tot);
+    if (mine * kWalkWaves < tot) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
     if (cur.len != kSegBytes) {  // (rare) w did not take the next segment's words yet
 #pragma unroll
       for (int i = 0; i < 4 * kBlocksPerSeg; ++i) {
@@ -937,8 +947,8 @@ template <class Geo>
 __global__ void __launch_bounds__(kWalkWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
 crc_walk_kernel(const Geo geo, int64_t total_segs, int64_t per_wg, const uint32_t* __restrict__ sc,
                 uint32_t* __restrict__ acc) {
-  constexpr uint32_t kFold = LdsLayout<32>::kBytes, kGapT = kFold + kWalkSlots * 8;
-  __shared__ uint4 lds_raw[(kGapT + 8 * 16 * 4) / 16];
+  constexpr uint32_t kFold = LdsLayout<32>::kBytes, kGapT = kFold + kWalkSlots * 8, kProg = kGapT + 8 * 16 * 4;
+  __shared__ uint4 lds_raw[(kProg + 16) / 16];
   uint8_t* lds = reinterpret_cast<uint8_t*>(lds_raw);
   uint32_t* fx = reinterpret_cast<uint32_t*>(lds + kFold);  // per item slot: XOR
   uint32_t* fn = fx + kWalkSlots;                           // ... and segment count
@@ -948,12 +958,14 @@ crc_walk_kernel(const Geo geo, int64_t total_segs, int64_t per_wg, const uint32_
   static_assert(2 * kWalkSlots <= NT, "one slot word per thread");
   const int tid = threadIdx.x;
   if (tid < 2 * kWalkSlots) fx[tid] = 0;
+  uint32_t* prog = reinterpret_cast<uint32_t*>(lds + kProg);  // segments the workgroup's waves have done
+  if (tid == 0) *prog = 0;
   const int64_t first_item = geo(g0).chunk;
   load_lds<32, NT>(lds, sc, kGapT);  // once per workgroup; its barrier also publishes the slots
   const Slice4T<32> st(lds);
   // two LDS atomics per run of a wave's segments in one item (the host keeps a range within kWalkSlots items)
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // uniform: g and its Seg in SGPRs
-  crc_walk(geo, g0 + wave, g1, sc, st, kGapT, [=](const Seg& sg, uint32_t v, uint32_t n) {
+  crc_walk(geo, g0 + wave, g1, sc, st, kGapT, prog, [=](const Seg& sg, uint32_t v, uint32_t n) {
     const int slot = int(sg.chunk - first_item);
     atomicXor(&fx[slot], v);
     atomicAdd(&fn[slot], n);
