@@ -45,10 +45,10 @@ from distributed_llm_dissemination_amd.parallel.runtime import Runtime  # noqa: 
 MiB = 1 << 20
 _n = [0]
 # The verify queue's device time (GB/s of checked bytes, us per launch), from
-# scripts/verify_bench.py on one MI355X (profiles/r6_verify4): with peers the
-# verify stream owns 32 CUs - 1.43 TB/s in 16-chunk launches, 57 us for a lone
-# 64 MiB chunk; alone it has every CU - 5.58 TB/s, 23.4 us for a lone chunk.
-VERIFY_MODEL = {"peers": (1430.0, 10.5), "alone": (5580.0, 11.4)}
+# scripts/verify_bench.py on one MI355X (profiles/r6_verify5): with peers the
+# verify stream owns 32 CUs - 1.64 TB/s in 16-chunk launches, 50 us for a lone
+# 64 MiB chunk; alone it has every CU - 5.69 TB/s, 23.4 us for a lone chunk.
+VERIFY_MODEL = {"peers": (1640.0, 9.3), "alone": (5690.0, 11.6)}
 
 
 def predict(n: int, *, layers: int = 80, layer_bytes: int = 1 << 30, chunk: int = 64 * MiB, pcie_gbps: float = 57.5,
