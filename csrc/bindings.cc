@@ -16,6 +16,7 @@
 #include "engine/engine.h"
 #include "engine/planned_engine.h"
 #include "gpu/gpu_api.h"
+#include "roles/plan_cache.h"
 #include "roles/node.h"
 #include "sched/lp.h"
 #include "sched/maxflow.h"
@@ -85,6 +86,8 @@ PYBIND11_MODULE(_core, m) {
 
   // ---- logging
   m.def("set_log_level", &log::set_level);
+  // The process-wide leader plan cache (roles/plan_cache.h): tests that count cache hits start empty.
+  m.def("plan_cache_clear", [] { PlanCache::instance().clear(); });
   m.def("log_level", [] { return int(log::level()); });
   m.def("set_log_file", &log::set_file);
   // ---- roctx (rocprofv3 --marker-trace)

@@ -225,27 +225,44 @@ __device__ __forceinline__ void load_lds(uint8_t* lds, const uint32_t* __restric
 template <int R>
 struct Slice4T {
   const uint8_t* lds;
-  uint32_t c3, c2, c1, c0;  // per table t: its entry-0 offset + replica * 4 (bits 0-7 and 16-23)
+  uint32_t c3, c2, c1, c0;  // per lookup k = 0..3: its table's entry-0 offset + replica * 4 (bits 0-7 and 16-23)
   uint32_t g;               // shift tables + replica * 4
+  // R = 16: lanes l and l + 16 share a replica, and a table's 16 replicas fill
+  // 16 of the banks, so one lookup of every lane in one table is 2-way
+  // conflicted. Instead each group of 16 lanes (q = (lane >> 4) & 3) does
+  // lookup k on byte k ^ q: in every lookup instruction the four groups read
+  // four different tables, which sit in different banks (entry(t, b) =
+  // b * 256 + t * 64) - conflict-free. The byte position is then per lane, so
+  // the v_perm selectors are registers (sel3..sel0) instead of immediates.
+  uint32_t sel3 = 0, sel2 = 0, sel1 = 0, sel0 = 0;
   __device__ explicit Slice4T(const uint8_t* l) : lds(l) {
     const uint32_t r = (threadIdx.x & uint32_t(R - 1)) * 4u;
-    c0 = LdsLayout<R>::entry(0, 0) + r;
-    c1 = LdsLayout<R>::entry(1, 0) + r;
-    c2 = LdsLayout<R>::entry(2, 0) + r;
-    c3 = LdsLayout<R>::entry(3, 0) + r;
+    const uint32_t q = R == 16 ? (threadIdx.x >> 4) & 3u : 0u;
+    // lookup k reads byte k ^ q with table 3 - (k ^ q)
+    c3 = LdsLayout<R>::entry(int(3 - (0 ^ q)), 0) + r;
+    c2 = LdsLayout<R>::entry(int(3 - (1 ^ q)), 0) + r;
+    c1 = LdsLayout<R>::entry(int(3 - (2 ^ q)), 0) + r;
+    c0 = LdsLayout<R>::entry(int(3 - (3 ^ q)), 0) + r;
+    if constexpr (R == 16) {
+      sel3 = 0x0C020000u | ((4u + (0 ^ q)) << 8);
+      sel2 = 0x0C020000u | ((4u + (1 ^ q)) << 8);
+      sel1 = 0x0C020000u | ((4u + (2 ^ q)) << 8);
+      sel0 = 0x0C020000u | ((4u + (3 ^ q)) << 8);
+    }
     g = LdsLayout<R>::kSh + r;
   }
-  // byte k of s at bits 8-15, the constant's bytes 0 and 2 around it (v_perm_b32:
+  // byte K of s at bits 8-15, the constant's bytes 0 and 2 around it (v_perm_b32:
   // selectors 0-3 pick bytes of the second operand, 4-7 of the first, 12 a zero)
   template <uint32_t K>
-  __device__ __forceinline__ uint32_t lk(uint32_t s, uint32_t c) const {
-    return lds_word(lds, __builtin_amdgcn_perm(s, c, 0x0C020000u | ((4u + K) << 8)));
+  __device__ __forceinline__ uint32_t lk(uint32_t s, uint32_t c, uint32_t sel) const {
+    if constexpr (R == 16) return lds_word(lds, __builtin_amdgcn_perm(s, c, sel));
+    else return lds_word(lds, __builtin_amdgcn_perm(s, c, 0x0C020000u | ((4u + K) << 8)));
   }
   // One slice-by-4 step on a register that already holds (crc ^ word), with the
   // NEXT word folded in: T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3] ^ next (byte k of
   // the word is followed by 3 - k bytes: table 3 - k) - two 3-input XORs.
   __device__ __forceinline__ uint32_t mix(uint32_t s, uint32_t next) const {
-    return x3(x3(lk<0>(s, c3), lk<1>(s, c2), lk<2>(s, c1)), lk<3>(s, c0), next);
+    return x3(x3(lk<0>(s, c3, sel3), lk<1>(s, c2, sel2), lk<2>(s, c1, sel1)), lk<3>(s, c0, sel0), next);
   }
   __device__ __forceinline__ uint32_t word16(uint32_t s, u32x4_t w) const {
     return mix(mix(mix(mix(s ^ w[0], w[1]), w[2]), w[3]), 0u);
