@@ -25,20 +25,6 @@ def pytest_cmdline_main(config):
     return None
 
 
-# Modules whose tests run longest (many simulated ranks, fresh processes):
-# scheduled first, so xdist's workers start on them instead of ending on them.
-_HEAVY = ("test_timing_sim", "test_supervise", "test_plan_cost", "test_recovery", "test_multihost",
-          "test_planned_sim", "test_cli_multiprocess")
-
-
-def pytest_collection_modifyitems(session, config, items):
-    def rank(item):
-        mod = item.module.__name__.rsplit(".", 1)[-1] if item.module else ""
-        return _HEAVY.index(mod) if mod in _HEAVY else len(_HEAVY)
-
-    items.sort(key=rank)  # stable: file order within a module
-
-
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: multi-second test")
