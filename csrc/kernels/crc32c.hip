@@ -166,6 +166,15 @@ struct LdsLayout {
   static_assert(R == 32 || R == 16, "32 or 16 table replicas");
   static constexpr uint32_t kSh = R == 32 ? 131072u : 65536u;  // shift tables after the byte tables
   static constexpr uint32_t kBytes = kSh + 8u * 16u * uint32_t(R) * 4u;
+  // shift table n, entry v (replica 0). R = 32: one entry after another (each
+  // entry's 32 replicas fill the 32 banks). R = 16: tables 2k and 2k + 1
+  // interleave per entry, so table n's replicas sit in banks 16 (n & 1) + r
+  // whatever the entry - lanes l and l + 16 then read different banks when they
+  // look up tables of different parity (Slice4T::gap).
+  static __device__ __host__ constexpr uint32_t gap_entry(int n, int v) {
+    return R == 32 ? uint32_t(n * 16 + v) * 128u
+                   : uint32_t(n >> 1) * 2048u + uint32_t(v) * 128u + uint32_t(n & 1) * 64u;
+  }
   // byte table t, entry b, replica r
   static __device__ __forceinline__ uint32_t entry(int t, int b) {
     return R == 32 ? uint32_t(t >> 1) * 65536u + uint32_t(b) * 256u + uint32_t(t & 1) * 128u
@@ -189,7 +198,8 @@ __device__ inline void load_lds_strided(uint8_t* lds, const uint32_t* __restrict
   for (int i = threadIdx.x; i < 8 * 16 * Q; i += blockDim.x) {
     const int e = i / Q, q = i % Q;
     const uint32_t v = sc[kGap + e];
-    reinterpret_cast<uint4*>(lds + LdsLayout<R>::kSh + uint32_t(e) * uint32_t(R * 4))[q] = make_uint4(v, v, v, v);
+    reinterpret_cast<uint4*>(lds + LdsLayout<R>::kSh + LdsLayout<R>::gap_entry(e >> 4, e & 15))[q] =
+        make_uint4(v, v, v, v);
   }
   __syncthreads();
 }
@@ -204,6 +214,7 @@ template <int R, int NT>
 __device__ __forceinline__ void load_lds(uint8_t* lds, const uint32_t* __restrict__ sc, uint32_t walk_gap = 0) {
   constexpr int kUnits = 4 * 256 * R / 4, kGapUnits = 8 * 16 * R / 4, K = kUnits / NT;
   static_assert(kUnits % NT == 0 && kGapUnits <= NT && 128 <= NT, "fill shape");
+  static_assert(R == 32, "shift tables written in entry order (LdsLayout<32>::gap_entry)");
   const int tid = threadIdx.x;
   uint32_t v[K];
 #pragma unroll
@@ -270,9 +281,22 @@ struct Slice4T {
   // shift over kGapBytes zeros, with `next` folded in
   __device__ __forceinline__ uint32_t gap(uint32_t s, uint32_t next) const {
     uint32_t r[8];
+    if constexpr (R == 16) {
+      // lanes 16-31 of each half-wave take table n ^ 1 where lanes 0-15 take
+      // table n (the other bank half, LdsLayout<16>::gap_entry): on the
+      // register with its nibbles swapped pairwise, nibble n is nibble n ^ 1
+      const bool h = (threadIdx.x >> 4) & 1u;
+      const uint32_t sw = ((s & 0x0F0F0F0Fu) << 4) | ((s >> 4) & 0x0F0F0F0Fu);
+      const uint32_t t = h ? sw : s;
+      const uint32_t ge = g + (h ? 64u : 0u), go = g + (h ? 0u : 64u);  // even / odd n
 #pragma unroll
-    for (int n = 0; n < 8; ++n)
-      r[n] = lds_word(lds, g + uint32_t(n) * uint32_t(16 * R * 4) + ((s >> (4 * n)) & 15u) * uint32_t(R * 4));
+      for (int n = 0; n < 8; ++n)
+        r[n] = lds_word(lds, (n & 1 ? go : ge) + uint32_t(n >> 1) * 2048u + ((t >> (4 * n)) & 15u) * 128u);
+    } else {
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        r[n] = lds_word(lds, g + LdsLayout<R>::gap_entry(n, 0) + ((s >> (4 * n)) & 15u) * uint32_t(R * 4));
+    }
     return x3(x3(x3(r[0], r[1], r[2]), r[3], r[4]), x3(r[5], r[6], r[7]), next);
   }
   // a ^ b ^ c in one v_bitop3_b32
@@ -553,14 +577,15 @@ __device__ inline void unpack16_nt(const u32x4_t& w, float s, uint4* __restrict_
 // stores. Stored directly, each of the two store instructions covers the 2 KiB
 // at half density (16 B in every 32). One wave's LDS operations run in issue
 // order, so no barrier is needed between its writes and reads.
-// The slot's 64 16-B granules are swizzled (g -> g ^ ((g >> 3) & 6)): the
+// The slot's 64 16-B granules are swizzled (g -> g ^ ((g >> 3) & 7)): the
 // writers of one 16-lane group (granules 8 m + 2 r, m = 0..7) then hit 8
 // distinct bank quads instead of 2 (4-way conflicts: 29 M conflict cycles per
-// 512 MiB, profiles/r3_kernels), and the readers (granule = lane) stay distinct.
+// 512 MiB, profiles/r3_kernels; the & 6 of rounds 3-5 left pairs of them in
+// one quad of the 32-lane half), and the readers (granule = lane) stay distinct.
 // The stores are nontemporal: the output is written once and never read back,
 // so it has no business in L2 or the Infinity Cache (5.04 -> 5.39-5.43 TB/s at
 // 512 MiB, profiles/r4_nt).
-__device__ __forceinline__ uint32_t swz(uint32_t g) { return g ^ ((g >> 3) & 6u); }
+__device__ __forceinline__ uint32_t swz(uint32_t g) { return g ^ ((g >> 3) & 7u); }
 __device__ __forceinline__ void store_staged(const uint32_t (&o)[8], uint8_t* slot, uint4* __restrict__ region) {
   const int lane = threadIdx.x & 63, m = lane & 15, r = lane >> 4;
   uint4* g = reinterpret_cast<uint4*>(slot);  // granules

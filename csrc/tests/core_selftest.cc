@@ -9,6 +9,7 @@
 #include <thread>
 
 #include "core/crc32c.h"
+#include "core/vclock.h"
 #include "core/log.h"
 #include "engine/planned_engine.h"
 #include "roles/node.h"
@@ -102,11 +103,23 @@ static void ring(bool tcp, int mode) {
 // mode-2 chunk jobs: steals move jobs between the holders, never a dest's own
 // load of a layer it holds (that would write its chunks twice: the race TSAN
 // found here in round 5).
-static void planned_sim(int mode, double corrupt = 0, int die = -1, bool crossing = false) {
+// virt: on the virtual clock with modeled link and staging rates (the
+// simulator's model-time mode, scripts/predict_scaling.py): every engine,
+// node and fabric thread waits through vclock, the main thread uncounted.
+static void planned_sim(int mode, double corrupt = 0, int die = -1, bool crossing = false, bool virt = false) {
   const int n = 4, L = 6;
   const int64_t chunk = 1 << 16, size = 3 * chunk + 100;
   static int uniq = 0;
   std::string key = "tsan" + std::to_string(++uniq);
+  if (virt) {
+    vclock::enable(true);
+    SimTiming t;
+    t.link_bps = 1e9;   // 64 KiB chunks: 65 us per transfer in model time
+    t.stage_bps = 2e9;
+    t.verify_bps = 50e9;
+    t.verify_launch_s = 10e-6;
+    sim_set_timing(key, t);
+  }
   AddrRegistry reg;
   for (int i = 0; i < n; ++i) reg[NodeID(i)] = key + "-" + std::to_string(i);
   std::vector<std::shared_ptr<Transport>> ts;
@@ -174,12 +187,16 @@ static void planned_sim(int mode, double corrupt = 0, int die = -1, bool crossin
   nodes.clear();
   for (auto& e : engines) e->shutdown();
   for (auto& t : ts) t->close();
+  if (virt) {
+    EXPECT(vclock::now() > 0);
+    vclock::enable(false);
+  }
 }
 
 int main(int argc, char** argv) {
   log::set_level(log::Error);
   // optional: run one case only (0-3 ring modes, 4-6 planned modes 1-3, 7 corruption, 8-9 rank death,
-  // 10 crossing mode-2 chunk jobs)
+  // 10 crossing mode-2 chunk jobs, 11-13 planned modes 1-3 on the virtual clock)
   const int only = argc > 1 ? atoi(argv[1]) : -1;
   auto on = [&](int k) { return only < 0 || only == k; };
   for (int mode = 0; mode <= 3; ++mode) {
@@ -193,6 +210,8 @@ int main(int argc, char** argv) {
   if (on(8)) planned_sim(1, 0, 3);  // a rank dies: suspect -> probe -> shrink -> re-plan
   if (on(9)) planned_sim(2, 0, 2);
   if (on(10)) planned_sim(2, 0, -1, true);
+  for (int mode = 1; mode <= 3; ++mode)
+    if (on(10 + mode)) planned_sim(mode, 0, -1, mode == 2, true);
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;
