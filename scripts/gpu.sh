@@ -65,9 +65,12 @@ case "$RECIPE" in
     timeout -k 10 1100 $PYTEST tests/test_gpu_multirank.py > $OUT/pytest.log 2>&1
     ;;
   shared8)
+    # SHARED8_SPECS="spec;spec": only these (e.g. a rerun of the last ones)
     rc=0
-    for spec in "1" "1 --seeding uniform" "2 --pull-window 2" "3" "0 --seeding leader" \
-                "0 --seeding leader --bcast collective" "1 --pack fp8 --layer-mib 96"; do
+    SPECS=("1" "1 --seeding uniform" "2 --pull-window 2" "3" "0 --seeding leader" \
+           "0 --seeding leader --bcast collective" "1 --pack fp8 --layer-mib 96")
+    [ -n "$SHARED8_SPECS" ] && IFS=';' read -r -a SPECS <<< "$SHARED8_SPECS"
+    for spec in "${SPECS[@]}"; do
       set -- $spec
       mode=$1; shift
       tag=m${mode}$(echo "$*" | tr -c 'a-z0-9' '_')
