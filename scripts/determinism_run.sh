@@ -31,6 +31,8 @@ fi
 } >> "$SUMMARY"
 XDIST=()
 [ "$WORKERS" -gt 0 ] && XDIST=(-n "$WORKERS")
+# tests/conftest.py runs -m "not gpu" on 4 workers unless told otherwise
+[ "$WORKERS" -eq 0 ] && export DISSEM_TEST_SERIAL=1
 rc=0
 for i in $(seq 1 "$RUNS"); do
   start=$(date +%s)
