@@ -16,12 +16,14 @@
 //    other lanes as zeros: a fixed GF(2)-linear map, 8 nibble lookups;
 //  * each lane's CRC is shifted to the END OF ITS SEGMENT with one GF(2)
 //    multiply by a per-lane constant (x^(8*64*(63-lane))), then the lanes are
-//    XOR-reduced with cross-lane shuffles: a segment's value is its raw CRC;
+//    XOR-reduced with cross-lane shuffles: a segment's value is its raw CRC
+//    (the walk does this once per run of a wave's segments of one chunk,
+//    carrying each lane's register across the segments between: crc_walk);
 //  * the wave then shifts that value to the END OF ITS CHUNK - x^(8*16 KiB*j)
 //    from three 1024-entry levels of a table, then x^(8*rem) for a chunk whose
 //    last segment is short (wave-uniform products);
 //  * the fold runs in the same launch: a workgroup XORs its waves' values per
-//    chunk (in LDS) and adds them to the chunk's {acc, count} words with
+//    chunk (in LDS) and adds them to the chunk's {acc, count} word with
 //    device-scope atomics; the workgroup that completes the count writes the standard
 //    CRC32C (fold_add below). The separate fold launch this replaced cost
 //    8.4-9.6 us per 64 MiB chunk in the round-4 engine traces.
@@ -45,10 +47,12 @@
 // conflict (2x the useful LDS cycles in round 1, profiles/r1_counters). Every
 // table entry is stored R times, replica r in bank r, and lane l reads replica
 // l mod R: R = 32 is conflict-free by construction (144 KiB: one workgroup
-// per CU, the CRC-only walk); the fused kernel uses R = 16 (lanes l and l + 16
-// share a bank, up to 2-way conflicts) in 72 KiB, so two 512-thread workgroups
-// share a CU and one fills its tables and waits for its first loads while the
-// other computes.
+// per CU, the CRC-only walk); the fused kernel uses R = 16 in 72 KiB, so two
+// 512-thread workgroups share a CU and one fills its tables and waits for its
+// first loads while the other computes. Lanes l and l + 16 then share a
+// replica, so each 16-lane group reads a different table in one instruction
+// (Slice4T: lookup k on byte k ^ group; LdsLayout<16>::gap_entry) - as
+// conflict-free as R = 32 (2.5e6 vs 2.95e7 conflict cycles, profiles/r6_pmc2).
 // The address of byte k of s is ONE v_perm_b32 of s with a per-lane constant,
 // then the ds_read_b32.
 //
