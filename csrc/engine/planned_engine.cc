@@ -159,7 +159,21 @@ void PlannedEngine::shutdown() {
     if (kv.second.out) backend_->free(kv.second.out);
   }
   layers_.clear();
+  for (uint8_t* b : scratch_all_) backend_->free(b);
+  scratch_all_.clear();
+  scratch_free_.clear();
   backend_->destroy(failed_.load());
+}
+
+uint8_t* PlannedEngine::scratch_take() {
+  if (!scratch_free_.empty()) {
+    uint8_t* b = scratch_free_.back();
+    scratch_free_.pop_back();
+    return b;
+  }
+  CallMark cm(this, "alloc", -1);
+  scratch_all_.push_back(backend_->alloc(cfg_.chunk_bytes));  // a full piece is at most one chunk
+  return scratch_all_.back();
 }
 
 int PlannedEngine::rank_of(NodeID n) const {
@@ -741,7 +755,7 @@ bool PlannedEngine::issue_lane(int lane) {
         // exactly one writer.
         const uint8_t s = L.st[size_t(p.chunk)];
         if (s == 1 || s == 2 || s == 3) {
-          p.scratch = backend_->alloc(p.len);
+          p.scratch = scratch_take();
           at = p.scratch;
         }
       }
@@ -920,7 +934,7 @@ void PlannedEngine::poll() {
       Layer& L = layers_[p.layer];
       if (p.scratch) {
         const bool bad = it->slots[i] != ~0u && backend_->crc_result(it->slots[i]) != p.crc;
-        backend_->free(p.scratch);
+        scratch_free_.push_back(p.scratch);  // its check has completed
         {
           std::lock_guard<std::mutex> lk(stats_mu_);
           stats_.scratch_landings++;

@@ -449,6 +449,13 @@ class PlannedEngine : public DataEngine {
 
   // disk tier: issue thread owns bounce_free_/disk_wait_; readers exchange via disk_mu_
   std::vector<uint8_t*> bounce_all_, bounce_free_;
+  // Scratch landings (a recv of a chunk this rank stages or holds): chunk-sized
+  // device buffers, reused and freed only at shutdown - a free mid-session
+  // (hipFree synchronizes the device) hung a rank-death recovery whose
+  // re-plan landed such chunks while its peers' RCCL kernels waited
+  // (profiles/r6_insure).
+  std::vector<uint8_t*> scratch_all_, scratch_free_;
+  uint8_t* scratch_take();
   std::deque<std::pair<Ev, uint8_t*>> bounce_busy_;  // H2D copy event -> its bounce buffer
   std::deque<DiskRead> disk_wait_;                 // waiting for a bounce buffer
   std::mutex disk_mu_;
