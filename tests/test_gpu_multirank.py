@@ -70,6 +70,9 @@ def n(request):
                                         (1, ["--pack", "fp8", "--layer-mib", "96"]),
                                         (1, ["--pack", "fp8", "--store", "bf16", "--layer-mib", "96"]),
                                         (1, ["--inject", "slow-link=0:1:2G"]),
+                                        # every rank holds every layer: mode 2 loads a dest's own copy and
+                                        # may let an idle peer steal it - scratch landings on the HIP backend
+                                        (2, ["--pull-window", "2", "--copies", "3"]),
                                         (1, ["--seeding", "uniform", "--source-pool", "3"])])
 def test_bench_modes(n, mode, extra, request):
     if n == 8 and _ngpus() < 2 and (extra or mode != 1) and os.environ.get("DISSEM_FULL_REHEARSAL") != "1":
