@@ -373,6 +373,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readonly("disk_wait_ms", &PlannedStats::disk_wait_ms)
       .def_readonly("disk_direct_bytes", &PlannedStats::disk_direct_bytes)
       .def_readonly("scratch_landings", &PlannedStats::scratch_landings)
+      .def_readonly("scratch_buffers", &PlannedStats::scratch_buffers)
       .def_readonly("disk_buffered_bytes", &PlannedStats::disk_buffered_bytes)
       .def_readonly("order_violations", &PlannedStats::order_violations);
   py::class_<PlannedEngine, DataEngine, std::shared_ptr<PlannedEngine>>(m, "PlannedEngine")

@@ -173,6 +173,10 @@ uint8_t* PlannedEngine::scratch_take() {
   }
   CallMark cm(this, "alloc", -1);
   scratch_all_.push_back(backend_->alloc(cfg_.chunk_bytes));  // a full piece is at most one chunk
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    stats_.scratch_buffers++;
+  }
   return scratch_all_.back();
 }
 

@@ -172,6 +172,7 @@ struct PlannedStats {
   int64_t disk_direct_bytes = 0, disk_buffered_bytes = 0;
   int64_t order_violations = 0;  // sends that waited on a recv with a larger key (must stay 0)
   int64_t scratch_landings = 0;  // recvs of chunks already staged / resident here (landed in scratch)
+  int64_t scratch_buffers = 0;   // scratch-landing buffers allocated (the pool grows only when all are busy)
   // device time the verify stream spent on checks (landing met -> check done):
   // against the session's wall time, the occupancy of the verify CUs
   double verify_busy_ms = 0;

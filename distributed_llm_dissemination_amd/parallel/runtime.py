@@ -998,7 +998,7 @@ class Runtime:
             for k in ("bytes_sent", "bytes_recv", "bytes_staged", "bytes_verified", "groups", "pieces",
                       "verify_failures", "unverified_pieces", "nacks", "injected", "issue_ms",
                       "suspects", "shrinks", "aborted_pieces", "paced", "order_violations", "disk_wait_ms",
-                      "disk_direct_bytes", "disk_buffered_bytes", "scratch_landings",
+                      "disk_direct_bytes", "disk_buffered_bytes", "scratch_landings", "scratch_buffers",
                       "group_us_hist", "land_us_hist", "verify_busy_ms", "verify_calls", "verify_chunks")
         }
 

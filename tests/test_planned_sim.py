@@ -173,6 +173,14 @@ def test_mode2_dest_holding_a_layer_loads_it_itself(n):
         for r in res:  # staged or received - a scratch landing is a received duplicate of a staged chunk
             held = r.engine_stats["bytes_staged"] + r.engine_stats["bytes_recv"] - r.engine_stats["scratch_landings"] * MiB
             assert held == 6 * 4 * MiB, r.engine_stats
+    # scratch buffers come from a pool: allocated when all are busy, never one per landing (a free per
+    # landing synchronized the GPU under live RCCL groups and hung a recovery, profiles/r6_insure)
+    for i in range(n):
+        landings = sum(res[i].engine_stats["scratch_landings"] for res in outs)
+        allocated = sum(res[i].engine_stats["scratch_buffers"] for res in outs)
+        assert allocated <= landings
+        if landings >= 4:
+            assert allocated < landings, (landings, allocated)
 
 
 def test_repeated_sessions_reset_state():
